@@ -1,0 +1,201 @@
+/* rlmd_abi.h — C ABI of librlmd_amd.so, the MI355X (gfx950) hot path of
+ * majidsina/rlmd re-designed as batched HIP kernels.
+ *
+ * The reference has no FFI: its boundary is a duck-typed Python interface
+ * (SURVEY.md §8b).  Each entry point below replaces one reference method,
+ * batched over lanes; the Python facade in rlmd_amd/ binds them with ctypes
+ * (INTEGRATION.md shows the binding a maintainer would add).
+ *
+ * Conventions
+ *   - every function returns 0 on success, non-zero on error; the message is
+ *     in rlmd_last_error() (thread-local);
+ *   - every pointer argument named *_dev is DEVICE memory (e.g. a torch CUDA
+ *     tensor's data_ptr()); *_host is host memory;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream); all
+ *     device work is enqueued asynchronously on it;
+ *   - the library owns the memory it allocates (env lane state, replay ring,
+ *     learner scratch) and never frees caller memory (torch-owned params).
+ */
+#ifndef RLMD_ABI_H
+#define RLMD_ABI_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ errors */
+const char* rlmd_last_error(void);
+int rlmd_device_sync(void);
+
+/* --------------------------------------------------------------------- env */
+/* families (envs/<family>_envs.py) and investors */
+enum { RLMD_COIN = 0, RLMD_DICE = 1, RLMD_GBM = 2, RLMD_DICE_SH = 3, RLMD_MARKET = 4 };
+enum { RLMD_INV_A = 0, RLMD_INV_B = 1, RLMD_INV_C = 2, RLMD_INV_INSURED = 3 };
+
+typedef struct rlmd_env_s* rlmd_env_t;
+
+typedef struct {
+  int32_t family;      /* RLMD_COIN .. RLMD_MARKET */
+  int32_t investor;    /* RLMD_INV_* (INSURED only with RLMD_DICE_SH) */
+  int32_t n_lanes;     /* independent trajectories stepped per launch */
+  int32_t n_gambles;   /* coin/dice/gbm: simultaneous gambles; market: n_assets */
+  int32_t obs_days;    /* market: observed days (1 = D1 envs, >1 = Dx envs) */
+  int32_t time_length; /* market: env time_length argument (train_days+obs_days-1) */
+  int32_t action_days; /* market: days between actions (reference default 1) */
+  int32_t shuffle_days;/* market: in-block shuffle interval (train 5, eval 3) */
+  int32_t sample_days; /* market: days excluded from the start draw (rl_market.py:59) */
+  int32_t pad0;
+  uint64_t seed;       /* Philox key for env draws */
+} rlmd_env_cfg;
+
+/* Replaces `Cls(n_gambles)` / `Cls()` / `Cls(n_assets, time_length, obs_days)`
+ * (envs/<family>_envs.py __init__).  prices_host: market close prices [n_days, n_assets]
+ * f64 row-major (tools/market_data/stooq_*.npy), NULL for other families. */
+int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t n_days,
+                    rlmd_env_t* out);
+int rlmd_env_destroy(rlmd_env_t env);
+/* observation_space.shape[0], action_space.shape[0], risk width, draws per step */
+int rlmd_env_dims(rlmd_env_t env, int32_t* state_dim, int32_t* action_dim, int32_t* risk_dim,
+                  int32_t* draw_dim);
+
+/* Replaces env.reset() (e.g. envs/gbm_envs.py:214-229; market: reset(obs) with
+ * the episode slicing of scripts/rl_market.py:202-214).  Resets the lanes whose
+ * lane_mask_dev byte is non-zero (NULL = all) and writes their state (f64, [N, S]). */
+int rlmd_env_reset(rlmd_env_t env, const uint8_t* lane_mask_dev, double* state_dev, void* stream);
+
+/* Replaces env.step(action) (e.g. envs/gbm_envs.py:147-212 + the *_dones of
+ * tools/env_resources.py).  actions_dev f32 [N, A]; draws_dev f64 [N, D] injected
+ * draws (uniforms for coin/dice/dice_sh, standard normals for gbm) or NULL for
+ * Philox draws at the env's internal step counter; outputs f64 next_state [N, S],
+ * reward [N], done/learn_done u8 [N, 2], risk [N, R] (nullable).  No auto-reset:
+ * the caller resets finished lanes, as the reference driver does. */
+int rlmd_env_step(rlmd_env_t env, const float* actions_dev, const double* draws_dev,
+                  double* next_state_dev, double* reward_dev, uint8_t* done_dev, double* risk_dev,
+                  void* stream);
+
+/* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
+int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
+
+/* ------------------------------------------------------------------ replay */
+typedef struct rlmd_replay_s* rlmd_replay_t;
+
+/* Replaces tools/replay_torch.py ReplayBufferTorch.__init__ (:57-115): an
+ * on-device ring of `capacity` transitions stored f32 SoA. */
+int rlmd_replay_create(int64_t capacity, int32_t state_dim, int32_t action_dim,
+                       rlmd_replay_t* out);
+int rlmd_replay_destroy(rlmd_replay_t rb);
+/* Replaces store_exp (tools/replay_torch.py:167-197): appends n transitions at
+ * mem_idx % capacity; reward stored as max(r, r_abs_zero = -inf). */
+int rlmd_replay_insert(rlmd_replay_t rb, int64_t n, const float* s_dev, const float* a_dev,
+                       const float* r_dev, const float* s2_dev, const uint8_t* done_dev,
+                       void* stream);
+int rlmd_replay_mem_idx(rlmd_replay_t rb, int64_t* mem_idx);
+/* Replaces sample_exp (tools/replay_torch.py:360-412): B DISTINCT uniform indices
+ * in [0, min(mem_idx, capacity)) drawn with Philox(seed, (slot, draw_ctr, TAG, round))
+ * and gathered; idx_dev i64 [B]; s/s2 f32 [B,S], a [B,A], r [B], done u8 [B]. */
+int rlmd_replay_sample(rlmd_replay_t rb, int32_t batch, uint64_t seed, uint64_t draw_ctr,
+                       int64_t* idx_dev, float* s_dev, float* a_dev, float* r_dev, float* s2_dev,
+                       uint8_t* done_dev, void* stream);
+
+/* ------------------------------------------------------------------- agent */
+enum { RLMD_SAC = 0, RLMD_TD3 = 1 };
+/* critic losses, tools/critic_loss.py:344-453 */
+enum {
+  RLMD_LOSS_MSE = 0, RLMD_LOSS_HUB = 1, RLMD_LOSS_MAE = 2, RLMD_LOSS_HSC = 3, RLMD_LOSS_CAU = 4,
+  RLMD_LOSS_TCAU = 5, RLMD_LOSS_CIM = 6, RLMD_LOSS_MSE2 = 7, RLMD_LOSS_MSE4 = 8, RLMD_LOSS_MSE6 = 9
+};
+enum { RLMD_FP32 = 0, RLMD_BF16 = 1 }; /* MLP GEMM operand precision (fp32 accumulate) */
+
+typedef struct rlmd_agent_s* rlmd_agent_t;
+
+typedef struct {
+  int32_t algo, state_dim, action_dim, h1, h2;
+  int32_t batch;       /* mini_batch_size (rl_multiplicative.py:108-113) */
+  int32_t topk;        /* optimise_count = batch_size[algo] */
+  int32_t loss_type;   /* RLMD_LOSS_* */
+  int32_t precision;   /* RLMD_FP32 | RLMD_BF16 */
+  int32_t actor_update_interval, target_critic_update, target_actor_update, temp_update_interval;
+  int32_t actor_topk;  /* 1: actor percentile != 100 (sort + top-k), 0: plain mean */
+  float gamma, tau, lr_actor, lr_critic, lr_temp, reward_scale, max_action;
+  float log_scale_min, log_scale_max, reparam_noise, log_noise, cauchy_scale, initial_logtemp;
+  float policy_noise, target_policy_noise, target_policy_clip; /* already x max_action */
+  uint64_t seed;
+} rlmd_agent_cfg;
+
+/* Number of f32 parameters in the trainable set [actor | critic_1 | critic_2]
+ * (torch nn.Linear layout, weight [out,in] then bias, per layer) and the
+ * offsets of the three nets within it. */
+int rlmd_agent_layout(const rlmd_agent_cfg* cfg, int64_t* n_params, int64_t* off_actor,
+                      int64_t* off_critic1, int64_t* off_critic2);
+
+/* Replaces Agent_sac.__init__ / Agent_td3.__init__ (algos/algo_sac.py:82-170,
+ * algos/algo_td3.py:84-176).  All five buffers are caller-owned device f32
+ * [n_params]: params (trainable), target params (same layout; SAC's
+ * target_actor slot is unused as in the reference), grads, Adam m and v. */
+int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params_dev, float* target_dev,
+                      float* grads_dev, float* adam_m_dev, float* adam_v_dev, rlmd_agent_t* out);
+int rlmd_agent_destroy(rlmd_agent_t ag);
+
+/* Replaces select_next_action (mode 0, algo_sac.py:192-218 / algo_td3.py:198-223)
+ * and eval_next_action (mode 1, :220-236 / :225-238), batched over n rows of
+ * obs_dev f32 [n, S]; actions_dev f32 [n, A].  noise_ctr selects the Philox
+ * counter of the acting noise; eps_dev (nullable) injects it instead. */
+int rlmd_agent_act(rlmd_agent_t ag, const float* obs_dev, int64_t n, float* actions_dev,
+                   int32_t mode, uint64_t noise_ctr, const float* eps_dev, void* stream);
+
+/* Replaces learn() (algo_sac.py:369-595 / algo_td3.py:363-531): k_updates
+ * updates, each sampling a fresh mini-batch from rb.  stats_dev (nullable) f32
+ * [k_updates, 16] = loss[11] | logtemp | loss_params[4] per update. */
+int rlmd_agent_learn(rlmd_agent_t ag, rlmd_replay_t rb, int32_t k_updates, float* stats_dev,
+                     void* stream);
+
+/* Parity hook: one learn() on a caller-supplied mini-batch with injected noise.
+ * s/s2 f32 [B,S], a [B,A], r [B], done u8 [B], eff i32 [B] (multi-step length,
+ * NULL = 1); eps_a / eps_b f32 [B,A]: SAC next / current eps, TD3 target noise
+ * (eps_b unused). */
+int rlmd_agent_learn_batch(rlmd_agent_t ag, const float* s_dev, const float* a_dev,
+                           const float* r_dev, const float* s2_dev, const uint8_t* done_dev,
+                           const int32_t* eff_dev, const float* eps_a_dev, const float* eps_b_dev,
+                           float* stats_dev, void* stream);
+
+/* Device scalars: [cauchy_1, cauchy_2, log_alpha, learn_step_cntr, nan_flag]. */
+int rlmd_agent_scalars(rlmd_agent_t ag, double* out_host5);
+
+/* ---------------------------------------------------------------- training */
+/* One fused vector step of rl_multiplicative.py:190-227 over all lanes:
+ * actions (random warm-up | policy), action_window clipping, env step,
+ * replay insert of (s, a, max(r,-inf), s', learn_done), auto-reset of finished
+ * lanes, then k_updates learn() calls.  obs_dev f32 [N, S] is the lanes'
+ * current state (read and advanced in place); actions_dev f32 [N, A] scratch.
+ * cum_step is the per-lane step counter of the warm-up / smoothing schedule
+ * (rl_multiplicative.py:192-211).  episode_stats_dev (nullable) f64 [4]
+ * accumulates {finished episodes, sum of final rewards, sum of lengths, steps}. */
+typedef struct {
+  int64_t cum_step;
+  int32_t warmup_steps;    /* inputs["random"] */
+  int32_t smoothing_window;/* inputs["smoothing_window"] */
+  int32_t abs_warmup;      /* np.abs on warm-up samples (all but GBM, rl_multiplicative.py:196-201) */
+  int32_t k_updates;
+} rlmd_train_cfg;
+
+int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlmd_train_cfg* cfg,
+                    float* obs_dev, float* actions_dev, double* episode_stats_dev,
+                    float* stats_dev, void* stream);
+
+/* Initialise obs_dev f32 [N, S] with every lane reset (episode start). */
+int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
+
+/* ------------------------------------------------------------- test hooks */
+/* One MLP-layer GEMM (mode 0 forward y = relu?(A W^T + b), 1 input-gradient
+ * C = mask(A W), 2 weight-gradient C = A^T W (+ bias_grad = colsum A)) on
+ * caller buffers; the kernel the learner uses for every nn.Linear. */
+int rlmd_gemm(int32_t precision, int32_t mode, int32_t M, int32_t N, int32_t K, int32_t relu,
+              const float* A_dev, int32_t lda, const float* B_dev, int32_t ldb,
+              const float* bias_dev, float* C_dev, int32_t ldc, const float* mask_dev,
+              int32_t ldm, float* bias_grad_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RLMD_ABI_H */

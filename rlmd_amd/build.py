@@ -1,0 +1,68 @@
+"""Build librlmd_amd.so (gfx950) in-tree with hipcc.
+
+The .so is the product: a C-ABI shared library (include/rlmd_abi.h) loaded by
+rlmd_amd/_abi.py with ctypes.  Objects are rebuilt only when a source or
+header is newer than the object.
+"""
+import os
+import subprocess
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "_build")
+LIB = os.path.join(HERE, "librlmd_amd.so")
+ARCH = os.environ.get("RLMD_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+SOURCES = ["abi.hip", "env.hip", "replay.hip", "gemm.hip", "learn.hip"]
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
+         "-Wno-unused-variable", "-ffp-contract=fast"]
+
+
+def _headers():
+    return [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith(".h")] + [
+        os.path.join(HERE, "..", "include", "rlmd_abi.h")]
+
+
+def _stale(obj, src, deps):
+    if not os.path.exists(obj):
+        return True
+    t = os.path.getmtime(obj)
+    return any(os.path.getmtime(d) > t for d in [src] + deps)
+
+
+def _compile(src):
+    obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+    path = os.path.join(CSRC, src)
+    if not _stale(obj, path, _headers()):
+        return obj, None
+    cmd = [HIPCC, *FLAGS, "-c", path, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    return obj, None
+
+
+def build(verbose=False, jobs=None):
+    os.makedirs(BUILD, exist_ok=True)
+    jobs = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 4) // 2), 8)
+    with ThreadPoolExecutor(jobs) as ex:
+        res = list(ex.map(_compile, SOURCES))
+    errs = [e for _, e in res if e]
+    if errs:
+        raise RuntimeError("hipcc failed:\n" + "\n".join(errs))
+    objs = [o for o, _ in res]
+    if not os.path.exists(LIB) or any(os.path.getmtime(o) > os.path.getmtime(LIB) for o in objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+    if verbose:
+        print("built", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(verbose=True)
+    sys.exit(0)

@@ -1,0 +1,641 @@
+// env.hip — batched multiplicative-gamble environments for gfx950.
+//
+// One lane = one independent Gym environment of the reference; one thread
+// steps one lane (the work per lane is ~100 FP64 ops and a few dozen bytes, so
+// the kernel is HBM/latency bound: SoA lane state, coalesced f32/f64 arrays).
+//
+// Reference semantics restated (file:line into majidsina/rlmd):
+//   coin   envs/coin_flip_envs.py:150-216 (A), :290-362 (B, stop-loss = |a0| :308),
+//          :436-521 (C); consts :40-93
+//   dice   envs/dice_roll_envs.py:153-219, :293-365, :439-524; consts :39-96
+//   gbm    envs/gbm_envs.py:147-212, :286-357, :431-515; consts :43-90
+//   dice_sh envs/dice_roll_sh_envs.py:160-235 (INSURED), :290-365, :420-502, :557-645
+//   market envs/market_envs.py:133-202 (D1), :611-682 (Dx) + B/C variants
+//   dones  tools/env_resources.py:26-80 (any lev_max), :83-137 (all), :140-200 (market)
+//   slicing tools/env_resources.py:203-291 (observed_market_state/time_slice/shuffle_data)
+//
+// Precision follows the reference's dtype flow under NumPy 2 for f32 actions
+// (restated and pinned bit-exactly in oracle/envs.py): wealth and
+// returns f64; GBM / market leverages f32 (`f32 * Python int`), coin / dice
+// leverages f64 (`f32 * np.float64`); stop-loss, retention, safe-haven leverage,
+// `1e4 * stop_loss`, `max(., MIN_VALUE)` and the first-step bet size f32;
+// Dice_SH_INSURED leverage f32.  FP contraction is off so every rounding
+// happens where NumPy's does.
+#pragma clang fp contract(off)
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../../include/rlmd_abi.h"
+#include "rlmd_common.h"
+#include "rlmd_internal.h"
+
+namespace {
+
+constexpr double kInitialValue = 1e4;
+constexpr double kMinValue = 100.0;  // max(MIN_VALUE_RATIO * INITIAL_VALUE, 1)
+constexpr double kMaxAbsAction = 0.99;
+constexpr double kMinWeight = 1e-5;
+
+struct FamConst {
+  double max_value, min_reward, min_return, max_return, lev_factor;
+};
+
+__host__ __device__ inline FamConst fam_const(int fam) {
+  switch (fam) {
+    case RLMD_COIN: return {1e18, 1e-3, -0.9, 1e10, 2.0};
+    case RLMD_DICE: return {1e18, 1e-3, -0.9, 1e10, 2.0};
+    case RLMD_GBM: return {1e18, 1e-3, -2.3025850929940455 /* np.log(0.1) */, 1e10, 5.0};
+    case RLMD_DICE_SH: return {1e18, 1e-6, -0.99, 1e10, 2.0};
+    default: return {1e34, 1e-3, -0.9, 1e10, 3.0};
+  }
+}
+
+// GBM: LOG_MEAN = DRIFT - VOL**2 / 2 (envs/gbm_envs.py:43-63)
+constexpr double kGbmDrift = 0.0540025395205692;
+constexpr double kGbmVol = 0.1897916175617430;
+// dice_sh: I_LEV_FACTOR = (-1 - 5) / (-0.5 - 5) (envs/dice_roll_sh_envs.py:70)
+constexpr double kShILev = (-1.0 - 5.0) / (-0.5 - 5.0);
+
+struct EnvParams {
+  int fam, inv, n_lanes, n, obs_days, time_length, action_days, shuffle_days;
+  int state_dim, action_dim, risk_dim, draw_dim, ext_len, start_range;
+  uint64_t seed;
+  const double* prices;  // market [n_days, n]
+  // lane state
+  double* wealth;
+  int32_t* time;
+  int32_t* start;
+  uint32_t* episode;
+};
+
+// --- categorical outcome from a uniform: NumPy legacy choice(a, p) =
+// a[searchsorted(cumsum(p)/cumsum(p)[-1], u, 'right')] (pinned by tests/golden/rng_kat.npz).
+__device__ __host__ inline double coin_outcome(double u) {
+  const double c0 = 0.5, c1 = 0.5 + 0.5;
+  const int idx = (c0 / c1 <= u) + (c1 / c1 <= u);
+  return idx == 0 ? 0.5 : -0.4;
+}
+__device__ __host__ inline int dice_index(double u) {
+  const double p0 = 1.0 / 6.0, p1 = 1.0 / 6.0, p2 = 1.0 - (1.0 / 6.0 + 1.0 / 6.0);
+  const double c0 = p0, c1 = c0 + p1, c2 = c1 + p2;
+  return (c0 / c2 <= u) + (c1 / c2 <= u) + (c2 / c2 <= u);
+}
+__device__ __host__ inline double dice_value(int idx) {
+  return idx == 0 ? 0.5 : (idx == 1 ? -0.5 : 0.05);
+}
+
+// Fisher–Yates permutation of a block of `bs` (<= 16) rows for market shuffles.
+__device__ inline int market_perm(uint64_t seed, uint32_t lane, uint32_t ep, uint32_t blk, int bs,
+                                  int pos) {
+  int p[16];
+  for (int i = 0; i < bs; ++i) p[i] = i;
+  rlmd_u32x4 w = {0, 0, 0, 0};
+  for (int i = bs - 1, k = 0; i >= 1; --i, ++k) {
+    if ((k & 3) == 0) w = rlmd_philox(seed, lane, ep, RLMD_TAG_MKT_PERM, blk * 4u + (k >> 2));
+    const uint32_t word = (k & 3) == 0 ? w.x : (k & 3) == 1 ? w.y : (k & 3) == 2 ? w.z : w.w;
+    const int j = (int)(((uint64_t)word * (uint64_t)(i + 1)) >> 32);
+    const int t = p[i];
+    p[i] = p[j];
+    p[j] = t;
+  }
+  return p[pos];
+}
+
+// source price row of extract row e (time_slice + shuffle_data)
+__device__ inline int market_row(const EnvParams& P, uint32_t lane, int start, uint32_t ep, int e) {
+  const int D = P.shuffle_days;
+  if (D <= 1) return start + e;
+  const int full = P.ext_len / D, blk = e / D, within = e % D;
+  const int bs = blk < full ? D : P.ext_len - full * D;
+  return start + blk * D + market_perm(P.seed, lane, ep, (uint32_t)blk, bs, within);
+}
+
+// observed_market_state element k (tools/env_resources.py:203-226): D1 -> row t*ad
+// asset k; Dx -> rows [t*ad, t*ad+d) flattened then reversed.
+__device__ inline double market_obs(const EnvParams& P, uint32_t lane, int start, uint32_t ep,
+                                    int t, int k) {
+  int row, asset;
+  if (P.obs_days == 1) {
+    row = t * P.action_days;
+    asset = k;
+  } else {
+    const int f = P.obs_days * P.n - 1 - k;
+    row = t * P.action_days + f / P.n;
+    asset = f % P.n;
+  }
+  return P.prices[(int64_t)market_row(P, lane, start, ep, row) * P.n + asset];
+}
+
+// np.sum / np.mean of a small array: NumPy's pairwise_sum for n <= 128
+// (sequential below 8 elements, 8 accumulators otherwise).
+template <typename T, typename GetF>
+__device__ inline T np_sum(int n, GetF get) {
+  T res;
+  if (n < 8) {
+    res = (T)0;
+    for (int i = 0; i < n; ++i) res += get(i);
+  } else {
+    T r[8];
+    for (int k = 0; k < 8; ++k) r[k] = get(k);
+    int i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int k = 0; k < 8; ++k) r[k] += get(i + k);
+    res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += get(i);
+  }
+  return res;
+}
+template <typename T, typename GetF>
+__device__ inline T np_mean(int n, GetF get) {
+  return np_sum<T>(n, get) / (T)n;
+}
+
+__device__ inline float half_shift32(float a) { return (a + (float)kMaxAbsAction) / 2.f; }
+
+struct StepOut {
+  double W, reward;
+  bool done, learn_done;
+};
+
+// One env step for one lane.  `act(i)` yields action i (f32), `draw(j)` the
+// j-th uniform/normal.  Writes state element k through st(k, v) and risk
+// element k through rk(k, v).
+template <typename ActF, typename DrawF, typename StF, typename RkF>
+__device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, double w0, int t,
+                                        int start, uint32_t ep, ActF act, DrawF draw, StF st,
+                                        RkF rk) {
+  const FamConst C = fam_const(P.fam);
+  const int fam = P.fam, inv = P.inv, n = P.n;
+  const bool f32lev = (fam == RLMD_GBM || fam == RLMD_MARKET);
+  const double lev_cap64 = kMaxAbsAction * C.lev_factor;
+  const float lev_cap32 = (float)lev_cap64;
+
+  float sl32 = NAN, ret32 = NAN, lev_sh32 = NAN;
+  double R = 0.0, lev_mean = 0.0, lev0 = 0.0, r_sh = 0.0, r_die = 0.0;
+  bool lev_max_any = false, lev_max_all = true, lev_min_all = true;
+  int lev_off = 0;
+
+  if (fam == RLMD_DICE_SH) {
+    const int idx = dice_index(draw(0));
+    r_die = dice_value(idx);
+    r_sh = idx == 2 ? -0.99 : (idx == 0 ? -0.99 : 5.0);  // MID, UP -> -0.99 ; DOWN -> 5
+    double lev;
+    if (inv == RLMD_INV_INSURED) {
+      const float lev32 = act(0) * (float)kShILev;  // f32 * Python float
+      lev = (double)lev32;
+      lev_sh32 = 1.f - lev32;
+      lev_min_all = fabsf(lev32) < (float)kMinWeight;
+    } else {
+      const int ai = inv == RLMD_INV_A ? 0 : (inv == RLMD_INV_B ? 1 : 2);
+      if (inv != RLMD_INV_A) sl32 = half_shift32(act(0));
+      if (inv == RLMD_INV_C) ret32 = half_shift32(act(1));
+      lev = (double)act(ai) * C.lev_factor;
+      lev_sh32 = half_shift32(act(ai + 1)) * 1.f;
+      lev_min_all = fabs(lev) < kMinWeight;
+    }
+    lev_max_any = fabs(lev) == lev_cap64;
+    R = lev * r_die + (double)(lev_sh32 * (float)r_sh);
+    lev_mean = lev;
+    lev0 = lev;
+  } else {
+    if (inv == RLMD_INV_B) {
+      sl32 = fam == RLMD_COIN ? fabsf(act(0)) : half_shift32(act(0));  // Coin_InvB: |a0| (Q1)
+      lev_off = 1;
+    } else if (inv == RLMD_INV_C) {
+      sl32 = half_shift32(act(0));
+      ret32 = half_shift32(act(1));
+      lev_off = 2;
+    }
+    auto ret_of = [&](int j) -> double {
+      if (fam == RLMD_COIN) return coin_outcome(draw(j));
+      if (fam == RLMD_DICE) return dice_value(dice_index(draw(j)));
+      if (fam == RLMD_GBM) return (kGbmDrift - kGbmVol * kGbmVol / 2) + kGbmVol * draw(j);
+      return market_obs(P, lane, start, ep, t, j) / market_obs(P, lane, start, ep, 0, j) - 1.0;
+    };
+    auto lev_of = [&](int j) -> double {
+      const float a = act(lev_off + j);
+      return f32lev ? (double)(a * (float)C.lev_factor) : (double)a * C.lev_factor;
+    };
+    R = np_sum<double>(n, [&](int j) { return lev_of(j) * ret_of(j); });  // np.sum(lev * r)
+    for (int j = 0; j < n; ++j) {
+      const float a = act(lev_off + j);
+      if (f32lev) {
+        const float l32 = a * (float)C.lev_factor;
+        lev_max_all &= fabsf(l32) == lev_cap32;
+        lev_min_all &= fabsf(l32) < (float)kMinWeight;
+      } else {
+        const double lev = (double)a * C.lev_factor;
+        lev_max_any |= fabs(lev) == lev_cap64;
+        lev_min_all &= fabs(lev) < kMinWeight;
+      }
+    }
+    lev0 = lev_of(0);
+    if (f32lev)
+      lev_mean = (double)np_mean<float>(n, [&](int j) { return act(lev_off + j) * (float)C.lev_factor; });
+    else
+      lev_mean = np_mean<double>(n, [&](int j) { return (double)act(lev_off + j) * C.lev_factor; });
+  }
+
+  // one-step return and growth factor
+  double g;
+  if (fam == RLMD_GBM) {
+    R = fmax(R, C.min_return);
+    g = fmin(exp(R), 1.0 + C.max_return);
+  } else {
+    R = fmin(fmax(R, C.min_return), C.max_return);
+    g = 1.0 + R;
+  }
+
+  double W, mw;
+  bool done_active = false;
+  if (inv == RLMD_INV_A || inv == RLMD_INV_INSURED) {
+    mw = kMinValue;
+    W = fmin(fmax(w0 * g, kMinValue), C.max_value);
+  } else {
+    const float mw32 = fmaxf((float)kInitialValue * sl32, (float)kMinValue);
+    if (inv == RLMD_INV_C && w0 > kInitialValue)
+      mw = kInitialValue + (w0 - kInitialValue) * (double)ret32;
+    else
+      mw = (double)mw32;
+    // episode's first step: wealth is still the Python float 1e4 -> f32 subtraction
+    const double active = t == 1 ? (double)fmaxf((float)kInitialValue - mw32, 0.f) : fmax(w0 - mw, 0.0);
+    W = fmin(fmax(mw + active * g, mw), C.max_value);
+    done_active = active == 0.0;
+  }
+  const double growth = W / kInitialValue;
+  const double reward = exp(log(growth) / (double)t);
+
+  // next state / MAX_VALUE (and done_state = any(next_state >= 1))
+  bool done_state = false;
+  auto put = [&](int k, double v) {
+    const double s = v / C.max_value;
+    done_state |= s >= 1.0;
+    st(k, s);
+  };
+  put(0, W);
+  put(1, R);
+  put(2, growth);
+  put(3, reward);
+  if (fam == RLMD_DICE_SH) {
+    put(4, r_die);
+    put(5, r_sh);
+  } else if (fam == RLMD_MARKET) {
+    const int m = P.obs_days * n;
+    for (int k = 0; k < m; ++k)
+      put(4 + k, market_obs(P, lane, start, ep, t, k) / market_obs(P, lane, start, ep, 0, k) - 1.0);
+  } else {
+    for (int j = 0; j < n; ++j) {
+      double r;
+      if (fam == RLMD_COIN) r = coin_outcome(draw(j));
+      else if (fam == RLMD_DICE) r = dice_value(dice_index(draw(j)));
+      else r = (kGbmDrift - kGbmVol * kGbmVol / 2) + kGbmVol * draw(j);
+      put(4 + j, r);
+    }
+  }
+
+  const bool lev_max = f32lev ? lev_max_all : lev_max_any;
+  const bool done_time = fam == RLMD_MARKET &&
+                         t == (P.obs_days == 1 ? P.time_length : P.time_length - P.obs_days + 1);
+  const bool done = done_time || W == mw || reward < C.min_reward || R == C.min_return || lev_max ||
+                    lev_min_all || done_state || done_active;
+  StepOut o;
+  o.W = W;
+  o.reward = reward;
+  o.done = done;
+  o.learn_done = done && !done_state && !done_time;
+
+  // risk vector
+  rk(0, reward);
+  rk(1, W);
+  rk(2, R);
+  if (fam == RLMD_DICE_SH) {
+    rk(3, lev0);
+    rk(4, (double)sl32);
+    rk(5, (double)ret32);
+    rk(6, (double)lev_sh32);
+  } else {
+    rk(3, lev_mean);
+    int k = 4;
+    if (inv == RLMD_INV_B || inv == RLMD_INV_C) rk(k++, (double)sl32);
+    if (inv == RLMD_INV_C) rk(k++, (double)ret32);
+    if (n > 1) {
+      for (int j = 0; j < n; ++j) {
+        const float a = act(lev_off + j);
+        rk(k + j, f32lev ? (double)(a * (float)C.lev_factor) : (double)a * C.lev_factor);
+      }
+    }
+  }
+  return o;
+}
+
+// draws for gamble j: Philox(seed, lane, step, ENV_DRAW, j/2), two per block
+__device__ inline double philox_draw(const EnvParams& P, uint32_t lane, uint32_t step, int j) {
+  const rlmd_u32x4 v = rlmd_philox(P.seed, lane, step, RLMD_TAG_ENV_DRAW, (uint32_t)(j >> 1));
+  if (P.fam == RLMD_GBM) {
+    double z0, z1;
+    rlmd_normal2(v, z0, z1);
+    return (j & 1) ? z1 : z0;
+  }
+  return (j & 1) ? rlmd_u01(v.z, v.w) : rlmd_u01(v.x, v.y);
+}
+
+// reset one lane: episode start (market: new slice), state element writer
+template <typename StF>
+__device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st) {
+  P.wealth[lane] = kInitialValue;
+  P.time[lane] = 1;
+  const uint32_t ep = P.episode[lane] + 1;
+  P.episode[lane] = ep;
+  const FamConst C = fam_const(P.fam);
+  st(0, kInitialValue / C.max_value);
+  st(1, 0.0);
+  st(2, 1.0 / C.max_value);
+  st(3, 1.0 / C.max_value);
+  if (P.fam == RLMD_MARKET) {
+    const rlmd_u32x4 v = rlmd_philox(P.seed, lane, ep, RLMD_TAG_MKT_START, 0);
+    const int start = (int)rlmd_below(v.x, v.y, (uint64_t)P.start_range);
+    P.start[lane] = start;
+    const int m = P.obs_days * P.n;
+    for (int k = 0; k < m; ++k)
+      st(4 + k, P.obs_days == 1 ? 0.0 : market_obs(P, lane, start, ep, 0, k) / C.max_value);
+  } else {
+    for (int k = 4; k < P.state_dim; ++k) st(k, 0.0);
+  }
+}
+
+__global__ void env_reset_kernel(EnvParams P, const uint8_t* mask, double* state) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= P.n_lanes) return;
+  if (mask && !mask[lane]) return;
+  env_reset_lane(P, lane, [&](int k, double v) {
+    if (state) state[(int64_t)lane * P.state_dim + k] = v;
+  });
+}
+
+__global__ void env_step_kernel(EnvParams P, uint32_t step, const float* __restrict__ actions,
+                                const double* __restrict__ draws, double* next_state,
+                                double* reward, uint8_t* done, double* risk) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= P.n_lanes) return;
+  const float* a = actions + (int64_t)lane * P.action_dim;
+  const double w0 = P.wealth[lane];
+  const int t = P.time[lane];
+  const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
+  const uint32_t ep = P.episode[lane];
+  StepOut o = env_step_lane(
+      P, lane, w0, t, start, ep, [&](int i) { return a[i]; },
+      [&](int j) {
+        return draws ? draws[(int64_t)lane * P.draw_dim + j] : philox_draw(P, lane, step, j);
+      },
+      [&](int k, double v) { next_state[(int64_t)lane * P.state_dim + k] = v; },
+      [&](int k, double v) {
+        if (risk) risk[(int64_t)lane * P.risk_dim + k] = v;
+      });
+  P.wealth[lane] = o.W;
+  P.time[lane] = t + 1;
+  reward[lane] = o.reward;
+  done[2 * lane] = o.done;
+  done[2 * lane + 1] = o.learn_done;
+}
+
+// ---------------------------------------------------------------------------
+// fused training step: action (warm-up draw | policy) -> action_window clip ->
+// env step -> replay insert (s, a, r, s', learn_done) -> auto reset.
+// ---------------------------------------------------------------------------
+__global__ void env_train_kernel(EnvParams P, uint32_t step, float* actions, int random_actions,
+                                 int abs_actions, float clip_lo, float clip_hi, float* obs,
+                                 rlmd::ReplayView rb, int64_t ring_base, double* ep_stats) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= P.n_lanes) return;
+  const int S = P.state_dim, A = P.action_dim;
+  float a[RLMD_MAX_ACTION];
+  for (int i = 0; i < A; ++i) {
+    float v;
+    if (random_actions) {
+      const rlmd_u32x4 w = rlmd_philox(P.seed, lane, step, RLMD_TAG_WARMUP_ACTION, (uint32_t)(i >> 1));
+      const double u = (i & 1) ? rlmd_u01(w.z, w.w) : rlmd_u01(w.x, w.y);
+      v = (float)(-kMaxAbsAction + 2.0 * kMaxAbsAction * u);
+      if (abs_actions) v = fabsf(v);
+    } else {
+      v = actions[(int64_t)lane * A + i];
+    }
+    a[i] = fminf(fmaxf(v, clip_lo), clip_hi);
+  }
+  const int64_t row = (ring_base + lane) % rb.capacity;
+  // s (current obs) goes to the ring unchanged
+  for (int k = 0; k < S; ++k) rb.state[row * S + k] = obs[(int64_t)lane * S + k];
+  for (int i = 0; i < A; ++i) rb.action[row * A + i] = a[i];
+
+  const double w0 = P.wealth[lane];
+  const int t = P.time[lane];
+  const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
+  const uint32_t ep = P.episode[lane];
+  StepOut o = env_step_lane(
+      P, lane, w0, t, start, ep, [&](int i) { return a[i]; },
+      [&](int j) { return philox_draw(P, lane, step, j); },
+      [&](int k, double v) {
+        const float f = (float)v;
+        rb.next_state[row * S + k] = f;
+        obs[(int64_t)lane * S + k] = f;
+      },
+      [&](int, double) {});
+  rb.reward[row] = (float)o.reward;  // max(reward, r_abs_zero = -inf)
+  rb.done[row] = o.learn_done;
+  if (o.done) {
+    if (ep_stats) {
+      atomicAdd(&ep_stats[0], 1.0);
+      atomicAdd(&ep_stats[1], o.reward);
+      atomicAdd(&ep_stats[2], (double)t);
+    }
+    env_reset_lane(P, lane, [&](int k, double v) { obs[(int64_t)lane * S + k] = (float)v; });
+  } else {
+    P.wealth[lane] = o.W;
+    P.time[lane] = t + 1;
+  }
+}
+
+__global__ void env_obs_reset_kernel(EnvParams P, float* obs) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= P.n_lanes) return;
+  env_reset_lane(P, lane, [&](int k, double v) { obs[(int64_t)lane * P.state_dim + k] = (float)v; });
+}
+
+}  // namespace
+
+// ============================================================================
+// host side
+// ============================================================================
+struct rlmd_env_s {
+  EnvParams P;
+  uint32_t step_ctr = 0;
+  double* d_prices = nullptr;
+};
+
+namespace rlmd {
+
+int env_dims_for(const rlmd_env_cfg& c, int& S, int& A, int& R, int& D) {
+  const int n = c.n_gambles;
+  switch (c.family) {
+    case RLMD_COIN:
+    case RLMD_DICE:
+    case RLMD_GBM:
+    case RLMD_MARKET: {
+      const int extra = c.investor == RLMD_INV_A ? 0 : (c.investor == RLMD_INV_B ? 1 : 2);
+      S = 4 + (c.family == RLMD_MARKET ? c.obs_days * n : n);
+      A = n + extra;
+      R = (n == 1 ? 4 : 4 + n) + extra;
+      D = c.family == RLMD_MARKET ? 0 : n;
+      return 0;
+    }
+    case RLMD_DICE_SH:
+      S = 6;
+      A = c.investor == RLMD_INV_INSURED ? 1 : (c.investor == RLMD_INV_A ? 2 : (c.investor == RLMD_INV_B ? 3 : 4));
+      R = 7;
+      D = 1;
+      return 0;
+  }
+  return 1;
+}
+
+void env_train_launch_params(rlmd_env_t env, EnvParams*& P);
+
+int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uint32_t step,
+              float* actions, int random_actions, int abs_actions, float clip_lo, float clip_hi,
+              float* obs, double* ep_stats, hipStream_t stream) {
+  const int N = env->P.n_lanes;
+  hipLaunchKernelGGL(env_train_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, env->P, step,
+                     actions, random_actions, abs_actions, clip_lo, clip_hi, obs, rb, ring_base,
+                     ep_stats);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int env_lanes(rlmd_env_t env) { return env->P.n_lanes; }
+int env_state_dim(rlmd_env_t env) { return env->P.state_dim; }
+int env_action_dim(rlmd_env_t env) { return env->P.action_dim; }
+
+}  // namespace rlmd
+
+extern "C" {
+
+int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t n_days,
+                    rlmd_env_t* out) {
+  RLMD_CHECK(cfg && out, "null argument");
+  RLMD_CHECK(cfg->family >= RLMD_COIN && cfg->family <= RLMD_MARKET, "bad family");
+  RLMD_CHECK(cfg->n_lanes > 0, "n_lanes must be > 0");
+  RLMD_CHECK(cfg->n_gambles >= 1 && cfg->n_gambles <= RLMD_MAX_GAMBLES, "n_gambles out of range");
+  if (cfg->family == RLMD_DICE_SH)
+    RLMD_CHECK(cfg->investor >= RLMD_INV_A && cfg->investor <= RLMD_INV_INSURED, "bad investor");
+  else
+    RLMD_CHECK(cfg->investor >= RLMD_INV_A && cfg->investor <= RLMD_INV_C, "bad investor");
+  int S, A, R, D;
+  rlmd::env_dims_for(*cfg, S, A, R, D);
+  RLMD_CHECK(A <= RLMD_MAX_ACTION, "action dim too large");
+  auto* e = new rlmd_env_s();
+  EnvParams& P = e->P;
+  memset(&P, 0, sizeof(P));
+  P.fam = cfg->family;
+  P.inv = cfg->investor;
+  P.n_lanes = cfg->n_lanes;
+  P.n = cfg->n_gambles;
+  P.obs_days = cfg->obs_days > 0 ? cfg->obs_days : 1;
+  P.time_length = cfg->time_length;
+  P.action_days = cfg->action_days > 0 ? cfg->action_days : 1;
+  P.shuffle_days = cfg->shuffle_days > 0 ? cfg->shuffle_days : 1;
+  P.state_dim = S;
+  P.action_dim = A;
+  P.risk_dim = R;
+  P.draw_dim = D;
+  P.seed = cfg->seed;
+  const size_t N = (size_t)cfg->n_lanes;
+  if (cfg->family == RLMD_MARKET) {
+    if (!prices_host || n_days <= 1 || cfg->time_length <= 0 || P.shuffle_days > 16) {
+      delete e;
+      RLMD_CHECK(false, "market env needs prices, time_length > 0 and shuffle_days <= 16");
+    }
+    P.ext_len = P.time_length * P.action_days + 1;
+    P.start_range = (int)(n_days - cfg->sample_days);
+    if (P.start_range < 1 || P.start_range - 1 + P.ext_len > n_days) {
+      delete e;
+      RLMD_CHECK(false, "market sample_days inconsistent with n_days / time_length");
+    }
+    RLMD_HIP(hipMalloc(&e->d_prices, sizeof(double) * n_days * P.n));
+    RLMD_HIP(hipMemcpy(e->d_prices, prices_host, sizeof(double) * n_days * P.n,
+                       hipMemcpyHostToDevice));
+    P.prices = e->d_prices;
+  }
+  RLMD_HIP(hipMalloc(&P.wealth, sizeof(double) * N));
+  RLMD_HIP(hipMalloc(&P.time, sizeof(int32_t) * N));
+  RLMD_HIP(hipMalloc(&P.start, sizeof(int32_t) * N));
+  RLMD_HIP(hipMalloc(&P.episode, sizeof(uint32_t) * N));
+  RLMD_HIP(hipMemset(P.episode, 0xff, sizeof(uint32_t) * N));  // first reset -> episode 0
+  RLMD_HIP(hipMemset(P.start, 0, sizeof(int32_t) * N));
+  hipLaunchKernelGGL(env_reset_kernel, dim3((N + 255) / 256), dim3(256), 0, 0, P, nullptr, nullptr);
+  RLMD_LAUNCH_CHECK();
+  RLMD_HIP(hipDeviceSynchronize());
+  *out = e;
+  return 0;
+}
+
+int rlmd_env_destroy(rlmd_env_t env) {
+  if (!env) return 0;
+  (void)hipFree(env->P.wealth);
+  (void)hipFree(env->P.time);
+  (void)hipFree(env->P.start);
+  (void)hipFree(env->P.episode);
+  if (env->d_prices) (void)hipFree(env->d_prices);
+  delete env;
+  return 0;
+}
+
+int rlmd_env_dims(rlmd_env_t env, int32_t* S, int32_t* A, int32_t* R, int32_t* D) {
+  RLMD_CHECK(env, "null env");
+  if (S) *S = env->P.state_dim;
+  if (A) *A = env->P.action_dim;
+  if (R) *R = env->P.risk_dim;
+  if (D) *D = env->P.draw_dim;
+  return 0;
+}
+
+int rlmd_env_reset(rlmd_env_t env, const uint8_t* mask, double* state, void* stream) {
+  RLMD_CHECK(env, "null env");
+  const int N = env->P.n_lanes;
+  hipLaunchKernelGGL(env_reset_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     env->P, mask, state);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int rlmd_env_step(rlmd_env_t env, const float* actions, const double* draws, double* next_state,
+                  double* reward, uint8_t* done, double* risk, void* stream) {
+  RLMD_CHECK(env && actions && next_state && reward && done, "null argument");
+  const int N = env->P.n_lanes;
+  hipLaunchKernelGGL(env_step_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     env->P, env->step_ctr, actions, draws, next_state, reward, done, risk);
+  RLMD_LAUNCH_CHECK();
+  env->step_ctr++;
+  return 0;
+}
+
+int rlmd_env_lane_state(rlmd_env_t env, double* wealth, int32_t* time) {
+  RLMD_CHECK(env, "null env");
+  RLMD_HIP(hipDeviceSynchronize());
+  const size_t N = env->P.n_lanes;
+  if (wealth) RLMD_HIP(hipMemcpy(wealth, env->P.wealth, N * sizeof(double), hipMemcpyDeviceToHost));
+  if (time) RLMD_HIP(hipMemcpy(time, env->P.time, N * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int rlmd_train_reset(rlmd_env_t env, float* obs, void* stream) {
+  RLMD_CHECK(env && obs, "null argument");
+  const int N = env->P.n_lanes;
+  hipLaunchKernelGGL(env_obs_reset_kernel, dim3((N + 255) / 256), dim3(256), 0,
+                     (hipStream_t)stream, env->P, obs);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,1247 @@
+// learn.hip — SAC / TD3 learn() for gfx950 as a chain of HIP kernels.
+//
+// Restated reference (majidsina/rlmd):
+//   SAC  algos/algo_sac.py:300-367 (_multi_step_target), :369-595 (learn),
+//        :597-615 (Polyak); networks algos/networks_sac.py:101-178, :337-362
+//   TD3  algos/algo_td3.py:302-361, :363-531, :533-563; algos/networks_td3.py:76-91, :152-168
+//   critic losses / tail index  tools/critic_loss.py:26-341 (loss_function :344-453)
+//   Adam (torch defaults, betas .9/.999, eps 1e-8), Polyak tau
+// The MLP contractions run on the MFMA GEMM of gemm.hip; everything else here
+// is row-parallel (one wave per mini-batch row) or a single-workgroup
+// reduction/sort over the mini-batch (B <= 1024: bitonic sorts in LDS).
+// All per-update scalars (Cauchy scales, log alpha, learn counter) stay on the
+// device in LearnState; nothing synchronises with the host inside learn().
+#include <math.h>
+#include <string.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "learn_kernels.h"
+#include "rlmd_gemm.h"
+
+namespace rlmd {
+namespace {
+
+constexpr float kLog2Pi_half = 0.91893853320467274178f;  // log(sqrt(2*pi))
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// orderable key of a float (ascending unsigned order == ascending float order)
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// bitonic sort of n_pow2 u64 keys in LDS, ascending; all threads of the block call it
+__device__ void block_sort(uint64_t* keys, int n_pow2) {
+  for (int k = 2; k <= n_pow2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t x = keys[i], y = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            keys[i] = y;
+            keys[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// deterministic block reduction (fixed tree) of one float per thread
+__device__ float block_sum(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+  if (threadIdx.x < 64) {
+    t = threadIdx.x < nw ? red[threadIdx.x] : 0.f;
+    t = wave_sum(t);
+    if (threadIdx.x == 0) red[32] = t;
+  }
+  __syncthreads();
+  return red[32];
+}
+
+__device__ float block_max(float v, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    float t = threadIdx.x < nw ? red[threadIdx.x] : -INFINITY;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) t = fmaxf(t, __shfl_xor(t, o, 64));
+    if (threadIdx.x == 0) red[32] = t;
+  }
+  __syncthreads();
+  return red[32];
+}
+
+__device__ float block_min(float v, float* red) { return -block_max(-v, red); }
+
+// ---------------------------------------------------------------------------
+// actor heads + policy sampling (networks_sac.py:101-178, :268-285;
+// networks_td3.py:76-91; algo_td3.py:198-223, :327-344).  One wave per row.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= h.n) return;
+  const NetOff& o = h.off;
+  const int H = o.h2, A = h.A;
+  const float* x = h.h2 + (int64_t)b * H;
+  const uint32_t c1 = h.ctr ? (uint32_t)*h.ctr : h.ctr_host;
+  if (h.xsa)
+    for (int k = lane; k < h.S; k += 64) h.xsa[(int64_t)b * (h.S + A) + k] = h.state[(int64_t)b * h.S + k];
+  float logp = 0.f;
+  for (int j = 0; j < A; ++j) {
+    float dm = 0.f, dl = 0.f;
+    const float* wm = h.params + o.w3 + (int64_t)j * H;
+    const float* wl = h.params + o.w4 + (int64_t)j * H;
+    for (int k = lane; k < H; k += 64) {
+      const float xv = x[k];
+      dm = fmaf(xv, wm[k], dm);
+      if (h.algo == RLMD_SAC) dl = fmaf(xv, wl[k], dl);
+    }
+    dm = wave_sum(dm);
+    if (h.algo == RLMD_SAC) dl = wave_sum(dl);
+    if (lane != 0) continue;
+    float mu = dm + h.params[o.b3 + j];
+    float a;
+    float eps = 0.f;
+    if (h.mode == 0 || h.algo == RLMD_TD3) {
+      if (h.eps_in) {
+        eps = h.eps_in[(int64_t)b * A + j];
+      } else if (h.mode == 0) {
+        double z0, z1;
+        rlmd_normal2(rlmd_philox(h.seed, (uint32_t)b, c1, h.tag, (uint32_t)(j >> 1)), z0, z1);
+        eps = (float)((j & 1) ? z1 : z0);
+      }
+    }
+    if (h.algo == RLMD_SAC) {
+      const float ls_raw = dl + h.params[o.b4 + j];
+      const float ls = fminf(fmaxf(ls_raw, h.ls_min), h.ls_max);
+      float sigma = expf(ls);
+      // NaN scrub (networks_sac.py:131-134), applied per element
+      if (!isfinite(mu)) mu = 0.f;
+      if (!isfinite(sigma)) sigma = 3.f;
+      if (h.mode == 1) {
+        a = tanhf(mu) * h.max_action;
+      } else {
+        const float u = mu + eps * sigma;
+        const float d = u - mu;
+        const float lpn = -(d * d) / (2.f * (sigma * sigma)) - logf(sigma) - kLog2Pi_half;
+        const float t = tanhf(u);
+        a = t * h.max_action;
+        const float an = a / h.max_action;
+        logp += lpn - logf(1.f - an * an + h.reparam_noise);
+        if (h.save) {
+          float* sv = h.save + (int64_t)b * 5 * A;
+          sv[j] = mu;
+          sv[A + j] = sigma;
+          sv[2 * A + j] = eps;
+          sv[3 * A + j] = u;
+          sv[4 * A + j] = ls_raw;
+        }
+      }
+    } else {
+      const float t = tanhf(mu);
+      a = t * h.max_action;
+      if (h.mode == 0) {
+        float nz = eps * h.noise_std;
+        if (h.clamp_noise) nz = fminf(fmaxf(nz, -h.noise_clip), h.noise_clip);
+        a = fminf(fmaxf(a + nz, -h.max_action), h.max_action);
+      }
+      if (h.save) h.save[(int64_t)b * 5 * A + j] = mu;  // pre-tanh for backward
+    }
+    if (h.actions) h.actions[(int64_t)b * A + j] = a;
+    if (h.xsa) h.xsa[(int64_t)b * (h.S + A) + h.S + j] = a;
+  }
+  if (lane == 0 && h.logp) h.logp[b] = logp;
+}
+
+// q[g][b] = X_g[b] . w_g + bias_g (critic q_value head, networks_sac.py:362).
+struct RowHeadArgs {
+  const float* X[2];
+  const float* w[2];
+  const float* bias[2];
+  float* out[2];
+  int32_t n, H;
+};
+__global__ void __launch_bounds__(256) row_head_kernel(RowHeadArgs r) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int g = blockIdx.y;
+  if (b >= r.n) return;
+  const float* x = r.X[g] + (int64_t)b * r.H;
+  float acc = 0.f;
+  for (int k = lane; k < r.H; k += 64) acc = fmaf(x[k], r.w[g][k], acc);
+  acc = wave_sum(acc);
+  if (lane == 0) r.out[g][b] = acc + r.bias[g][0];
+}
+
+// Bootstrapped target (algo_sac.py:347-365 / algo_td3.py:346-359).
+__global__ void critic_target_kernel(const float* qt1, const float* qt2, const float* r,
+                                     const uint8_t* done, const int32_t* eff, const float* logp,
+                                     const LearnState* st, float* y, int n, int algo, float gamma,
+                                     float reward_scale) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  float q1 = qt1[b], q2 = qt2[b];
+  if (done[b]) q1 = q2 = 0.f;
+  const float m = fminf(q1, q2);
+  const int e = eff ? eff[b] : 1;
+  const float ge = powf(gamma, (float)e);
+  if (algo == RLMD_SAC) {
+    const float soft = reward_scale * r[b] + ge * m;
+    y[b] = soft - expf(st->log_alpha) * logp[b];
+  } else {
+    y[b] = r[b] + ge * m;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Critic loss, top-k, tail index, CIM kernel, Nagy scale
+// (tools/critic_loss.py:26-341, loss_function :344-453; algo_sac.py:419-473).
+// One workgroup of 1024 threads; thread b owns mini-batch row b.
+// ---------------------------------------------------------------------------
+struct LossArgs {
+  const float* q[2];
+  const float* y;
+  float* dq[2];
+  const float* zipf_x;
+  float zipf_x2;
+  LearnState* st;
+  float* stats;  // [16]
+  int32_t B, k, loss_type, algo;
+  float log_noise, grad_scale;
+};
+
+__device__ __forceinline__ void loss_and_grad(int lt, float q, float t, float c, float kern,
+                                              float& l, float& dl) {
+  const float d = t - q;
+  switch (lt) {
+    case RLMD_LOSS_MSE: l = d * d; dl = -2.f * d; break;
+    case RLMD_LOSS_MSE2: l = d * d * d * d; dl = -4.f * d * d * d; break;
+    case RLMD_LOSS_MSE4: { const float d2 = d * d; l = d2 * d2 * d2; dl = -6.f * d2 * d2 * d; break; }
+    case RLMD_LOSS_MSE6: { const float d2 = d * d; l = d2 * d2 * d2 * d2; dl = -8.f * d2 * d2 * d2 * d; break; }
+    case RLMD_LOSS_MAE: l = fabsf(d); dl = d > 0.f ? -1.f : (d < 0.f ? 1.f : 0.f); break;
+    case RLMD_LOSS_HUB: {
+      const float ad = fabsf(d);
+      const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      if (ad < 1.f) { l = 0.5f * ad * ad; dl = -ad * sg; }
+      else { l = ad - 0.5f; dl = -sg; }
+      break;
+    }
+    case RLMD_LOSS_HSC: { const float s = sqrtf(1.f + d * d); l = s - 1.f; dl = -d / s; break; }
+    case RLMD_LOSS_CAU:
+    case RLMD_LOSS_TCAU: {
+      const float z = d / c;
+      l = logf(1.f + z * z);
+      dl = -(2.f * z / c) / (1.f + z * z);
+      break;
+    }
+    default: {  // CIM
+      const float e = expf(-(d * d) / (2.f * kern * kern)) / sqrtf(2.f * 3.14159265358979323846f * kern);
+      l = 1.f - e;
+      dl = -e * d / (kern * kern);
+      break;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
+  __shared__ uint64_t keys[1024];
+  __shared__ float red[33];
+  __shared__ float lsel[2][1024];
+  __shared__ int rank_of[1024];
+  const int b = threadIdx.x, B = a.B;
+  const bool in = b < B;
+  const float y = in ? a.y[b] : 0.f;
+  float q[2] = {in ? a.q[0][b] : 0.f, in ? a.q[1][b] : 0.f};
+  LearnState* st = a.st;
+  const float scale[2] = {st->cauchy[0], st->cauchy[1]};
+  float kern[2];
+  // CIM kernel size: population std of (t - q)^2 (critic_loss.py:125-140)
+  for (int g = 0; g < 2; ++g) {
+    const float e = in ? (y - q[g]) * (y - q[g]) : 0.f;
+    const float mean = block_sum(e, red) / B;
+    const float dv = in ? (e - mean) * (e - mean) : 0.f;
+    kern[g] = sqrtf(block_sum(dv, red) / B);
+  }
+  // TCAU 3-sigma truncation (critic_loss.py:26-50): estimated and target zeroed
+  // where they lie more than 3 population std from their mean
+  float yt[2] = {y, y}, qt[2] = {q[0], q[1]};
+  bool qtr[2] = {false, false};
+  if (a.loss_type == RLMD_LOSS_TCAU) {
+    const float my = block_sum(in ? y : 0.f, red) / B;
+    const float sy = sqrtf(block_sum(in ? (y - my) * (y - my) : 0.f, red) / B);
+    const bool ytr = fabsf(y - my) > 3.f * sy;
+    for (int g = 0; g < 2; ++g) {
+      const float mq = block_sum(in ? q[g] : 0.f, red) / B;
+      const float sq = sqrtf(block_sum(in ? (q[g] - mq) * (q[g] - mq) : 0.f, red) / B);
+      qtr[g] = fabsf(q[g] - mq) > 3.f * sq;
+      qt[g] = qtr[g] ? 0.f : q[g];
+      yt[g] = ytr ? 0.f : y;
+    }
+  }
+  float l[2], dl[2];
+  for (int g = 0; g < 2; ++g) {
+    loss_and_grad(a.loss_type, qt[g], yt[g], scale[g], kern[g], l[g], dl[g]);
+    if (qtr[g]) dl[g] = 0.f;
+  }
+  // top-k by l1 + l2, descending (critic_loss.py:438-441)
+  const int k = B > a.k ? a.k : B;
+  int npow = 1;
+  while (npow < B) npow <<= 1;
+  bool sel = in;
+  if (B > a.k) {
+    for (int i = b; i < npow; i += blockDim.x)
+      keys[i] = i < B ? 0ull : ~0ull;
+    __syncthreads();
+    if (in) keys[b] = ((uint64_t)(~f2key(l[0] + l[1])) << 32) | (uint32_t)b;
+    __syncthreads();
+    block_sort(keys, npow);
+    // rank of my row
+    if (b < B) rank_of[(int)(keys[b] & 0xffffffffu)] = b;
+    __syncthreads();
+    sel = in && rank_of[b] < k;
+  }
+  // aggregate per critic: mean / min / max over the selected losses and the
+  // Zipf-plot tail index of their order statistics (critic_loss.py:238-341)
+  for (int g = 0; g < 2; ++g) {
+    const float mean = block_sum(sel ? l[g] : 0.f, red) / k;
+    const float mn = block_min(sel ? l[g] : INFINITY, red);
+    const float mx = block_max(sel ? l[g] : -INFINITY, red);
+    // sort selected losses descending
+    int kp = 1;
+    while (kp < k) kp <<= 1;
+    const int npw = npow > kp ? npow : kp;
+    for (int i = b; i < npw; i += blockDim.x) keys[i] = ~0ull;
+    if (in) lsel[g][b] = l[g];
+    __syncthreads();
+    if (sel) keys[b] = ((uint64_t)(~f2key(l[g])) << 32) | (uint32_t)b;
+    __syncthreads();
+    block_sort(keys, npw);
+    float lg = 0.f;
+    if (b < k) lg = logf(lsel[g][(int)(keys[b] & 0xffffffffu)] + a.log_noise);
+    const float lmean = block_sum(b < k ? lg : 0.f, red) / k;
+    const float num = block_sum(b < k ? a.zipf_x[b] * (lg - lmean) : 0.f, red);
+    const float alpha = 1.f / (num / a.zipf_x2);
+    if (b == 0) {
+      a.stats[0 + g] = mean;
+      a.stats[2 + g] = mn;
+      a.stats[4 + g] = mx;
+      a.stats[6 + g] = NAN;
+      a.stats[8 + g] = alpha;
+    }
+    if (in) a.dq[g][b] = sel ? a.grad_scale * dl[g] / (float)k : 0.f;
+  }
+  // Nagy Cauchy-scale update over the whole mini-batch (critic_loss.py:74-101)
+  float newc[2];
+  for (int g = 0; g < 2; ++g) {
+    const float z = (y - q[g]) / scale[g];
+    const float inv = block_sum(in ? 1.f / (1.f + z * z) : 0.f, red) / B;
+    const float ie = 1.f / inv;
+    newc[g] = ie > 1.f ? scale[g] * sqrtf(ie - 1.f) : scale[g];
+  }
+  const float nanq = block_max(in ? ((isnan(q[0]) || isnan(q[1]) || isnan(y)) ? 1.f : 0.f) : 0.f, red);
+  if (b == 0) {
+    st->cauchy[0] = newc[0];
+    st->cauchy[1] = newc[1];
+    st->kernel[0] = kern[0];
+    st->kernel[1] = kern[1];
+    if (nanq > 0.f) st->nan_flag = 1;
+    a.stats[10] = NAN;
+    a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
+    a.stats[12] = newc[0];
+    a.stats[13] = newc[1];
+    a.stats[14] = kern[0];
+    a.stats[15] = kern[1];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Actor loss (algo_sac.py:524-562 / algo_td3.py:507-523) and the temperature
+// gradient (algo_sac.py:580-587).  One workgroup; writes dL/dq per critic and
+// dL/dlogp per row.
+// ---------------------------------------------------------------------------
+struct ActorLossArgs {
+  const float* q[2];  // q[1] null for TD3 (critic_1 only)
+  const float* logp;  // SAC
+  float* dq[2];
+  float* dlogp;
+  LearnState* st;
+  float* stats;
+  int32_t B, k, algo, topk;
+  float target_entropy;
+};
+
+__global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
+  __shared__ uint64_t keys[1024];
+  __shared__ float red[33];
+  __shared__ int rank_of[1024];
+  const int b = threadIdx.x, B = a.B;
+  const bool in = b < B;
+  LearnState* st = a.st;
+  const float alpha = a.algo == RLMD_SAC ? expf(st->log_alpha) : 0.f;
+  float q1 = in ? a.q[0][b] : 0.f;
+  float q2 = (in && a.q[1]) ? a.q[1][b] : q1;
+  const float lp = (in && a.logp) ? a.logp[b] : 0.f;
+  float v;
+  if (a.algo == RLMD_SAC) v = fminf(q1, q2) - alpha * lp;
+  else v = q1;
+  const int k = a.topk ? (B < a.k ? B : a.k) : B;
+  int npow = 1;
+  while (npow < B) npow <<= 1;
+  bool sel = in;
+  if (a.topk) {
+    for (int i = b; i < npow; i += blockDim.x) keys[i] = ~0ull;
+    __syncthreads();
+    // SAC sorts descending, TD3 ascending
+    if (in) keys[b] = ((uint64_t)(a.algo == RLMD_SAC ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)b;
+    __syncthreads();
+    block_sort(keys, npow);
+    if (b < B) rank_of[(int)(keys[b] & 0xffffffffu)] = b;
+    __syncthreads();
+    sel = in && rank_of[b] < k;
+  }
+  const float loss = -block_sum(sel ? v : 0.f, red) / k;
+  const float dv = sel ? -1.f / (float)k : 0.f;
+  if (in) {
+    if (a.algo == RLMD_SAC) {
+      // d min(q1, q2): ties split evenly (torch.minimum backward)
+      const float g1 = q1 < q2 ? 1.f : (q1 > q2 ? 0.f : 0.5f);
+      a.dq[0][b] = dv * g1;
+      a.dq[1][b] = dv * (1.f - g1);
+      a.dlogp[b] = -alpha * dv;
+    } else {
+      a.dq[0][b] = dv;
+    }
+  }
+  // temperature: d/dlog_alpha mean(-alpha (logp + target_entropy))
+  if (a.algo == RLMD_SAC) {
+    const float tg = block_sum(in ? -(lp + a.target_entropy) : 0.f, red) / B * alpha;
+    if (b == 0) st->pad_temp_grad = tg;
+  }
+  if (b == 0) a.stats[10] = loss;
+}
+
+// ---------------------------------------------------------------------------
+// Policy backward through sampling + heads (autograd of networks_sac.py:163-178
+// / networks_td3.py:91).  One wave per row.  Input dxa_g: dL/da from critic g
+// (BWD_X of the critics restricted to the action columns).  Output: head
+// gradients gh [n, 2A] (dmu | dlog_scale_raw) and dH2 [n, H2] (ReLU-masked).
+// ---------------------------------------------------------------------------
+struct ActorBwdArgs {
+  const float* dxa[2];  // [n, A] each; dxa[1] null for TD3
+  const float* dlogp;   // SAC
+  const float* save;    // [n, 5A]
+  const float* h2;
+  const float* params;
+  NetOff off;
+  float* gh;   // [n, 2A]
+  float* dh2;  // [n, H2]
+  int32_t n, A, algo;
+  float max_action, ls_min, ls_max, reparam_noise;
+};
+
+__global__ void __launch_bounds__(256) actor_bwd_kernel(ActorBwdArgs a) {
+  __shared__ float gsh[4][2 * RLMD_MAX_ACTION];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x * 4 + w;
+  const bool valid = b < a.n;  // wave-uniform
+  const int A = a.A;
+  if (valid) {
+    const float* sv = a.save + (int64_t)b * 5 * A;
+    for (int j = lane; j < A; j += 64) {
+      const float da = a.dxa[0][(int64_t)b * A + j] + (a.dxa[1] ? a.dxa[1][(int64_t)b * A + j] : 0.f);
+      if (a.algo == RLMD_SAC) {
+        const float mu = sv[j], sigma = sv[A + j], eps = sv[2 * A + j], u = sv[3 * A + j];
+        const float ls_raw = sv[4 * A + j];
+        const float dlp = a.dlogp[b];
+        const float t = tanhf(u);
+        const float om = 1.f - t * t;
+        const float d = u - mu;
+        // logp = -d^2/(2 s^2) - log s - c - log(1 - t^2 + noise), u = mu + eps s
+        const float dlogp_du = -d / (sigma * sigma) + 2.f * t * om / (om + a.reparam_noise);
+        const float du = da * a.max_action * om + dlp * dlogp_du;
+        const float dmu = du + dlp * (d / (sigma * sigma));
+        const float dsig = du * eps + dlp * ((d * d) / (sigma * sigma * sigma) - 1.f / sigma);
+        const bool live = ls_raw >= a.ls_min && ls_raw <= a.ls_max;  // clamp passes [min, max]
+        const float dls = live ? dsig * sigma : 0.f;
+        gsh[w][j] = dmu;
+        gsh[w][A + j] = dls;
+        a.gh[(int64_t)b * 2 * A + j] = dmu;
+        a.gh[(int64_t)b * 2 * A + A + j] = dls;
+      } else {
+        const float t = tanhf(sv[j]);
+        const float dpre = da * a.max_action * (1.f - t * t);
+        gsh[w][j] = dpre;
+        a.gh[(int64_t)b * 2 * A + j] = dpre;
+      }
+    }
+  }
+  __syncthreads();
+  if (!valid) return;
+  const NetOff& o = a.off;
+  const int H = o.h2;
+  for (int kx = lane; kx < H; kx += 64) {
+    float acc = 0.f;
+    for (int j = 0; j < A; ++j) {
+      acc = fmaf(gsh[w][j], a.params[o.w3 + (int64_t)j * H + kx], acc);
+      if (a.algo == RLMD_SAC) acc = fmaf(gsh[w][A + j], a.params[o.w4 + (int64_t)j * H + kx], acc);
+    }
+    const float hv = a.h2[(int64_t)b * H + kx];
+    a.dh2[(int64_t)b * H + kx] = hv > 0.f ? acc : 0.f;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Adam (torch.optim.Adam defaults, _single_tensor_adam) + optional Polyak
+// target update (algo_sac.py:597-615) + optional temperature Adam.
+// ---------------------------------------------------------------------------
+struct AdamArgs {
+  float* p;
+  const float* g;
+  float* m;
+  float* v;
+  float* target;  // Polyak target (nullable)
+  int64_t n;
+  float lr, tau;
+  int32_t interval;        // Adam step count t = learn_cntr / interval
+  int32_t polyak_interval; // Polyak when learn_cntr % polyak_interval == 0 (0 = never)
+  LearnState* st;
+  int32_t temp;            // thread 0 also steps log_alpha (SAC)
+  float lr_temp;
+  int32_t temp_interval;
+  float* stats;
+};
+
+__global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
+  const int cnt = a.st->learn_cntr;
+  const int t = cnt / a.interval;
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+  const double bc1 = 1.0 - pow(0.9, (double)t);
+  const double bc2 = 1.0 - pow(0.999, (double)t);
+  const float step_size = (float)(a.lr / bc1);
+  const float bc2_sqrt = (float)sqrt(bc2);
+  const bool polyak = a.target && a.polyak_interval > 0 && (cnt % a.polyak_interval) == 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float g = a.g[i];
+    float m = a.m[i], v = a.v[i];
+    m = m + (1.f - b1) * (g - m);
+    v = v * b2 + (1.f - b2) * g * g;
+    a.m[i] = m;
+    a.v[i] = v;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    const float p = a.p[i] - step_size * (m / denom);
+    a.p[i] = p;
+    if (polyak) a.target[i] = a.tau * p + (1.f - a.tau) * a.target[i];
+  }
+  if (a.temp && blockIdx.x == 0 && threadIdx.x == 0) {
+    LearnState* st = a.st;
+    if (cnt % a.temp_interval == 0) {
+      const int tt = cnt / a.temp_interval;
+      const double c1 = 1.0 - pow(0.9, (double)tt), c2 = 1.0 - pow(0.999, (double)tt);
+      const float g = st->pad_temp_grad;
+      float m = st->temp_m + (1.f - b1) * (g - st->temp_m);
+      float v = st->temp_v * b2 + (1.f - b2) * g * g;
+      st->temp_m = m;
+      st->temp_v = v;
+      const float denom = sqrtf(v) / (float)sqrt(c2) + eps;
+      st->log_alpha = st->log_alpha - (float)(a.lr_temp / c1) * (m / denom);
+    }
+    if (a.stats) a.stats[11] = st->log_alpha;
+  }
+}
+
+__global__ void bump_kernel(LearnState* st) { st->learn_cntr += 1; }
+
+}  // namespace
+}  // namespace rlmd
+
+// ============================================================================
+// host orchestration
+// ============================================================================
+namespace rlmd {
+namespace {
+
+NetOff make_net(int in, int h1, int h2, int out, bool two_heads) {
+  NetOff o{};
+  o.in = in;
+  o.h1 = h1;
+  o.h2 = h2;
+  o.out = out;
+  o.w1 = 0;
+  o.b1 = o.w1 + (int64_t)h1 * in;
+  o.w2 = o.b1 + h1;
+  o.b2 = o.w2 + (int64_t)h2 * h1;
+  o.w3 = o.b2 + h2;
+  o.b3 = o.w3 + (int64_t)out * h2;
+  if (two_heads) {
+    o.w4 = o.b3 + out;
+    o.b4 = o.w4 + (int64_t)out * h2;
+    o.size = o.b4 + out;
+  } else {
+    o.w4 = o.b4 = -1;
+    o.size = o.b3 + out;
+  }
+  return o;
+}
+
+struct Scratch {
+  // mini-batch
+  float *s, *a, *r, *s2, *xsa;
+  uint8_t* done;
+  int64_t* idx;
+  // target path
+  float *ha1, *ha2, *logp_next, *xs2a2;
+  float *tc1[2], *tc2[2], *qt[2], *y;
+  // critic path
+  float *c1[2], *c2[2], *q[2], *dq[2], *dc2[2], *dc1[2];
+  // actor path
+  float *h1, *h2, *logp, *xsan, *save;
+  float *e1[2], *e2[2], *qn[2], *dqn[2], *dlogp, *de2[2], *de1[2], *dxa[2];
+  float *gh, *dh2, *dh1;
+  float* stats;  // [16] when the caller passes none
+};
+
+}  // namespace
+}  // namespace rlmd
+
+struct rlmd_agent_s {
+  rlmd_agent_cfg cfg;
+  float *params, *target, *grads, *m, *v;
+  int64_t n_params, off_actor, off_c[2];
+  rlmd::NetOff actor, critic;
+  rlmd::LearnState* st;
+  float* zipf_x;
+  float zipf_x2;
+  rlmd::Scratch sc;
+  std::vector<void*> allocs;
+  float *act_h1 = nullptr, *act_h2 = nullptr;
+  int64_t act_cap = 0;
+  int64_t host_cntr = 0;
+};
+
+namespace rlmd {
+namespace {
+
+int agent_alloc(rlmd_agent_s* ag, void** p, size_t bytes) {
+  RLMD_HIP(hipMalloc(p, bytes < 16 ? 16 : bytes));
+  ag->allocs.push_back(*p);
+  return 0;
+}
+#define RLMD_ALLOC(ptr, count)                                                             \
+  do {                                                                                     \
+    int _r = rlmd::agent_alloc(ag, (void**)&(ptr), sizeof(*(ptr)) * (size_t)(count));             \
+    if (_r) return _r;                                                                     \
+  } while (0)
+
+// y = relu?(x W^T + b) for up to two nets of identical shape
+int fwd(rlmd_agent_s* ag, int groups, int M, int N, int K, bool relu, const float* const* X,
+        int ldx, const float* const* W, const float* const* bias, float* const* Y,
+        hipStream_t s) {
+  GemmBatch b{};
+  b.shape = {M, N, K, relu ? 1 : 0};
+  for (int g = 0; g < groups; ++g) b.prob[g] = {X[g], ldx, W[g], K, bias[g], Y[g], N, nullptr, 0, nullptr};
+  return gemm_launch(ag->cfg.precision, GEMM_FWD, b, groups, s);
+}
+
+// dX = mask(G W): G [M, K] (ldg), W [K, N] rows of stride ldw
+int bwd_x(rlmd_agent_s* ag, int groups, int M, int N, int K, const float* const* G, int ldg,
+          const float* const* W, int ldw, const float* const* mask, float* const* DX,
+          hipStream_t s) {
+  GemmBatch b{};
+  b.shape = {M, N, K, 0};
+  for (int g = 0; g < groups; ++g)
+    b.prob[g] = {G[g], ldg, W[g], ldw, nullptr, DX[g], N, mask ? mask[g] : nullptr, N, nullptr};
+  return gemm_launch(ag->cfg.precision, GEMM_BWD_X, b, groups, s);
+}
+
+// dW [M=out, N=in] = G^T X over K = batch rows; db = colsum(G)
+int bwd_w(rlmd_agent_s* ag, int groups, int M, int N, int K, const float* const* G, int ldg,
+          const float* const* X, int ldx, float* const* DW, float* const* DB, hipStream_t s) {
+  GemmBatch b{};
+  b.shape = {M, N, K, 0};
+  for (int g = 0; g < groups; ++g) b.prob[g] = {G[g], ldg, X[g], ldx, nullptr, DW[g], N, nullptr, 0, DB[g]};
+  return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, groups, s);
+}
+
+#define RLMD_TRY(x)         \
+  do {                      \
+    int _r = (x);           \
+    if (_r) return _r;      \
+  } while (0)
+
+HeadArgs head_args(rlmd_agent_s* ag, const float* params, const float* h2, const float* state, int n) {
+  const rlmd_agent_cfg& c = ag->cfg;
+  HeadArgs h{};
+  h.h2 = h2;
+  h.params = params;
+  h.off = ag->actor;
+  h.state = state;
+  h.n = n;
+  h.S = c.state_dim;
+  h.A = c.action_dim;
+  h.algo = c.algo;
+  h.seed = c.seed;
+  h.max_action = c.max_action;
+  h.ls_min = c.log_scale_min;
+  h.ls_max = c.log_scale_max;
+  h.reparam_noise = c.reparam_noise;
+  return h;
+}
+
+int launch_head(const HeadArgs& h, hipStream_t s) {
+  hipLaunchKernelGGL(actor_head_kernel, dim3((h.n + 3) / 4), dim3(256), 0, s, h);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int launch_row_head(int groups, int n, int H, const float* const* X, const float* const* w,
+                    const float* const* bias, float* const* out, hipStream_t s) {
+  RowHeadArgs r{};
+  for (int g = 0; g < groups; ++g) {
+    r.X[g] = X[g];
+    r.w[g] = w[g];
+    r.bias[g] = bias[g];
+    r.out[g] = out[g];
+  }
+  r.n = n;
+  r.H = H;
+  hipLaunchKernelGGL(row_head_kernel, dim3((n + 3) / 4, groups), dim3(256), 0, s, r);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int adam_launch(const AdamArgs& a, hipStream_t s) {
+  const int64_t blocks = std::min<int64_t>((a.n + 255) / 256, 1024);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, a);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+// One learn() on the mini-batch already in ag->sc (s, r, s2, done, xsa).
+// eps_a / eps_b: injected noise (nullable).  stats: [16] device.
+int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const float* eps_b,
+               float* stats, hipStream_t st) {
+  const rlmd_agent_cfg& c = ag->cfg;
+  Scratch& S_ = ag->sc;
+  const int B = c.batch, S = c.state_dim, A = c.action_dim, X = S + A, H1 = c.h1, H2 = c.h2;
+  const bool sac = c.algo == RLMD_SAC;
+  float* P = ag->params;
+  float* T = ag->target;
+  float* G = ag->grads;
+  const NetOff& ao = ag->actor;
+  const NetOff& co = ag->critic;
+  const int64_t cntr = ++ag->host_cntr;  // learn_step_cntr after this update's increment
+
+  float* Pa = P + ag->off_actor;
+  float* Ta = T + ag->off_actor;
+  float* Pc[2] = {P + ag->off_c[0], P + ag->off_c[1]};
+  float* Tc[2] = {T + ag->off_c[0], T + ag->off_c[1]};
+  float* Gc[2] = {G + ag->off_c[0], G + ag->off_c[1]};
+  float* Ga = G + ag->off_actor;
+
+  // ---- target (algo_sac.py:300-367 / algo_td3.py:302-361)
+  {
+    const float* pa = sac ? Pa : Ta;  // SAC samples next actions from the online actor
+    const float* x[1] = {S_.s2};
+    const float* w1[1] = {pa + ao.w1};
+    const float* b1[1] = {pa + ao.b1};
+    float* y1[1] = {S_.ha1};
+    RLMD_TRY(fwd(ag, 1, B, H1, S, true, x, S, w1, b1, y1, st));
+    const float* x2[1] = {S_.ha1};
+    const float* w2[1] = {pa + ao.w2};
+    const float* b2[1] = {pa + ao.b2};
+    float* y2[1] = {S_.ha2};
+    RLMD_TRY(fwd(ag, 1, B, H2, H1, true, x2, H1, w2, b2, y2, st));
+    HeadArgs h = head_args(ag, pa, S_.ha2, S_.s2, B);
+    h.xsa = S_.xs2a2;
+    h.logp = S_.logp_next;
+    h.ctr = &ag->st->learn_cntr;
+    h.mode = 0;
+    if (sac) {
+      h.eps_in = eps_a;
+      h.tag = RLMD_TAG_EPS_NEXT;
+    } else {
+      h.eps_in = eps_a;
+      h.tag = RLMD_TAG_TD3_TARGET;
+      h.noise_std = c.target_policy_noise;
+      h.noise_clip = c.target_policy_clip;
+      h.clamp_noise = 1;
+    }
+    if (!h.eps_in && !sac) {
+      // TD3 target noise drawn in the head kernel (mode 0 draws when eps_in is null)
+    }
+    RLMD_TRY(launch_head(h, st));
+    const float* tx[2] = {S_.xs2a2, S_.xs2a2};
+    const float* tw1[2] = {Tc[0] + co.w1, Tc[1] + co.w1};
+    const float* tb1[2] = {Tc[0] + co.b1, Tc[1] + co.b1};
+    RLMD_TRY(fwd(ag, 2, B, H1, X, true, tx, X, tw1, tb1, S_.tc1, st));
+    const float* tx2[2] = {S_.tc1[0], S_.tc1[1]};
+    const float* tw2[2] = {Tc[0] + co.w2, Tc[1] + co.w2};
+    const float* tb2[2] = {Tc[0] + co.b2, Tc[1] + co.b2};
+    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, tx2, H1, tw2, tb2, S_.tc2, st));
+    const float* hx[2] = {S_.tc2[0], S_.tc2[1]};
+    const float* hw[2] = {Tc[0] + co.w3, Tc[1] + co.w3};
+    const float* hb[2] = {Tc[0] + co.b3, Tc[1] + co.b3};
+    RLMD_TRY(launch_row_head(2, B, H2, hx, hw, hb, S_.qt, st));
+    hipLaunchKernelGGL(critic_target_kernel, dim3((B + 255) / 256), dim3(256), 0, st, S_.qt[0],
+                       S_.qt[1], S_.r, S_.done, eff, S_.logp_next, ag->st, S_.y, B, c.algo,
+                       c.gamma, c.reward_scale);
+    RLMD_LAUNCH_CHECK();
+  }
+  // ---- critics, loss (algo_sac.py:413-465)
+  {
+    const float* x[2] = {S_.xsa, S_.xsa};
+    const float* w1[2] = {Pc[0] + co.w1, Pc[1] + co.w1};
+    const float* b1[2] = {Pc[0] + co.b1, Pc[1] + co.b1};
+    RLMD_TRY(fwd(ag, 2, B, H1, X, true, x, X, w1, b1, S_.c1, st));
+    const float* x2[2] = {S_.c1[0], S_.c1[1]};
+    const float* w2[2] = {Pc[0] + co.w2, Pc[1] + co.w2};
+    const float* b2[2] = {Pc[0] + co.b2, Pc[1] + co.b2};
+    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, x2, H1, w2, b2, S_.c2, st));
+    const float* hx[2] = {S_.c2[0], S_.c2[1]};
+    const float* hw[2] = {Pc[0] + co.w3, Pc[1] + co.w3};
+    const float* hb[2] = {Pc[0] + co.b3, Pc[1] + co.b3};
+    RLMD_TRY(launch_row_head(2, B, H2, hx, hw, hb, S_.q, st));
+    LossArgs la{};
+    la.q[0] = S_.q[0];
+    la.q[1] = S_.q[1];
+    la.y = S_.y;
+    la.dq[0] = S_.dq[0];
+    la.dq[1] = S_.dq[1];
+    la.zipf_x = ag->zipf_x;
+    la.zipf_x2 = ag->zipf_x2;
+    la.st = ag->st;
+    la.stats = stats;
+    la.B = B;
+    la.k = c.topk;
+    la.loss_type = c.loss_type;
+    la.algo = c.algo;
+    la.log_noise = c.log_noise;
+    la.grad_scale = sac ? 0.5f : 1.0f;  // SAC: 0.5 (q1_loss + q2_loss)
+    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, st, la);
+    RLMD_LAUNCH_CHECK();
+    // backward (both critics in one launch per layer)
+    const float* g3[2] = {S_.dq[0], S_.dq[1]};
+    float* dw3[2] = {Gc[0] + co.w3, Gc[1] + co.w3};
+    float* db3[2] = {Gc[0] + co.b3, Gc[1] + co.b3};
+    RLMD_TRY(bwd_w(ag, 2, 1, H2, B, g3, 1, hx, H2, dw3, db3, st));
+    RLMD_TRY(bwd_x(ag, 2, B, H2, 1, g3, 1, hw, H2, hx, S_.dc2, st));
+    const float* g2[2] = {S_.dc2[0], S_.dc2[1]};
+    float* dw2[2] = {Gc[0] + co.w2, Gc[1] + co.w2};
+    float* db2[2] = {Gc[0] + co.b2, Gc[1] + co.b2};
+    RLMD_TRY(bwd_w(ag, 2, H2, H1, B, g2, H2, x2, H1, dw2, db2, st));
+    RLMD_TRY(bwd_x(ag, 2, B, H1, H2, g2, H2, w2, H1, x2, S_.dc1, st));
+    const float* g1[2] = {S_.dc1[0], S_.dc1[1]};
+    float* dw1[2] = {Gc[0] + co.w1, Gc[1] + co.w1};
+    float* db1[2] = {Gc[0] + co.b1, Gc[1] + co.b1};
+    RLMD_TRY(bwd_w(ag, 2, H1, X, B, g1, H1, x, X, dw1, db1, st));
+    AdamArgs ad{};
+    ad.p = Pc[0];
+    ad.g = Gc[0];
+    ad.m = ag->m + ag->off_c[0];
+    ad.v = ag->v + ag->off_c[0];
+    ad.target = Tc[0];
+    ad.n = 2 * co.size;
+    ad.lr = c.lr_critic;
+    ad.tau = c.tau;
+    ad.interval = 1;
+    ad.polyak_interval = c.target_critic_update;
+    ad.st = ag->st;
+    RLMD_TRY(adam_launch(ad, st));
+  }
+  // ---- actor (+ temperature) update every actor_update_interval
+  if (cntr % c.actor_update_interval != 0) return 0;
+  {
+    const int nq = sac ? 2 : 1;
+    const float* x[1] = {S_.s};
+    const float* w1[1] = {Pa + ao.w1};
+    const float* b1[1] = {Pa + ao.b1};
+    float* y1[1] = {S_.h1};
+    RLMD_TRY(fwd(ag, 1, B, H1, S, true, x, S, w1, b1, y1, st));
+    const float* x2[1] = {S_.h1};
+    const float* w2[1] = {Pa + ao.w2};
+    const float* b2[1] = {Pa + ao.b2};
+    float* y2[1] = {S_.h2};
+    RLMD_TRY(fwd(ag, 1, B, H2, H1, true, x2, H1, w2, b2, y2, st));
+    HeadArgs h = head_args(ag, Pa, S_.h2, S_.s, B);
+    h.xsa = S_.xsan;
+    h.logp = S_.logp;
+    h.save = S_.save;
+    h.ctr = &ag->st->learn_cntr;
+    if (sac) {
+      h.mode = 0;
+      h.eps_in = eps_b;
+      h.tag = RLMD_TAG_EPS_CUR;
+    } else {
+      h.mode = 1;  // TD3 actor.forward: tanh(mu) * max_action, no noise
+    }
+    RLMD_TRY(launch_head(h, st));
+    const float* ex[2] = {S_.xsan, S_.xsan};
+    const float* cw1[2] = {Pc[0] + co.w1, Pc[1] + co.w1};
+    const float* cb1[2] = {Pc[0] + co.b1, Pc[1] + co.b1};
+    RLMD_TRY(fwd(ag, nq, B, H1, X, true, ex, X, cw1, cb1, S_.e1, st));
+    const float* ex2[2] = {S_.e1[0], S_.e1[1]};
+    const float* cw2[2] = {Pc[0] + co.w2, Pc[1] + co.w2};
+    const float* cb2[2] = {Pc[0] + co.b2, Pc[1] + co.b2};
+    RLMD_TRY(fwd(ag, nq, B, H2, H1, true, ex2, H1, cw2, cb2, S_.e2, st));
+    const float* hx[2] = {S_.e2[0], S_.e2[1]};
+    const float* hw[2] = {Pc[0] + co.w3, Pc[1] + co.w3};
+    const float* hb[2] = {Pc[0] + co.b3, Pc[1] + co.b3};
+    RLMD_TRY(launch_row_head(nq, B, H2, hx, hw, hb, S_.qn, st));
+    ActorLossArgs al{};
+    al.q[0] = S_.qn[0];
+    al.q[1] = sac ? S_.qn[1] : nullptr;
+    al.logp = sac ? S_.logp : nullptr;
+    al.dq[0] = S_.dqn[0];
+    al.dq[1] = S_.dqn[1];
+    al.dlogp = S_.dlogp;
+    al.st = ag->st;
+    al.stats = stats;
+    al.B = B;
+    al.k = c.topk;
+    al.algo = c.algo;
+    al.topk = c.actor_topk;
+    al.target_entropy = -(float)A;
+    hipLaunchKernelGGL(actor_loss_kernel, dim3(1), dim3(1024), 0, st, al);
+    RLMD_LAUNCH_CHECK();
+    // dL/da through the (updated) critics: only the action columns of fc1
+    const float* g3[2] = {S_.dqn[0], S_.dqn[1]};
+    RLMD_TRY(bwd_x(ag, nq, B, H2, 1, g3, 1, hw, H2, hx, S_.de2, st));
+    const float* g2[2] = {S_.de2[0], S_.de2[1]};
+    RLMD_TRY(bwd_x(ag, nq, B, H1, H2, g2, H2, cw2, H1, ex2, S_.de1, st));
+    const float* g1[2] = {S_.de1[0], S_.de1[1]};
+    const float* w1a[2] = {Pc[0] + co.w1 + S, Pc[1] + co.w1 + S};
+    RLMD_TRY(bwd_x(ag, nq, B, A, H1, g1, H1, w1a, X, nullptr, S_.dxa, st));
+    ActorBwdArgs ab{};
+    ab.dxa[0] = S_.dxa[0];
+    ab.dxa[1] = sac ? S_.dxa[1] : nullptr;
+    ab.dlogp = S_.dlogp;
+    ab.save = S_.save;
+    ab.h2 = S_.h2;
+    ab.params = Pa;
+    ab.off = ao;
+    ab.gh = S_.gh;
+    ab.dh2 = S_.dh2;
+    ab.n = B;
+    ab.A = A;
+    ab.algo = c.algo;
+    ab.max_action = c.max_action;
+    ab.ls_min = c.log_scale_min;
+    ab.ls_max = c.log_scale_max;
+    ab.reparam_noise = c.reparam_noise;
+    hipLaunchKernelGGL(actor_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, ab);
+    RLMD_LAUNCH_CHECK();
+    // head weight gradients (pi and log_scale as two groups)
+    const float* gh[2] = {S_.gh, S_.gh + A};
+    const float* h2x[2] = {S_.h2, S_.h2};
+    float* dwh[2] = {Ga + ao.w3, sac ? Ga + ao.w4 : nullptr};
+    float* dbh[2] = {Ga + ao.b3, sac ? Ga + ao.b4 : nullptr};
+    RLMD_TRY(bwd_w(ag, sac ? 2 : 1, A, H2, B, gh, 2 * A, h2x, H2, dwh, dbh, st));
+    const float* gd2[1] = {S_.dh2};
+    const float* hh1[1] = {S_.h1};
+    float* dw2[1] = {Ga + ao.w2};
+    float* db2[1] = {Ga + ao.b2};
+    RLMD_TRY(bwd_w(ag, 1, H2, H1, B, gd2, H2, hh1, H1, dw2, db2, st));
+    float* dh1[1] = {S_.dh1};
+    RLMD_TRY(bwd_x(ag, 1, B, H1, H2, gd2, H2, w2, H1, hh1, dh1, st));
+    const float* gd1[1] = {S_.dh1};
+    float* dw1[1] = {Ga + ao.w1};
+    float* db1[1] = {Ga + ao.b1};
+    RLMD_TRY(bwd_w(ag, 1, H1, S, B, gd1, H1, x, S, dw1, db1, st));
+    AdamArgs ad{};
+    ad.p = Pa;
+    ad.g = Ga;
+    ad.m = ag->m + ag->off_actor;
+    ad.v = ag->v + ag->off_actor;
+    ad.target = sac ? nullptr : Ta;
+    ad.n = ao.size;
+    ad.lr = c.lr_actor;
+    ad.tau = c.tau;
+    ad.interval = c.actor_update_interval;
+    ad.polyak_interval = sac ? 0 : c.target_actor_update;
+    ad.st = ag->st;
+    ad.temp = sac ? 1 : 0;
+    ad.lr_temp = c.lr_temp;
+    ad.temp_interval = c.temp_update_interval;
+    ad.stats = stats;
+    RLMD_TRY(adam_launch(ad, st));
+  }
+  return 0;
+}
+
+float* stats_slot(rlmd_agent_s* ag, float* stats, int i) {
+  return stats ? stats + 16 * (int64_t)i : ag->sc.stats;
+}
+
+int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipStream_t st) {
+  const rlmd_agent_cfg& c = ag->cfg;
+  const ReplayView v = replay_view(rb);
+  const int64_t mem = replay_mem_idx(rb);
+  const int64_t M = mem < v.capacity ? mem : v.capacity;
+  RLMD_CHECK(v.S == c.state_dim && v.A == c.action_dim, "replay / agent dims differ");
+  for (int i = 0; i < k; ++i) {
+    Scratch& S_ = ag->sc;
+    RLMD_TRY(replay_sample_launch(v, M, c.batch, c.seed ^ 0x5eed5eed5eedull, 0, &ag->st->learn_cntr,
+                                  S_.idx, S_.s, S_.a, S_.r, S_.s2, S_.done, S_.xsa, st));
+    RLMD_TRY(learn_body(ag, nullptr, nullptr, nullptr, stats_slot(ag, stats, i), st));
+  }
+  return 0;
+}
+
+int agent_act(rlmd_agent_s* ag, const float* obs, int64_t n, float* actions, int mode,
+              uint64_t noise_ctr, const float* eps, hipStream_t st) {
+  const rlmd_agent_cfg& c = ag->cfg;
+  if (n <= 0) return 0;
+  if (n > ag->act_cap) {
+    if (ag->act_h1) {
+      RLMD_HIP(hipFree(ag->act_h1));
+      RLMD_HIP(hipFree(ag->act_h2));
+    }
+    RLMD_HIP(hipMalloc(&ag->act_h1, sizeof(float) * n * c.h1));
+    RLMD_HIP(hipMalloc(&ag->act_h2, sizeof(float) * n * c.h2));
+    ag->act_cap = n;
+  }
+  RLMD_CHECK(n <= INT32_MAX, "too many rows");
+  const float* Pa = ag->params + ag->off_actor;
+  const NetOff& ao = ag->actor;
+  const float* x[1] = {obs};
+  const float* w1[1] = {Pa + ao.w1};
+  const float* b1[1] = {Pa + ao.b1};
+  float* y1[1] = {ag->act_h1};
+  RLMD_TRY(fwd(ag, 1, (int)n, c.h1, c.state_dim, true, x, c.state_dim, w1, b1, y1, st));
+  const float* x2[1] = {ag->act_h1};
+  const float* w2[1] = {Pa + ao.w2};
+  const float* b2[1] = {Pa + ao.b2};
+  float* y2[1] = {ag->act_h2};
+  RLMD_TRY(fwd(ag, 1, (int)n, c.h2, c.h1, true, x2, c.h1, w2, b2, y2, st));
+  HeadArgs h = head_args(ag, Pa, ag->act_h2, obs, (int)n);
+  h.actions = actions;
+  h.mode = mode;
+  h.eps_in = eps;
+  h.tag = RLMD_TAG_ACT_NOISE;
+  h.ctr_host = (uint32_t)noise_ctr;
+  h.seed = c.seed ^ 0xac7ac7ac7ull;
+  if (c.algo == RLMD_TD3) {
+    h.noise_std = c.policy_noise;
+    h.clamp_noise = 0;
+  }
+  return launch_head(h, st);
+}
+
+}  // namespace
+}  // namespace rlmd
+
+extern "C" {
+
+int rlmd_agent_layout(const rlmd_agent_cfg* c, int64_t* n, int64_t* oa, int64_t* o1, int64_t* o2) {
+  RLMD_CHECK(c, "null cfg");
+  const rlmd::NetOff a = rlmd::make_net(c->state_dim, c->h1, c->h2, c->action_dim, c->algo == RLMD_SAC);
+  const rlmd::NetOff q = rlmd::make_net(c->state_dim + c->action_dim, c->h1, c->h2, 1, false);
+  if (oa) *oa = 0;
+  if (o1) *o1 = a.size;
+  if (o2) *o2 = a.size + q.size;
+  if (n) *n = a.size + 2 * q.size;
+  return 0;
+}
+
+int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, float* grads,
+                      float* m, float* v, rlmd_agent_t* out) {
+  RLMD_CHECK(cfg && params && target && grads && m && v && out, "null argument");
+  const rlmd_agent_cfg& c = *cfg;
+  RLMD_CHECK(c.algo == RLMD_SAC || c.algo == RLMD_TD3, "bad algo");
+  RLMD_CHECK(c.batch >= 2 && c.batch <= RLMD_MAX_BATCH, "mini-batch must be in [2, 1024]");
+  RLMD_CHECK(c.topk >= 1, "topk must be >= 1");
+  RLMD_CHECK(c.action_dim >= 1 && c.action_dim <= RLMD_MAX_ACTION, "action dim out of range");
+  RLMD_CHECK(c.precision == RLMD_FP32 || c.precision == RLMD_BF16, "bad precision");
+  RLMD_CHECK(c.loss_type >= RLMD_LOSS_MSE && c.loss_type <= RLMD_LOSS_MSE6, "bad loss type");
+  RLMD_CHECK(c.actor_update_interval >= 1 && c.target_critic_update >= 1 && c.temp_update_interval >= 1 &&
+                 c.target_actor_update >= 1,
+             "update intervals must be >= 1");
+  auto* ag = new rlmd_agent_s();
+  ag->cfg = c;
+  ag->params = params;
+  ag->target = target;
+  ag->grads = grads;
+  ag->m = m;
+  ag->v = v;
+  ag->actor = rlmd::make_net(c.state_dim, c.h1, c.h2, c.action_dim, c.algo == RLMD_SAC);
+  ag->critic = rlmd::make_net(c.state_dim + c.action_dim, c.h1, c.h2, 1, false);
+  rlmd_agent_layout(cfg, &ag->n_params, &ag->off_actor, &ag->off_c[0], &ag->off_c[1]);
+  const int B = c.batch, S = c.state_dim, A = c.action_dim, X = S + A, H1 = c.h1, H2 = c.h2;
+  rlmd::Scratch& s = ag->sc;
+  RLMD_ALLOC(s.s, B * S);
+  RLMD_ALLOC(s.a, B * A);
+  RLMD_ALLOC(s.r, B);
+  RLMD_ALLOC(s.s2, B * S);
+  RLMD_ALLOC(s.xsa, B * X);
+  RLMD_ALLOC(s.done, B);
+  RLMD_ALLOC(s.idx, B);
+  RLMD_ALLOC(s.ha1, B * H1);
+  RLMD_ALLOC(s.ha2, B * H2);
+  RLMD_ALLOC(s.logp_next, B);
+  RLMD_ALLOC(s.xs2a2, B * X);
+  RLMD_ALLOC(s.y, B);
+  RLMD_ALLOC(s.h1, B * H1);
+  RLMD_ALLOC(s.h2, B * H2);
+  RLMD_ALLOC(s.logp, B);
+  RLMD_ALLOC(s.xsan, B * X);
+  RLMD_ALLOC(s.save, B * 5 * A);
+  RLMD_ALLOC(s.dlogp, B);
+  RLMD_ALLOC(s.gh, B * 2 * A);
+  RLMD_ALLOC(s.dh2, B * H2);
+  RLMD_ALLOC(s.dh1, B * H1);
+  RLMD_ALLOC(s.stats, 16);
+  for (int g = 0; g < 2; ++g) {
+    RLMD_ALLOC(s.tc1[g], B * H1);
+    RLMD_ALLOC(s.tc2[g], B * H2);
+    RLMD_ALLOC(s.qt[g], B);
+    RLMD_ALLOC(s.c1[g], B * H1);
+    RLMD_ALLOC(s.c2[g], B * H2);
+    RLMD_ALLOC(s.q[g], B);
+    RLMD_ALLOC(s.dq[g], B);
+    RLMD_ALLOC(s.dc2[g], B * H2);
+    RLMD_ALLOC(s.dc1[g], B * H1);
+    RLMD_ALLOC(s.e1[g], B * H1);
+    RLMD_ALLOC(s.e2[g], B * H2);
+    RLMD_ALLOC(s.qn[g], B);
+    RLMD_ALLOC(s.dqn[g], B);
+    RLMD_ALLOC(s.de2[g], B * H2);
+    RLMD_ALLOC(s.de1[g], B * H1);
+    RLMD_ALLOC(s.dxa[g], B * A);
+  }
+  // Zipf-plot x axis (algo_sac.py:157-162): x_j = log((1 + k) / j), centred
+  const int k = c.topk;
+  std::vector<float> zx(k);
+  for (int j = 0; j < k; ++j) zx[j] = logf((1.0f + (float)k) / (float)(j + 1));
+  double mean = 0.0;
+  for (int j = 0; j < k; ++j) mean += zx[j];
+  const float meanf = (float)(mean / k);
+  double x2 = 0.0;
+  for (int j = 0; j < k; ++j) {
+    zx[j] -= meanf;
+    x2 += (double)zx[j] * zx[j];
+  }
+  ag->zipf_x2 = (float)x2;
+  RLMD_ALLOC(ag->zipf_x, k);
+  RLMD_HIP(hipMemcpy(ag->zipf_x, zx.data(), sizeof(float) * k, hipMemcpyHostToDevice));
+  RLMD_ALLOC(ag->st, 1);
+  rlmd::LearnState st{};
+  st.cauchy[0] = st.cauchy[1] = c.cauchy_scale;
+  st.log_alpha = c.initial_logtemp;
+  RLMD_HIP(hipMemcpy(ag->st, &st, sizeof(st), hipMemcpyHostToDevice));
+  RLMD_HIP(hipMemset(m, 0, sizeof(float) * ag->n_params));
+  RLMD_HIP(hipMemset(v, 0, sizeof(float) * ag->n_params));
+  RLMD_HIP(hipMemset(grads, 0, sizeof(float) * ag->n_params));
+  RLMD_HIP(hipDeviceSynchronize());
+  *out = ag;
+  return 0;
+}
+
+int rlmd_agent_destroy(rlmd_agent_t ag) {
+  if (!ag) return 0;
+  for (void* p : ag->allocs) (void)hipFree(p);
+  if (ag->act_h1) (void)hipFree(ag->act_h1);
+  if (ag->act_h2) (void)hipFree(ag->act_h2);
+  delete ag;
+  return 0;
+}
+
+int rlmd_agent_act(rlmd_agent_t ag, const float* obs, int64_t n, float* actions, int32_t mode,
+                   uint64_t noise_ctr, const float* eps, void* stream) {
+  RLMD_CHECK(ag && obs && actions, "null argument");
+  RLMD_CHECK(mode == 0 || mode == 1, "mode must be 0 (stochastic) or 1 (deterministic)");
+  return rlmd::agent_act(ag, obs, n, actions, mode, noise_ctr, eps, (hipStream_t)stream);
+}
+
+int rlmd_agent_learn(rlmd_agent_t ag, rlmd_replay_t rb, int32_t k, float* stats, void* stream) {
+  RLMD_CHECK(ag && rb, "null argument");
+  return rlmd::agent_learn_k(ag, rb, k, stats, (hipStream_t)stream);
+}
+
+int rlmd_agent_learn_batch(rlmd_agent_t ag, const float* s, const float* a, const float* r,
+                           const float* s2, const uint8_t* done, const int32_t* eff,
+                           const float* eps_a, const float* eps_b, float* stats, void* stream) {
+  RLMD_CHECK(ag && s && a && r && s2 && done, "null argument");
+  const rlmd_agent_cfg& c = ag->cfg;
+  hipStream_t st = (hipStream_t)stream;
+  rlmd::Scratch& S_ = ag->sc;
+  const int B = c.batch, S = c.state_dim, A = c.action_dim;
+  RLMD_HIP(hipMemcpyAsync(S_.s, s, sizeof(float) * B * S, hipMemcpyDeviceToDevice, st));
+  RLMD_HIP(hipMemcpyAsync(S_.s2, s2, sizeof(float) * B * S, hipMemcpyDeviceToDevice, st));
+  RLMD_HIP(hipMemcpyAsync(S_.r, r, sizeof(float) * B, hipMemcpyDeviceToDevice, st));
+  RLMD_HIP(hipMemcpyAsync(S_.done, done, B, hipMemcpyDeviceToDevice, st));
+  RLMD_HIP(hipMemcpy2DAsync(S_.xsa, sizeof(float) * (S + A), s, sizeof(float) * S, sizeof(float) * S,
+                            B, hipMemcpyDeviceToDevice, st));
+  RLMD_HIP(hipMemcpy2DAsync(S_.xsa + S, sizeof(float) * (S + A), a, sizeof(float) * A,
+                            sizeof(float) * A, B, hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(rlmd::bump_kernel, dim3(1), dim3(1), 0, st, ag->st);
+  RLMD_LAUNCH_CHECK();
+  return rlmd::learn_body(ag, eff, eps_a, eps_b, rlmd::stats_slot(ag, stats, 0), st);
+}
+
+int rlmd_agent_scalars(rlmd_agent_t ag, double* out) {
+  RLMD_CHECK(ag && out, "null argument");
+  rlmd::LearnState st;
+  RLMD_HIP(hipDeviceSynchronize());
+  RLMD_HIP(hipMemcpy(&st, ag->st, sizeof(st), hipMemcpyDeviceToHost));
+  out[0] = st.cauchy[0];
+  out[1] = st.cauchy[1];
+  out[2] = st.log_alpha;
+  out[3] = st.learn_cntr;
+  out[4] = st.nan_flag;
+  return 0;
+}
+
+int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlmd_train_cfg* cfg,
+                    float* obs, float* actions, double* ep_stats, float* stats, void* stream) {
+  RLMD_CHECK(env && rb && cfg && obs && actions, "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  const int N = rlmd::env_lanes(env);
+  const rlmd::ReplayView v = rlmd::replay_view(rb);
+  RLMD_CHECK(v.S == rlmd::env_state_dim(env) && v.A == rlmd::env_action_dim(env),
+             "replay / env dims differ");
+  const int64_t cs = cfg->cum_step;
+  const bool random = cs < cfg->warmup_steps;
+  if (!random) {
+    RLMD_CHECK(ag, "policy acting needs an agent");
+    RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st));
+  }
+  // action_window (tools/utils.py:345-373): only warmup < cum_step <= smoothing_window
+  float lo = -INFINITY, hi = INFINITY;
+  if (cs <= cfg->smoothing_window && cs > cfg->warmup_steps) {
+    const double ratio = (double)cs / (double)cfg->smoothing_window;
+    const double width = (sin(M_PI * (ratio - 0.5)) + 1.0) / 2.0;
+    lo = (float)(width * -0.99);
+    hi = (float)(width * 0.99);
+  }
+  const int64_t base = rlmd::replay_mem_idx(rb);
+  RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, lo,
+                           hi, obs, ep_stats, st));
+  rlmd::replay_advance(rb, N);
+  if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch)
+    RLMD_TRY(rlmd::agent_learn_k(ag, rb, cfg->k_updates, stats, st));
+  return 0;
+}
+
+}  // extern "C"

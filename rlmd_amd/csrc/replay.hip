@@ -1,0 +1,225 @@
+// replay.hip — on-device replay ring + fused sample/gather for gfx950.
+//
+// Replaces tools/replay_torch.py (ReplayBufferTorch) / tools/replay.py:
+//   store_exp   :167-197 (torch) / :143-174 (numpy): ring slot mem_idx % mem_size,
+//               reward stored as max(r, r_abs_zero = -inf) == r;
+//   sample_exp  :360-412 (torch randperm(max_mem)[:B]) / :334-376 (numpy
+//               choice(max_mem, B, replace=False)): B DISTINCT uniform indices
+//               over the filled part of the ring, then row gathers.
+// Distinct indices on the GPU, two regimes (both restated in oracle/replay.py,
+// so a sample is reproducible on the CPU index for index):
+//   M <= 8192: a uniformly random B-subset as the B smallest of M random keys
+//              (one LDS bitonic sort of (philox32 << 32 | index));
+//   M >  8192: draw B candidates with Philox, sort (index, slot) pairs in LDS,
+//              redraw every slot whose index already appeared at a smaller slot,
+//              repeat (collision rate <= B/M <= 1/8 per round).
+#include <string.h>
+
+#include <string>
+
+#include "rlmd_common.h"
+#include "rlmd_internal.h"
+
+struct rlmd_replay_s {
+  rlmd::ReplayView v;
+  int64_t mem_idx = 0;
+};
+
+namespace {
+
+constexpr int kSampleThreads = RLMD_MAX_BATCH;
+constexpr int kMaxRounds = 64;
+constexpr int kSortPopulation = 8192;  // M at or below: sort-based subset
+
+__global__ void __launch_bounds__(kSampleThreads)
+    replay_sample_kernel(rlmd::ReplayView rb, int64_t M, int B, uint64_t seed, uint32_t ctr_lo,
+                         uint32_t ctr_hi, int32_t* dev_ctr, int64_t* idx_out, float* s, float* a,
+                         float* r, float* s2, uint8_t* done, float* xsa) {
+  __shared__ uint64_t keys[kSortPopulation];
+  __shared__ int64_t cand[kSampleThreads];
+  __shared__ int any_dup;
+  const int i = threadIdx.x;
+  // learner path: the draw counter is the device learn counter, bumped here
+  // (every thread reads it before the first barrier; thread 0 writes after the last)
+  if (dev_ctr) ctr_lo = (uint32_t)*dev_ctr;
+  const uint32_t c2 = RLMD_TAG_REPLAY_IDX | (ctr_hi << 8);
+  if (M <= kSortPopulation) {
+    int npow = 1;
+    while (npow < M) npow <<= 1;
+    for (int e = i; e < npow; e += kSampleThreads) {
+      if (e < M) {
+        const rlmd_u32x4 v = rlmd_philox(seed, (uint32_t)e, ctr_lo, c2, 0xFFFFFFFFu);
+        keys[e] = ((uint64_t)v.x << 32) | (uint64_t)e;
+      } else {
+        keys[e] = ~0ull;
+      }
+    }
+    __syncthreads();
+    for (int k = 2; k <= npow; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int e = i; e < npow; e += kSampleThreads) {
+          const int exj = e ^ j;
+          if (exj > e) {
+            const uint64_t x = keys[e], y = keys[exj];
+            const bool up = (e & k) == 0;
+            if ((x > y) == up) {
+              keys[e] = y;
+              keys[exj] = x;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    if (i < B) cand[i] = (int64_t)(keys[i] & 0xFFFFFFFFu);
+  } else {
+  if (i < B) {
+    const rlmd_u32x4 v = rlmd_philox(seed, (uint32_t)i, ctr_lo, c2, 0u);
+    cand[i] = (int64_t)rlmd_below(v.x, v.y, (uint64_t)M);
+  }
+  for (int round = 1; round <= kMaxRounds; ++round) {
+    __syncthreads();
+    keys[i] = i < B ? (((uint64_t)cand[i] << 11) | (uint64_t)i) : ~0ull;
+    if (i == 0) any_dup = 0;
+    __syncthreads();
+    // bitonic sort of kSampleThreads keys (ascending)
+    for (int k = 2; k <= kSampleThreads; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t x = keys[i], y = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) {
+            keys[i] = y;
+            keys[ixj] = x;
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // a sorted key whose index equals its predecessor's is a duplicate slot
+    if (i > 0 && i < B) {
+      const uint64_t cur = keys[i], prev = keys[i - 1];
+      if ((cur >> 11) == (prev >> 11)) {
+        const int slot = (int)(cur & 2047u);
+        const rlmd_u32x4 v = rlmd_philox(seed, (uint32_t)slot, ctr_lo, c2, (uint32_t)round);
+        cand[slot] = (int64_t)rlmd_below(v.x, v.y, (uint64_t)M);
+        any_dup = 1;
+      }
+    }
+    __syncthreads();
+    if (!any_dup) break;
+  }
+  }
+  __syncthreads();
+  if (dev_ctr && i == 0) *dev_ctr = (int32_t)ctr_lo + 1;
+  if (i >= B) return;
+  const int64_t row = cand[i];
+  const int S = rb.S, A = rb.A;
+  if (idx_out) idx_out[i] = row;
+  for (int k = 0; k < S; ++k) {
+    const float v = rb.state[row * S + k];
+    if (s) s[(int64_t)i * S + k] = v;
+    if (xsa) xsa[(int64_t)i * (S + A) + k] = v;
+    if (s2) s2[(int64_t)i * S + k] = rb.next_state[row * S + k];
+  }
+  for (int k = 0; k < A; ++k) {
+    const float v = rb.action[row * A + k];
+    if (a) a[(int64_t)i * A + k] = v;
+    if (xsa) xsa[(int64_t)i * (S + A) + S + k] = v;
+  }
+  if (r) r[i] = rb.reward[row];
+  if (done) done[i] = rb.done[row];
+}
+
+__global__ void replay_insert_kernel(rlmd::ReplayView rb, int64_t base, int64_t n, const float* s,
+                                     const float* a, const float* r, const float* s2,
+                                     const uint8_t* d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t row = (base + i) % rb.capacity;
+  for (int k = 0; k < rb.S; ++k) {
+    rb.state[row * rb.S + k] = s[i * rb.S + k];
+    rb.next_state[row * rb.S + k] = s2[i * rb.S + k];
+  }
+  for (int k = 0; k < rb.A; ++k) rb.action[row * rb.A + k] = a[i * rb.A + k];
+  rb.reward[row] = r[i];
+  rb.done[row] = d[i];
+}
+
+}  // namespace
+
+namespace rlmd {
+
+ReplayView replay_view(rlmd_replay_t rb) { return rb->v; }
+int64_t replay_mem_idx(rlmd_replay_t rb) { return rb->mem_idx; }
+void replay_advance(rlmd_replay_t rb, int64_t n) { rb->mem_idx += n; }
+
+int replay_sample_launch(const ReplayView& rb, int64_t M, int B, uint64_t seed, uint64_t ctr,
+                         int32_t* dev_ctr, int64_t* idx, float* s, float* a, float* r, float* s2,
+                         uint8_t* done, float* xsa, hipStream_t stream) {
+  RLMD_CHECK(B >= 1 && B <= RLMD_MAX_BATCH, "batch must be in [1, 1024]");
+  RLMD_CHECK(M >= B, "replay holds fewer transitions than the mini-batch");
+  RLMD_CHECK(M <= (int64_t)1 << 52, "replay too large");
+  hipLaunchKernelGGL(replay_sample_kernel, dim3(1), dim3(kSampleThreads), 0, stream, rb, M, B, seed,
+                     (uint32_t)ctr, (uint32_t)(ctr >> 32), dev_ctr, idx, s, a, r, s2, done, xsa);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+}  // namespace rlmd
+
+extern "C" {
+
+int rlmd_replay_create(int64_t capacity, int32_t S, int32_t A, rlmd_replay_t* out) {
+  RLMD_CHECK(out && capacity > 0 && S > 0 && A > 0, "bad replay arguments");
+  auto* rb = new rlmd_replay_s();
+  rb->v.capacity = capacity;
+  rb->v.S = S;
+  rb->v.A = A;
+  RLMD_HIP(hipMalloc(&rb->v.state, sizeof(float) * capacity * S));
+  RLMD_HIP(hipMalloc(&rb->v.next_state, sizeof(float) * capacity * S));
+  RLMD_HIP(hipMalloc(&rb->v.action, sizeof(float) * capacity * A));
+  RLMD_HIP(hipMalloc(&rb->v.reward, sizeof(float) * capacity));
+  RLMD_HIP(hipMalloc(&rb->v.done, capacity));
+  *out = rb;
+  return 0;
+}
+
+int rlmd_replay_destroy(rlmd_replay_t rb) {
+  if (!rb) return 0;
+  (void)hipFree(rb->v.state);
+  (void)hipFree(rb->v.next_state);
+  (void)hipFree(rb->v.action);
+  (void)hipFree(rb->v.reward);
+  (void)hipFree(rb->v.done);
+  delete rb;
+  return 0;
+}
+
+int rlmd_replay_insert(rlmd_replay_t rb, int64_t n, const float* s, const float* a, const float* r,
+                       const float* s2, const uint8_t* d, void* stream) {
+  RLMD_CHECK(rb && s && a && r && s2 && d, "null argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(replay_insert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, rb->v, rb->mem_idx, n, s, a, r, s2, d);
+  RLMD_LAUNCH_CHECK();
+  rb->mem_idx += n;
+  return 0;
+}
+
+int rlmd_replay_mem_idx(rlmd_replay_t rb, int64_t* m) {
+  RLMD_CHECK(rb && m, "null argument");
+  *m = rb->mem_idx;
+  return 0;
+}
+
+int rlmd_replay_sample(rlmd_replay_t rb, int32_t B, uint64_t seed, uint64_t ctr, int64_t* idx,
+                       float* s, float* a, float* r, float* s2, uint8_t* done, void* stream) {
+  RLMD_CHECK(rb, "null replay");
+  const int64_t M = rb->mem_idx < rb->v.capacity ? rb->mem_idx : rb->v.capacity;
+  return rlmd::replay_sample_launch(rb->v, M, B, seed, ctr, nullptr, idx, s, a, r, s2, done, nullptr,
+                                    (hipStream_t)stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+// rlmd_common.h — shared device/host helpers for the rlmd_amd HIP library (gfx950).
+//
+// Counter-based randomness: every random draw in the library is
+//   Philox4x32-10(key = seed, counter = (c0, c1, c2, c3))
+// with a fixed meaning per draw site (see RLMD_TAG_*), so a draw is a pure
+// function of (seed, lane/row, step, site, index).  No per-lane RNG state lives
+// in HBM, graph replays stay deterministic, and the CPU oracle (oracle/philox.py)
+// regenerates the same bits.  The generator core is the standard Philox4x32-10
+// (Salmon et al., SC'11) — the same core rocRAND's philox4x32_10 uses; the
+// uniform and normal transforms below are ours and are restated in the oracle.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define RLMD_TAG_ENV_DRAW 1u       // env gamble outcomes (c0 = lane, c1 = step, c3 = pair index)
+#define RLMD_TAG_WARMUP_ACTION 2u  // warm-up random actions (c0 = lane, c1 = step)
+#define RLMD_TAG_ACT_NOISE 3u      // acting noise (SAC eps / TD3 policy noise)
+#define RLMD_TAG_REPLAY_IDX 4u     // replay sample indices (c0 = slot, c1 = update, c3 = round)
+#define RLMD_TAG_EPS_NEXT 5u       // SAC eps for next-state actions in the target
+#define RLMD_TAG_EPS_CUR 6u        // SAC eps for current-state actions in the actor update
+#define RLMD_TAG_TD3_TARGET 7u     // TD3 target policy smoothing noise
+#define RLMD_TAG_MKT_START 8u      // market episode start index (c0 = lane, c1 = episode)
+#define RLMD_TAG_MKT_PERM 9u       // market in-block shuffles (c0 = lane, c1 = episode, c3 = block)
+
+struct rlmd_u32x4 {
+  uint32_t x, y, z, w;
+};
+
+__host__ __device__ __forceinline__ uint32_t rlmd_mulhi32(uint32_t a, uint32_t b) {
+  return (uint32_t)(((uint64_t)a * (uint64_t)b) >> 32);
+}
+
+__host__ __device__ __forceinline__ rlmd_u32x4 rlmd_philox(uint64_t seed, uint32_t c0, uint32_t c1,
+                                                           uint32_t c2, uint32_t c3) {
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = c3;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * x0, hi0 = rlmd_mulhi32(0xD2511F53u, x0);
+    const uint32_t lo1 = 0xCD9E8D57u * x2, hi1 = rlmd_mulhi32(0xCD9E8D57u, x2);
+    const uint32_t n0 = hi1 ^ x1 ^ k0, n2 = hi0 ^ x3 ^ k1;
+    x0 = n0;
+    x1 = lo1;
+    x2 = n2;
+    x3 = lo0;
+  }
+  return {x0, x1, x2, x3};
+}
+
+// 53-bit uniform in [0, 1) from two words (NumPy's random_sample construction).
+__host__ __device__ __forceinline__ double rlmd_u01(uint32_t a, uint32_t b) {
+  return ((double)(a >> 5) * 67108864.0 + (double)(b >> 6)) * (1.0 / 9007199254740992.0);
+}
+
+// Box–Muller pair from one Philox block: z0 = r cos(2πu2), z1 = r sin(2πu2),
+// r = sqrt(-2 ln(1 - u1)) (1 - u1 in (0, 1], so the log is finite).
+__device__ __forceinline__ void rlmd_normal2(rlmd_u32x4 v, double& z0, double& z1) {
+  const double u1 = rlmd_u01(v.x, v.y), u2 = rlmd_u01(v.z, v.w);
+  const double r = sqrt(-2.0 * log(1.0 - u1));
+  double s, c;
+  sincospi(2.0 * u2, &s, &c);
+  z0 = r * c;
+  z1 = r * s;
+}
+
+// Uniform integer in [0, n) from one 32-bit word and a second for 64-bit range
+// (multiply-shift; bias < n / 2^64, negligible).
+__host__ __device__ __forceinline__ uint64_t rlmd_below(uint32_t a, uint32_t b, uint64_t n) {
+  const uint64_t x = ((uint64_t)a << 32) | b;
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __umul64hi(x, n);
+#else
+  return (uint64_t)(((unsigned __int128)x * n) >> 64);
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// host-side error plumbing for the C ABI
+// ---------------------------------------------------------------------------
+#include <string>
+namespace rlmd {
+void set_error(const std::string& msg);
+}
+#define RLMD_HIP(call)                                                                     \
+  do {                                                                                     \
+    hipError_t _e = (call);                                                                \
+    if (_e != hipSuccess) {                                                                \
+      rlmd::set_error(std::string(#call) + " failed: " + hipGetErrorString(_e) + " at " + \
+                      __FILE__ + ":" + std::to_string(__LINE__));                          \
+      return 2;                                                                            \
+    }                                                                                      \
+  } while (0)
+#define RLMD_CHECK(cond, msg)                                          \
+  do {                                                                 \
+    if (!(cond)) {                                                     \
+      rlmd::set_error(std::string("rlmd: ") + (msg) + " [" #cond "]"); \
+      return 1;                                                        \
+    }                                                                  \
+  } while (0)
+#define RLMD_LAUNCH_CHECK()                                                                   \
+  do {                                                                                        \
+    hipError_t _e = hipGetLastError();                                                        \
+    if (_e != hipSuccess) {                                                                   \
+      rlmd::set_error(std::string("kernel launch failed: ") + hipGetErrorString(_e) + " at " + \
+                      __FILE__ + ":" + std::to_string(__LINE__));                             \
+      return 3;                                                                               \
+    }                                                                                         \
+  } while (0)

@@ -1,0 +1,40 @@
+// rlmd_gemm.h — internal GEMM launch interface (see gemm.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rlmd_abi.h"
+
+#define RLMD_GEMM_MAX_GROUPS 2
+
+namespace rlmd {
+
+enum { GEMM_FWD = 0, GEMM_BWD_X = 1, GEMM_BWD_W = 2 };
+
+// Output C is [M, N] (BWD_W: the weight-gradient [out, in] with M = out, N = in,
+// K = batch).  All pointers f32 device memory.
+struct GemmProblem {
+  const float* A;
+  int32_t lda;
+  const float* B;
+  int32_t ldb;
+  const float* bias;  // FWD: bias[N]
+  float* C;
+  int32_t ldc;
+  const float* mask;  // BWD_X: ReLU mask source [M, N] (element > 0 keeps)
+  int32_t ldm;
+  float* bias_grad;   // BWD_W: bias gradient [M]
+};
+
+struct GemmShape {
+  int32_t M, N, K, relu;
+};
+
+struct GemmBatch {
+  GemmShape shape;
+  GemmProblem prob[RLMD_GEMM_MAX_GROUPS];
+};
+
+int gemm_launch(int prec, int mode, const GemmBatch& b, int groups, hipStream_t stream);
+
+}  // namespace rlmd

@@ -1,0 +1,162 @@
+"""Batched MI355X environments behind the reference's env interface.
+
+``VecEnv`` steps N independent lanes of one reference env class per launch
+(rlmd_env_step / rlmd_env_reset of librlmd_amd.so).  The reference-named
+classes (``Coin_InvA`` ... ``Dice_SH_InvC``, ``Market_InvA_D1`` ...) keep the
+Gym-style single-env API of envs/*_envs.py — ``reset()``, ``step(action)``
+returning ``(next_state, reward, [done, learn_done], risk)``, plus
+``observation_space`` / ``action_space`` / ``reward_range`` — on one lane of
+the same kernels, so reference drivers can swap them in.
+"""
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import check, ptr, stream_ptr
+
+FAMILY = {"coin": _abi.COIN, "dice": _abi.DICE, "gbm": _abi.GBM, "dice_sh": _abi.DICE_SH,
+          "market": _abi.MARKET}
+INVESTOR = {"A": _abi.INV_A, "B": _abi.INV_B, "C": _abi.INV_C, "INSURED": _abi.INV_INSURED}
+MAX_VALUE = {_abi.COIN: 1e18, _abi.DICE: 1e18, _abi.GBM: 1e18, _abi.DICE_SH: 1e18, _abi.MARKET: 1e34}
+MIN_REWARD = {_abi.COIN: 1e-3, _abi.DICE: 1e-3, _abi.GBM: 1e-3, _abi.DICE_SH: 1e-6, _abi.MARKET: 1e-3}
+MAX_ABS_ACTION = 0.99
+
+
+class VecEnv:
+    """N lanes of one reference env class, stepped by one HIP kernel launch."""
+
+    def __init__(self, family, investor, n_lanes, n_gambles=1, seed=0, prices=None, obs_days=1,
+                 time_length=0, action_days=1, shuffle_days=1, sample_days=0, device="cuda:0"):
+        self.family = FAMILY[family] if isinstance(family, str) else family
+        self.investor = INVESTOR[investor] if isinstance(investor, str) else investor
+        self.n_lanes, self.n_gambles, self.device = n_lanes, n_gambles, torch.device(device)
+        cfg = _abi.EnvCfg(self.family, self.investor, n_lanes, n_gambles, obs_days, time_length,
+                          action_days, shuffle_days, sample_days, 0, seed)
+        self._prices = None
+        n_days = 0
+        pp = None
+        if prices is not None:
+            self._prices = np.ascontiguousarray(prices, dtype=np.float64)
+            n_days = self._prices.shape[0]
+            pp = self._prices.ctypes.data_as(C.c_void_p)
+        h = C.c_void_p()
+        check(_abi.lib().rlmd_env_create(C.byref(cfg), pp, n_days, C.byref(h)))
+        self.h = h
+        S, A, R, D = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+        check(_abi.lib().rlmd_env_dims(h, C.byref(S), C.byref(A), C.byref(R), C.byref(D)))
+        self.state_dim, self.action_dim, self.risk_dim, self.draw_dim = S.value, A.value, R.value, D.value
+        dev = self.device
+        self.next_state = torch.empty(n_lanes, self.state_dim, dtype=torch.float64, device=dev)
+        self.reward = torch.empty(n_lanes, dtype=torch.float64, device=dev)
+        self.done = torch.empty(n_lanes, 2, dtype=torch.uint8, device=dev)
+        self.risk = torch.empty(n_lanes, self.risk_dim, dtype=torch.float64, device=dev)
+        self.state = torch.empty(n_lanes, self.state_dim, dtype=torch.float64, device=dev)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and _abi._LIB is not None:
+            _abi.lib().rlmd_env_destroy(h)
+            self.h = None
+
+    def reset(self, mask=None):
+        """Reset lanes (mask: bool/uint8 [N] on device, None = all); returns state f64 [N, S]."""
+        m = None if mask is None else mask.to(torch.uint8).contiguous()
+        check(_abi.lib().rlmd_env_reset(self.h, ptr(m), ptr(self.state), stream_ptr()))
+        return self.state
+
+    def step(self, actions, draws=None, risk=True):
+        """actions f32 [N, A] (device); draws f64 [N, D] to inject (None: Philox)."""
+        a = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        assert a.shape == (self.n_lanes, self.action_dim), a.shape
+        d = None
+        if draws is not None:
+            d = draws.to(device=self.device, dtype=torch.float64).contiguous()
+            assert d.shape == (self.n_lanes, self.draw_dim), d.shape
+        check(_abi.lib().rlmd_env_step(self.h, ptr(a), ptr(d), ptr(self.next_state), ptr(self.reward),
+                                       ptr(self.done), ptr(self.risk) if risk else None, stream_ptr()))
+        return self.next_state, self.reward, self.done, self.risk
+
+    def lane_state(self):
+        w = np.empty(self.n_lanes, dtype=np.float64)
+        t = np.empty(self.n_lanes, dtype=np.int32)
+        check(_abi.lib().rlmd_env_lane_state(self.h, w.ctypes.data_as(C.c_void_p), t.ctypes.data_as(C.c_void_p)))
+        return w, t
+
+
+# ----------------------------------------------------------------------------
+# Reference-named single-env classes (Gym interface of envs/*_envs.py)
+# ----------------------------------------------------------------------------
+class Box:
+    """gym.spaces.Box subset used by the reference drivers."""
+
+    def __init__(self, low, high, shape, dtype=np.float64):
+        self.shape = tuple(shape)
+        self.dtype = np.dtype(dtype)
+        self.low = np.full(self.shape, low, dtype=self.dtype)
+        self.high = np.full(self.shape, high, dtype=self.dtype)
+
+    def sample(self):
+        return np.random.uniform(self.low, self.high).astype(self.dtype)
+
+
+class _SingleEnv:
+    family = None
+    investor = None
+
+    def __init__(self, n_gambles=1, device="cuda:0", seed=None, **kw):
+        seed = int(np.random.randint(0, 2**31)) if seed is None else seed
+        self._v = VecEnv(self.family, self.investor, 1, n_gambles, seed=seed, device=device, **kw)
+        self.n_gambles = n_gambles
+        self.reward_range = (MIN_REWARD[self._v.family], np.inf)
+        self.observation_space = Box(-np.inf, np.inf, (self._v.state_dim,))
+        self.action_space = Box(-MAX_ABS_ACTION, MAX_ABS_ACTION, (self._v.action_dim,))
+
+    def reset(self):
+        return self._v.reset()[0].cpu().numpy().copy()
+
+    def step(self, action):
+        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, -1))
+        ns, r, d, risk = self._v.step(a)
+        d = d[0].cpu().numpy()
+        return (ns[0].cpu().numpy().copy(), np.float64(r[0].item()), [bool(d[0]), bool(d[1])],
+                risk[0].cpu().numpy().copy())
+
+
+def _make(name, fam, inv, sh=False):
+    if sh:
+        def __init__(self, device="cuda:0", seed=None):
+            _SingleEnv.__init__(self, 1, device=device, seed=seed)
+    else:
+        def __init__(self, n_gambles=1, device="cuda:0", seed=None):
+            _SingleEnv.__init__(self, n_gambles, device=device, seed=seed)
+    return type(name, (_SingleEnv,), {"family": fam, "investor": inv, "__init__": __init__})
+
+
+_CLASSES = {}
+for _p, _f in (("Coin", "coin"), ("Dice", "dice"), ("GBM", "gbm")):
+    for _i in "ABC":
+        _CLASSES[f"{_p}_Inv{_i}"] = _make(f"{_p}_Inv{_i}", _f, _i)
+for _i, _inv in (("INSURED", "INSURED"), ("InvA", "A"), ("InvB", "B"), ("InvC", "C")):
+    _CLASSES[f"Dice_SH_{_i}"] = _make(f"Dice_SH_{_i}", "dice_sh", _inv, sh=True)
+globals().update(_CLASSES)
+
+
+class _MarketEnv(_SingleEnv):
+    """Market_Inv{A,B,C}_{D1,Dx}(n_assets, time_length, obs_days): the price
+    window is supplied at construction (the driver's shuffled extract)."""
+
+    def __init__(self, n_assets, time_length, obs_days, prices, device="cuda:0", seed=None):
+        ext = np.ascontiguousarray(prices, dtype=np.float64)
+        _SingleEnv.__init__(self, n_assets, device=device, seed=seed, prices=ext,
+                            obs_days=obs_days, time_length=time_length, sample_days=ext.shape[0] - 1)
+
+
+for _i in "ABC":
+    for _d in ("D1", "Dx"):
+        _CLASSES[f"Market_Inv{_i}_{_d}"] = type(f"Market_Inv{_i}_{_d}", (_MarketEnv,),
+                                                {"family": "market", "investor": _i})
+globals().update(_CLASSES)
+
+ENV_CLASSES = dict(_CLASSES)

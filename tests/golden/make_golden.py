@@ -1,0 +1,559 @@
+"""Generate golden vectors from the reference (majidsina/rlmd) itself.
+
+Runs ONLY in the build container, where /root/reference exists, via the import
+shims of ``_refshim.py``.  The outputs are small ``.npz``
+fixtures committed under ``tests/golden/``; the reference never travels.
+
+Every fixture is data: inputs we chose (actions, injected random draws, batch
+indices, network initial parameters) and the outputs the REFERENCE computed on
+them.  Random draws are injected by replacing the ``np`` / distribution
+attributes the reference calls with proxies that hand out our draws through
+the same formulae the reference's libraries use (verified against a real
+``numpy.random.RandomState`` in ``rng_choice_kat``).
+
+Usage (from anywhere):  python tests/golden/make_golden.py
+"""
+import os
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _refshim  # noqa: E402
+
+_refshim.install()
+
+import torch as T  # noqa: E402
+
+np.set_printoptions(precision=17)
+
+
+# ----------------------------------------------------------------------------
+# draw-injection proxies
+# ----------------------------------------------------------------------------
+class _InjectedRandom:
+    """Stand-in for ``np.random`` inside a reference module.
+
+    ``normal(loc, scale, size)`` returns ``loc + scale * z`` with z injected
+    (NumPy's legacy ``normal`` is ``loc + scale * gauss``); ``choice(a, p=p)``
+    returns ``a[searchsorted(cumsum(p)/cumsum(p)[-1], u, 'right')]`` with u
+    injected (NumPy legacy ``RandomState.choice``; pinned by rng_choice_kat).
+    """
+
+    def __init__(self):
+        self.queue = []
+        self.log = []
+
+    def push(self, vals):
+        self.queue.extend(list(np.atleast_1d(vals)))
+
+    def _take(self, size):
+        n = 1 if size is None else int(np.prod(size))
+        out = np.array(self.queue[:n], dtype=np.float64)
+        assert out.size == n, "ran out of injected draws"
+        del self.queue[:n]
+        self.log.extend(out.tolist())
+        return out if size is not None else out[0]
+
+    def normal(self, loc=0.0, scale=1.0, size=None):
+        z = self._take(size)
+        return loc + scale * z
+
+    def choice(self, a, size=None, replace=True, p=None):
+        u = self._take(size)
+        p = np.asarray(p, dtype=np.float64)
+        cdf = p.cumsum()
+        cdf /= cdf[-1]
+        idx = cdf.searchsorted(u, side="right")
+        return np.asarray(a)[idx]
+
+    def randint(self, low, high=None, size=None):
+        v = self._take(size)
+        return v.astype(np.int64) if size is not None else int(v)
+
+    def permutation(self, x):
+        raise NotImplementedError
+
+
+class _NpProxy(types.ModuleType):
+    """``np`` replacement: numpy everywhere except ``random`` (+ ``array`` fix)."""
+
+    def __init__(self, rnd, flatten_array=False):
+        super().__init__("np_proxy")
+        self.random = rnd
+        self._flatten = flatten_array
+
+    def __getattr__(self, name):
+        return getattr(np, name)
+
+    def array(self, obj, *args, **kw):
+        # Dice_SH_INSURED builds a risk list holding a size-1 ndarray, which
+        # NumPy 2 rejects; flatten size-1 elements as NumPy 1.22 did.
+        if self._flatten and isinstance(obj, list):
+            obj = [o.reshape(()) if isinstance(o, np.ndarray) and o.size == 1 else o for o in obj]
+        return np.array(obj, *args, **kw)
+
+
+# ----------------------------------------------------------------------------
+# F0: RNG known-answer pins for the restatement's draw conventions
+# ----------------------------------------------------------------------------
+def rng_choice_kat():
+    """Pin legacy ``choice(a, p)`` == a[searchsorted(cumsum(p), random_sample(), 'right')]."""
+    out = {}
+    for name, a, p in (
+        ("coin", [0.5, -0.4], [0.5, 0.5]),
+        ("dice", [0.5, -0.5, 0.05], [1 / 6, 1 / 6, 1 - 2 / 6]),
+    ):
+        rs = np.random.RandomState(1234)
+        u = rs.random_sample(4096)
+        rs = np.random.RandomState(1234)
+        ch = np.array([rs.choice(a, p=p) for _ in range(4096)])
+        out[name + "_u"] = u
+        out[name + "_choice"] = ch
+    return out
+
+
+# ----------------------------------------------------------------------------
+# F1: env step traces
+# ----------------------------------------------------------------------------
+ENV_SPECS = []
+for fam, mod in (("coin", "coin_flip_envs"), ("dice", "dice_roll_envs"), ("gbm", "gbm_envs")):
+    pref = {"coin": "Coin", "dice": "Dice", "gbm": "GBM"}[fam]
+    for inv in ("A", "B", "C"):
+        for n in (1, 5):
+            ENV_SPECS.append((fam, mod, f"{pref}_Inv{inv}", inv, n))
+for inv in ("INSURED", "InvA", "InvB", "InvC"):
+    ENV_SPECS.append(("sh", "dice_roll_sh_envs", f"Dice_SH_{inv}", inv, 1))
+
+
+def _action_schedule(rng, n_steps, a_dim):
+    """f32 actions in [-0.99, 0.99] with the edge cases the done logic keys on."""
+    acts = rng.uniform(-0.99, 0.99, size=(n_steps, a_dim)).astype(np.float32)
+    # sprinkle edges: exact +-0.99 (lev_max), 0 (lev_min), tiny, and long runs of
+    # large leverage so wealth walks to its floor / ceiling.
+    for t in range(n_steps):
+        k = t % 37
+        if k == 5:
+            acts[t, :] = np.float32(0.99)
+        elif k == 11:
+            acts[t, :] = np.float32(-0.99)
+        elif k == 17:
+            acts[t, :] = 0.0
+        elif k == 23:
+            acts[t, :] = np.float32(1e-6)
+        elif 25 <= k <= 33:
+            acts[t, :] = np.float32(0.9) * np.sign(acts[t, :] + 1e-3)
+    return acts
+
+
+EDGE_SPECS = [  # all-favourable draws so wealth reaches MAX_VALUE (done_state)
+    ("gbm", "gbm_envs", "GBM_InvA", "A", 1),
+    ("gbm", "gbm_envs", "GBM_InvC", "C", 2),
+    ("coin", "coin_flip_envs", "Coin_InvA", "A", 1),
+    ("coin", "coin_flip_envs", "Coin_InvC", "C", 1),
+    ("dice", "dice_roll_envs", "Dice_InvB", "B", 1),
+    ("sh", "dice_roll_sh_envs", "Dice_SH_InvA", "InvA", 1),
+]
+
+
+def env_traces(n_steps=240, seed=7):
+    import importlib
+
+    out = {}
+    rng = np.random.default_rng(seed)
+    specs = [(s, False) for s in ENV_SPECS] + [(s, True) for s in EDGE_SPECS]
+    for (fam, modname, cls, inv, n), edge in specs:
+        mod = importlib.import_module("envs." + modname)
+        rnd = _InjectedRandom()
+        saved = mod.np
+        mod.np = _NpProxy(rnd, flatten_array=True)
+        try:
+            env = getattr(mod, cls)() if fam == "sh" else getattr(mod, cls)(n)
+            a_dim = env.action_space.shape[0]
+            s_dim = env.observation_space.shape[0]
+            acts = _action_schedule(rng, n_steps, a_dim)
+            n_draw = 1 if fam == "sh" else n
+            if fam == "gbm":
+                draws = rng.standard_normal((n_steps, n_draw))
+                # fat left tail occasionally so MIN_RETURN clipping is exercised
+                draws[::29] -= 8.0
+            else:
+                draws = rng.random((n_steps, n_draw))
+            if edge:
+                acts = np.full((n_steps, a_dim), np.float32(0.7), dtype=np.float32)
+                if fam == "sh":
+                    acts[:, 1:] = np.float32(-0.99)  # no safe haven: pure up-moves
+                draws = np.full((n_steps, n_draw), 3.0 if fam == "gbm" else 0.01)
+            S = np.zeros((n_steps, s_dim))  # state before the step
+            S2 = np.zeros((n_steps, s_dim))
+            R = np.zeros(n_steps)
+            D = np.zeros((n_steps, 2), dtype=np.bool_)
+            risk_dim = None
+            RISK = []
+            state = env.reset().copy()
+            for t in range(n_steps):
+                S[t] = state
+                rnd.push(draws[t])
+                s2, rew, done, risk = env.step(acts[t])
+                S2[t] = s2
+                R[t] = rew
+                D[t] = done
+                RISK.append(np.array(risk, dtype=np.float64).ravel().copy())
+                state = s2.copy()
+                if done[0]:
+                    state = env.reset().copy()
+            risk_dim = RISK[0].size
+            key = f"{cls}_n{n}" + ("_edge" if edge else "")
+            out[key + "/actions"] = acts
+            out[key + "/draws"] = draws
+            out[key + "/state"] = S
+            out[key + "/next_state"] = S2
+            out[key + "/reward"] = R
+            out[key + "/done"] = D
+            out[key + "/risk"] = np.stack(RISK).reshape(n_steps, risk_dim)
+        finally:
+            mod.np = saved
+    return out
+
+
+# ----------------------------------------------------------------------------
+# F2: market slicing / shuffling / observation
+# ----------------------------------------------------------------------------
+def market_fixtures(seed=11):
+    import tools.env_resources as er
+
+    rng = np.random.default_rng(seed)
+    prices = np.load("/root/reference/tools/market_data/stooq_usei.npy")[:600]
+    out = {"prices": prices}
+    # time_slice with injected randint
+    rnd = _InjectedRandom()
+    saved = er.np
+    er.np = _NpProxy(rnd)
+    try:
+        starts = rng.integers(0, 600 - 130, size=4)
+        for i, st in enumerate(starts):
+            rnd.push([st])
+            ext, s_idx = er.time_slice(prices, 100, 1, 130)
+            out[f"slice{i}/start"] = np.int64(s_idx)
+            out[f"slice{i}/extract"] = ext
+    finally:
+        er.np = saved
+
+    # shuffle_data with injected permutations: record the permutation of row
+    # indices each block received (the reference permutes row blocks).
+    perms = []
+
+    class _PermRandom:
+        def permutation(self, x):
+            p = rng.permutation(len(x))
+            perms.append(p)
+            return np.asarray(x)[p]
+
+    er.np = _NpProxy(_PermRandom())
+    try:
+        for i, (L, d) in enumerate(((101, 5), (103, 5), (250, 3), (251, 3))):
+            perms.clear()
+            block = prices[17 : 17 + L]
+            sh = er.shuffle_data(block, d)
+            out[f"shuffle{i}/input"] = block
+            out[f"shuffle{i}/interval"] = np.int64(d)
+            out[f"shuffle{i}/perms"] = np.concatenate(perms).astype(np.int64)
+            out[f"shuffle{i}/output"] = sh
+    finally:
+        er.np = saved
+
+    # observed_market_state
+    ext = prices[40:140]
+    for d in (1, 5):
+        obs = np.stack([er.observed_market_state(ext, t, 1, d) for t in range(0, 90)])
+        out[f"obs_d{d}"] = obs
+    out["obs_extract"] = ext
+    return out
+
+
+def market_env_traces(seed=13):
+    """One D1 and one Dx episode per investor on stooq_usei (3 assets)."""
+    import envs.market_envs as me
+
+    rng = np.random.default_rng(seed)
+    prices = np.load("/root/reference/tools/market_data/stooq_usei.npy")
+    out = {}
+    T_len = 60
+    for dname, d in (("D1", 1), ("Dx", 4)):
+        for inv in ("A", "B", "C"):
+            cls = getattr(me, f"Market_Inv{inv}_{dname}")
+            n = prices.shape[1]
+            env = cls(n, T_len + d - 1, d)
+            a_dim = env.action_space.shape[0]
+            st = int(rng.integers(0, prices.shape[0] - 200))
+            ext = prices[st : st + T_len + d + 5]
+            import tools.env_resources as er
+
+            obs0 = er.observed_market_state(ext, 0, 1, d)
+            state = env.reset(obs0).copy()
+            acts = rng.uniform(-0.99, 0.99, size=(T_len + 5, a_dim)).astype(np.float32)
+            S, S2, R, D, RK = [], [], [], [], []
+            t = 0
+            done = False
+            while not done:
+                t += 1
+                o = er.observed_market_state(ext, t, 1, d)
+                s2, r, dn, risk = env.step(acts[t - 1], o)
+                S.append(state)
+                S2.append(s2.copy())
+                R.append(r)
+                D.append(dn)
+                RK.append(np.array(risk).copy())
+                state = s2.copy()
+                done = dn[0]
+            key = f"Market_Inv{inv}_{dname}"
+            out[key + "/extract"] = ext
+            out[key + "/obs_days"] = np.int64(d)
+            out[key + "/time_length"] = np.int64(T_len + d - 1)
+            out[key + "/actions"] = acts[: len(R)]
+            out[key + "/state"] = np.stack(S)
+            out[key + "/next_state"] = np.stack(S2)
+            out[key + "/reward"] = np.array(R)
+            out[key + "/done"] = np.array(D)
+            out[key + "/risk"] = np.stack(RK)
+    return out
+
+
+# ----------------------------------------------------------------------------
+# F3: critic losses, tail index, side estimators
+# ----------------------------------------------------------------------------
+LOSSES = ["MSE", "HUB", "MAE", "HSC", "CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"]
+
+
+def _zipf(k):
+    zx = (T.ones((k,)) + k).view(-1)
+    for x in range(k):
+        zx[x] = zx[x] / (x + 1)
+    zx = T.log(zx)
+    zx = zx - T.mean(zx)
+    return zx, T.sum(zx**2)
+
+
+def critic_loss_fixtures(seed=3):
+    import tools.critic_loss as cl
+
+    g = T.Generator().manual_seed(seed)
+    out = {}
+    for B, k in ((512, 256), (200, 100)):
+        # fat-tailed targets (Student-t nu=2 via normal/sqrt(chi2/2))
+        base = T.randn(B, 1, generator=g)
+        chi = (T.randn(B, 2, generator=g) ** 2).sum(1, keepdim=True) / 2
+        target = (base / T.sqrt(chi + 1e-3)).float()
+        q1 = (target + 0.3 * T.randn(B, 1, generator=g)).float()
+        q2 = (target + 0.5 * T.randn(B, 1, generator=g)).float()
+        zx, zx2 = _zipf(k)
+        log_noise = T.tensor(1e-6)
+        kern1 = cl.cim_size(q1, target).numpy()
+        kern2 = cl.cim_size(q2, target).numpy()
+        key0 = f"B{B}"
+        out[key0 + "/q1"] = q1.numpy()
+        out[key0 + "/q2"] = q2.numpy()
+        out[key0 + "/target"] = target.numpy()
+        out[key0 + "/k"] = np.int64(k)
+        out[key0 + "/cim1"] = kern1
+        out[key0 + "/cim2"] = kern2
+        for sc in (1.0, 0.37):
+            out[key0 + f"/nagy_s{sc}_1"] = cl.nagy_algo(q1, target, sc).numpy()
+            out[key0 + f"/nagy_s{sc}_2"] = cl.nagy_algo(q2, target, sc).numpy()
+        scale1, scale2 = 0.8, 1.3
+        out[key0 + "/scale1"] = np.float64(scale1)
+        out[key0 + "/scale2"] = np.float64(scale2)
+        for lt in LOSSES:
+            a = q1.clone().requires_grad_(True)
+            b = q2.clone().requires_grad_(True)
+            res = cl.loss_function(a, scale1, float(kern1), b, scale2, float(kern2),
+                                   target, B, k, log_noise, zx, zx2, lt)
+            m1, mn1, mx1, _, al1, m2, mn2, mx2, _, al2 = res
+            (m1 + m2).backward()
+            key = f"{key0}/{lt}"
+            out[key + "/stats"] = np.array(
+                [m1.item(), m2.item(), mn1.item(), mn2.item(), mx1.item(), mx2.item(),
+                 al1.item(), al2.item()], dtype=np.float64)
+            out[key + "/grad1"] = a.grad.numpy().copy()
+            out[key + "/grad2"] = b.grad.numpy().copy()
+    return out
+
+
+def shadow_fixtures():
+    import tools.utils as ut
+
+    alphas = np.linspace(0.05, 0.95, 19)
+    mins = np.linspace(0.01, 2.0, 19)
+    maxs = np.linspace(3.0, 50.0, 19)
+    sh = np.array([ut.shadow_means(a, lo, hi, 1.0, 10.0) for a, lo, hi in zip(alphas, mins, maxs)])
+    # action window
+    acts = np.linspace(-0.99, 0.99, 11)
+    steps = np.array([0, 500, 1000, 1001, 1200, 1500, 1999, 2000])
+    win = np.stack([ut.action_window(acts.copy(), 0.99, -0.99, s, 2000, 1000) for s in steps])
+    return {"alpha": alphas, "min": mins, "max": maxs, "shadow": sh,
+            "aw_actions": acts, "aw_steps": steps, "aw_out": win}
+
+
+# ----------------------------------------------------------------------------
+# F5: learn() steps for SAC and TD3
+# ----------------------------------------------------------------------------
+def _inputs(algo, S, A, hidden, loss_fn="MSE", B=None, k=None):
+    inputs = {
+        "test_agent": True, "ENV_KEY": 14, "env_id": "GOLDEN_n1", "dynamics": "M",
+        "input_dims": (S,), "num_actions": A, "max_action": 0.99, "min_action": -0.99,
+        "algo": algo, "s_dist": "N", "loss_fn": loss_fn, "multi_steps": 1,
+        "n_trials": 1, "trial": 1, "n_cumsteps": 5e4, "buffer": 1e6,
+        "mini_batch_size": B, "actor_percentile": 50, "critic_percentile": 50,
+        "batch_size": {"SAC": k, "TD3": k}, "discount": 0.99, "r_abs_zero": None,
+        "cauchy_scale": 1, "critic_mean_type": "E", "log_noise": 1e-6, "gpu": "cpu",
+        "buffer_gpu": False, "continue": False,
+        "sac_actor_learn_rate": 3e-4, "sac_critic_learn_rate": 3e-4,
+        "sac_temp_learn_rate": 3e-4, "sac_layer_1_units": hidden[0],
+        "sac_layer_2_units": hidden[1], "sac_actor_step_update": 1,
+        "sac_temp_step_update": 1, "sac_target_critic_update": 1,
+        "sac_target_update_rate": 5e-3, "initial_logtemp": 0, "reward_scale": 1,
+        "log_scale_min": -20, "log_scale_max": 2, "reparam_noise": 1e-6,
+        "td3_actor_learn_rate": 1e-3, "td3_critic_learn_rate": 1e-3,
+        "td3_layer_1_units": hidden[0], "td3_layer_2_units": hidden[1],
+        "td3_actor_step_update": 2, "td3_target_actor_update": 2,
+        "td3_target_critic_update": 2, "td3_target_update_rate": 5e-3,
+        "policy_noise": 0.1, "target_policy_noise": 0.2, "target_policy_clip": 0.5,
+    }
+    return inputs
+
+
+def _net_names(algo):
+    return ["actor", "target_actor", "critic_1", "target_critic_1", "critic_2", "target_critic_2"]
+
+
+def learn_fixtures(seed=5):
+    import algos.algo_sac as asac
+    import algos.algo_td3 as atd3
+    import tools.replay as rp
+
+    out = {}
+    cases = [
+        ("SAC", 5, 1, (64, 64), 512, 256, "MSE"),
+        ("SAC", 6, 2, (64, 48), 512, 256, "HUB"),
+        ("TD3", 6, 2, (64, 48), 200, 100, "MSE"),
+        ("TD3", 5, 1, (40, 32), 200, 100, "HSC"),
+    ]
+    n_steps = 4
+    for ci, (algo, S, A, hid, B, k, lt) in enumerate(cases):
+        T.manual_seed(seed + ci)
+        rng = np.random.default_rng(seed + ci)
+        inputs = _inputs(algo, S, A, hid, lt, B, k)
+        agent = asac.Agent_sac(inputs) if algo == "SAC" else atd3.Agent_td3(inputs)
+        nets = _net_names(algo)
+        init = {}
+        for nm in nets:
+            for pn, p in getattr(agent, nm).named_parameters():
+                init[f"{nm}.{pn}"] = p.detach().numpy().copy()
+        # replay contents: small (MAX_VALUE-normalised) states like the envs make
+        M = B + 37
+        st = (rng.random((M, S)) * 3e-14).astype(np.float64)
+        ac = rng.uniform(-0.99, 0.99, (M, A)).astype(np.float32)
+        rw = rng.uniform(0.5, 1.5, M)
+        st2 = (rng.random((M, S)) * 3e-14).astype(np.float64)
+        dn = rng.random(M) < 0.1
+        for i in range(M):
+            agent.store_transistion(st[i], ac[i], rw[i], st2[i], bool(dn[i]))
+        # inject replay indices, and policy noise
+        idx_q = []
+        rnd = _InjectedRandom()
+
+        class _IdxRandom:
+            def choice(self, a, size=None, replace=True, p=None):
+                return idx_q.pop(0)
+
+        saved_np = rp.np
+        rp.np = _NpProxy(_IdxRandom())
+        eps_q = []
+        from torch.distributions import Normal
+
+        saved_rs = Normal.rsample
+
+        def _rsample(self, sample_shape=T.Size()):
+            e = eps_q.pop(0)
+            assert tuple(e.shape) == tuple(self.loc.shape)
+            return self.loc + e * self.scale
+
+        Normal.rsample = _rsample
+        saved_normal_ = T.Tensor.normal_
+
+        def _normal_(self, mean=0.0, std=1.0, generator=None):
+            e = eps_q.pop(0)
+            assert tuple(e.shape) == tuple(self.shape)
+            with T.no_grad():
+                self.copy_(mean + std * e)
+            return self
+
+        T.Tensor.normal_ = _normal_
+        key = f"case{ci}"
+        try:
+            for s in range(n_steps):
+                idx = rng.choice(M, size=B, replace=False)
+                idx_q.append(idx)
+                if algo == "SAC":
+                    e1 = T.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+                    e2 = T.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+                    eps_q.extend([e1, e2])
+                    out[f"{key}/step{s}/eps_next"] = e1.numpy()
+                    out[f"{key}/step{s}/eps_cur"] = e2.numpy()
+                else:
+                    e1 = T.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+                    eps_q.append(e1)
+                    out[f"{key}/step{s}/eps_target"] = e1.numpy()
+                out[f"{key}/step{s}/idx"] = idx.astype(np.int64)
+                loss, logtemp, lp = agent.learn()
+                out[f"{key}/step{s}/loss"] = np.array([float(x) for x in loss])
+                out[f"{key}/step{s}/logtemp"] = np.float64(logtemp)
+                out[f"{key}/step{s}/loss_params"] = np.array([float(x) for x in lp])
+                assert not eps_q and not idx_q
+                for nm in nets:
+                    for pn, p in getattr(agent, nm).named_parameters():
+                        out[f"{key}/step{s}/{nm}.{pn}"] = p.detach().numpy().copy()
+        finally:
+            rp.np = saved_np
+            Normal.rsample = saved_rs
+            T.Tensor.normal_ = saved_normal_
+        out[f"{key}/algo"] = np.array(algo)
+        out[f"{key}/loss_fn"] = np.array(lt)
+        out[f"{key}/dims"] = np.array([S, A, hid[0], hid[1], B, k], dtype=np.int64)
+        out[f"{key}/n_steps"] = np.int64(n_steps)
+        for kk, v in init.items():
+            out[f"{key}/init/{kk}"] = v
+        out[f"{key}/replay/state"] = st
+        out[f"{key}/replay/action"] = ac
+        out[f"{key}/replay/reward"] = rw
+        out[f"{key}/replay/next_state"] = st2
+        out[f"{key}/replay/done"] = dn
+    return out
+
+
+def main():
+    work = tempfile.mkdtemp(prefix="rlmd_golden_")
+    os.chdir(work)  # the reference creates ./results/... relative to cwd
+    jobs = {
+        "rng_kat.npz": rng_choice_kat,
+        "env_traces.npz": env_traces,
+        "market.npz": market_fixtures,
+        "market_env.npz": market_env_traces,
+        "critic_loss.npz": critic_loss_fixtures,
+        "shadow.npz": shadow_fixtures,
+        "learn.npz": learn_fixtures,
+    }
+    only = sys.argv[1:]
+    for fn, job in jobs.items():
+        if only and fn not in only:
+            continue
+        data = job()
+        np.savez_compressed(os.path.join(HERE, fn), **data)
+        print("wrote", fn, len(data), "arrays,", os.path.getsize(os.path.join(HERE, fn)), "bytes")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+"""Pin the CPU oracle against vectors produced by the reference itself.
+
+Golden files come from tests/golden/make_golden.py (reference imported in the
+build container).  These run on CPU; they make the oracle trustworthy as the
+checker of the HIP path (tests/test_*_gpu.py).
+"""
+import numpy as np
+import pytest
+
+from oracle import envs as oe
+from oracle import philox as px
+
+ENV_CLASSES = {
+    "Coin": oe.COIN, "Dice": oe.DICE, "GBM": oe.GBM,
+}
+INV = {"InvA": oe.INV_A, "InvB": oe.INV_B, "InvC": oe.INV_C, "INSURED": oe.INV_INSURED}
+
+# The oracle reproduces the reference's NumPy-2 dtype flow (oracle/envs.py);
+# it is bit-exact on these traces today, the tolerance only absorbs libm ulps.
+RTOL = 1e-13
+
+
+def parse_env_key(key):
+    parts = key.split("_")
+    if parts[0] == "Dice" and parts[1] == "SH":
+        return oe.DICE_SH, INV[parts[2]], 1
+    fam = ENV_CLASSES[parts[0]]
+    n = int(parts[2][1:])
+    return fam, INV[parts[1]], n
+
+
+def env_keys(g):
+    return sorted(set(k.split("/")[0] for k in g.files))
+
+
+def test_philox_known_answers():
+    # Random123 kat_vectors, philox4x32 R=10
+    assert [hex(x) for x in px.philox(0, 0, 0, 0, 0)] == ["0x6627e8d5", "0xe169c58d", "0xbc57ac4c", "0x9b00dbd8"]
+    m = 0xFFFFFFFF
+    assert [hex(x) for x in px.philox((m << 32) | m, m, m, m, m)] == [
+        "0x408f276d", "0x41c83b0e", "0xa20bc7c6", "0x6d5451fd"]
+    key = 0xA4093822 | (0x299F31D0 << 32)
+    assert [hex(x) for x in px.philox(key, 0x243F6A88, 0x85A308D3, 0x13198A2E, 0x03707344)] == [
+        "0xd16cfe09", "0x94fdcceb", "0x5001e420", "0x24126ea1"]
+
+
+def test_choice_convention_matches_numpy_legacy(golden):
+    g = golden("rng_kat.npz")
+    for name, vals, p in (("coin", oe.COIN_VALS, oe.COIN_P), ("dice", oe.DICE_VALS, oe.DICE_P)):
+        idx = oe.choice_index(g[name + "_u"], p)
+        np.testing.assert_array_equal(vals[idx], g[name + "_choice"])
+
+
+def test_uniform_is_numpy_random_sample_construction():
+    # 53-bit construction: (a>>5)*2^26 + (b>>6) over 2^53, as RandomState.random_sample
+    a = np.array([0xFFFFFFFF, 0, 0x80000000], dtype=np.uint32)
+    b = np.array([0xFFFFFFFF, 0, 0], dtype=np.uint32)
+    u = px.u01(a, b)
+    assert u[0] < 1.0 and u[1] == 0.0 and u[2] == 0.5
+
+
+@pytest.mark.parametrize("key", env_keys(np.load(
+    __import__("os").path.join(__import__("os").path.dirname(__file__), "golden", "env_traces.npz"))))
+def test_env_trace_matches_reference(golden, key):
+    g = golden("env_traces.npz")
+    fam, inv, n = parse_env_key(key)
+    env = oe.OracleVecEnv(fam, inv, 1, n)
+    acts, draws = g[key + "/actions"], g[key + "/draws"]
+    S, S2, R, D, RK = (g[key + "/" + x] for x in ("state", "next_state", "reward", "done", "risk"))
+    state = env.reset()
+    for t in range(acts.shape[0]):
+        np.testing.assert_allclose(state[0], S[t], rtol=RTOL, atol=0, err_msg=f"{key} t={t} state")
+        ns, rew, dn, risk = env.step(acts[t:t + 1], draws[t:t + 1])
+        np.testing.assert_allclose(ns[0], S2[t], rtol=RTOL, atol=0, err_msg=f"{key} t={t}")
+        np.testing.assert_allclose(rew[0], R[t], rtol=RTOL, err_msg=f"{key} t={t} reward")
+        np.testing.assert_array_equal(dn[0], D[t], err_msg=f"{key} t={t} done")
+        np.testing.assert_allclose(risk[0], RK[t], rtol=RTOL, equal_nan=True, err_msg=f"{key} t={t} risk")
+        state = ns
+        if dn[0, 0]:
+            state = env.reset()
+
+
+# ---------------------------------------------------------------------------
+# market slicing / shuffling / observation (tools/env_resources.py:203-291)
+# ---------------------------------------------------------------------------
+def test_market_time_slice(golden):
+    g = golden("market.npz")
+    prices = g["prices"]
+    for i in range(4):
+        st = int(g[f"slice{i}/start"])
+        # time_slice(prices, extract_days=100, action_days=1, sample_days=130)
+        np.testing.assert_array_equal(prices[st: st + 100 * 1 + 1], g[f"slice{i}/extract"])
+
+
+def test_market_shuffle_rows(golden):
+    g = golden("market.npz")
+    for i in range(4):
+        x = g[f"shuffle{i}/input"]
+        d = int(g[f"shuffle{i}/interval"])
+        flat = g[f"shuffle{i}/perms"]
+        L = x.shape[0]
+        sizes = [d] * (L // d) + ([L % d] if L % d else [])
+        perms, o = [], 0
+        for s in sizes:
+            perms.append(flat[o:o + s])
+            o += s
+        rows = oe.shuffle_rows(L, d, perms)
+        np.testing.assert_array_equal(x[rows], g[f"shuffle{i}/output"])
+
+
+def test_market_observed_state(golden):
+    g = golden("market.npz")
+    ext = g["obs_extract"]
+    n = ext.shape[1]
+    for d in (1, 5):
+        obs = g[f"obs_d{d}"]
+        for t in range(obs.shape[0]):
+            rows, assets = oe.observed_rows(t, 1, d, n)
+            np.testing.assert_array_equal(ext[rows, assets], obs[t])
+
+
+@pytest.mark.parametrize("key", ["Market_Inv%s_%s" % (i, d) for i in "ABC" for d in ("D1", "Dx")])
+def test_market_env_episode_matches_reference(golden, key):
+    g = golden("market_env.npz")
+    ext = g[key + "/extract"]
+    d = int(g[key + "/obs_days"])
+    tl = int(g[key + "/time_length"])
+    inv = {"A": oe.INV_A, "B": oe.INV_B, "C": oe.INV_C}[key[10]]
+    # the extract is the episode's window: no shuffle, start fixed at 0
+    env = oe.OracleVecEnv(oe.MARKET, inv, 1, ext.shape[1], prices=ext, obs_days=d,
+                          time_length=tl, shuffle_days=1, sample_days=ext.shape[0] - 1)
+    acts = g[key + "/actions"]
+    state = env.reset()
+    for t in range(acts.shape[0]):
+        np.testing.assert_allclose(state[0], g[key + "/state"][t], rtol=RTOL)
+        ns, r, dn, risk = env.step(acts[t:t + 1])
+        np.testing.assert_allclose(ns[0], g[key + "/next_state"][t], rtol=RTOL, err_msg=f"t={t}")
+        np.testing.assert_allclose(r[0], g[key + "/reward"][t], rtol=RTOL)
+        np.testing.assert_array_equal(dn[0], g[key + "/done"][t])
+        np.testing.assert_allclose(risk[0], g[key + "/risk"][t], rtol=RTOL, equal_nan=True)
+        state = ns
+    assert g[key + "/done"][-1][0]  # the episode ran to its done flag
