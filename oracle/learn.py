@@ -1,0 +1,292 @@
+"""SAC / TD3 learn() restated in PyTorch-CPU fp32 — TEST INFRASTRUCTURE.
+
+(see oracle/__init__.py).  Restates majidsina/rlmd:
+  SAC  algos/algo_sac.py:300-367 (_multi_step_target), :369-595 (learn), :597-615 (Polyak)
+       algos/networks_sac.py:101-178 (forward, stochastic_uv_gaussian), :346-362 (critic)
+  TD3  algos/algo_td3.py:302-361, :363-531, :533-563; algos/networks_td3.py:76-91, :152-168
+  losses tools/critic_loss.py:26-453 (per-sample losses, top-k, aggregator_fast, zipf_plot,
+       cim_size, nagy_algo)
+  Adam torch.optim.Adam defaults (the reference's optimiser), written out here.
+Parameters live in one flat f32 tensor per role in the same layout as
+librlmd_amd.so: trainable [actor | critic_1 | critic_2], targets alike.
+Random draws (mini-batch, policy noise) are injected, as in the GPU parity hook.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+LOSSES = ["MSE", "HUB", "MAE", "HSC", "CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"]
+
+
+def net_layout(inp, h1, h2, out, heads):
+    """[(name, shape)] in torch nn.Linear parameter order; heads = head layer names."""
+    lay = [("fc1.weight", (h1, inp)), ("fc1.bias", (h1,)), ("fc2.weight", (h2, h1)), ("fc2.bias", (h2,))]
+    for hd in heads:
+        lay += [(hd + ".weight", (out, h2)), (hd + ".bias", (out,))]
+    return lay
+
+
+def layout(algo, S, A, h1, h2):
+    """{net: [(name, shape, offset)]}, total size; nets actor, critic_1, critic_2."""
+    nets = {"actor": net_layout(S, h1, h2, A, ("pi", "log_scale") if algo == "SAC" else ("mu",)),
+            "critic_1": net_layout(S + A, h1, h2, 1, ("q_value",)),
+            "critic_2": net_layout(S + A, h1, h2, 1, ("q_value",))}
+    out, off = {}, 0
+    for nm, lay in nets.items():
+        out[nm] = []
+        for pn, shp in lay:
+            out[nm].append((pn, shp, off))
+            off += int(np.prod(shp))
+    return out, off
+
+
+def views(flat, lay):
+    return {nm: {pn: flat[o:o + int(np.prod(shp))].view(shp) for pn, shp, o in entries}
+            for nm, entries in lay.items()}
+
+
+def flatten(state_dicts, lay, total):
+    """state_dicts: {net: {param_name: array}} -> flat f32 numpy."""
+    out = np.zeros(total, dtype=np.float32)
+    for nm, entries in lay.items():
+        for pn, shp, o in entries:
+            out[o:o + int(np.prod(shp))] = np.asarray(state_dicts[nm][pn], dtype=np.float32).ravel()
+    return out
+
+
+def mlp(p, x, head):
+    h = F.relu(F.linear(x, p["fc1.weight"], p["fc1.bias"]))
+    h = F.relu(F.linear(h, p["fc2.weight"], p["fc2.bias"]))
+    return h, F.linear(h, p[head + ".weight"], p[head + ".bias"])
+
+
+def zipf_axis(k):
+    zx = (torch.ones(k) + k).view(-1)
+    zx = zx / torch.arange(1, k + 1, dtype=torch.float32)
+    zx = torch.log(zx)
+    zx = zx - torch.mean(zx)
+    return zx, torch.sum(zx**2)
+
+
+def per_sample_loss(lt, est, tgt, scale, kernel):
+    d = tgt - est
+    if lt == "MSE":
+        return d**2
+    if lt in ("MSE2", "MSE4", "MSE6"):
+        return d ** (2 + int(lt[3:]))
+    if lt == "MAE":
+        return torch.abs(d)
+    if lt == "HUB":
+        a = torch.abs(d)
+        return torch.where(a < 1, 0.5 * a**2, a - 0.5)
+    if lt == "HSC":
+        return torch.sqrt(1 + d**2) - 1
+    if lt in ("CAU", "TCAU"):
+        return torch.log(1 + (d / scale) ** 2)
+    if lt == "CIM":
+        return 1 - torch.exp(-(d**2) / (2 * kernel**2)) / math.sqrt(2 * math.pi * kernel)
+    raise ValueError(lt)
+
+
+def truncate(x):
+    """3-sigma rejection to zero (critic_loss.py:26-50)."""
+    sigma, mean = torch.std_mean(x, unbiased=False)
+    return torch.where(torch.abs(x - mean) > 3 * sigma, x - x, x)
+
+
+def critic_losses(q1, q2, y, B, k, lt, scale, kern, zx, zx2, log_noise):
+    """loss_function + aggregator_fast: (mean, min, max, alpha) per critic."""
+    if lt == "TCAU":
+        e1, t1 = truncate(q1), truncate(y)
+        e2, t2 = truncate(q2), truncate(y)
+    else:
+        e1, t1, e2, t2 = q1, y, q2, y
+    l1 = per_sample_loss(lt, e1, t1, scale[0], kern[0]).view(-1)
+    l2 = per_sample_loss(lt, e2, t2, scale[1], kern[1]).view(-1)
+    if B > k:
+        order = torch.argsort((l1 + l2).detach(), descending=True, stable=True)[:k]
+        l1, l2 = l1[order], l2[order]
+    out = []
+    for l in (l1, l2):
+        ls = torch.sort(l.detach(), descending=True)[0]
+        lg = torch.log(ls + log_noise)
+        alpha = 1 / (torch.sum(zx * (lg - torch.mean(lg))) / zx2)
+        out.append((torch.mean(l), torch.min(l), torch.max(l), alpha))
+    return out
+
+
+def cim_size(q, y):
+    return torch.std(((y - q) ** 2).detach(), unbiased=False)
+
+
+def nagy(q, y, scale):
+    arg = ((y - q).detach() / scale) ** 2
+    inv = 1 / torch.mean(1 / (1 + arg))
+    return float(scale * torch.sqrt(inv - 1)) if inv > 1 else float(scale)
+
+
+class Adam:
+    """torch.optim.Adam(lr) single-tensor update (betas .9/.999, eps 1e-8)."""
+
+    def __init__(self, n, lr):
+        self.m = torch.zeros(n)
+        self.v = torch.zeros(n)
+        self.t = 0
+        self.lr = lr
+
+    def step(self, p, g):
+        self.t += 1
+        self.m.lerp_(g, 1 - 0.9)
+        self.v.mul_(0.999).addcmul_(g, g, value=1 - 0.999)
+        bc1 = 1 - 0.9**self.t
+        bc2 = 1 - 0.999**self.t
+        denom = (self.v.sqrt() / math.sqrt(bc2)).add_(1e-8)
+        p.addcdiv_(self.m, denom, value=-self.lr / bc1)
+
+
+class OracleLearner:
+    def __init__(self, algo, S, A, h1, h2, B, k, loss_type, params, targets, *, gamma=0.99,
+                 tau=5e-3, lr_actor=None, lr_critic=None, lr_temp=3e-4, reward_scale=1.0,
+                 max_action=0.99, ls_min=-20.0, ls_max=2.0, reparam_noise=1e-6, log_noise=1e-6,
+                 cauchy=1.0, logtemp=0.0, policy_noise=0.1, target_noise=0.2, target_clip=0.5,
+                 actor_interval=None, target_critic_update=None, target_actor_update=2,
+                 temp_interval=1, actor_topk=True):
+        sac = algo == "SAC"
+        self.algo, self.S, self.A, self.B, self.k, self.lt = algo, S, A, B, k, loss_type
+        self.lay, self.n = layout(algo, S, A, h1, h2)
+        self.P = torch.tensor(params, dtype=torch.float32).clone()
+        self.T = torch.tensor(targets, dtype=torch.float32).clone()
+        self.gamma, self.tau, self.reward_scale, self.max_action = gamma, tau, reward_scale, max_action
+        self.ls_min, self.ls_max, self.reparam_noise = ls_min, ls_max, reparam_noise
+        self.log_noise = torch.tensor(log_noise)
+        self.cauchy = [cauchy, cauchy]
+        self.log_alpha = torch.tensor(float(logtemp))
+        self.policy_noise = policy_noise * max_action
+        self.target_noise = target_noise * max_action
+        self.target_clip = target_clip * max_action
+        self.actor_interval = actor_interval or (1 if sac else 2)
+        self.target_critic_update = target_critic_update or (1 if sac else 2)
+        self.target_actor_update = target_actor_update
+        self.temp_interval = temp_interval
+        self.actor_topk = actor_topk
+        lr_a = lr_actor or (3e-4 if sac else 1e-3)
+        lr_c = lr_critic or (3e-4 if sac else 1e-3)
+        a0 = self.lay["actor"][0][2]
+        c0 = self.lay["critic_1"][0][2]
+        self.a_rng = (a0, c0)
+        self.c_rng = (c0, self.n)
+        self.opt_a = Adam(c0 - a0, lr_a)
+        self.opt_c = Adam(self.n - c0, lr_c)
+        self.opt_t = Adam(1, lr_temp)
+        self.zx, self.zx2 = zipf_axis(k)
+        self.cntr = 0
+
+    def nets(self, flat):
+        return views(flat, self.lay)
+
+    def policy(self, p, s, eps, stochastic=True):
+        """SAC stochastic_uv_gaussian / deterministic_policy; TD3 forward."""
+        h, mu = mlp(p, s, "pi" if self.algo == "SAC" else "mu")
+        if self.algo == "TD3":
+            return torch.tanh(mu) * self.max_action, None
+        if not stochastic:
+            return torch.tanh(mu) * self.max_action, None
+        ls = F.linear(h, p["log_scale.weight"], p["log_scale.bias"])
+        ls = torch.clamp(ls, self.ls_min, self.ls_max)
+        scale = ls.exp()
+        u = mu + eps * scale
+        lp = (-((u - mu) ** 2) / (2 * scale**2) - torch.log(scale) - math.log(math.sqrt(2 * math.pi))).sum(1)
+        a = torch.tanh(u) * self.max_action
+        lp = lp - torch.log(1 - (a / self.max_action) ** 2 + self.reparam_noise).sum(1)
+        return a, lp
+
+    def learn(self, s, a, r, s2, done, eps_a, eps_b=None, eff=None):
+        """One learn() on an injected mini-batch; returns (loss[11], logtemp, loss_params[4])."""
+        sac = self.algo == "SAC"
+        s, a, r, s2 = (torch.as_tensor(x, dtype=torch.float32) for x in (s, a, r, s2))
+        done = torch.as_tensor(done, dtype=torch.bool)
+        eff = torch.ones(self.B, dtype=torch.int32) if eff is None else torch.as_tensor(eff)
+        eps_a = torch.as_tensor(eps_a, dtype=torch.float32)
+        B, k = self.B, self.k
+        with torch.no_grad():
+            Pn, Tn = self.nets(self.P), self.nets(self.T)
+            if sac:
+                a2, lp2 = self.policy(Pn["actor"], s2, eps_a)
+            else:
+                noise = (eps_a * self.target_noise).clamp(-self.target_clip, self.target_clip)
+                a2 = (mlp(Tn["actor"], s2, "mu")[1].tanh() * self.max_action + noise).clamp(
+                    -self.max_action, self.max_action)
+            x2 = torch.cat([s2, a2], 1)
+            qt1 = mlp(Tn["critic_1"], x2, "q_value")[1].view(-1)
+            qt2 = mlp(Tn["critic_2"], x2, "q_value")[1].view(-1)
+            qt1[done], qt2[done] = 0.0, 0.0
+            m = torch.min(qt1, qt2)
+            g = self.gamma ** eff.to(torch.float32)
+            if sac:
+                y = self.reward_scale * r + g * m - self.log_alpha.exp() * lp2
+            else:
+                y = r + g * m
+        y = y.view(B, 1)
+        # critics
+        P = self.P.clone().requires_grad_(True)
+        Pn = self.nets(P)
+        x = torch.cat([s, a], 1)
+        q1 = mlp(Pn["critic_1"], x, "q_value")[1]
+        q2 = mlp(Pn["critic_2"], x, "q_value")[1]
+        kern = [float(cim_size(q1, y)), float(cim_size(q2, y))]
+        (m1, mn1, mx1, al1), (m2, mn2, mx2, al2) = critic_losses(
+            q1, q2, y, B, k, self.lt, self.cauchy, kern, self.zx, self.zx2, self.log_noise)
+        closs = 0.5 * (m1 + m2) if sac else m1 + m2
+        gP = torch.autograd.grad(closs, P)[0]
+        c0, c1 = self.c_rng
+        with torch.no_grad():
+            self.opt_c.step(self.P[c0:c1], gP[c0:c1])
+        self.cauchy = [nagy(q1, y, self.cauchy[0]), nagy(q2, y, self.cauchy[1])]
+        self.cntr += 1
+        if self.cntr % self.target_critic_update == 0:
+            with torch.no_grad():
+                self.T[c0:c1] = self.tau * self.P[c0:c1] + (1 - self.tau) * self.T[c0:c1]
+        loss = [m1.item(), m2.item(), mn1.item(), mn2.item(), mx1.item(), mx2.item(), np.nan, np.nan,
+                al1.item(), al2.item(), np.nan]
+        logtemp = float(self.log_alpha) if sac else np.nan
+        lp_out = [self.cauchy[0], self.cauchy[1], kern[0], kern[1]]
+        if self.cntr % self.actor_interval != 0:
+            return loss, logtemp, lp_out
+        # actor
+        P = self.P.clone().requires_grad_(True)
+        Pn = self.nets(P)
+        a0, a1 = self.a_rng
+        if sac:
+            an, lp = self.policy(Pn["actor"], s, torch.as_tensor(eps_b, dtype=torch.float32))
+            xn = torch.cat([s, an], 1)
+            qa = mlp(Pn["critic_1"], xn, "q_value")[1]
+            qb = mlp(Pn["critic_2"], xn, "q_value")[1]
+            v = (torch.min(qa, qb).view(-1) - self.log_alpha.exp() * lp).view(-1)
+            if self.actor_topk:
+                v = v.sort(descending=True)[0][:k]
+        else:
+            an = mlp(Pn["actor"], s, "mu")[1].tanh() * self.max_action
+            v = mlp(Pn["critic_1"], torch.cat([s, an], 1), "q_value")[1].view(-1)
+            if self.actor_topk:
+                v = v.sort(descending=False)[0][:k]
+        aloss = -torch.mean(v)
+        gP = torch.autograd.grad(aloss, P)[0]
+        with torch.no_grad():
+            self.opt_a.step(self.P[a0:a1], gP[a0:a1])
+        loss[-1] = aloss.item()
+        if not sac:
+            if self.cntr % self.target_actor_update == 0:
+                with torch.no_grad():
+                    self.T[a0:a1] = self.tau * self.P[a0:a1] + (1 - self.tau) * self.T[a0:a1]
+            return loss, logtemp, lp_out
+        if self.cntr % self.temp_interval == 0:
+            la = self.log_alpha.clone().requires_grad_(True)
+            tl = torch.mean(-(la.exp() * (lp.detach() + (-self.A))))
+            gl = torch.autograd.grad(tl, la)[0]
+            t = self.log_alpha.view(1).clone()
+            self.opt_t.step(t, gl.view(1))
+            self.log_alpha = t[0].clone()
+            logtemp = float(self.log_alpha)
+        return loss, logtemp, lp_out

@@ -17,7 +17,10 @@ ARCH = os.environ.get("RLMD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["abi.hip", "env.hip", "replay.hip", "gemm.hip", "learn.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-         "-Wno-unused-variable", "-ffp-contract=fast"]
+         "-Wno-unused-variable"]
+# env math must round where NumPy rounds (no FMA contraction); GEMM/learner may fuse
+PER_FILE = {"env.hip": ["-ffp-contract=off"]}
+DEFAULT_EXTRA = ["-ffp-contract=fast"]
 
 
 def _headers():
@@ -28,6 +31,7 @@ def _headers():
 def _stale(obj, src, deps):
     if not os.path.exists(obj):
         return True
+    deps = deps + [os.path.abspath(__file__)]
     t = os.path.getmtime(obj)
     return any(os.path.getmtime(d) > t for d in [src] + deps)
 
@@ -37,7 +41,7 @@ def _compile(src):
     path = os.path.join(CSRC, src)
     if not _stale(obj, path, _headers()):
         return obj, None
-    cmd = [HIPCC, *FLAGS, "-c", path, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *PER_FILE.get(src, DEFAULT_EXTRA), "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"

@@ -1,0 +1,58 @@
+"""Pin the learn() oracle (oracle/learn.py) against the reference's learn().
+
+tests/golden/learn.npz holds, for SAC and TD3 cases, the reference agents'
+initial parameters, replay contents, injected mini-batch indices and policy
+noise, and every net's parameters + the loss / logtemp / loss_params lists
+after each learn() call (tests/golden/make_golden.py:learn_fixtures).
+"""
+import numpy as np
+import pytest
+
+from oracle import learn as ol
+
+NETS = ["actor", "critic_1", "critic_2"]
+TNETS = ["target_actor", "target_critic_1", "target_critic_2"]
+
+
+def case_names(g):
+    return sorted(set(k.split("/")[0] for k in g.files if k.startswith("case")))
+
+
+def sd(g, prefix, net):
+    pre = f"{prefix}/{net}."
+    return {k[len(pre):]: g[k] for k in g.files if k.startswith(pre)}
+
+
+def build(g, c):
+    algo = str(g[c + "/algo"])
+    S, A, h1, h2, B, k = (int(x) for x in g[c + "/dims"])
+    lay, n = ol.layout(algo, S, A, h1, h2)
+    p = ol.flatten({nm: sd(g, c + "/init", nm) for nm in NETS}, lay, n)
+    t = ol.flatten({nm: sd(g, c + "/init", tn) for nm, tn in zip(NETS, TNETS)}, lay, n)
+    return algo, (S, A, h1, h2, B, k), lay, n, p, t
+
+
+@pytest.mark.parametrize("case", ["case0", "case1", "case2", "case3"])
+def test_learn_steps_match_reference(golden, case):
+    g = golden("learn.npz")
+    algo, (S, A, h1, h2, B, k), lay, n, p, t = build(g, case)
+    lt = str(g[case + "/loss_fn"])
+    L = ol.OracleLearner(algo, S, A, h1, h2, B, k, lt, p, t)
+    rep = {x: g[f"{case}/replay/{x}"] for x in ("state", "action", "reward", "next_state", "done")}
+    for s in range(int(g[case + "/n_steps"])):
+        idx = g[f"{case}/step{s}/idx"]
+        if algo == "SAC":
+            ea, eb = g[f"{case}/step{s}/eps_next"], g[f"{case}/step{s}/eps_cur"]
+        else:
+            ea, eb = g[f"{case}/step{s}/eps_target"], None
+        loss, logtemp, lp = L.learn(rep["state"][idx], rep["action"][idx], rep["reward"][idx],
+                                    rep["next_state"][idx], rep["done"][idx], ea, eb)
+        np.testing.assert_allclose(loss, g[f"{case}/step{s}/loss"], rtol=2e-5, atol=1e-7, equal_nan=True,
+                                   err_msg=f"{case} step {s} loss")
+        np.testing.assert_allclose(lp, g[f"{case}/step{s}/loss_params"], rtol=2e-5, atol=1e-7)
+        if algo == "SAC":
+            np.testing.assert_allclose(logtemp, g[f"{case}/step{s}/logtemp"], rtol=1e-5, atol=1e-8)
+        ref_p = ol.flatten({nm: sd(g, f"{case}/step{s}", nm) for nm in NETS}, lay, n)
+        ref_t = ol.flatten({nm: sd(g, f"{case}/step{s}", tn) for nm, tn in zip(NETS, TNETS)}, lay, n)
+        np.testing.assert_allclose(L.P.numpy(), ref_p, rtol=0, atol=2e-6, err_msg=f"{case} step {s} params")
+        np.testing.assert_allclose(L.T.numpy(), ref_t, rtol=0, atol=2e-6, err_msg=f"{case} step {s} targets")
