@@ -187,6 +187,9 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
 int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
 
 /* ------------------------------------------------------------- test hooks */
+/* Copy ring rows (start + i) % capacity, i < n, into caller buffers (nullable). */
+int rlmd_replay_read(rlmd_replay_t rb, int64_t start, int64_t n, float* s_dev, float* a_dev,
+                     float* r_dev, float* s2_dev, uint8_t* done_dev, void* stream);
 /* One MLP-layer GEMM (mode 0 forward y = relu?(A W^T + b), 1 input-gradient
  * C = mask(A W), 2 weight-gradient C = A^T W (+ bias_grad = colsum A)) on
  * caller buffers; the kernel the learner uses for every nn.Linear. */

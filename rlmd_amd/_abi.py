@@ -69,6 +69,7 @@ SIGNATURES = {
     "rlmd_replay_destroy": (C.c_int, [P]),
     "rlmd_replay_insert": (C.c_int, [P, I64, P, P, P, P, P, P]),
     "rlmd_replay_mem_idx": (C.c_int, [P, C.POINTER(I64)]),
+    "rlmd_replay_read": (C.c_int, [P, I64, I64, P, P, P, P, P, P]),
     "rlmd_replay_sample": (C.c_int, [P, I32, U64, U64, P, P, P, P, P, P, P]),
     "rlmd_agent_layout": (C.c_int, [C.POINTER(AgentCfg), C.POINTER(I64), C.POINTER(I64),
                                     C.POINTER(I64), C.POINTER(I64)]),

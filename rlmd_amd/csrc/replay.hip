@@ -147,6 +147,21 @@ __global__ void replay_insert_kernel(rlmd::ReplayView rb, int64_t base, int64_t 
   rb.done[row] = d[i];
 }
 
+__global__ void replay_read_kernel(rlmd::ReplayView rb, int64_t start, int64_t n, float* s, float* a,
+                                   float* r, float* s2, uint8_t* d) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int64_t row = (start + i) % rb.capacity;
+  for (int k = 0; k < rb.S; ++k) {
+    if (s) s[i * rb.S + k] = rb.state[row * rb.S + k];
+    if (s2) s2[i * rb.S + k] = rb.next_state[row * rb.S + k];
+  }
+  for (int k = 0; k < rb.A; ++k)
+    if (a) a[i * rb.A + k] = rb.action[row * rb.A + k];
+  if (r) r[i] = rb.reward[row];
+  if (d) d[i] = rb.done[row];
+}
+
 }  // namespace
 
 namespace rlmd {
@@ -205,6 +220,16 @@ int rlmd_replay_insert(rlmd_replay_t rb, int64_t n, const float* s, const float*
                      (hipStream_t)stream, rb->v, rb->mem_idx, n, s, a, r, s2, d);
   RLMD_LAUNCH_CHECK();
   rb->mem_idx += n;
+  return 0;
+}
+
+int rlmd_replay_read(rlmd_replay_t rb, int64_t start, int64_t n, float* s, float* a, float* r,
+                     float* s2, uint8_t* d, void* stream) {
+  RLMD_CHECK(rb && start >= 0, "bad argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(replay_read_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, rb->v, start, n, s, a, r, s2, d);
+  RLMD_LAUNCH_CHECK();
   return 0;
 }
 

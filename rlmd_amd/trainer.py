@@ -1,0 +1,81 @@
+"""Vectorised training loop: N lanes of one env class + one shared learner.
+
+One ``step()`` is one fused vector step of scripts/rl_multiplicative.py:190-227
+(and scripts/rl_market.py:217-270) over all lanes, in librlmd_amd.so
+(rlmd_train_step): actions (random warm-up draws, or the policy), the
+action_window clip, the env step, the replay insert of (s, a, r, s',
+learn_done), auto-reset of finished lanes, then K learn() updates.
+
+Semantics decisions versus the reference's single stream: warm-up
+and smoothing schedules count vector steps per lane; K updates of batch B per
+vector step (UTD = K / N per env step, reported with every metric); one agent
+shared by all lanes; uniform sampling over all lanes' transitions.
+"""
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import check, ptr, stream_ptr
+from .agent import DeviceAgent, ReplayMemory
+from .envs import VecEnv
+
+# reference defaults (main.py:144-259, rl_multiplicative.py:108-113)
+DEFAULTS = {
+    "SAC": dict(h1=256, h2=256, batch=512, topk=256),
+    "TD3": dict(h1=400, h2=300, batch=200, topk=100),
+}
+
+
+class VecTrainer:
+    def __init__(self, env="gbm", investor="A", n_lanes=65536, n_gambles=1, algo="SAC", loss="MSE",
+                 k_updates=1, replay_capacity=1 << 20, seed=0, warmup_steps=1000,
+                 smoothing_window=2000, precision="bf16", hidden=None, batch=None, topk=None,
+                 prices=None, obs_days=1, time_length=0, shuffle_days=5, sample_days=0,
+                 device="cuda:0", init_seed=None):
+        self.device = torch.device(device)
+        self.env = VecEnv(env, investor, n_lanes, n_gambles, seed=seed, prices=prices, obs_days=obs_days,
+                          time_length=time_length, shuffle_days=shuffle_days, sample_days=sample_days,
+                          device=device)
+        d = DEFAULTS[algo]
+        h1, h2 = hidden or (d["h1"], d["h2"])
+        self.batch = batch or d["batch"]
+        self.topk = topk or d["topk"]
+        S, A = self.env.state_dim, self.env.action_dim
+        self.agent = DeviceAgent(algo, S, A, h1, h2, self.batch, self.topk, loss=loss, precision=precision,
+                                 seed=seed, init_seed=init_seed, device=device)
+        self.replay = ReplayMemory(replay_capacity, S, A, device=device)
+        self.n_lanes, self.k_updates = n_lanes, k_updates
+        self.cfg = _abi.TrainCfg()
+        self.cfg.cum_step = 0
+        self.cfg.warmup_steps = warmup_steps
+        self.cfg.smoothing_window = smoothing_window
+        self.cfg.abs_warmup = 0 if self.env.family == _abi.GBM or self.env.family == _abi.MARKET else 1
+        self.cfg.k_updates = k_updates
+        self.obs = torch.empty(n_lanes, S, dtype=torch.float32, device=self.device)
+        self.actions = torch.zeros(n_lanes, A, dtype=torch.float32, device=self.device)
+        self.ep_stats = torch.zeros(4, dtype=torch.float64, device=self.device)
+        self.stats = torch.full((max(k_updates, 1), 16), float("nan"), dtype=torch.float32, device=self.device)
+        check(_abi.lib().rlmd_train_reset(self.env.h, ptr(self.obs), stream_ptr()))
+
+    @property
+    def cum_step(self):
+        return self.cfg.cum_step
+
+    def step(self, k_updates=None):
+        if k_updates is not None:
+            self.cfg.k_updates = k_updates
+        check(_abi.lib().rlmd_train_step(self.env.h, self.replay.h, self.agent.h, self.cfg, ptr(self.obs),
+                                         ptr(self.actions), ptr(self.ep_stats), ptr(self.stats), stream_ptr()))
+        self.cfg.cum_step += 1
+
+    def run(self, n_steps):
+        for _ in range(n_steps):
+            self.step()
+
+    def last_stats(self):
+        """loss[11] | logtemp | loss_params[4] of the last update (numpy f64)."""
+        return self.stats[max(self.cfg.k_updates, 1) - 1].double().cpu().numpy()
+
+    def episode_stats(self):
+        n, rsum, lsum, _ = self.ep_stats.cpu().numpy()
+        return {"episodes": int(n), "mean_final_reward": rsum / max(n, 1), "mean_length": lsum / max(n, 1)}

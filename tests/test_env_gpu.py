@@ -12,6 +12,10 @@ from tests.test_oracle_golden import env_keys, parse_env_key
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-12
+# Philox-mode GBM: z comes from Box–Muller with device vs glibc log/cos (1 ulp);
+# r = LOG_MEAN + VOL*z cancels near r = 0, so the error is absolute: 1e-16 in
+# return units = 1e-34 in MAX_VALUE-normalised state units.
+ATOL_STATE, ATOL_RISK = 1e-30, 1e-12
 
 
 def _venv(fam, inv, n_lanes, n, **kw):
@@ -65,9 +69,9 @@ def test_philox_lanes_match_oracle(fam, inv, n, dev):
         ns, r, d, risk = (x.cpu().numpy() for x in env.step(torch.from_numpy(a).to(dev)))
         ons, orr, od, orisk = ora.step(a)
         np.testing.assert_array_equal(d.astype(bool), od, err_msg=f"t={t}")
-        np.testing.assert_allclose(ns, ons, rtol=RTOL, err_msg=f"t={t}")
+        np.testing.assert_allclose(ns, ons, rtol=RTOL, atol=ATOL_STATE, err_msg=f"t={t}")
         np.testing.assert_allclose(r, orr, rtol=RTOL)
-        np.testing.assert_allclose(risk, orisk, rtol=RTOL, equal_nan=True)
+        np.testing.assert_allclose(risk, orisk, rtol=RTOL, atol=ATOL_RISK, equal_nan=True)
         mask = od[:, 0]
         if mask.any():
             s_gpu = env.reset(torch.from_numpy(mask).to(dev)).cpu().numpy()

@@ -1,0 +1,127 @@
+"""HIP learn() (SAC / TD3) vs the reference's learn() and the oracle — GPU only.
+
+fp32 mode (exact-f32 MFMA operands): parameters after each update within
+2e-6 absolute of the reference / oracle (Adam steps are ~lr = 3e-4..1e-3, so
+this is < 1 % of one step); loss statistics within 1e-4 relative.
+bf16 mode (bf16 GEMM operands, f32 accumulate, f32 master weights): statistics
+within 3e-2 relative; parameter updates within one Adam step on >= 99 % of
+entries (sign flips of near-zero gradients are expected).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import learn as ol
+from tests.test_oracle_learn import NETS, TNETS, build, sd
+
+pytestmark = pytest.mark.gpu
+
+
+def device_agent(algo, S, A, h1, h2, B, k, loss, init, precision="fp32", **kw):
+    from rlmd_amd.agent import DeviceAgent
+
+    return DeviceAgent(algo, S, A, h1, h2, B, k, loss=loss, precision=precision, init=init, **kw)
+
+
+def golden_init(g, case):
+    out = {}
+    for nm, tn in zip(NETS, TNETS):
+        out[nm] = [torch.from_numpy(v) for v in sd(g, case + "/init", nm).values()]
+        out[tn] = [torch.from_numpy(v) for v in sd(g, case + "/init", tn).values()]
+    return out
+
+
+@pytest.mark.parametrize("case", ["case0", "case1", "case2", "case3"])
+def test_learn_matches_reference_golden(golden, dev, case):
+    g = golden("learn.npz")
+    algo, (S, A, h1, h2, B, k), lay, n, _, _ = build(g, case)
+    lt = str(g[case + "/loss_fn"])
+    ag = device_agent(algo, S, A, h1, h2, B, k, lt, golden_init(g, case))
+    rep = {x: torch.from_numpy(g[f"{case}/replay/{x}"]) for x in ("state", "action", "reward", "next_state", "done")}
+    for s in range(int(g[case + "/n_steps"])):
+        idx = torch.from_numpy(g[f"{case}/step{s}/idx"])
+        if algo == "SAC":
+            ea, eb = (torch.from_numpy(g[f"{case}/step{s}/eps_{x}"]) for x in ("next", "cur"))
+        else:
+            ea, eb = torch.from_numpy(g[f"{case}/step{s}/eps_target"]), None
+        st = ag.learn_batch(rep["state"][idx], rep["action"][idx], rep["reward"][idx], rep["next_state"][idx],
+                            rep["done"][idx], ea, eb).double().cpu().numpy()
+        ref_loss = g[f"{case}/step{s}/loss"]
+        np.testing.assert_allclose(st[:11], ref_loss, rtol=1e-4, atol=1e-6, equal_nan=True, err_msg=f"step {s}")
+        np.testing.assert_allclose(st[12:16], g[f"{case}/step{s}/loss_params"], rtol=1e-4, atol=1e-6)
+        if algo == "SAC":
+            np.testing.assert_allclose(st[11], g[f"{case}/step{s}/logtemp"], rtol=1e-5, atol=1e-7)
+        ref_p = ol.flatten({nm: sd(g, f"{case}/step{s}", nm) for nm in NETS}, lay, n)
+        ref_t = ol.flatten({nm: sd(g, f"{case}/step{s}", tn) for nm, tn in zip(NETS, TNETS)}, lay, n)
+        np.testing.assert_allclose(ag.params.cpu().numpy(), ref_p, rtol=0, atol=2e-6, err_msg=f"step {s} params")
+        np.testing.assert_allclose(ag.target.cpu().numpy(), ref_t, rtol=0, atol=2e-6, err_msg=f"step {s} targets")
+
+
+FULL = [("SAC", 5, 1, 256, 256, 512, 256), ("TD3", 6, 2, 400, 300, 200, 100), ("SAC", 6, 2, 256, 256, 512, 256)]
+
+
+def _random_batch(rng, B, S, A):
+    s = torch.from_numpy((rng.random((B, S)) * 3e-14).astype(np.float32))
+    a = torch.from_numpy(rng.uniform(-0.99, 0.99, (B, A)).astype(np.float32))
+    r = torch.from_numpy(rng.uniform(0.5, 1.5, B).astype(np.float32))
+    s2 = torch.from_numpy((rng.random((B, S)) * 3e-14).astype(np.float32))
+    d = torch.from_numpy(rng.random(B) < 0.1)
+    return s, a, r, s2, d
+
+
+@pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL)
+@pytest.mark.parametrize("loss", ["MSE", "HUB", "MAE", "HSC"])
+def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss):
+    from rlmd_amd.agent import reference_init
+
+    init = reference_init(algo, S, A, h1, h2, seed=11)
+    lay, n = ol.layout(algo, S, A, h1, h2)
+    p = ol.flatten({nm: dict(zip([x[0] for x in lay[nm]], [t.numpy() for t in init[nm]])) for nm in NETS}, lay, n)
+    t = ol.flatten({nm: dict(zip([x[0] for x in lay[nm]], [t.numpy() for t in init[tn]]))
+                    for nm, tn in zip(NETS, TNETS)}, lay, n)
+    ora = ol.OracleLearner(algo, S, A, h1, h2, B, k, loss, p, t)
+    ag = device_agent(algo, S, A, h1, h2, B, k, loss, init)
+    rng = np.random.default_rng(3)
+    for step in range(4):
+        s, a, r, s2, d = _random_batch(rng, B, S, A)
+        ea = torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+        eb = torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+        st = ag.learn_batch(s, a, r, s2, d, ea, eb if algo == "SAC" else None).double().cpu().numpy()
+        loss_o, lt_o, lp_o = ora.learn(s.numpy(), a.numpy(), r.numpy(), s2.numpy(), d.numpy(), ea.numpy(),
+                                       eb.numpy() if algo == "SAC" else None)
+        np.testing.assert_allclose(st[:11], loss_o, rtol=2e-4, atol=1e-6, equal_nan=True, err_msg=f"step {step}")
+        np.testing.assert_allclose(st[12:16], lp_o, rtol=2e-4, atol=1e-6)
+        np.testing.assert_allclose(ag.params.cpu().numpy(), ora.P.numpy(), rtol=0, atol=5e-6, err_msg=f"step {step}")
+        np.testing.assert_allclose(ag.target.cpu().numpy(), ora.T.numpy(), rtol=0, atol=5e-6)
+
+
+@pytest.mark.parametrize("loss", ["CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"])
+def test_remaining_losses_fp32(dev, loss):
+    test_full_size_fp32_matches_oracle(dev, "SAC", 5, 1, 256, 256, 512, 256, loss)
+
+
+@pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL[:2])
+def test_bf16_tracks_oracle(dev, algo, S, A, h1, h2, B, k):
+    from rlmd_amd.agent import reference_init
+
+    init = reference_init(algo, S, A, h1, h2, seed=5)
+    lay, n = ol.layout(algo, S, A, h1, h2)
+    p = ol.flatten({nm: dict(zip([x[0] for x in lay[nm]], [t.numpy() for t in init[nm]])) for nm in NETS}, lay, n)
+    t = ol.flatten({nm: dict(zip([x[0] for x in lay[nm]], [t.numpy() for t in init[tn]]))
+                    for nm, tn in zip(NETS, TNETS)}, lay, n)
+    ora = ol.OracleLearner(algo, S, A, h1, h2, B, k, "MSE", p, t)
+    ag = device_agent(algo, S, A, h1, h2, B, k, "MSE", init, precision="bf16")
+    rng = np.random.default_rng(4)
+    lr = 3e-4 if algo == "SAC" else 1e-3
+    # scale states to O(1) so bf16 operands carry signal
+    s, a, r, s2, d = _random_batch(rng, B, S, A)
+    s, s2 = s * 1e13, s2 * 1e13
+    ea = torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+    eb = torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+    for step in range(2):
+        st = ag.learn_batch(s, a, r, s2, d, ea, eb if algo == "SAC" else None).double().cpu().numpy()
+        lo, _, _ = ora.learn(s.numpy(), a.numpy(), r.numpy(), s2.numpy(), d.numpy(), ea.numpy(),
+                             eb.numpy() if algo == "SAC" else None)
+        np.testing.assert_allclose(st[:6], lo[:6], rtol=3e-2, err_msg=f"step {step}")
+        diff = np.abs(ag.params.cpu().numpy() - ora.P.numpy())
+        assert np.mean(diff <= lr * 1.01 * (step + 1)) >= 0.99, np.quantile(diff, [0.5, 0.99, 1.0])

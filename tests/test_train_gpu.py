@@ -1,0 +1,122 @@
+"""Fused vector step (rlmd_train_step) vs the oracle, and acting parity — GPU only."""
+import ctypes as C
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import envs as oe
+from oracle import learn as ol
+from oracle import philox as px
+from tests.test_oracle_learn import NETS, TNETS
+
+pytestmark = pytest.mark.gpu
+
+
+def read_ring(tr, start, n):
+    from rlmd_amd import _abi
+
+    S, A, dev = tr.replay.S, tr.replay.A, tr.device
+    s = torch.empty(n, S, device=dev)
+    a = torch.empty(n, A, device=dev)
+    r = torch.empty(n, device=dev)
+    s2 = torch.empty(n, S, device=dev)
+    d = torch.empty(n, dtype=torch.uint8, device=dev)
+    P = _abi.ptr
+    _abi.check(_abi.lib().rlmd_replay_read(tr.replay.h, start, n, P(s), P(a), P(r), P(s2), P(d), _abi.stream_ptr()))
+    return [x.cpu().numpy() for x in (s, a, r, s2, d)]
+
+
+@pytest.mark.parametrize("env,inv,fam,oinv,n", [("gbm", "A", oe.GBM, oe.INV_A, 1), ("coin", "B", oe.COIN, oe.INV_B, 2),
+                                                ("dice_sh", "C", oe.DICE_SH, oe.INV_C, 1)])
+def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
+    from rlmd_amd.trainer import VecTrainer
+
+    N, T, seed = 512, 25, 17
+    tr = VecTrainer(env=env, investor=inv, n_lanes=N, n_gambles=n, algo="SAC", k_updates=0, seed=seed,
+                    warmup_steps=10_000, smoothing_window=20_000, replay_capacity=N * T, precision="fp32",
+                    device=dev)
+    ora = oe.OracleVecEnv(fam, oinv, N, n, seed=seed)
+    obs = ora.reset()
+    absw = fam != oe.GBM
+    for t in range(T):
+        tr.step()
+        a = np.empty((N, ora.A), dtype=np.float32)
+        for i in range(ora.A):
+            v = px.philox(seed, np.arange(N), t, px.TAG_WARMUP_ACTION, i >> 1)
+            u = px.u01(v[0], v[1]) if i % 2 == 0 else px.u01(v[2], v[3])
+            a[:, i] = (-0.99 + 2 * 0.99 * u).astype(np.float32)
+        if absw:
+            a = np.abs(a)
+        ns, r, d, _ = ora.step(a)
+        s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
+        np.testing.assert_array_equal(a_r, a, err_msg=f"t={t} actions")
+        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s")
+        np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s2")
+        np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6)
+        np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
+        obs = ns.copy()
+        m = d[:, 0]
+        if m.any():
+            obs[m] = ora.reset(m)[m]
+    np.testing.assert_allclose(tr.obs.cpu().numpy(), obs.astype(np.float32), rtol=1e-6, atol=1e-30)
+    st = tr.episode_stats()
+    assert st["episodes"] >= 0
+
+
+def _flat_init(algo, S, A, h1, h2, init):
+    lay, n = ol.layout(algo, S, A, h1, h2)
+    names = {nm: [x[0] for x in lay[nm]] for nm in NETS}
+    p = ol.flatten({nm: dict(zip(names[nm], [t.numpy() for t in init[nm]])) for nm in NETS}, lay, n)
+    t = ol.flatten({nm: dict(zip(names[nm], [t.numpy() for t in init[tn]])) for nm, tn in zip(NETS, TNETS)}, lay, n)
+    return p, t
+
+
+@pytest.mark.parametrize("algo,S,A,h1,h2", [("SAC", 5, 1, 256, 256), ("TD3", 6, 2, 400, 300), ("SAC", 6, 4, 256, 256)])
+def test_act_matches_oracle_policy(dev, algo, S, A, h1, h2):
+    from rlmd_amd.agent import DeviceAgent, reference_init
+
+    init = reference_init(algo, S, A, h1, h2, seed=2)
+    ag = DeviceAgent(algo, S, A, h1, h2, 512, 256, init=init, precision="fp32", device=dev)
+    p, t = _flat_init(algo, S, A, h1, h2, init)
+    ora = ol.OracleLearner(algo, S, A, h1, h2, 512, 256, "MSE", p, t)
+    rng = np.random.default_rng(0)
+    n = 4099
+    obs = torch.from_numpy(rng.standard_normal((n, S)).astype(np.float32))
+    eps = torch.from_numpy(rng.standard_normal((n, A)).astype(np.float32))
+    Pn = ora.nets(ora.P)
+    with torch.no_grad():
+        det = ag.act(obs, mode=1).cpu()
+        ref_det = ora.policy(Pn["actor"], obs, None, stochastic=False)[0]
+        torch.testing.assert_close(det, ref_det, rtol=1e-5, atol=1e-6)
+        sto = ag.act(obs, mode=0, eps=eps).cpu()
+        if algo == "SAC":
+            ref = ora.policy(Pn["actor"], obs, eps)[0]
+        else:  # select_next_action: actor(s) + N(0, policy_noise), clamp to +-max_action
+            ref = (ref_det + eps * ora.policy_noise).clamp(-ora.max_action, ora.max_action)
+        torch.testing.assert_close(sto, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_policy_steps_apply_action_window_and_learn(dev):
+    from rlmd_amd.trainer import VecTrainer
+
+    N = 2048
+    tr = VecTrainer(env="gbm", investor="A", n_lanes=N, algo="SAC", k_updates=2, seed=4, warmup_steps=3,
+                    smoothing_window=8, replay_capacity=N * 16, precision="fp32", device=dev)
+    for t in range(12):
+        tr.step()
+        cs = t
+        if cs >= 3:  # policy acted: tr.actions holds the raw policy actions
+            raw = tr.actions.cpu().numpy()
+            _, stored, _, _, _ = read_ring(tr, (t * N) % (N * 16), N)
+            if 3 < cs <= 8:
+                w = (math.sin(math.pi * (cs / 8 - 0.5)) + 1) / 2
+                lo, hi = np.float32(w * -0.99), np.float32(w * 0.99)
+                np.testing.assert_array_equal(stored, np.clip(raw, lo, hi))
+            else:
+                np.testing.assert_array_equal(stored, raw)
+    st = tr.last_stats()
+    assert np.all(np.isfinite(st[[0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 12, 13, 14, 15]])), st
+    assert tr.agent.scalars()["learn_step_cntr"] == 2 * 12
+    assert tr.agent.scalars()["nan_flag"] == 0
