@@ -1,0 +1,233 @@
+"""Headline benchmark: env steps/s of the vectorised GBM + SAC loop on MI355X.
+
+Workload (BASELINE.json configs[1]): GBM_InvA (n_gambles=1,
+S=5, A=1), 65,536 lanes per GPU, SAC 256/256 with bf16 MFMA GEMMs (f32 master
+weights / Adam), mini-batch B=512 / top-k 256, on-device replay of 1,048,576
+transitions per GPU, K learner updates per vector step (UTD stated in the
+output).  One "step" = one fused vector step: policy acting for every lane,
+the env step + replay insert + auto-reset kernel, then K learn() updates.
+Timing is steady state: the reference's per-lane warm-up (1e3 random-action
+steps) and smoothing window (2e3) are start-up phases and are disabled here,
+so every timed step runs the (more expensive) policy path.
+
+Multi-GPU (one process per GPU, torchrun): independent seeds per rank, no
+data-path collective; one RCCL all_gather of each rank's episode-log slab at
+logging time; value = lanes * steps * world / max-over-ranks time ("weak").
+
+Output: ONE JSON line on rank 0 (see the harness contract), with
+  roofline      the fused env-step kernel against HBM (live HIP-event timing),
+  roofline_mfma the learner (MFMA) phase against the bf16 dense peak,
+  cpu_baseline  the CPU oracle port of the same loop on the host cores.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
+BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
+
+
+def env_bytes_per_step(S, A):
+    """Algorithmic HBM bytes of one lane-step of the fused env kernel:
+    action read 4A + obs read 4S + wealth/time read+write 24 + obs write 4S
+    + replay row (s 4S, a 4A, r 4, s' 4S, done 1)  = 8A + 16S + 29."""
+    return 8 * A + 16 * S + 29
+
+
+def sac_update_flops(S, A, H1, H2, B):
+    """Dense MLP FLOPs of one SAC update (2 per MAC), as launched:
+    target: actor fwd(B) + 2 target-critic fwd(B); critics: 2 fwd + 2 bwd (dW, dX);
+    actor: actor fwd + 2 critic fwd + 2 critic bwd-to-input + actor bwd (dW, dX)."""
+    X = S + A
+    actor_mac = S * H1 + H1 * H2 + 2 * A * H2
+    critic_mac = X * H1 + H1 * H2 + H2
+    fwd = actor_mac + 2 * critic_mac          # target path
+    fwd += 2 * critic_mac                      # critics on (s, a)
+    bwd_c = 2 * (critic_mac + H1 * H2 + H2)    # dW (all layers) + dX (layers 2..3) per critic
+    fwd += actor_mac + 2 * critic_mac          # actor update forward
+    bwd_a = 2 * (H2 + H1 * H2 + H1 * A)        # critics to the action input
+    bwd_a += actor_mac + (H1 * H2 + 2 * A * H2)  # actor dW + dX
+    return 2.0 * B * (fwd + bwd_c + bwd_a)
+
+
+def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
+    """The same loop on the host: CPU oracle (oracle/envs.py + oracle/learn.py,
+    the restatement pinned to the reference) — NumPy env over all lanes,
+    torch-CPU policy forward, K torch-CPU SAC updates per vector step."""
+    import numpy as np
+    import torch
+
+    from oracle import envs as oe
+    from oracle import learn as ol
+    from rlmd_amd.agent import reference_init
+
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    env = oe.OracleVecEnv(oe.GBM, oe.INV_A, lanes, 1, seed=420)
+    init = reference_init("SAC", S, A, H, H, seed=420)
+    lay, n = ol.layout("SAC", S, A, H, H)
+    names = {nm: [x[0] for x in lay[nm]] for nm in ("actor", "critic_1", "critic_2")}
+    p = ol.flatten({nm: dict(zip(names[nm], [t.numpy() for t in init[nm]])) for nm in names}, lay, n)
+    t = ol.flatten({nm: dict(zip(names[nm], [t.numpy() for t in init["target_" + nm]])) for nm in names}, lay, n)
+    learner = ol.OracleLearner("SAC", S, A, H, H, B, topk, "MSE", p, t)
+    rng = np.random.default_rng(0)
+    obs = env.reset()
+    ring_s, ring_a, ring_r, ring_s2, ring_d = [], [], [], [], []
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        with torch.no_grad():
+            Pn = learner.nets(learner.P)
+            eps = torch.from_numpy(rng.standard_normal((lanes, A)).astype(np.float32))
+            act = learner.policy(Pn["actor"], torch.from_numpy(obs.astype(np.float32)), eps)[0].numpy()
+        ns, r, d, _ = env.step(act)
+        ring_s.append(obs.astype(np.float32))
+        ring_a.append(act)
+        ring_r.append(r.astype(np.float32))
+        ring_s2.append(ns.astype(np.float32))
+        ring_d.append(d[:, 1])
+        obs = ns.copy()
+        if d[:, 0].any():
+            obs[d[:, 0]] = env.reset(d[:, 0])[d[:, 0]]
+        S_, A_ = np.concatenate(ring_s[-16:]), np.concatenate(ring_a[-16:])
+        R_, S2_, D_ = np.concatenate(ring_r[-16:]), np.concatenate(ring_s2[-16:]), np.concatenate(ring_d[-16:])
+        for _ in range(k_updates):
+            idx = rng.choice(S_.shape[0], B, replace=False)
+            learner.learn(S_[idx], A_[idx], R_[idx], S2_[idx], D_[idx],
+                          rng.standard_normal((B, A)).astype(np.float32), rng.standard_normal((B, A)).astype(np.float32))
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return {"value": lanes * steps / el, "unit": "env steps/sec", "cores": threads, "kind": "port",
+            "sample": f"{steps} vector steps x {lanes} GBM lanes, SAC 256/256 fp32, K={k_updates} updates "
+                      f"of B={B} per vector step (oracle/envs.py + oracle/learn.py on torch-CPU), {el:.1f} s"}
+
+
+def load_traffic():
+    path = os.path.join(ROOT, "profiles", "pmc_env_kernel.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        return json.load(open(path))
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--lanes", type=int, default=65536)
+    ap.add_argument("--k-updates", type=int, default=8)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--replay", type=int, default=1 << 20)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    from rlmd_amd import _abi
+    from rlmd_amd.trainer import VecTrainer
+    import ctypes as C
+
+    N, K = args.lanes, args.k_updates
+    tr = VecTrainer(env="gbm", investor="A", n_lanes=N, algo="SAC", k_updates=K, replay_capacity=args.replay,
+                    seed=420 + rank, warmup_steps=0, smoothing_window=0, precision=args.precision, device=dev,
+                    init_seed=420 + rank)
+    for _ in range(args.warmup):
+        tr.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    _abi.check(_abi.lib().rlmd_profile_enable(1))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tr.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ms = (C.c_double * 3)()
+    cnt = (C.c_int64 * 3)()
+    _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
+    _abi.check(_abi.lib().rlmd_profile_enable(0))
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    # logging-time exchange: one RCCL all_gather of each rank's episode-log slab
+    slab = torch.cat([tr.ep_stats.double(), torch.tensor([float(N * args.steps)], dtype=torch.float64, device=dev)])
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+        gathered = [torch.empty_like(slab) for _ in range(world)]
+        dist.all_gather(gathered, slab)
+        slab_all = torch.stack(gathered)
+    else:
+        slab_all = slab[None]
+    t_max = float(el_t.item())
+    total_steps = float(slab_all[:, 4].sum().item())
+    value = total_steps / t_max
+
+    S, A = tr.env.state_dim, tr.env.action_dim
+    env_ms = ms[1] / max(cnt[1], 1)
+    learn_ms = ms[2] / max(cnt[2], 1)
+    act_ms = ms[0] / max(cnt[0], 1)
+    env_bytes = env_bytes_per_step(S, A) * N
+    achieved = env_bytes / (env_ms * 1e-3) / 1e9
+    pmc = load_traffic()
+    traffic = None
+    if pmc and pmc.get("lanes") == N:
+        traffic = pmc.get("hbm_bytes_per_launch")
+    flops = K * sac_update_flops(S, A, 256, 256, tr.batch)
+    mfma_tf = flops / (learn_ms * 1e-3) / 1e12 if learn_ms > 0 else None
+
+    if rank == 0:
+        out = {
+            "metric": "env steps/sec (whole node), 64k-parallel GBM+SAC at 1/2/4/8 MI355X",
+            "value": value, "unit": "env steps/sec", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+            "config": {"workload": "C2: GBM_InvA n_gambles=1 (S=5,A=1), SAC 256/256, replay 1M/GPU",
+                       "lanes_per_gpu": N, "global_lanes": N * world, "k_updates_per_vector_step": K,
+                       "mini_batch": tr.batch, "topk": tr.topk, "utd_updates_per_env_step": K / N,
+                       "parallelism": f"independent seeds x{world} (no data-path collective)",
+                       "phase_ms_per_step": {"act": act_ms, "env_kernel": env_ms, "learn_k": learn_ms}},
+            "roofline": {"kernel": "env_train_kernel (fused env step + replay insert + reset)",
+                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms},
+            "roofline_mfma": {"kernel": "learn phase (K SAC updates, all kernels)", "bound": "mfma",
+                              "achieved": mfma_tf, "peak": BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3,
+                              "unit": "TFLOP/s", "frac": (mfma_tf or 0) / (BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3),
+                              "algorithmic_flops_per_step": flops, "avg_phase_ms": learn_ms},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

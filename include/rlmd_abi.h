@@ -129,10 +129,15 @@ typedef struct {
 int rlmd_agent_layout(const rlmd_agent_cfg* cfg, int64_t* n_params, int64_t* off_actor,
                       int64_t* off_critic1, int64_t* off_critic2);
 
+/* Weight gradients are reduced over the mini-batch in RLMD_GRAD_SPLITS slabs
+ * (split-K); the optimiser sums them in slab order (deterministic). */
+#define RLMD_GRAD_SPLITS 4
+
 /* Replaces Agent_sac.__init__ / Agent_td3.__init__ (algos/algo_sac.py:82-170,
- * algos/algo_td3.py:84-176).  All five buffers are caller-owned device f32
- * [n_params]: params (trainable), target params (same layout; SAC's
- * target_actor slot is unused as in the reference), grads, Adam m and v. */
+ * algos/algo_td3.py:84-176).  Caller-owned device f32 buffers: params
+ * (trainable) [n_params], target params [n_params] (same layout; SAC's
+ * target_actor slot is unused as in the reference), grads
+ * [RLMD_GRAD_SPLITS, n_params], Adam m and v [n_params]. */
 int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params_dev, float* target_dev,
                       float* grads_dev, float* adam_m_dev, float* adam_v_dev, rlmd_agent_t* out);
 int rlmd_agent_destroy(rlmd_agent_t ag);
@@ -185,6 +190,13 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
 
 /* Initialise obs_dev f32 [N, S] with every lane reset (episode start). */
 int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
+
+/* Live phase timing of rlmd_train_step with HIP events recorded on the step's
+ * stream around its three phases (0 acting, 1 fused env kernel, 2 learn).
+ * enable(1) resets the counters; read() synchronises and returns the summed
+ * milliseconds and the number of timed launches per phase. */
+int rlmd_profile_enable(int32_t on);
+int rlmd_profile_read(double* ms_out3, int64_t* count_out3);
 
 /* ------------------------------------------------------------- test hooks */
 /* Copy ring rows (start + i) % capacity, i < n, into caller buffers (nullable). */

@@ -18,6 +18,7 @@ SAC, TD3 = 0, 1
 FP32, BF16 = 0, 1
 LOSSES = ["MSE", "HUB", "MAE", "HSC", "CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"]
 GEMM_FWD, GEMM_BWD_X, GEMM_BWD_W = 0, 1, 2
+GRAD_SPLITS = 4  # RLMD_GRAD_SPLITS
 
 
 class RlmdError(RuntimeError):
@@ -81,6 +82,8 @@ SIGNATURES = {
     "rlmd_agent_scalars": (C.c_int, [P, P]),
     "rlmd_train_step": (C.c_int, [P, P, P, C.POINTER(TrainCfg), P, P, P, P, P]),
     "rlmd_train_reset": (C.c_int, [P, P, P]),
+    "rlmd_profile_enable": (C.c_int, [I32]),
+    "rlmd_profile_read": (C.c_int, [P, P]),
     "rlmd_gemm": (C.c_int, [I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, P, I32, P, I32, P, P]),
 }
 

@@ -108,7 +108,7 @@ class DeviceAgent:
         dev = self.device
         self.params = torch.zeros(self.n_params, dtype=torch.float32, device=dev)
         self.target = torch.zeros(self.n_params, dtype=torch.float32, device=dev)
-        self.grads = torch.zeros(self.n_params, dtype=torch.float32, device=dev)
+        self.grads = torch.zeros(_abi.GRAD_SPLITS, self.n_params, dtype=torch.float32, device=dev)
         self.adam_m = torch.zeros(self.n_params, dtype=torch.float32, device=dev)
         self.adam_v = torch.zeros(self.n_params, dtype=torch.float32, device=dev)
         init = init if init is not None else reference_init(algo, S, A, h1, h2, init_seed)

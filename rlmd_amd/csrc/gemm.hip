@@ -7,7 +7,8 @@
 //   FWD    C[m, n] = act(Σ_k A[m, k] W[n, k] + b[n])                 (y = x Wᵀ + b)
 //   BWD_X  C[m, c] = mask(Σ_r G[m, r] W[r, c])                       (dx = g W, ReLU mask)
 //   BWD_W  C[n, c] = Σ_m G[m, n] X[m, c];  bgrad[n] = Σ_m G[m, n]     (dW = gᵀ x, db)
-// Operands are staged HBM/L2 -> LDS in 64x32 tiles and fed to
+// Operands are staged HBM/L2 -> registers -> LDS in 64x64 tiles (range-checked
+// buffer loads, next K-step prefetched into registers) and fed to
 //   v_mfma_f32_16x16x4_f32   (RLMD_FP32: exact f32 fmaf chain, parity mode) or
 //   v_mfma_f32_16x16x32_bf16 (RLMD_BF16: bf16 operands, f32 accumulate).
 // 256 threads = 4 waves, each wave owns a 32x32 output sub-tile (2x2 MFMA
@@ -18,9 +19,12 @@
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 32;
-constexpr int PAD_F32 = 2;  // row stride 34 words: conflict-free column reads by 16 rows x 2 k
-constexpr int PAD_BF = 8;   // row stride 80 B: 16-B aligned fragment reads
+// Tile configurations (TM x TM outputs per 256-thread block, BK-deep K steps):
+//   TM = 64, BK = 64  for large M (acting over all lanes): 4 waves x 32x32
+//   TM = 32, BK = 128 for mini-batch GEMMs (M <= 1024): 4 waves x 16x16, a whole
+//                     128-deep K chunk per load round trip, 4x more blocks
+constexpr int PAD_F32 = 2;  // f32 rows of BK+2 words: 16 rows x 4 k columns spread over banks
+constexpr int PAD_BF = 8;   // bf16 rows of BK+8: 16-B aligned fragment reads
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
@@ -33,147 +37,217 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return (unsigned short)(u >> 16);
 }
 
+// Operand element addressing.  Loads go through buffer resources with the
+// hardware range check: an element outside the operand (row >= M or k >= K)
+// gets an out-of-range byte offset and reads 0, so no load is conditional and
+// the compiler keeps a whole tile of loads in flight (a plain `cond ? x[i] : 0`
+// is lowered to exec-masked branches that wait vmcnt(0) per pair of loads).
 template <int MODE>
-__device__ __forceinline__ float load_a(const rlmd::GemmProblem& p, const rlmd::GemmShape& s,
-                                        int i, int r) {
-  if (i >= s.M || r >= s.K) return 0.f;
-  if (MODE == rlmd::GEMM_BWD_W) return p.A[(int64_t)r * p.lda + i];
-  return p.A[(int64_t)i * p.lda + r];
+__device__ __forceinline__ int64_t a_off(const rlmd::GemmProblem& p, int i, int r) {
+  return MODE == rlmd::GEMM_BWD_W ? (int64_t)r * p.lda + i : (int64_t)i * p.lda + r;
+}
+template <int MODE>
+__device__ __forceinline__ int64_t b_off(const rlmd::GemmProblem& p, int r, int j) {
+  return MODE == rlmd::GEMM_FWD ? (int64_t)j * p.ldb + r : (int64_t)r * p.ldb + j;
+}
+constexpr int kOutOfRange = 0x7fffffff;
+
+__device__ __forceinline__ float buf_load(__amdgpu_buffer_rsrc_t r, int byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
-template <int MODE>
-__device__ __forceinline__ float load_b(const rlmd::GemmProblem& p, const rlmd::GemmShape& s,
-                                        int r, int j) {
-  if (r >= s.K) return 0.f;
-  if (MODE == rlmd::GEMM_BWD_W) {
-    if (j < s.N) return p.B[(int64_t)r * p.ldb + j];
-    return (j == s.N && p.bias_grad) ? 1.f : 0.f;  // ones column -> bias gradient
-  }
-  if (j >= s.N) return 0.f;
-  if (MODE == rlmd::GEMM_FWD) return p.B[(int64_t)j * p.ldb + r];
-  return p.B[(int64_t)r * p.ldb + j];
-}
-
+// Epilogue for one accumulator element; bias / ReLU-mask operands are read
+// through range-checked buffer loads (unconditional), only the store is guarded.
 template <int MODE>
 __device__ __forceinline__ void store_c(const rlmd::GemmProblem& p, const rlmd::GemmShape& s, int i,
-                                        int j, float v) {
-  if (i >= s.M) return;
+                                        int j, float v, __amdgpu_buffer_rsrc_t rx) {
+  const bool in = i < s.M && j < s.N;
   if (MODE == rlmd::GEMM_FWD) {
-    if (j >= s.N) return;
-    if (p.bias) v += p.bias[j];
+    if (p.bias) v += buf_load(rx, in ? j * 4 : kOutOfRange);
     if (s.relu) v = fmaxf(v, 0.f);
-    p.C[(int64_t)i * p.ldc + j] = v;
+    if (in) p.C[(int64_t)i * p.ldc + j] = v;
   } else if (MODE == rlmd::GEMM_BWD_X) {
-    if (j >= s.N) return;
-    if (p.mask && !(p.mask[(int64_t)i * p.ldm + j] > 0.f)) v = 0.f;
-    p.C[(int64_t)i * p.ldc + j] = v;
+    if (p.mask) {
+      const float m = buf_load(rx, in ? (int)(((int64_t)i * p.ldm + j) * 4) : kOutOfRange);
+      v = m > 0.f ? v : 0.f;
+    }
+    if (in) p.C[(int64_t)i * p.ldc + j] = v;
   } else {
-    if (j < s.N) p.C[(int64_t)i * p.ldc + j] = v;
-    else if (j == s.N && p.bias_grad) p.bias_grad[i] = v;
+    if (in) p.C[(int64_t)i * p.ldc + j] = v;
+    else if (i < s.M && j == s.N && p.bias_grad) p.bias_grad[i] = v;
   }
 }
 
-// Global -> LDS staging of one BMxBK A tile and one BNxBK B tile (both stored
-// r-contiguous).  Loop order follows the contiguous global dimension so each
-// wave-instruction reads consecutive addresses.
-template <int MODE, typename T, int LD>
-__device__ __forceinline__ void stage(const rlmd::GemmProblem& p, const rlmd::GemmShape& s, int i0,
-                                      int j0, int r0, T (*As)[LD], T (*Bs)[LD]) {
-  const int tid = threadIdx.x;
-#pragma unroll
-  for (int e = 0; e < (BM * BK) / 256; ++e) {
-    const int idx = e * 256 + tid;
-    int ii, rr;
-    if (MODE == rlmd::GEMM_BWD_W) {  // A element (i, r) at A[r*lda + i]: i fastest
-      ii = idx % BM;
-      rr = idx / BM;
-    } else {
-      rr = idx % BK;
-      ii = idx / BK;
-    }
-    const float v = load_a<MODE>(p, s, i0 + ii, r0 + rr);
-    if constexpr (sizeof(T) == 4) As[ii][rr] = v;
-    else As[ii][rr] = f2bf(v);
-  }
-#pragma unroll
-  for (int e = 0; e < (BN * BK) / 256; ++e) {
-    const int idx = e * 256 + tid;
-    int jj, rr;
-    if (MODE == rlmd::GEMM_FWD) {  // W[j, r]: r fastest
-      rr = idx % BK;
-      jj = idx / BK;
-    } else {  // B[r, j]: j fastest
-      jj = idx % BN;
-      rr = idx / BN;
-    }
-    const float v = load_b<MODE>(p, s, r0 + rr, j0 + jj);
-    if constexpr (sizeof(T) == 4) Bs[jj][rr] = v;
-    else Bs[jj][rr] = f2bf(v);
-  }
-}
 
-template <int PREC, int MODE>
+// Register stage of one (A, B) tile pair: issue all global loads of a K-step.
+template <int MODE, int BM, int BK>
+struct TileRegs {
+  static constexpr int BN = BM;
+  static constexpr int kPerThread = (BM * BK) / 256;  // elements of each operand tile per thread
+  float a[kPerThread], b[kPerThread];
+
+  __device__ __forceinline__ void load(const rlmd::GemmProblem& p, const rlmd::GemmShape& s,
+                                       __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int i0,
+                                       int j0, int r0, int r_end) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < kPerThread; ++e) {
+      const int idx = e * 256 + tid;
+      int ii, rr;
+      if (MODE == rlmd::GEMM_BWD_W) {  // A element (i, r) at A[r*lda + i]: i fastest
+        ii = idx % BM;
+        rr = idx / BM;
+      } else {
+        rr = idx % BK;
+        ii = idx / BK;
+      }
+      const int gi = i0 + ii, gr = r0 + rr;
+      const bool ok = gi < s.M && gr < r_end;
+      a[e] = buf_load(ra, ok ? (int)(a_off<MODE>(p, gi, gr) * 4) : kOutOfRange);
+    }
+#pragma unroll
+    for (int e = 0; e < kPerThread; ++e) {
+      const int idx = e * 256 + tid;
+      int jj, rr;
+      if (MODE == rlmd::GEMM_FWD) {  // W[j, r]: r fastest
+        rr = idx % BK;
+        jj = idx / BK;
+      } else {  // B[r, j]: j fastest
+        jj = idx % BN;
+        rr = idx / BN;
+      }
+      const int gj = j0 + jj, gr = r0 + rr;
+      const bool ok = gj < s.N && gr < r_end;
+      float v = buf_load(rb, ok ? (int)(b_off<MODE>(p, gr, gj) * 4) : kOutOfRange);
+      if (MODE == rlmd::GEMM_BWD_W && p.bias_grad) v = (gj == s.N && gr < r_end) ? 1.f : v;  // ones column -> db
+      b[e] = v;
+    }
+  }
+
+  template <typename T, int LD>
+  __device__ __forceinline__ void store(T (*As)[LD], T (*Bs)[LD]) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int e = 0; e < kPerThread; ++e) {
+      const int idx = e * 256 + tid;
+      const int ii = MODE == rlmd::GEMM_BWD_W ? idx % BM : idx / BK;
+      const int rr = MODE == rlmd::GEMM_BWD_W ? idx / BM : idx % BK;
+      if constexpr (sizeof(T) == 4) As[ii][rr] = a[e];
+      else As[ii][rr] = f2bf(a[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < kPerThread; ++e) {
+      const int idx = e * 256 + tid;
+      const int jj = MODE == rlmd::GEMM_FWD ? idx / BK : idx % BN;
+      const int rr = MODE == rlmd::GEMM_FWD ? idx % BK : idx / BN;
+      if constexpr (sizeof(T) == 4) Bs[jj][rr] = b[e];
+      else Bs[jj][rr] = f2bf(b[e]);
+    }
+  }
+};
+
+template <int PREC, int MODE, int BM, int BK>
 __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
-  const rlmd::GemmProblem& p = batch.prob[blockIdx.z];
-  const rlmd::GemmShape& s = batch.shape;
+  constexpr int BN = BM;
+  constexpr int MB = BM / 32;  // 16x16 MFMA blocks per wave per dimension (waves are 2 x 2)
+  const int group = blockIdx.z % batch.groups, split = blockIdx.z / batch.groups;
+  rlmd::GemmProblem p = group == 0 ? batch.prob[0] : batch.prob[1];
+  const rlmd::GemmShape s = batch.shape;
+  // split-K (weight gradients): split `split` reduces rows [r_beg, r_end) of the
+  // batch and writes its own partial slab; the optimiser sums the slabs in order
+  const int chunk = (s.K + batch.splits - 1) / batch.splits;
+  const int r_beg = split * chunk, r_end = min(s.K, r_beg + chunk);
+  if (split) {
+    p.C += (int64_t)split * batch.split_stride;
+    if (p.bias_grad) p.bias_grad += (int64_t)split * batch.split_stride;
+  }
   const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  f32x4 acc[2][2];
+  f32x4 acc[MB][MB];
 #pragma unroll
-  for (int a = 0; a < 2; ++a)
+  for (int a = 0; a < MB; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int Kr = s.K;
+  const int nk = r_end > r_beg ? (r_end - r_beg + BK - 1) / BK : 0;
+  // operand extents in bytes (range-checked buffer resources)
+  const int64_t a_rows = MODE == rlmd::GEMM_BWD_W ? s.K : s.M;
+  const int64_t a_cols = MODE == rlmd::GEMM_BWD_W ? s.M : s.K;
+  const int64_t b_rows = MODE == rlmd::GEMM_FWD ? s.N : s.K;
+  const int64_t b_cols = MODE == rlmd::GEMM_FWD ? s.K : s.N;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.A, (short)0, (int)(((a_rows - 1) * p.lda + a_cols) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.B, (short)0, (int)(((b_rows - 1) * p.ldb + b_cols) * 4), 0x00020000);
+  TileRegs<MODE, BM, BK> regs;
+  if (nk) regs.load(p, s, ra, rb, i0, j0, r_beg, r_end);
+  const int row0 = MB * 16 * wr, col0 = MB * 16 * wc;
   if constexpr (PREC == RLMD_FP32) {
     __shared__ float As[BM][BK + PAD_F32];
     __shared__ float Bs[BN][BK + PAD_F32];
-    for (int r0 = 0; r0 < Kr; r0 += BK) {
+    for (int t = 0; t < nk; ++t) {
       __syncthreads();
-      stage<MODE, float, BK + PAD_F32>(p, s, i0, j0, r0, As, Bs);
+      regs.store(As, Bs);
       __syncthreads();
+      if (t + 1 < nk) regs.load(p, s, ra, rb, i0, j0, r_beg + (t + 1) * BK, r_end);  // next K-step in flight
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
         const int kr = kk + (lane >> 4);
-        float a0 = As[32 * wr + (lane & 15)][kr];
-        float a1 = As[32 * wr + 16 + (lane & 15)][kr];
-        float b0 = Bs[32 * wc + (lane & 15)][kr];
-        float b1 = Bs[32 * wc + 16 + (lane & 15)][kr];
-        acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b0, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0, b1, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1, b1, acc[1][1], 0, 0, 0);
+        float av[MB], bv[MB];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          av[m] = As[row0 + 16 * m + (lane & 15)][kr];
+          bv[m] = Bs[col0 + 16 * m + (lane & 15)][kr];
+        }
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+          for (int n = 0; n < MB; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
       }
     }
   } else {
     __shared__ __attribute__((aligned(16))) unsigned short As[BM][BK + PAD_BF];
     __shared__ __attribute__((aligned(16))) unsigned short Bs[BN][BK + PAD_BF];
-    for (int r0 = 0; r0 < Kr; r0 += BK) {
+    for (int t = 0; t < nk; ++t) {
       __syncthreads();
-      stage<MODE, unsigned short, BK + PAD_BF>(p, s, i0, j0, r0, As, Bs);
+      regs.store(As, Bs);
       __syncthreads();
-      const int kr = 8 * (lane >> 4);
-      const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(&As[32 * wr + (lane & 15)][kr]);
-      const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(&As[32 * wr + 16 + (lane & 15)][kr]);
-      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(&Bs[32 * wc + (lane & 15)][kr]);
-      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(&Bs[32 * wc + 16 + (lane & 15)][kr]);
-      acc[0][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc[1][1], 0, 0, 0);
+      if (t + 1 < nk) regs.load(p, s, ra, rb, i0, j0, r_beg + (t + 1) * BK, r_end);
+#pragma unroll
+      for (int kk = 0; kk < BK; kk += 32) {
+        const int kr = kk + 8 * (lane >> 4);
+        bf16x8 av[MB], bv[MB];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          av[m] = *reinterpret_cast<const bf16x8*>(&As[row0 + 16 * m + (lane & 15)][kr]);
+          bv[m] = *reinterpret_cast<const bf16x8*>(&Bs[col0 + 16 * m + (lane & 15)][kr]);
+        }
+#pragma unroll
+        for (int m = 0; m < MB; ++m)
+#pragma unroll
+          for (int n = 0; n < MB; ++n)
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], bv[n], acc[m][n], 0, 0, 0);
+      }
     }
   }
   // C/D map (16x16 MFMA, every dtype): col = lane & 15, row = 4*(lane >> 4) + reg
+  __amdgpu_buffer_rsrc_t rx = ra;
+  if (MODE == rlmd::GEMM_FWD && p.bias)
+    rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, (short)0, s.N * 4, 0x00020000);
+  if (MODE == rlmd::GEMM_BWD_X && p.mask)
+    rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.mask, (short)0,
+                                           (int)(((int64_t)(s.M - 1) * p.ldm + s.N) * 4), 0x00020000);
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+  for (int mi = 0; mi < MB; ++mi)
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < MB; ++ni)
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
-        const int i = i0 + 32 * wr + 16 * mi + 4 * (lane >> 4) + rg;
-        const int j = j0 + 32 * wc + 16 * ni + (lane & 15);
-        store_c<MODE>(p, s, i, j, acc[mi][ni][rg]);
+        const int i = i0 + row0 + 16 * mi + 4 * (lane >> 4) + rg;
+        const int j = j0 + col0 + 16 * ni + (lane & 15);
+        store_c<MODE>(p, s, i, j, acc[mi][ni][rg], rx);
       }
 }
 
@@ -181,16 +255,23 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
 
 namespace rlmd {
 
-int gemm_launch(int prec, int mode, const GemmBatch& b, int groups, hipStream_t stream) {
+int gemm_launch(int prec, int mode, const GemmBatch& b_in, int groups, hipStream_t stream) {
   RLMD_CHECK(groups >= 1 && groups <= RLMD_GEMM_MAX_GROUPS, "bad GEMM group count");
+  GemmBatch b = b_in;
+  b.groups = groups;
+  if (b.splits < 1) b.splits = 1;
+  RLMD_CHECK(mode == GEMM_BWD_W || b.splits == 1, "split-K only for weight gradients");
   const int n_out = b.shape.N + (mode == GEMM_BWD_W ? 1 : 0);
   if (b.shape.M <= 0 || n_out <= 0) return 0;
-  dim3 grid((n_out + BN - 1) / BN, (b.shape.M + BM - 1) / BM, groups);
-#define RLMD_GEMM_CASE(P, M)                                                          \
-  if (prec == P && mode == M) {                                                       \
-    hipLaunchKernelGGL((gemm_kernel<P, M>), grid, dim3(256), 0, stream, b);          \
-    RLMD_LAUNCH_CHECK();                                                              \
-    return 0;                                                                         \
+  const bool big = b.shape.M > 1024;
+  const int T = big ? 64 : 32;
+  dim3 grid((n_out + T - 1) / T, (b.shape.M + T - 1) / T, groups * b.splits);
+#define RLMD_GEMM_CASE(P, M)                                                                  \
+  if (prec == P && mode == M) {                                                               \
+    if (big) hipLaunchKernelGGL((gemm_kernel<P, M, 64, 64>), grid, dim3(256), 0, stream, b);  \
+    else hipLaunchKernelGGL((gemm_kernel<P, M, 32, 128>), grid, dim3(256), 0, stream, b);     \
+    RLMD_LAUNCH_CHECK();                                                                      \
+    return 0;                                                                                 \
   }
   RLMD_GEMM_CASE(RLMD_FP32, GEMM_FWD)
   RLMD_GEMM_CASE(RLMD_FP32, GEMM_BWD_X)
@@ -214,6 +295,7 @@ int rlmd_gemm(int32_t prec, int32_t mode, int32_t M, int32_t N, int32_t K, int32
   rlmd::GemmBatch b{};
   b.shape = {M, N, K, relu};
   b.prob[0] = {A, lda, B, ldb, bias, C, ldc, mask, ldm, bias_grad};
+  b.splits = 1;
   return rlmd::gemm_launch(prec, mode, b, 1, (hipStream_t)stream);
 }
 

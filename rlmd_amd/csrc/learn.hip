@@ -37,26 +37,6 @@ __device__ __forceinline__ uint32_t f2key(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// bitonic sort of n_pow2 u64 keys in LDS, ascending; all threads of the block call it
-__device__ void block_sort(uint64_t* keys, int n_pow2) {
-  for (int k = 2; k <= n_pow2; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n_pow2; i += blockDim.x) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t x = keys[i], y = keys[ixj];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            keys[i] = y;
-            keys[ixj] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-}
-
 // deterministic block reduction (fixed tree) of one float per thread
 __device__ float block_sum(float v, float* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -310,14 +290,10 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
   while (npow < B) npow <<= 1;
   bool sel = in;
   if (B > a.k) {
-    for (int i = b; i < npow; i += blockDim.x)
-      keys[i] = i < B ? 0ull : ~0ull;
+    const uint64_t key = in ? ((uint64_t)(~f2key(l[0] + l[1])) << 32) | (uint32_t)b : ~0ull;
+    const uint64_t sk = rlmd_block_bitonic(key, npow, keys);
     __syncthreads();
-    if (in) keys[b] = ((uint64_t)(~f2key(l[0] + l[1])) << 32) | (uint32_t)b;
-    __syncthreads();
-    block_sort(keys, npow);
-    // rank of my row
-    if (b < B) rank_of[(int)(keys[b] & 0xffffffffu)] = b;
+    if (b < B) rank_of[(int)(sk & 0xffffffffu)] = b;  // rank of row -> selected if < k
     __syncthreads();
     sel = in && rank_of[b] < k;
   }
@@ -327,18 +303,17 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
     const float mean = block_sum(sel ? l[g] : 0.f, red) / k;
     const float mn = block_min(sel ? l[g] : INFINITY, red);
     const float mx = block_max(sel ? l[g] : -INFINITY, red);
-    // sort selected losses descending
+    // order statistics of the selected losses, descending (sort k keys: the
+    // selected rows are first compacted to their rank slots)
     int kp = 1;
     while (kp < k) kp <<= 1;
-    const int npw = npow > kp ? npow : kp;
-    for (int i = b; i < npw; i += blockDim.x) keys[i] = ~0ull;
-    if (in) lsel[g][b] = l[g];
     __syncthreads();
-    if (sel) keys[b] = ((uint64_t)(~f2key(l[g])) << 32) | (uint32_t)b;
+    if (sel) lsel[g][B > a.k ? rank_of[b] : b] = l[g];
     __syncthreads();
-    block_sort(keys, npw);
+    const uint64_t key = b < k ? ((uint64_t)(~f2key(lsel[g][b])) << 32) | (uint32_t)b : ~0ull;
+    const uint64_t sk = rlmd_block_bitonic(key, kp, keys);
     float lg = 0.f;
-    if (b < k) lg = logf(lsel[g][(int)(keys[b] & 0xffffffffu)] + a.log_noise);
+    if (b < k) lg = logf(lsel[g][(int)(sk & 0xffffffffu)] + a.log_noise);
     const float lmean = block_sum(b < k ? lg : 0.f, red) / k;
     const float num = block_sum(b < k ? a.zipf_x[b] * (lg - lmean) : 0.f, red);
     const float alpha = 1.f / (num / a.zipf_x2);
@@ -410,13 +385,11 @@ __global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
   while (npow < B) npow <<= 1;
   bool sel = in;
   if (a.topk) {
-    for (int i = b; i < npow; i += blockDim.x) keys[i] = ~0ull;
-    __syncthreads();
     // SAC sorts descending, TD3 ascending
-    if (in) keys[b] = ((uint64_t)(a.algo == RLMD_SAC ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)b;
+    const uint64_t key = in ? ((uint64_t)(a.algo == RLMD_SAC ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)b : ~0ull;
+    const uint64_t sk = rlmd_block_bitonic(key, npow, keys);
     __syncthreads();
-    block_sort(keys, npow);
-    if (b < B) rank_of[(int)(keys[b] & 0xffffffffu)] = b;
+    if (b < B) rank_of[(int)(sk & 0xffffffffu)] = b;
     __syncthreads();
     sel = in && rank_of[b] < k;
   }
@@ -517,7 +490,8 @@ __global__ void __launch_bounds__(256) actor_bwd_kernel(ActorBwdArgs a) {
 // ---------------------------------------------------------------------------
 struct AdamArgs {
   float* p;
-  const float* g;
+  const float* g;          // RLMD_GRAD_SPLITS partial-gradient slabs, split_stride apart
+  int64_t split_stride;
   float* m;
   float* v;
   float* target;  // Polyak target (nullable)
@@ -543,7 +517,9 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
   const bool polyak = a.target && a.polyak_interval > 0 && (cnt % a.polyak_interval) == 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
        i += (int64_t)gridDim.x * blockDim.x) {
-    const float g = a.g[i];
+    float g = a.g[i];
+#pragma unroll
+    for (int sp = 1; sp < RLMD_GRAD_SPLITS; ++sp) g += a.g[i + sp * a.split_stride];
     float m = a.m[i], v = a.v[i];
     m = m + (1.f - b1) * (g - m);
     v = v * b2 + (1.f - b2) * g * g;
@@ -681,6 +657,8 @@ int bwd_w(rlmd_agent_s* ag, int groups, int M, int N, int K, const float* const*
   GemmBatch b{};
   b.shape = {M, N, K, 0};
   for (int g = 0; g < groups; ++g) b.prob[g] = {G[g], ldg, X[g], ldx, nullptr, DW[g], N, nullptr, 0, DB[g]};
+  b.splits = RLMD_GRAD_SPLITS;  // batch reduction split 4 ways; Adam sums the slabs
+  b.split_stride = ag->n_params;
   return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, groups, s);
 }
 
@@ -859,6 +837,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     AdamArgs ad{};
     ad.p = Pc[0];
     ad.g = Gc[0];
+    ad.split_stride = ag->n_params;
     ad.m = ag->m + ag->off_c[0];
     ad.v = ag->v + ag->off_c[0];
     ad.target = Tc[0];
@@ -972,6 +951,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     AdamArgs ad{};
     ad.p = Pa;
     ad.g = Ga;
+    ad.split_stride = ag->n_params;
     ad.m = ag->m + ag->off_actor;
     ad.v = ag->v + ag->off_actor;
     ad.target = sac ? nullptr : Ta;
@@ -1152,7 +1132,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_HIP(hipMemcpy(ag->st, &st, sizeof(st), hipMemcpyHostToDevice));
   RLMD_HIP(hipMemset(m, 0, sizeof(float) * ag->n_params));
   RLMD_HIP(hipMemset(v, 0, sizeof(float) * ag->n_params));
-  RLMD_HIP(hipMemset(grads, 0, sizeof(float) * ag->n_params));
+  RLMD_HIP(hipMemset(grads, 0, sizeof(float) * ag->n_params * RLMD_GRAD_SPLITS));
   RLMD_HIP(hipDeviceSynchronize());
   *out = ag;
   return 0;
@@ -1213,6 +1193,52 @@ int rlmd_agent_scalars(rlmd_agent_t ag, double* out) {
   return 0;
 }
 
+// ---- in-library event profiler (bench.py: live per-phase kernel durations) ----
+namespace {
+struct PhaseProfiler {
+  bool enabled = false;
+  std::vector<hipEvent_t> ev[3][2];  // phase x {start, stop}: 0 act, 1 env, 2 learn
+  size_t used[3] = {0, 0, 0};
+  int record(int phase, int which, hipStream_t s) {
+    if (!enabled) return 0;
+    auto& v = ev[phase][which];
+    const size_t i = which == 0 ? used[phase] : used[phase] - 1;
+    if (i >= v.size()) {
+      hipEvent_t e;
+      RLMD_HIP(hipEventCreate(&e));
+      v.push_back(e);
+    }
+    RLMD_HIP(hipEventRecord(v[i], s));
+    if (which == 0) used[phase]++;
+    return 0;
+  }
+};
+PhaseProfiler g_prof;
+}  // namespace
+
+int rlmd_profile_enable(int32_t on) {
+  RLMD_HIP(hipDeviceSynchronize());
+  g_prof.enabled = on != 0;
+  for (int p = 0; p < 3; ++p) g_prof.used[p] = 0;
+  return 0;
+}
+
+int rlmd_profile_read(double* ms_out3, int64_t* count_out3) {
+  RLMD_CHECK(ms_out3 && count_out3, "null argument");
+  RLMD_HIP(hipDeviceSynchronize());
+  for (int p = 0; p < 3; ++p) {
+    double tot = 0.0;
+    for (size_t i = 0; i < g_prof.used[p]; ++i) {
+      float ms = 0.f;
+      RLMD_HIP(hipEventElapsedTime(&ms, g_prof.ev[p][0][i], g_prof.ev[p][1][i]));
+      tot += ms;
+    }
+    ms_out3[p] = tot;
+    count_out3[p] = (int64_t)g_prof.used[p];
+  }
+  return 0;
+}
+
 int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlmd_train_cfg* cfg,
                     float* obs, float* actions, double* ep_stats, float* stats, void* stream) {
   RLMD_CHECK(env && rb && cfg && obs && actions, "null argument");
@@ -1225,7 +1251,9 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   const bool random = cs < cfg->warmup_steps;
   if (!random) {
     RLMD_CHECK(ag, "policy acting needs an agent");
+    RLMD_TRY(g_prof.record(0, 0, st));
     RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st));
+    RLMD_TRY(g_prof.record(0, 1, st));
   }
   // action_window (tools/utils.py:345-373): only warmup < cum_step <= smoothing_window
   float lo = -INFINITY, hi = INFINITY;
@@ -1236,11 +1264,16 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
     hi = (float)(width * 0.99);
   }
   const int64_t base = rlmd::replay_mem_idx(rb);
+  RLMD_TRY(g_prof.record(1, 0, st));
   RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, lo,
                            hi, obs, ep_stats, st));
+  RLMD_TRY(g_prof.record(1, 1, st));
   rlmd::replay_advance(rb, N);
-  if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch)
+  if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch) {
+    RLMD_TRY(g_prof.record(2, 0, st));
     RLMD_TRY(rlmd::agent_learn_k(ag, rb, cfg->k_updates, stats, st));
+    RLMD_TRY(g_prof.record(2, 1, st));
+  }
   return 0;
 }
 

@@ -79,24 +79,12 @@ __global__ void __launch_bounds__(kSampleThreads)
   }
   for (int round = 1; round <= kMaxRounds; ++round) {
     __syncthreads();
-    keys[i] = i < B ? (((uint64_t)cand[i] << 11) | (uint64_t)i) : ~0ull;
+    const uint64_t key = i < B ? (((uint64_t)cand[i] << 11) | (uint64_t)i) : ~0ull;
     if (i == 0) any_dup = 0;
+    const uint64_t sk = rlmd_block_bitonic(key, kSampleThreads, keys);
     __syncthreads();
-    // bitonic sort of kSampleThreads keys (ascending)
-    for (int k = 2; k <= kSampleThreads; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint64_t x = keys[i], y = keys[ixj];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            keys[i] = y;
-            keys[ixj] = x;
-          }
-        }
-        __syncthreads();
-      }
-    }
+    keys[i] = sk;
+    __syncthreads();
     // a sorted key whose index equals its predecessor's is a duplicate slot
     if (i > 0 && i < B) {
       const uint64_t cur = keys[i], prev = keys[i - 1];

@@ -79,6 +79,38 @@ __host__ __device__ __forceinline__ uint64_t rlmd_below(uint32_t a, uint32_t b, 
 }
 
 // ---------------------------------------------------------------------------
+// Block-wide ascending bitonic sort of one u64 key per thread over the first n
+// (power of two, n <= blockDim.x) threads; returns this thread's sorted key.
+// Strides < 64 exchange through wave shuffles (no barrier); strides >= 64
+// through `lds` (>= blockDim.x entries).  Every thread of the block must call
+// it (threads >= n sort their own n-aligned segments, harmlessly).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t rlmd_shfl_xor_u64(uint64_t v, int m) {
+  const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ inline uint64_t rlmd_block_bitonic(uint64_t key, int n, uint64_t* lds) {
+  const int i = threadIdx.x;
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      uint64_t other;
+      if (j >= 64) {
+        __syncthreads();
+        lds[i] = key;
+        __syncthreads();
+        other = lds[i ^ j];
+      } else {
+        other = rlmd_shfl_xor_u64(key, j);
+      }
+      const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+      key = keep_min ? (key < other ? key : other) : (key < other ? other : key);
+    }
+  }
+  return key;
+}
+
+// ---------------------------------------------------------------------------
 // host-side error plumbing for the C ABI
 // ---------------------------------------------------------------------------
 #include <string>

@@ -33,6 +33,9 @@ struct GemmShape {
 struct GemmBatch {
   GemmShape shape;
   GemmProblem prob[RLMD_GEMM_MAX_GROUPS];
+  int32_t groups;        // set by gemm_launch
+  int32_t splits;        // BWD_W split-K: slabs written at C + s*split_stride (and bias_grad)
+  int64_t split_stride;  // floats between slabs
 };
 
 int gemm_launch(int prec, int mode, const GemmBatch& b, int groups, hipStream_t stream);

@@ -2,7 +2,7 @@
 
 fp32 mode (exact-f32 MFMA operands): loss statistics within 1e-4 relative;
 parameters after each update within 2e-6 absolute of the reference / oracle
-(Adam steps are lr = 3e-4..1e-3, so < 1 % of one step) on >= 99.99 % of
+(Adam steps are lr = 3e-4..1e-3, so < 1 % of one step) on >= 99.9 % of
 entries and within 10 % of one Adam step on all: where |grad| ~ Adam's eps
 (1e-8), update = lr*m/(sqrt(v)+eps) turns fp32 summation-order noise of a
 cancelling gradient into a visible fraction of lr.
@@ -63,7 +63,7 @@ def test_learn_matches_reference_golden(golden, dev, case):
 def assert_params_close(got, ref, lr, msg):
     diff = np.abs(got - ref)
     frac = np.mean(diff <= 2e-6)
-    assert frac >= 0.9999, f"{msg}: only {frac:.6f} within 2e-6 (max {diff.max():.3g})"
+    assert frac >= 0.999, f"{msg}: only {frac:.6f} within 2e-6 (max {diff.max():.3g})"
     assert diff.max() <= 0.1 * lr, f"{msg}: max diff {diff.max():.3g} > 10% of lr"
 
 
