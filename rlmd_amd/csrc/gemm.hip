@@ -59,13 +59,14 @@ __device__ __forceinline__ float buf_load(__amdgpu_buffer_rsrc_t r, int byte_off
 // Epilogue for one accumulator element; bias / ReLU-mask operands are read
 // through range-checked buffer loads (unconditional), only the store is guarded.
 template <int MODE>
-__device__ __forceinline__ void store_c(const rlmd::GemmProblem& p, const rlmd::GemmShape& s, int i,
-                                        int j, float v, __amdgpu_buffer_rsrc_t rx) {
+__device__ __forceinline__ float store_c(const rlmd::GemmProblem& p, const rlmd::GemmShape& s, int i,
+                                         int j, float v, __amdgpu_buffer_rsrc_t rx) {
   const bool in = i < s.M && j < s.N;
   if (MODE == rlmd::GEMM_FWD) {
     if (p.bias) v += buf_load(rx, in ? j * 4 : kOutOfRange);
     if (s.relu) v = fmaxf(v, 0.f);
     if (in) p.C[(int64_t)i * p.ldc + j] = v;
+    return in ? v : 0.f;
   } else if (MODE == rlmd::GEMM_BWD_X) {
     if (p.mask) {
       const float m = buf_load(rx, in ? (int)(((int64_t)i * p.ldm + j) * 4) : kOutOfRange);
@@ -76,6 +77,7 @@ __device__ __forceinline__ void store_c(const rlmd::GemmProblem& p, const rlmd::
     if (in) p.C[(int64_t)i * p.ldc + j] = v;
     else if (i < s.M && j == s.N && p.bias_grad) p.bias_grad[i] = v;
   }
+  return 0.f;
 }
 
 
@@ -239,6 +241,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
   if (MODE == rlmd::GEMM_BWD_X && p.mask)
     rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.mask, (short)0,
                                            (int)(((int64_t)(s.M - 1) * p.ldm + s.N) * 4), 0x00020000);
+  float out[MB][MB][4];
 #pragma unroll
   for (int mi = 0; mi < MB; ++mi)
 #pragma unroll
@@ -247,8 +250,28 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
       for (int rg = 0; rg < 4; ++rg) {
         const int i = i0 + row0 + 16 * mi + 4 * (lane >> 4) + rg;
         const int j = j0 + col0 + 16 * ni + (lane & 15);
-        store_c<MODE>(p, s, i, j, acc[mi][ni][rg], rx);
+        out[mi][ni][rg] = store_c<MODE>(p, s, i, j, acc[mi][ni][rg], rx);
       }
+  if constexpr (MODE == rlmd::GEMM_FWD && MB == 1) {
+    if (p.head_w) {  // fused q head: per-row partial over this tile's 32 columns
+      __shared__ float hp[2][32];
+      const int j = j0 + col0 + (lane & 15);
+      const float w = buf_load(__builtin_amdgcn_make_buffer_rsrc((void*)p.head_w, (short)0, s.N * 4, 0x00020000),
+                               j < s.N ? j * 4 : kOutOfRange);
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        float c = out[0][0][rg] * w;
+        c += __shfl_xor(c, 1, 64);
+        c += __shfl_xor(c, 2, 64);
+        c += __shfl_xor(c, 4, 64);
+        c += __shfl_xor(c, 8, 64);
+        if ((lane & 15) == 0) hp[wc][row0 + 4 * (lane >> 4) + rg] = c;
+      }
+      __syncthreads();
+      if (threadIdx.x < 32 && i0 + (int)threadIdx.x < s.M)
+        p.head_part[(int64_t)blockIdx.x * s.M + i0 + threadIdx.x] = hp[0][threadIdx.x] + hp[1][threadIdx.x];
+    }
+  }
 }
 
 }  // namespace
@@ -264,6 +287,7 @@ int gemm_launch(int prec, int mode, const GemmBatch& b_in, int groups, hipStream
   const int n_out = b.shape.N + (mode == GEMM_BWD_W ? 1 : 0);
   if (b.shape.M <= 0 || n_out <= 0) return 0;
   const bool big = b.shape.M > 1024;
+  RLMD_CHECK(!big || (!b.prob[0].head_w && !b.prob[1].head_w), "fused head only on mini-batch GEMMs");
   const int T = big ? 64 : 32;
   dim3 grid((n_out + T - 1) / T, (b.shape.M + T - 1) / T, groups * b.splits);
 #define RLMD_GEMM_CASE(P, M)                                                                  \
@@ -294,7 +318,7 @@ int rlmd_gemm(int32_t prec, int32_t mode, int32_t M, int32_t N, int32_t K, int32
               void* stream) {
   rlmd::GemmBatch b{};
   b.shape = {M, N, K, relu};
-  b.prob[0] = {A, lda, B, ldb, bias, C, ldc, mask, ldm, bias_grad};
+  b.prob[0] = {A, lda, B, ldb, bias, C, ldc, mask, ldm, bias_grad, nullptr, nullptr};
   b.splits = 1;
   return rlmd::gemm_launch(prec, mode, b, 1, (hipStream_t)stream);
 }

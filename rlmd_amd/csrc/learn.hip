@@ -73,6 +73,40 @@ __device__ float block_max(float v, float* red) {
 
 __device__ float block_min(float v, float* red) { return -block_max(-v, red); }
 
+// Block all-reduce of NS sums and NM maxima at once (2 barriers).  Each wave
+// reduces with shuffles; every thread then combines the per-wave partials in
+// wave order (deterministic).  red: >= 16 * (NS + NM) floats.
+template <int NS, int NM>
+__device__ void block_allreduce(float* sm, float* mx, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int v = 0; v < NS; ++v) sm[v] = wave_sum(sm[v]);
+#pragma unroll
+  for (int v = 0; v < NM; ++v)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx[v] = fmaxf(mx[v], __shfl_xor(mx[v], o, 64));
+  __syncthreads();
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < NS; ++v) red[v * 16 + w] = sm[v];
+#pragma unroll
+    for (int v = 0; v < NM; ++v) red[(NS + v) * 16 + w] = mx[v];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < NS; ++v) {
+    float t = 0.f;
+    for (int q = 0; q < nw; ++q) t += red[v * 16 + q];
+    sm[v] = t;
+  }
+#pragma unroll
+  for (int v = 0; v < NM; ++v) {
+    float t = -INFINITY;
+    for (int q = 0; q < nw; ++q) t = fmaxf(t, red[(NS + v) * 16 + q]);
+    mx[v] = t;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // actor heads + policy sampling (networks_sac.py:101-178, :268-285;
 // networks_td3.py:76-91; algo_td3.py:198-223, :327-344).  One wave per row.
@@ -154,55 +188,24 @@ __global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
   if (lane == 0 && h.logp) h.logp[b] = logp;
 }
 
-// q[g][b] = X_g[b] . w_g + bias_g (critic q_value head, networks_sac.py:362).
-struct RowHeadArgs {
-  const float* X[2];
-  const float* w[2];
-  const float* bias[2];
-  float* out[2];
-  int32_t n, H;
-};
-__global__ void __launch_bounds__(256) row_head_kernel(RowHeadArgs r) {
-  const int lane = threadIdx.x & 63;
-  const int b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int g = blockIdx.y;
-  if (b >= r.n) return;
-  const float* x = r.X[g] + (int64_t)b * r.H;
-  float acc = 0.f;
-  for (int k = lane; k < r.H; k += 64) acc = fmaf(x[k], r.w[g][k], acc);
-  acc = wave_sum(acc);
-  if (lane == 0) r.out[g][b] = acc + r.bias[g][0];
-}
-
-// Bootstrapped target (algo_sac.py:347-365 / algo_td3.py:346-359).
-__global__ void critic_target_kernel(const float* qt1, const float* qt2, const float* r,
-                                     const uint8_t* done, const int32_t* eff, const float* logp,
-                                     const LearnState* st, float* y, int n, int algo, float gamma,
-                                     float reward_scale) {
-  const int b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
-  float q1 = qt1[b], q2 = qt2[b];
-  if (done[b]) q1 = q2 = 0.f;
-  const float m = fminf(q1, q2);
-  const int e = eff ? eff[b] : 1;
-  const float ge = powf(gamma, (float)e);
-  if (algo == RLMD_SAC) {
-    const float soft = reward_scale * r[b] + ge * m;
-    y[b] = soft - expf(st->log_alpha) * logp[b];
-  } else {
-    y[b] = r[b] + ge * m;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Critic loss, top-k, tail index, CIM kernel, Nagy scale
 // (tools/critic_loss.py:26-341, loss_function :344-453; algo_sac.py:419-473).
 // One workgroup of 1024 threads; thread b owns mini-batch row b.
 // ---------------------------------------------------------------------------
 struct LossArgs {
-  const float* q[2];
-  const float* y;
+  const float* qpart[2];  // online critics' fused-head partials [tiles][B]
+  const float* qb[2];     // q_value.bias (online)
+  const float* tpart[2];  // target critics' partials [tiles][B]
+  const float* tb[2];     // q_value.bias (target)
+  int32_t tiles;
+  const float* r;
+  const uint8_t* done;
+  const int32_t* eff;
+  const float* logp_next;  // SAC
+  float gamma, reward_scale;
   float* dq[2];
+  float* y_out;  // nullable
   const float* zipf_x;
   float zipf_x2;
   LearnState* st;
@@ -244,103 +247,136 @@ __device__ __forceinline__ void loss_and_grad(int lt, float q, float t, float c,
   }
 }
 
+// Bootstrapped target (algo_sac.py:347-365 / algo_td3.py:346-359) + critic loss,
+// top-k, tail index, CIM kernel and Nagy scale (tools/critic_loss.py:26-453,
+// algo_sac.py:413-473).  One workgroup; thread b owns mini-batch row b.
 __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
   __shared__ uint64_t keys[1024];
-  __shared__ float red[33];
+  __shared__ float red[16 * 12];
   __shared__ float lsel[2][1024];
   __shared__ int rank_of[1024];
-  const int b = threadIdx.x, B = a.B;
+  const int b = threadIdx.x, B = a.B, T = a.tiles;
   const bool in = b < B;
-  const float y = in ? a.y[b] : 0.f;
-  float q[2] = {in ? a.q[0][b] : 0.f, in ? a.q[1][b] : 0.f};
   LearnState* st = a.st;
-  const float scale[2] = {st->cauchy[0], st->cauchy[1]};
-  float kern[2];
-  // CIM kernel size: population std of (t - q)^2 (critic_loss.py:125-140)
-  for (int g = 0; g < 2; ++g) {
-    const float e = in ? (y - q[g]) * (y - q[g]) : 0.f;
-    const float mean = block_sum(e, red) / B;
-    const float dv = in ? (e - mean) * (e - mean) : 0.f;
-    kern[g] = sqrtf(block_sum(dv, red) / B);
+  // -- target and current q from the fused-head partials
+  float y = 0.f, q[2] = {0.f, 0.f};
+  if (in) {
+    float qt[2];
+    for (int g = 0; g < 2; ++g) {
+      float t = 0.f, c = 0.f;
+      for (int u = 0; u < T; ++u) {
+        t += a.tpart[g][(int64_t)u * B + b];
+        c += a.qpart[g][(int64_t)u * B + b];
+      }
+      qt[g] = t + a.tb[g][0];
+      q[g] = c + a.qb[g][0];
+    }
+    if (a.done[b]) qt[0] = qt[1] = 0.f;
+    const float m = fminf(qt[0], qt[1]);
+    const float ge = powf(a.gamma, (float)(a.eff ? a.eff[b] : 1));
+    if (a.algo == RLMD_SAC) y = (a.reward_scale * a.r[b] + ge * m) - expf(st->log_alpha) * a.logp_next[b];
+    else y = a.r[b] + ge * m;
+    if (a.y_out) a.y_out[b] = y;
   }
-  // TCAU 3-sigma truncation (critic_loss.py:26-50): estimated and target zeroed
-  // where they lie more than 3 population std from their mean
-  float yt[2] = {y, y}, qt[2] = {q[0], q[1]};
+  const float scale[2] = {st->cauchy[0], st->cauchy[1]};
+  // -- R1: means of (t - q)^2 (CIM kernel), of y, q (TCAU), Nagy terms; NaN flag
+  const float e0 = (y - q[0]) * (y - q[0]), e1 = (y - q[1]) * (y - q[1]);
+  const float z0 = (y - q[0]) / scale[0], z1 = (y - q[1]) / scale[1];
+  float s1[7] = {in ? e0 : 0.f, in ? e1 : 0.f, in ? y : 0.f, in ? q[0] : 0.f, in ? q[1] : 0.f,
+                 in ? 1.f / (1.f + z0 * z0) : 0.f, in ? 1.f / (1.f + z1 * z1) : 0.f};
+  float m1[1] = {(in && (isnan(q[0]) || isnan(q[1]) || isnan(y))) ? 1.f : 0.f};
+  block_allreduce<7, 1>(s1, m1, red);
+  const float me0 = s1[0] / B, me1 = s1[1] / B, my = s1[2] / B, mq0 = s1[3] / B, mq1 = s1[4] / B;
+  // -- R2: population variances (two-pass, like torch.std(unbiased=False))
+  float s2[5] = {in ? (e0 - me0) * (e0 - me0) : 0.f, in ? (e1 - me1) * (e1 - me1) : 0.f,
+                 in ? (y - my) * (y - my) : 0.f, in ? (q[0] - mq0) * (q[0] - mq0) : 0.f,
+                 in ? (q[1] - mq1) * (q[1] - mq1) : 0.f};
+  float m2[1] = {-INFINITY};
+  block_allreduce<5, 0>(s2, m2, red);
+  const float kern[2] = {sqrtf(s2[0] / B), sqrtf(s2[1] / B)};
+  // TCAU 3-sigma truncation (critic_loss.py:26-50)
+  float yt[2] = {y, y}, qt_[2] = {q[0], q[1]};
   bool qtr[2] = {false, false};
   if (a.loss_type == RLMD_LOSS_TCAU) {
-    const float my = block_sum(in ? y : 0.f, red) / B;
-    const float sy = sqrtf(block_sum(in ? (y - my) * (y - my) : 0.f, red) / B);
-    const bool ytr = fabsf(y - my) > 3.f * sy;
+    const bool ytr = fabsf(y - my) > 3.f * sqrtf(s2[2] / B);
+    const float mq[2] = {mq0, mq1}, sq[2] = {sqrtf(s2[3] / B), sqrtf(s2[4] / B)};
     for (int g = 0; g < 2; ++g) {
-      const float mq = block_sum(in ? q[g] : 0.f, red) / B;
-      const float sq = sqrtf(block_sum(in ? (q[g] - mq) * (q[g] - mq) : 0.f, red) / B);
-      qtr[g] = fabsf(q[g] - mq) > 3.f * sq;
-      qt[g] = qtr[g] ? 0.f : q[g];
+      qtr[g] = fabsf(q[g] - mq[g]) > 3.f * sq[g];
+      qt_[g] = qtr[g] ? 0.f : q[g];
       yt[g] = ytr ? 0.f : y;
     }
   }
   float l[2], dl[2];
   for (int g = 0; g < 2; ++g) {
-    loss_and_grad(a.loss_type, qt[g], yt[g], scale[g], kern[g], l[g], dl[g]);
+    loss_and_grad(a.loss_type, qt_[g], yt[g], scale[g], kern[g], l[g], dl[g]);
     if (qtr[g]) dl[g] = 0.f;
   }
-  // top-k by l1 + l2, descending (critic_loss.py:438-441)
+  // -- top-k rows by l1 + l2, descending (critic_loss.py:438-441)
   const int k = B > a.k ? a.k : B;
   int npow = 1;
   while (npow < B) npow <<= 1;
   bool sel = in;
+  int rank = b;
   if (B > a.k) {
     const uint64_t key = in ? ((uint64_t)(~f2key(l[0] + l[1])) << 32) | (uint32_t)b : ~0ull;
     const uint64_t sk = rlmd_block_bitonic(key, npow, keys);
     __syncthreads();
-    if (b < B) rank_of[(int)(sk & 0xffffffffu)] = b;  // rank of row -> selected if < k
+    if (b < B) rank_of[(int)(sk & 0xffffffffu)] = b;
     __syncthreads();
-    sel = in && rank_of[b] < k;
+    rank = in ? rank_of[b] : B;
+    sel = in && rank < k;
   }
-  // aggregate per critic: mean / min / max over the selected losses and the
-  // Zipf-plot tail index of their order statistics (critic_loss.py:238-341)
-  for (int g = 0; g < 2; ++g) {
-    const float mean = block_sum(sel ? l[g] : 0.f, red) / k;
-    const float mn = block_min(sel ? l[g] : INFINITY, red);
-    const float mx = block_max(sel ? l[g] : -INFINITY, red);
-    // order statistics of the selected losses, descending (sort k keys: the
-    // selected rows are first compacted to their rank slots)
-    int kp = 1;
-    while (kp < k) kp <<= 1;
-    __syncthreads();
-    if (sel) lsel[g][B > a.k ? rank_of[b] : b] = l[g];
-    __syncthreads();
-    const uint64_t key = b < k ? ((uint64_t)(~f2key(lsel[g][b])) << 32) | (uint32_t)b : ~0ull;
-    const uint64_t sk = rlmd_block_bitonic(key, kp, keys);
-    float lg = 0.f;
-    if (b < k) lg = logf(lsel[g][(int)(sk & 0xffffffffu)] + a.log_noise);
-    const float lmean = block_sum(b < k ? lg : 0.f, red) / k;
-    const float num = block_sum(b < k ? a.zipf_x[b] * (lg - lmean) : 0.f, red);
-    const float alpha = 1.f / (num / a.zipf_x2);
-    if (b == 0) {
-      a.stats[0 + g] = mean;
-      a.stats[2 + g] = mn;
-      a.stats[4 + g] = mx;
-      a.stats[6 + g] = NAN;
-      a.stats[8 + g] = alpha;
-    }
-    if (in) a.dq[g][b] = sel ? a.grad_scale * dl[g] / (float)k : 0.f;
+  // -- R3: mean / min / max of the selected losses per critic
+  float s3[2] = {sel ? l[0] : 0.f, sel ? l[1] : 0.f};
+  float m3[4] = {sel ? l[0] : -INFINITY, sel ? l[1] : -INFINITY, sel ? -l[0] : -INFINITY,
+                 sel ? -l[1] : -INFINITY};
+  block_allreduce<2, 4>(s3, m3, red);
+  // -- Zipf-plot tail index of the selected losses' order statistics
+  //    (critic_loss.py:238-266): both critics sorted in one pass, critic g in
+  //    the g-th kp-aligned thread segment
+  int kp = 1;
+  while (kp < k) kp <<= 1;
+  __syncthreads();
+  if (sel) {
+    lsel[0][rank] = l[0];
+    lsel[1][rank] = l[1];
   }
-  // Nagy Cauchy-scale update over the whole mini-batch (critic_loss.py:74-101)
-  float newc[2];
-  for (int g = 0; g < 2; ++g) {
-    const float z = (y - q[g]) / scale[g];
-    const float inv = block_sum(in ? 1.f / (1.f + z * z) : 0.f, red) / B;
-    const float ie = 1.f / inv;
-    newc[g] = ie > 1.f ? scale[g] * sqrtf(ie - 1.f) : scale[g];
+  __syncthreads();
+  const int g_seg = b / kp, slot = b % kp;
+  uint64_t key = ~0ull;
+  if (g_seg < 2 && slot < k) key = ((uint64_t)(~f2key(lsel[g_seg][slot])) << 32) | (uint32_t)slot;
+  const uint64_t sk = rlmd_block_bitonic(key, kp, keys);
+  float lg = 0.f;
+  const bool zin = g_seg < 2 && slot < k;
+  if (zin) lg = logf(lsel[g_seg][(int)(sk & 0xffffffffu)] + a.log_noise);
+  float s4[2] = {zin && g_seg == 0 ? lg : 0.f, zin && g_seg == 1 ? lg : 0.f};
+  float m4[1] = {-INFINITY};
+  block_allreduce<2, 0>(s4, m4, red);
+  const float lmean = zin ? s4[g_seg] / k : 0.f;
+  const float zx = zin ? a.zipf_x[slot] : 0.f;
+  float s5[2] = {zin && g_seg == 0 ? zx * (lg - lmean) : 0.f, zin && g_seg == 1 ? zx * (lg - lmean) : 0.f};
+  block_allreduce<2, 0>(s5, m4, red);
+  // -- gradients of grad_scale * (mean(l1[sel]) + mean(l2[sel])) w.r.t. q
+  if (in) {
+    a.dq[0][b] = sel ? a.grad_scale * dl[0] / (float)k : 0.f;
+    a.dq[1][b] = sel ? a.grad_scale * dl[1] / (float)k : 0.f;
   }
-  const float nanq = block_max(in ? ((isnan(q[0]) || isnan(q[1]) || isnan(y)) ? 1.f : 0.f) : 0.f, red);
   if (b == 0) {
+    float newc[2];
+    for (int g = 0; g < 2; ++g) {  // Nagy Cauchy-scale update (critic_loss.py:74-101)
+      const float ie = 1.f / (s1[5 + g] / B);
+      newc[g] = ie > 1.f ? scale[g] * sqrtf(ie - 1.f) : scale[g];
+      a.stats[0 + g] = s3[g] / k;
+      a.stats[2 + g] = -m3[2 + g];
+      a.stats[4 + g] = m3[g];
+      a.stats[6 + g] = NAN;
+      a.stats[8 + g] = 1.f / (s5[g] / a.zipf_x2);
+    }
     st->cauchy[0] = newc[0];
     st->cauchy[1] = newc[1];
     st->kernel[0] = kern[0];
     st->kernel[1] = kern[1];
-    if (nanq > 0.f) st->nan_flag = 1;
+    if (m1[0] > 0.f) st->nan_flag = 1;
     a.stats[10] = NAN;
     a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
     a.stats[12] = newc[0];
@@ -356,7 +392,9 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
 // dL/dlogp per row.
 // ---------------------------------------------------------------------------
 struct ActorLossArgs {
-  const float* q[2];  // q[1] null for TD3 (critic_1 only)
+  const float* qpart[2];  // fused-head partials [tiles][B]; qpart[1] null for TD3
+  const float* qb[2];
+  int32_t tiles;
   const float* logp;  // SAC
   float* dq[2];
   float* dlogp;
@@ -368,18 +406,25 @@ struct ActorLossArgs {
 
 __global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
   __shared__ uint64_t keys[1024];
-  __shared__ float red[33];
+  __shared__ float red[16 * 4];
   __shared__ int rank_of[1024];
   const int b = threadIdx.x, B = a.B;
   const bool in = b < B;
   LearnState* st = a.st;
   const float alpha = a.algo == RLMD_SAC ? expf(st->log_alpha) : 0.f;
-  float q1 = in ? a.q[0][b] : 0.f;
-  float q2 = (in && a.q[1]) ? a.q[1][b] : q1;
+  float q1 = 0.f, q2 = 0.f;
+  if (in) {
+    for (int u = 0; u < a.tiles; ++u) q1 += a.qpart[0][(int64_t)u * B + b];
+    q1 += a.qb[0][0];
+    if (a.qpart[1]) {
+      for (int u = 0; u < a.tiles; ++u) q2 += a.qpart[1][(int64_t)u * B + b];
+      q2 += a.qb[1][0];
+    } else {
+      q2 = q1;
+    }
+  }
   const float lp = (in && a.logp) ? a.logp[b] : 0.f;
-  float v;
-  if (a.algo == RLMD_SAC) v = fminf(q1, q2) - alpha * lp;
-  else v = q1;
+  const float v = a.algo == RLMD_SAC ? fminf(q1, q2) - alpha * lp : q1;
   const int k = a.topk ? (B < a.k ? B : a.k) : B;
   int npow = 1;
   while (npow < B) npow <<= 1;
@@ -393,7 +438,10 @@ __global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
     __syncthreads();
     sel = in && rank_of[b] < k;
   }
-  const float loss = -block_sum(sel ? v : 0.f, red) / k;
+  float sm[2] = {sel ? v : 0.f, in ? -(lp + a.target_entropy) : 0.f};
+  float mx[1] = {-INFINITY};
+  block_allreduce<2, 0>(sm, mx, red);
+  const float loss = -sm[0] / k;
   const float dv = sel ? -1.f / (float)k : 0.f;
   if (in) {
     if (a.algo == RLMD_SAC) {
@@ -406,12 +454,11 @@ __global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
       a.dq[0][b] = dv;
     }
   }
-  // temperature: d/dlog_alpha mean(-alpha (logp + target_entropy))
-  if (a.algo == RLMD_SAC) {
-    const float tg = block_sum(in ? -(lp + a.target_entropy) : 0.f, red) / B * alpha;
-    if (b == 0) st->pad_temp_grad = tg;
+  if (b == 0) {
+    // temperature: d/dlog_alpha mean(-alpha (logp + target_entropy)) (algo_sac.py:580-587)
+    if (a.algo == RLMD_SAC) st->pad_temp_grad = sm[1] / B * alpha;
+    a.stats[10] = loss;
   }
-  if (b == 0) a.stats[10] = loss;
 }
 
 // ---------------------------------------------------------------------------
@@ -588,12 +635,12 @@ struct Scratch {
   int64_t* idx;
   // target path
   float *ha1, *ha2, *logp_next, *xs2a2;
-  float *tc1[2], *tc2[2], *qt[2], *y;
+  float *tc1[2], *tc2[2], *tpart[2], *y;
   // critic path
-  float *c1[2], *c2[2], *q[2], *dq[2], *dc2[2], *dc1[2];
+  float *c1[2], *c2[2], *qpart[2], *dq[2], *dc2[2], *dc1[2];
   // actor path
   float *h1, *h2, *logp, *xsan, *save;
-  float *e1[2], *e2[2], *qn[2], *dqn[2], *dlogp, *de2[2], *de1[2], *dxa[2];
+  float *e1[2], *e2[2], *qnpart[2], *dqn[2], *dlogp, *de2[2], *de1[2], *dxa[2];
   float *gh, *dh2, *dh1;
   float* stats;  // [16] when the caller passes none
 };
@@ -633,10 +680,13 @@ int agent_alloc(rlmd_agent_s* ag, void** p, size_t bytes) {
 // y = relu?(x W^T + b) for up to two nets of identical shape
 int fwd(rlmd_agent_s* ag, int groups, int M, int N, int K, bool relu, const float* const* X,
         int ldx, const float* const* W, const float* const* bias, float* const* Y,
-        hipStream_t s) {
+        hipStream_t s, const float* const* head_w = nullptr, float* const* head_part = nullptr) {
   GemmBatch b{};
   b.shape = {M, N, K, relu ? 1 : 0};
-  for (int g = 0; g < groups; ++g) b.prob[g] = {X[g], ldx, W[g], K, bias[g], Y[g], N, nullptr, 0, nullptr};
+  for (int g = 0; g < groups; ++g)
+    b.prob[g] = {X[g], ldx, W[g], K, bias[g], Y[g], N, nullptr, 0, nullptr,
+                 head_w ? head_w[g] : nullptr, head_part ? head_part[g] : nullptr};
+  b.splits = 1;
   return gemm_launch(ag->cfg.precision, GEMM_FWD, b, groups, s);
 }
 
@@ -647,7 +697,8 @@ int bwd_x(rlmd_agent_s* ag, int groups, int M, int N, int K, const float* const*
   GemmBatch b{};
   b.shape = {M, N, K, 0};
   for (int g = 0; g < groups; ++g)
-    b.prob[g] = {G[g], ldg, W[g], ldw, nullptr, DX[g], N, mask ? mask[g] : nullptr, N, nullptr};
+    b.prob[g] = {G[g], ldg, W[g], ldw, nullptr, DX[g], N, mask ? mask[g] : nullptr, N, nullptr, nullptr, nullptr};
+  b.splits = 1;
   return gemm_launch(ag->cfg.precision, GEMM_BWD_X, b, groups, s);
 }
 
@@ -656,7 +707,8 @@ int bwd_w(rlmd_agent_s* ag, int groups, int M, int N, int K, const float* const*
           const float* const* X, int ldx, float* const* DW, float* const* DB, hipStream_t s) {
   GemmBatch b{};
   b.shape = {M, N, K, 0};
-  for (int g = 0; g < groups; ++g) b.prob[g] = {G[g], ldg, X[g], ldx, nullptr, DW[g], N, nullptr, 0, DB[g]};
+  for (int g = 0; g < groups; ++g)
+    b.prob[g] = {G[g], ldg, X[g], ldx, nullptr, DW[g], N, nullptr, 0, DB[g], nullptr, nullptr};
   b.splits = RLMD_GRAD_SPLITS;  // batch reduction split 4 ways; Adam sums the slabs
   b.split_stride = ag->n_params;
   return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, groups, s);
@@ -689,22 +741,6 @@ HeadArgs head_args(rlmd_agent_s* ag, const float* params, const float* h2, const
 
 int launch_head(const HeadArgs& h, hipStream_t s) {
   hipLaunchKernelGGL(actor_head_kernel, dim3((h.n + 3) / 4), dim3(256), 0, s, h);
-  RLMD_LAUNCH_CHECK();
-  return 0;
-}
-
-int launch_row_head(int groups, int n, int H, const float* const* X, const float* const* w,
-                    const float* const* bias, float* const* out, hipStream_t s) {
-  RowHeadArgs r{};
-  for (int g = 0; g < groups; ++g) {
-    r.X[g] = X[g];
-    r.w[g] = w[g];
-    r.bias[g] = bias[g];
-    r.out[g] = out[g];
-  }
-  r.n = n;
-  r.H = H;
-  hipLaunchKernelGGL(row_head_kernel, dim3((n + 3) / 4, groups), dim3(256), 0, s, r);
   RLMD_LAUNCH_CHECK();
   return 0;
 }
@@ -766,9 +802,6 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
       h.noise_clip = c.target_policy_clip;
       h.clamp_noise = 1;
     }
-    if (!h.eps_in && !sac) {
-      // TD3 target noise drawn in the head kernel (mode 0 draws when eps_in is null)
-    }
     RLMD_TRY(launch_head(h, st));
     const float* tx[2] = {S_.xs2a2, S_.xs2a2};
     const float* tw1[2] = {Tc[0] + co.w1, Tc[1] + co.w1};
@@ -777,15 +810,8 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     const float* tx2[2] = {S_.tc1[0], S_.tc1[1]};
     const float* tw2[2] = {Tc[0] + co.w2, Tc[1] + co.w2};
     const float* tb2[2] = {Tc[0] + co.b2, Tc[1] + co.b2};
-    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, tx2, H1, tw2, tb2, S_.tc2, st));
-    const float* hx[2] = {S_.tc2[0], S_.tc2[1]};
-    const float* hw[2] = {Tc[0] + co.w3, Tc[1] + co.w3};
-    const float* hb[2] = {Tc[0] + co.b3, Tc[1] + co.b3};
-    RLMD_TRY(launch_row_head(2, B, H2, hx, hw, hb, S_.qt, st));
-    hipLaunchKernelGGL(critic_target_kernel, dim3((B + 255) / 256), dim3(256), 0, st, S_.qt[0],
-                       S_.qt[1], S_.r, S_.done, eff, S_.logp_next, ag->st, S_.y, B, c.algo,
-                       c.gamma, c.reward_scale);
-    RLMD_LAUNCH_CHECK();
+    const float* thw[2] = {Tc[0] + co.w3, Tc[1] + co.w3};  // fused q_value heads
+    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, tx2, H1, tw2, tb2, S_.tc2, st, thw, S_.tpart));
   }
   // ---- critics, loss (algo_sac.py:413-465)
   {
@@ -796,15 +822,24 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     const float* x2[2] = {S_.c1[0], S_.c1[1]};
     const float* w2[2] = {Pc[0] + co.w2, Pc[1] + co.w2};
     const float* b2[2] = {Pc[0] + co.b2, Pc[1] + co.b2};
-    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, x2, H1, w2, b2, S_.c2, st));
-    const float* hx[2] = {S_.c2[0], S_.c2[1]};
     const float* hw[2] = {Pc[0] + co.w3, Pc[1] + co.w3};
-    const float* hb[2] = {Pc[0] + co.b3, Pc[1] + co.b3};
-    RLMD_TRY(launch_row_head(2, B, H2, hx, hw, hb, S_.q, st));
+    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, x2, H1, w2, b2, S_.c2, st, hw, S_.qpart));
+    const float* hx[2] = {S_.c2[0], S_.c2[1]};
     LossArgs la{};
-    la.q[0] = S_.q[0];
-    la.q[1] = S_.q[1];
-    la.y = S_.y;
+    for (int g = 0; g < 2; ++g) {
+      la.qpart[g] = S_.qpart[g];
+      la.qb[g] = Pc[g] + co.b3;
+      la.tpart[g] = S_.tpart[g];
+      la.tb[g] = Tc[g] + co.b3;
+    }
+    la.tiles = (H2 + 31) / 32;
+    la.r = S_.r;
+    la.done = S_.done;
+    la.eff = eff;
+    la.logp_next = S_.logp_next;
+    la.gamma = c.gamma;
+    la.reward_scale = c.reward_scale;
+    la.y_out = S_.y;
     la.dq[0] = S_.dq[0];
     la.dq[1] = S_.dq[1];
     la.zipf_x = ag->zipf_x;
@@ -883,14 +918,15 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     const float* ex2[2] = {S_.e1[0], S_.e1[1]};
     const float* cw2[2] = {Pc[0] + co.w2, Pc[1] + co.w2};
     const float* cb2[2] = {Pc[0] + co.b2, Pc[1] + co.b2};
-    RLMD_TRY(fwd(ag, nq, B, H2, H1, true, ex2, H1, cw2, cb2, S_.e2, st));
-    const float* hx[2] = {S_.e2[0], S_.e2[1]};
     const float* hw[2] = {Pc[0] + co.w3, Pc[1] + co.w3};
-    const float* hb[2] = {Pc[0] + co.b3, Pc[1] + co.b3};
-    RLMD_TRY(launch_row_head(nq, B, H2, hx, hw, hb, S_.qn, st));
+    RLMD_TRY(fwd(ag, nq, B, H2, H1, true, ex2, H1, cw2, cb2, S_.e2, st, hw, S_.qnpart));
+    const float* hx[2] = {S_.e2[0], S_.e2[1]};
     ActorLossArgs al{};
-    al.q[0] = S_.qn[0];
-    al.q[1] = sac ? S_.qn[1] : nullptr;
+    al.qpart[0] = S_.qnpart[0];
+    al.qpart[1] = sac ? S_.qnpart[1] : nullptr;
+    al.qb[0] = Pc[0] + co.b3;
+    al.qb[1] = Pc[1] + co.b3;
+    al.tiles = (H2 + 31) / 32;
     al.logp = sac ? S_.logp : nullptr;
     al.dq[0] = S_.dqn[0];
     al.dq[1] = S_.dqn[1];
@@ -1095,16 +1131,16 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   for (int g = 0; g < 2; ++g) {
     RLMD_ALLOC(s.tc1[g], B * H1);
     RLMD_ALLOC(s.tc2[g], B * H2);
-    RLMD_ALLOC(s.qt[g], B);
+    RLMD_ALLOC(s.tpart[g], B * ((H2 + 31) / 32));
     RLMD_ALLOC(s.c1[g], B * H1);
     RLMD_ALLOC(s.c2[g], B * H2);
-    RLMD_ALLOC(s.q[g], B);
+    RLMD_ALLOC(s.qpart[g], B * ((H2 + 31) / 32));
     RLMD_ALLOC(s.dq[g], B);
     RLMD_ALLOC(s.dc2[g], B * H2);
     RLMD_ALLOC(s.dc1[g], B * H1);
     RLMD_ALLOC(s.e1[g], B * H1);
     RLMD_ALLOC(s.e2[g], B * H2);
-    RLMD_ALLOC(s.qn[g], B);
+    RLMD_ALLOC(s.qnpart[g], B * ((H2 + 31) / 32));
     RLMD_ALLOC(s.dqn[g], B);
     RLMD_ALLOC(s.de2[g], B * H2);
     RLMD_ALLOC(s.de1[g], B * H1);

@@ -10,9 +10,10 @@
 // so a sample is reproducible on the CPU index for index):
 //   M <= 8192: a uniformly random B-subset as the B smallest of M random keys
 //              (one LDS bitonic sort of (philox32 << 32 | index));
-//   M >  8192: draw B candidates with Philox, sort (index, slot) pairs in LDS,
-//              redraw every slot whose index already appeared at a smaller slot,
-//              repeat (collision rate <= B/M <= 1/8 per round).
+//   M >  8192: draw B candidates with Philox, redraw every slot whose index
+//              already appeared at a smaller slot (found through an LDS hash
+//              table whose entries keep the minimum owning slot), repeat
+//              (collision rate <= B/M <= 1/8 per round).
 #include <string.h>
 
 #include <string>
@@ -73,31 +74,40 @@ __global__ void __launch_bounds__(kSampleThreads)
     }
     if (i < B) cand[i] = (int64_t)(keys[i] & 0xFFFFFFFFu);
   } else {
-  if (i < B) {
-    const rlmd_u32x4 v = rlmd_philox(seed, (uint32_t)i, ctr_lo, c2, 0u);
-    cand[i] = (int64_t)rlmd_below(v.x, v.y, (uint64_t)M);
-  }
-  for (int round = 1; round <= kMaxRounds; ++round) {
-    __syncthreads();
-    const uint64_t key = i < B ? (((uint64_t)cand[i] << 11) | (uint64_t)i) : ~0ull;
-    if (i == 0) any_dup = 0;
-    const uint64_t sk = rlmd_block_bitonic(key, kSampleThreads, keys);
-    __syncthreads();
-    keys[i] = sk;
-    __syncthreads();
-    // a sorted key whose index equals its predecessor's is a duplicate slot
-    if (i > 0 && i < B) {
-      const uint64_t cur = keys[i], prev = keys[i - 1];
-      if ((cur >> 11) == (prev >> 11)) {
-        const int slot = (int)(cur & 2047u);
-        const rlmd_u32x4 v = rlmd_philox(seed, (uint32_t)slot, ctr_lo, c2, (uint32_t)round);
-        cand[slot] = (int64_t)rlmd_below(v.x, v.y, (uint64_t)M);
-        any_dup = 1;
-      }
+    // rounds of: hash every candidate into an LDS table; the smallest slot per
+    // index owns it (atomicMin: order-independent); the other slots redraw
+    __shared__ unsigned long long tab_key[2 * kSampleThreads];
+    __shared__ int tab_own[2 * kSampleThreads];
+    constexpr int H = 2 * kSampleThreads;
+    if (i < B) {
+      const rlmd_u32x4 v = rlmd_philox(seed, (uint32_t)i, ctr_lo, c2, 0u);
+      cand[i] = (int64_t)rlmd_below(v.x, v.y, (uint64_t)M);
     }
-    __syncthreads();
-    if (!any_dup) break;
-  }
+    for (int round = 1; round <= kMaxRounds; ++round) {
+      for (int e = i; e < H; e += kSampleThreads) {
+        tab_key[e] = ~0ull;
+        tab_own[e] = 0x7fffffff;
+      }
+      __syncthreads();
+      int h = 0;
+      const unsigned long long c = i < B ? (unsigned long long)cand[i] : 0ull;
+      if (i < B) {
+        h = (int)((c * 0x9E3779B97F4A7C15ull) >> 52) & (H - 1);
+        for (int probe = 0; probe < H; ++probe) {
+          const unsigned long long old = atomicCAS(&tab_key[h], ~0ull, c);
+          if (old == ~0ull || old == c) break;
+          h = (h + 1) & (H - 1);
+        }
+        atomicMin(&tab_own[h], i);
+      }
+      __syncthreads();
+      const bool dup = i < B && tab_own[h] != i;
+      if (dup) {
+        const rlmd_u32x4 v = rlmd_philox(seed, (uint32_t)i, ctr_lo, c2, (uint32_t)round);
+        cand[i] = (int64_t)rlmd_below(v.x, v.y, (uint64_t)M);
+      }
+      if (!__syncthreads_or(dup)) break;
+    }
   }
   __syncthreads();
   if (dev_ctr && i == 0) *dev_ctr = (int32_t)ctr_lo + 1;

@@ -83,7 +83,8 @@ __host__ __device__ __forceinline__ uint64_t rlmd_below(uint32_t a, uint32_t b, 
 // (power of two, n <= blockDim.x) threads; returns this thread's sorted key.
 // Strides < 64 exchange through wave shuffles (no barrier); strides >= 64
 // through `lds` (>= blockDim.x entries).  Every thread of the block must call
-// it (threads >= n sort their own n-aligned segments, harmlessly).
+// it; threads >= n sort their own n-aligned segments, each ascending, so several
+// independent sorts of n keys can share one call.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t rlmd_shfl_xor_u64(uint64_t v, int m) {
   const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
@@ -103,7 +104,10 @@ __device__ inline uint64_t rlmd_block_bitonic(uint64_t key, int n, uint64_t* lds
       } else {
         other = rlmd_shfl_xor_u64(key, j);
       }
-      const bool keep_min = ((i & j) == 0) == ((i & k) == 0);
+      // ascending sub-sequences alternate with descending ones while merging;
+      // the final merge (k == n) is ascending in every n-aligned segment
+      const bool up = k == n || (i & k) == 0;
+      const bool keep_min = ((i & j) == 0) == up;
       key = keep_min ? (key < other ? key : other) : (key < other ? other : key);
     }
   }

@@ -24,6 +24,11 @@ struct GemmProblem {
   const float* mask;  // BWD_X: ReLU mask source [M, N] (element > 0 keeps)
   int32_t ldm;
   float* bias_grad;   // BWD_W: bias gradient [M]
+  // FWD (mini-batch tiles only): fused single-output head.  Each 32-column tile
+  // writes head_part[tile][i] = sum over its columns j of act(C[i, j]) * head_w[j];
+  // consumers add the ceil(N/32) partials in tile order (deterministic).
+  const float* head_w;
+  float* head_part;
 };
 
 struct GemmShape {
