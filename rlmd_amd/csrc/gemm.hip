@@ -12,8 +12,8 @@
 //   v_mfma_f32_16x16x4_f32   (RLMD_FP32: exact f32 fmaf chain, parity mode) or
 //   v_mfma_f32_16x16x32_bf16 (RLMD_BF16: bf16 operands, f32 accumulate).
 // 256 threads = 4 waves, each wave owns a 32x32 output sub-tile (2x2 MFMA
-// blocks).  Up to two independent problems (the twin critics) share a launch
-// through gridDim.z.
+// blocks).  Up to six independent problems of different shapes (e.g. every
+// weight gradient of both critics) share a launch through blockIdx.x.
 #include "rlmd_common.h"
 #include "rlmd_gemm.h"
 
@@ -152,9 +152,13 @@ template <int PREC, int MODE, int BM, int BK>
 __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
   constexpr int BN = BM;
   constexpr int MB = BM / 32;  // 16x16 MFMA blocks per wave per dimension (waves are 2 x 2)
-  const int group = blockIdx.z % batch.groups, split = blockIdx.z / batch.groups;
-  rlmd::GemmProblem p = group == 0 ? batch.prob[0] : batch.prob[1];
-  const rlmd::GemmShape s = batch.shape;
+  const int split = blockIdx.z;
+  int pi = 0;
+  while (pi + 1 < batch.nprob && (int)blockIdx.x >= batch.tile_begin[pi + 1]) ++pi;
+  rlmd::GemmProblem p = batch.prob[pi];
+  const rlmd::GemmShape s = batch.shape[pi];
+  const int tile = (int)blockIdx.x - batch.tile_begin[pi];
+  const int tile_x = tile % batch.tiles_n[pi], tile_y = tile / batch.tiles_n[pi];
   // split-K (weight gradients): split `split` reduces rows [r_beg, r_end) of the
   // batch and writes its own partial slab; the optimiser sums the slabs in order
   const int chunk = (s.K + batch.splits - 1) / batch.splits;
@@ -163,7 +167,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
     p.C += (int64_t)split * batch.split_stride;
     if (p.bias_grad) p.bias_grad += (int64_t)split * batch.split_stride;
   }
-  const int i0 = blockIdx.y * BM, j0 = blockIdx.x * BN;
+  const int i0 = tile_y * BM, j0 = tile_x * BN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 1, wc = wave & 1;
   f32x4 acc[MB][MB];
@@ -269,7 +273,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
       }
       __syncthreads();
       if (threadIdx.x < 32 && i0 + (int)threadIdx.x < s.M)
-        p.head_part[(int64_t)blockIdx.x * s.M + i0 + threadIdx.x] = hp[0][threadIdx.x] + hp[1][threadIdx.x];
+        p.head_part[(int64_t)tile_x * s.M + i0 + threadIdx.x] = hp[0][threadIdx.x] + hp[1][threadIdx.x];
     }
   }
 }
@@ -278,18 +282,26 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
 
 namespace rlmd {
 
-int gemm_launch(int prec, int mode, const GemmBatch& b_in, int groups, hipStream_t stream) {
-  RLMD_CHECK(groups >= 1 && groups <= RLMD_GEMM_MAX_GROUPS, "bad GEMM group count");
+int gemm_launch(int prec, int mode, const GemmBatch& b_in, hipStream_t stream) {
+  RLMD_CHECK(b_in.nprob >= 1 && b_in.nprob <= RLMD_GEMM_MAX_PROBS, "bad GEMM problem count");
   GemmBatch b = b_in;
-  b.groups = groups;
   if (b.splits < 1) b.splits = 1;
   RLMD_CHECK(mode == GEMM_BWD_W || b.splits == 1, "split-K only for weight gradients");
-  const int n_out = b.shape.N + (mode == GEMM_BWD_W ? 1 : 0);
-  if (b.shape.M <= 0 || n_out <= 0) return 0;
-  const bool big = b.shape.M > 1024;
-  RLMD_CHECK(!big || (!b.prob[0].head_w && !b.prob[1].head_w), "fused head only on mini-batch GEMMs");
+  bool big = false;
+  for (int i = 0; i < b.nprob; ++i) big = big || b.shape[i].M > 1024;
   const int T = big ? 64 : 32;
-  dim3 grid((n_out + T - 1) / T, (b.shape.M + T - 1) / T, groups * b.splits);
+  int tiles = 0;
+  for (int i = 0; i < b.nprob; ++i) {
+    RLMD_CHECK(!big || !b.prob[i].head_w, "fused head only on mini-batch GEMMs");
+    const int n_out = b.shape[i].N + (mode == GEMM_BWD_W ? 1 : 0);
+    const bool empty = b.shape[i].M <= 0 || n_out <= 0;
+    b.tiles_n[i] = empty ? 1 : (n_out + T - 1) / T;
+    b.tile_begin[i] = tiles;
+    tiles += empty ? 0 : b.tiles_n[i] * ((b.shape[i].M + T - 1) / T);
+  }
+  b.tile_begin[b.nprob] = tiles;
+  if (tiles == 0) return 0;
+  dim3 grid(tiles, 1, b.splits);
 #define RLMD_GEMM_CASE(P, M)                                                                  \
   if (prec == P && mode == M) {                                                               \
     if (big) hipLaunchKernelGGL((gemm_kernel<P, M, 64, 64>), grid, dim3(256), 0, stream, b);  \
@@ -317,10 +329,9 @@ int rlmd_gemm(int32_t prec, int32_t mode, int32_t M, int32_t N, int32_t K, int32
               float* C, int32_t ldc, const float* mask, int32_t ldm, float* bias_grad,
               void* stream) {
   rlmd::GemmBatch b{};
-  b.shape = {M, N, K, relu};
-  b.prob[0] = {A, lda, B, ldb, bias, C, ldc, mask, ldm, bias_grad, nullptr, nullptr};
+  rlmd::gemm_add(b, {M, N, K, relu}, {A, lda, B, ldb, bias, C, ldc, mask, ldm, bias_grad, nullptr, nullptr});
   b.splits = 1;
-  return rlmd::gemm_launch(prec, mode, b, 1, (hipStream_t)stream);
+  return rlmd::gemm_launch(prec, mode, b, (hipStream_t)stream);
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@
 // All per-update scalars (Cauchy scales, log alpha, learn counter) stay on the
 // device in LearnState; nothing synchronises with the host inside learn().
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -462,76 +463,6 @@ __global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Policy backward through sampling + heads (autograd of networks_sac.py:163-178
-// / networks_td3.py:91).  One wave per row.  Input dxa_g: dL/da from critic g
-// (BWD_X of the critics restricted to the action columns).  Output: head
-// gradients gh [n, 2A] (dmu | dlog_scale_raw) and dH2 [n, H2] (ReLU-masked).
-// ---------------------------------------------------------------------------
-struct ActorBwdArgs {
-  const float* dxa[2];  // [n, A] each; dxa[1] null for TD3
-  const float* dlogp;   // SAC
-  const float* save;    // [n, 5A]
-  const float* h2;
-  const float* params;
-  NetOff off;
-  float* gh;   // [n, 2A]
-  float* dh2;  // [n, H2]
-  int32_t n, A, algo;
-  float max_action, ls_min, ls_max, reparam_noise;
-};
-
-__global__ void __launch_bounds__(256) actor_bwd_kernel(ActorBwdArgs a) {
-  __shared__ float gsh[4][2 * RLMD_MAX_ACTION];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b = blockIdx.x * 4 + w;
-  const bool valid = b < a.n;  // wave-uniform
-  const int A = a.A;
-  if (valid) {
-    const float* sv = a.save + (int64_t)b * 5 * A;
-    for (int j = lane; j < A; j += 64) {
-      const float da = a.dxa[0][(int64_t)b * A + j] + (a.dxa[1] ? a.dxa[1][(int64_t)b * A + j] : 0.f);
-      if (a.algo == RLMD_SAC) {
-        const float mu = sv[j], sigma = sv[A + j], eps = sv[2 * A + j], u = sv[3 * A + j];
-        const float ls_raw = sv[4 * A + j];
-        const float dlp = a.dlogp[b];
-        const float t = tanhf(u);
-        const float om = 1.f - t * t;
-        const float d = u - mu;
-        // logp = -d^2/(2 s^2) - log s - c - log(1 - t^2 + noise), u = mu + eps s
-        const float dlogp_du = -d / (sigma * sigma) + 2.f * t * om / (om + a.reparam_noise);
-        const float du = da * a.max_action * om + dlp * dlogp_du;
-        const float dmu = du + dlp * (d / (sigma * sigma));
-        const float dsig = du * eps + dlp * ((d * d) / (sigma * sigma * sigma) - 1.f / sigma);
-        const bool live = ls_raw >= a.ls_min && ls_raw <= a.ls_max;  // clamp passes [min, max]
-        const float dls = live ? dsig * sigma : 0.f;
-        gsh[w][j] = dmu;
-        gsh[w][A + j] = dls;
-        a.gh[(int64_t)b * 2 * A + j] = dmu;
-        a.gh[(int64_t)b * 2 * A + A + j] = dls;
-      } else {
-        const float t = tanhf(sv[j]);
-        const float dpre = da * a.max_action * (1.f - t * t);
-        gsh[w][j] = dpre;
-        a.gh[(int64_t)b * 2 * A + j] = dpre;
-      }
-    }
-  }
-  __syncthreads();
-  if (!valid) return;
-  const NetOff& o = a.off;
-  const int H = o.h2;
-  for (int kx = lane; kx < H; kx += 64) {
-    float acc = 0.f;
-    for (int j = 0; j < A; ++j) {
-      acc = fmaf(gsh[w][j], a.params[o.w3 + (int64_t)j * H + kx], acc);
-      if (a.algo == RLMD_SAC) acc = fmaf(gsh[w][A + j], a.params[o.w4 + (int64_t)j * H + kx], acc);
-    }
-    const float hv = a.h2[(int64_t)b * H + kx];
-    a.dh2[(int64_t)b * H + kx] = hv > 0.f ? acc : 0.f;
-  }
-}
-
-// ---------------------------------------------------------------------------
 // Adam (torch.optim.Adam defaults, _single_tensor_adam) + optional Polyak
 // target update (algo_sac.py:597-615) + optional temperature Adam.
 // ---------------------------------------------------------------------------
@@ -551,7 +482,26 @@ struct AdamArgs {
   float lr_temp;
   int32_t temp_interval;
   float* stats;
+  // compute copies of fc2.weight (rows.hip RowNet) refreshed for the updated
+  // nets: net = i / net_size (ncopy nets), element (n, k) of its fc2.weight
+  int32_t ncopy, bf16;
+  int64_t net_size, w2_off;
+  int32_t H1, H2, H1p, H2p;
+  void* wc[2];
+  void* wt[2];
+  void* twc[2];  // Polyak targets' copies (nullable)
+  void* twt[2];
 };
+
+__device__ __forceinline__ void store_copy(void* base, int64_t i, float v, int bf16) {
+  if (bf16) {
+    unsigned u = __float_as_uint(v);
+    u += 0x7fffu + ((u >> 16) & 1u);  // RNE (finite weights)
+    static_cast<unsigned short*>(base)[i] = (unsigned short)(u >> 16);
+  } else {
+    static_cast<float*>(base)[i] = v;
+  }
+}
 
 __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
   const int cnt = a.st->learn_cntr;
@@ -575,7 +525,24 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
     const float denom = sqrtf(v) / bc2_sqrt + eps;
     const float p = a.p[i] - step_size * (m / denom);
     a.p[i] = p;
-    if (polyak) a.target[i] = a.tau * p + (1.f - a.tau) * a.target[i];
+    float tv = 0.f;
+    if (polyak) {
+      tv = a.tau * p + (1.f - a.tau) * a.target[i];
+      a.target[i] = tv;
+    }
+    if (a.ncopy) {
+      const int net = (int)(i / a.net_size);
+      const int64_t j = i - net * a.net_size - a.w2_off;
+      if (net < a.ncopy && j >= 0 && j < (int64_t)a.H1 * a.H2) {
+        const int n = (int)(j / a.H1), k = (int)(j - (int64_t)n * a.H1);
+        store_copy(a.wc[net], (int64_t)n * a.H1p + k, p, a.bf16);
+        store_copy(a.wt[net], (int64_t)k * a.H2p + n, p, a.bf16);
+        if (polyak && a.twc[net]) {
+          store_copy(a.twc[net], (int64_t)n * a.H1p + k, tv, a.bf16);
+          store_copy(a.twt[net], (int64_t)k * a.H2p + n, tv, a.bf16);
+        }
+      }
+    }
   }
   if (a.temp && blockIdx.x == 0 && threadIdx.x == 0) {
     LearnState* st = a.st;
@@ -633,14 +600,13 @@ struct Scratch {
   float *s, *a, *r, *s2, *xsa;
   uint8_t* done;
   int64_t* idx;
-  // target path
-  float *ha1, *ha2, *logp_next, *xs2a2;
-  float *tc1[2], *tc2[2], *tpart[2], *y;
+  // target path: target q per row (no head bias), logp of the next actions
+  float *logp_next, *tpart[2], *y;
   // critic path
   float *c1[2], *c2[2], *qpart[2], *dq[2], *dc2[2], *dc1[2];
   // actor path
   float *h1, *h2, *logp, *xsan, *save;
-  float *e1[2], *e2[2], *qnpart[2], *dqn[2], *dlogp, *de2[2], *de1[2], *dxa[2];
+  float *e1[2], *e2[2], *qnpart[2], *dqn[2], *dlogp;
   float *gh, *dh2, *dh1;
   float* stats;  // [16] when the caller passes none
 };
@@ -658,7 +624,12 @@ struct rlmd_agent_s {
   float zipf_x2;
   rlmd::Scratch sc;
   std::vector<void*> allocs;
+  // fc2.weight compute copies (rows.hip RowNet), slot x {wc, wt}:
+  // 0 actor, 1 target actor, 2/3 critics, 4/5 target critics
+  unsigned char* wcopy = nullptr;
+  size_t wcopy_bytes = 0;  // per copy
   float *act_h1 = nullptr, *act_h2 = nullptr;
+  unsigned short* act_w2bf = nullptr;  // fused acting: bf16 copy of the actor's fc2.weight
   int64_t act_cap = 0;
   int64_t host_cntr = 0;
 };
@@ -682,36 +653,25 @@ int fwd(rlmd_agent_s* ag, int groups, int M, int N, int K, bool relu, const floa
         int ldx, const float* const* W, const float* const* bias, float* const* Y,
         hipStream_t s, const float* const* head_w = nullptr, float* const* head_part = nullptr) {
   GemmBatch b{};
-  b.shape = {M, N, K, relu ? 1 : 0};
   for (int g = 0; g < groups; ++g)
-    b.prob[g] = {X[g], ldx, W[g], K, bias[g], Y[g], N, nullptr, 0, nullptr,
-                 head_w ? head_w[g] : nullptr, head_part ? head_part[g] : nullptr};
+    gemm_add(b, {M, N, K, relu ? 1 : 0},
+             {X[g], ldx, W[g], K, bias[g], Y[g], N, nullptr, 0, nullptr, head_w ? head_w[g] : nullptr,
+              head_part ? head_part[g] : nullptr});
   b.splits = 1;
-  return gemm_launch(ag->cfg.precision, GEMM_FWD, b, groups, s);
+  return gemm_launch(ag->cfg.precision, GEMM_FWD, b, s);
 }
 
-// dX = mask(G W): G [M, K] (ldg), W [K, N] rows of stride ldw
-int bwd_x(rlmd_agent_s* ag, int groups, int M, int N, int K, const float* const* G, int ldg,
-          const float* const* W, int ldw, const float* const* mask, float* const* DX,
-          hipStream_t s) {
-  GemmBatch b{};
-  b.shape = {M, N, K, 0};
-  for (int g = 0; g < groups; ++g)
-    b.prob[g] = {G[g], ldg, W[g], ldw, nullptr, DX[g], N, mask ? mask[g] : nullptr, N, nullptr, nullptr, nullptr};
-  b.splits = 1;
-  return gemm_launch(ag->cfg.precision, GEMM_BWD_X, b, groups, s);
+// dW [M=out, N=in] = G^T X over K = batch rows; db = colsum(G).  Appends to a
+// multi-problem batch launched once per phase (gemm_launch, RLMD_GRAD_SPLITS slabs).
+void add_bwd_w(GemmBatch& b, int M, int N, int K, const float* G, int ldg, const float* X, int ldx,
+               float* DW, float* DB) {
+  gemm_add(b, {M, N, K, 0}, {G, ldg, X, ldx, nullptr, DW, N, nullptr, 0, DB, nullptr, nullptr});
 }
 
-// dW [M=out, N=in] = G^T X over K = batch rows; db = colsum(G)
-int bwd_w(rlmd_agent_s* ag, int groups, int M, int N, int K, const float* const* G, int ldg,
-          const float* const* X, int ldx, float* const* DW, float* const* DB, hipStream_t s) {
-  GemmBatch b{};
-  b.shape = {M, N, K, 0};
-  for (int g = 0; g < groups; ++g)
-    b.prob[g] = {G[g], ldg, X[g], ldx, nullptr, DW[g], N, nullptr, 0, DB[g], nullptr, nullptr};
+int launch_bwd_w(rlmd_agent_s* ag, GemmBatch& b, hipStream_t s) {
   b.splits = RLMD_GRAD_SPLITS;  // batch reduction split 4 ways; Adam sums the slabs
   b.split_stride = ag->n_params;
-  return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, groups, s);
+  return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, s);
 }
 
 #define RLMD_TRY(x)         \
@@ -752,8 +712,69 @@ int adam_launch(const AdamArgs& a, hipStream_t s) {
   return 0;
 }
 
+enum { SLOT_ACTOR = 0, SLOT_TACTOR = 1, SLOT_C0 = 2, SLOT_TC0 = 4 };
+
+RowDims row_dims(const rlmd_agent_s* ag) {
+  const rlmd_agent_cfg& c = ag->cfg;
+  RowDims d{};
+  d.S = c.state_dim;
+  d.A = c.action_dim;
+  d.X = c.state_dim + c.action_dim;
+  d.H1 = c.h1;
+  d.H2 = c.h2;
+  d.H1p = pad32(c.h1);
+  d.H2p = pad32(c.h2);
+  d.B = c.batch;
+  d.algo = c.algo;
+  d.prec = c.precision;
+  return d;
+}
+
+void* copy_wc(rlmd_agent_s* ag, int slot) { return ag->wcopy + (size_t)(2 * slot) * ag->wcopy_bytes; }
+void* copy_wt(rlmd_agent_s* ag, int slot) { return ag->wcopy + (size_t)(2 * slot + 1) * ag->wcopy_bytes; }
+
+RowNet row_net(rlmd_agent_s* ag, int slot) {
+  const float* base = (slot == SLOT_TACTOR || slot >= SLOT_TC0) ? ag->target : ag->params;
+  const int64_t off = slot <= SLOT_TACTOR ? ag->off_actor : ag->off_c[(slot - SLOT_C0) & 1];
+  return RowNet{base + off, copy_wc(ag, slot), copy_wt(ag, slot)};
+}
+
+// Re-derive every compute copy from the f32 masters (start of each learn call:
+// the host may have written parameters through the tensor views in between).
+int refresh_copies(rlmd_agent_s* ag, hipStream_t st) {
+  CopyJob jobs[6];
+  for (int slot = 0; slot < 6; ++slot) {
+    const RowNet n = row_net(ag, slot);
+    const NetOff& o = slot <= SLOT_TACTOR ? ag->actor : ag->critic;
+    jobs[slot] = CopyJob{n.p + o.w2, copy_wc(ag, slot), copy_wt(ag, slot)};
+  }
+  return w2_copies_launch(jobs, 6, row_dims(ag), st);
+}
+
+void adam_copies(rlmd_agent_s* ag, AdamArgs& ad, const NetOff& o, int slot0, int n, bool targets) {
+  const rlmd_agent_cfg& c = ag->cfg;
+  ad.ncopy = n;
+  ad.bf16 = c.precision == RLMD_BF16;
+  ad.net_size = o.size;
+  ad.w2_off = o.w2;
+  ad.H1 = c.h1;
+  ad.H2 = c.h2;
+  ad.H1p = pad32(c.h1);
+  ad.H2p = pad32(c.h2);
+  const int tslot0 = slot0 == SLOT_ACTOR ? SLOT_TACTOR : SLOT_TC0;
+  for (int i = 0; i < n; ++i) {
+    ad.wc[i] = copy_wc(ag, slot0 + i);
+    ad.wt[i] = copy_wt(ag, slot0 + i);
+    ad.twc[i] = targets ? copy_wc(ag, tslot0 + i) : nullptr;
+    ad.twt[i] = targets ? copy_wt(ag, tslot0 + i) : nullptr;
+  }
+}
+
 // One learn() on the mini-batch already in ag->sc (s, r, s2, done, xsa).
 // eps_a / eps_b: injected noise (nullable).  stats: [16] device.
+// Launches (SAC, actor step): fwd rows | critic loss | critic bwd rows | critic
+// dW | Adam critics | q rows on (s, a_new) | actor loss | actor bwd rows |
+// actor dW | Adam actor (+ temperature).
 int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const float* eps_b,
                float* stats, hipStream_t st) {
   const rlmd_agent_cfg& c = ag->cfg;
@@ -766,65 +787,58 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
   const NetOff& ao = ag->actor;
   const NetOff& co = ag->critic;
   const int64_t cntr = ++ag->host_cntr;  // learn_step_cntr after this update's increment
-
-  float* Pa = P + ag->off_actor;
-  float* Ta = T + ag->off_actor;
+  const bool actor_step = cntr % c.actor_update_interval == 0;
+  const int nq = sac ? 2 : 1;
+  const RowDims d = row_dims(ag);
+  const SampleCfg smp{c.seed, &ag->st->learn_cntr, c.max_action, c.log_scale_min, c.log_scale_max,
+                      c.reparam_noise};
   float* Pc[2] = {P + ag->off_c[0], P + ag->off_c[1]};
   float* Tc[2] = {T + ag->off_c[0], T + ag->off_c[1]};
   float* Gc[2] = {G + ag->off_c[0], G + ag->off_c[1]};
   float* Ga = G + ag->off_actor;
+  const RowNet crit[2] = {row_net(ag, SLOT_C0), row_net(ag, SLOT_C0 + 1)};
 
-  // ---- target (algo_sac.py:300-367 / algo_td3.py:302-361)
+  // ---- forward rows: target path (algo_sac.py:300-367 / algo_td3.py:302-361),
+  //      critics on (s, a) (algo_sac.py:413-417), policy on s for the actor step
   {
-    const float* pa = sac ? Pa : Ta;  // SAC samples next actions from the online actor
-    const float* x[1] = {S_.s2};
-    const float* w1[1] = {pa + ao.w1};
-    const float* b1[1] = {pa + ao.b1};
-    float* y1[1] = {S_.ha1};
-    RLMD_TRY(fwd(ag, 1, B, H1, S, true, x, S, w1, b1, y1, st));
-    const float* x2[1] = {S_.ha1};
-    const float* w2[1] = {pa + ao.w2};
-    const float* b2[1] = {pa + ao.b2};
-    float* y2[1] = {S_.ha2};
-    RLMD_TRY(fwd(ag, 1, B, H2, H1, true, x2, H1, w2, b2, y2, st));
-    HeadArgs h = head_args(ag, pa, S_.ha2, S_.s2, B);
-    h.xsa = S_.xs2a2;
-    h.logp = S_.logp_next;
-    h.ctr = &ag->st->learn_cntr;
-    h.mode = 0;
-    if (sac) {
-      h.eps_in = eps_a;
-      h.tag = RLMD_TAG_EPS_NEXT;
-    } else {
-      h.eps_in = eps_a;
-      h.tag = RLMD_TAG_TD3_TARGET;
-      h.noise_std = c.target_policy_noise;
-      h.noise_clip = c.target_policy_clip;
-      h.clamp_noise = 1;
+    FwdRowsArgs f{};
+    f.d = d;
+    f.ao = ao;
+    f.co = co;
+    f.smp = smp;
+    f.tactor = row_net(ag, sac ? SLOT_ACTOR : SLOT_TACTOR);  // SAC samples next actions from the online actor
+    f.tcrit[0] = row_net(ag, SLOT_TC0);
+    f.tcrit[1] = row_net(ag, SLOT_TC0 + 1);
+    f.s2 = S_.s2;
+    f.eps_next = eps_a;
+    f.t_tag = sac ? RLMD_TAG_EPS_NEXT : RLMD_TAG_TD3_TARGET;
+    f.t_clamp = sac ? 0 : 1;
+    f.t_noise_std = c.target_policy_noise;
+    f.t_noise_clip = c.target_policy_clip;
+    f.logp_next = S_.logp_next;
+    for (int g = 0; g < 2; ++g) {
+      f.qt[g] = S_.tpart[g];
+      f.crit[g] = crit[g];
+      f.c1[g] = S_.c1[g];
+      f.c2[g] = S_.c2[g];
+      f.q[g] = S_.qpart[g];
     }
-    RLMD_TRY(launch_head(h, st));
-    const float* tx[2] = {S_.xs2a2, S_.xs2a2};
-    const float* tw1[2] = {Tc[0] + co.w1, Tc[1] + co.w1};
-    const float* tb1[2] = {Tc[0] + co.b1, Tc[1] + co.b1};
-    RLMD_TRY(fwd(ag, 2, B, H1, X, true, tx, X, tw1, tb1, S_.tc1, st));
-    const float* tx2[2] = {S_.tc1[0], S_.tc1[1]};
-    const float* tw2[2] = {Tc[0] + co.w2, Tc[1] + co.w2};
-    const float* tb2[2] = {Tc[0] + co.b2, Tc[1] + co.b2};
-    const float* thw[2] = {Tc[0] + co.w3, Tc[1] + co.w3};  // fused q_value heads
-    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, tx2, H1, tw2, tb2, S_.tc2, st, thw, S_.tpart));
+    f.xsa = S_.xsa;
+    f.with_actor = actor_step ? 1 : 0;
+    f.a_mode = sac ? 0 : 1;  // TD3 actor.forward: tanh(mu) * max_action, no noise
+    f.a_tag = RLMD_TAG_EPS_CUR;
+    f.actor = row_net(ag, SLOT_ACTOR);
+    f.s = S_.s;
+    f.eps_cur = eps_b;
+    f.h1a = S_.h1;
+    f.h2a = S_.h2;
+    f.xsan = S_.xsan;
+    f.logp = S_.logp;
+    f.save = S_.save;
+    RLMD_TRY(fwd_rows_launch(f, st));
   }
-  // ---- critics, loss (algo_sac.py:413-465)
+  // ---- critic loss (algo_sac.py:413-465)
   {
-    const float* x[2] = {S_.xsa, S_.xsa};
-    const float* w1[2] = {Pc[0] + co.w1, Pc[1] + co.w1};
-    const float* b1[2] = {Pc[0] + co.b1, Pc[1] + co.b1};
-    RLMD_TRY(fwd(ag, 2, B, H1, X, true, x, X, w1, b1, S_.c1, st));
-    const float* x2[2] = {S_.c1[0], S_.c1[1]};
-    const float* w2[2] = {Pc[0] + co.w2, Pc[1] + co.w2};
-    const float* b2[2] = {Pc[0] + co.b2, Pc[1] + co.b2};
-    const float* hw[2] = {Pc[0] + co.w3, Pc[1] + co.w3};
-    RLMD_TRY(fwd(ag, 2, B, H2, H1, true, x2, H1, w2, b2, S_.c2, st, hw, S_.qpart));
-    const float* hx[2] = {S_.c2[0], S_.c2[1]};
     LossArgs la{};
     for (int g = 0; g < 2; ++g) {
       la.qpart[g] = S_.qpart[g];
@@ -832,7 +846,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
       la.tpart[g] = S_.tpart[g];
       la.tb[g] = Tc[g] + co.b3;
     }
-    la.tiles = (H2 + 31) / 32;
+    la.tiles = 1;
     la.r = S_.r;
     la.done = S_.done;
     la.eff = eff;
@@ -854,21 +868,28 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     la.grad_scale = sac ? 0.5f : 1.0f;  // SAC: 0.5 (q1_loss + q2_loss)
     hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, st, la);
     RLMD_LAUNCH_CHECK();
-    // backward (both critics in one launch per layer)
-    const float* g3[2] = {S_.dq[0], S_.dq[1]};
-    float* dw3[2] = {Gc[0] + co.w3, Gc[1] + co.w3};
-    float* db3[2] = {Gc[0] + co.b3, Gc[1] + co.b3};
-    RLMD_TRY(bwd_w(ag, 2, 1, H2, B, g3, 1, hx, H2, dw3, db3, st));
-    RLMD_TRY(bwd_x(ag, 2, B, H2, 1, g3, 1, hw, H2, hx, S_.dc2, st));
-    const float* g2[2] = {S_.dc2[0], S_.dc2[1]};
-    float* dw2[2] = {Gc[0] + co.w2, Gc[1] + co.w2};
-    float* db2[2] = {Gc[0] + co.b2, Gc[1] + co.b2};
-    RLMD_TRY(bwd_w(ag, 2, H2, H1, B, g2, H2, x2, H1, dw2, db2, st));
-    RLMD_TRY(bwd_x(ag, 2, B, H1, H2, g2, H2, w2, H1, x2, S_.dc1, st));
-    const float* g1[2] = {S_.dc1[0], S_.dc1[1]};
-    float* dw1[2] = {Gc[0] + co.w1, Gc[1] + co.w1};
-    float* db1[2] = {Gc[0] + co.b1, Gc[1] + co.b1};
-    RLMD_TRY(bwd_w(ag, 2, H1, X, B, g1, H1, x, X, dw1, db1, st));
+  }
+  // ---- critic backward: data gradients per row, then all weight gradients
+  {
+    CBwdArgs cb{};
+    cb.d = d;
+    cb.co = co;
+    for (int g = 0; g < 2; ++g) {
+      cb.crit[g] = crit[g];
+      cb.dq[g] = S_.dq[g];
+      cb.c1[g] = S_.c1[g];
+      cb.c2[g] = S_.c2[g];
+      cb.dc2[g] = S_.dc2[g];
+      cb.dc1[g] = S_.dc1[g];
+    }
+    RLMD_TRY(cbwd_rows_launch(cb, st));
+    GemmBatch gb{};
+    for (int g = 0; g < 2; ++g) {
+      add_bwd_w(gb, 1, H2, B, S_.dq[g], 1, S_.c2[g], H2, Gc[g] + co.w3, Gc[g] + co.b3);
+      add_bwd_w(gb, H2, H1, B, S_.dc2[g], H2, S_.c1[g], H1, Gc[g] + co.w2, Gc[g] + co.b2);
+      add_bwd_w(gb, H1, X, B, S_.dc1[g], H1, S_.xsa, X, Gc[g] + co.w1, Gc[g] + co.b1);
+    }
+    RLMD_TRY(launch_bwd_w(ag, gb, st));
     AdamArgs ad{};
     ad.p = Pc[0];
     ad.g = Gc[0];
@@ -882,51 +903,29 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     ad.interval = 1;
     ad.polyak_interval = c.target_critic_update;
     ad.st = ag->st;
+    adam_copies(ag, ad, co, SLOT_C0, 2, true);
     RLMD_TRY(adam_launch(ad, st));
   }
   // ---- actor (+ temperature) update every actor_update_interval
-  if (cntr % c.actor_update_interval != 0) return 0;
+  if (!actor_step) return 0;
   {
-    const int nq = sac ? 2 : 1;
-    const float* x[1] = {S_.s};
-    const float* w1[1] = {Pa + ao.w1};
-    const float* b1[1] = {Pa + ao.b1};
-    float* y1[1] = {S_.h1};
-    RLMD_TRY(fwd(ag, 1, B, H1, S, true, x, S, w1, b1, y1, st));
-    const float* x2[1] = {S_.h1};
-    const float* w2[1] = {Pa + ao.w2};
-    const float* b2[1] = {Pa + ao.b2};
-    float* y2[1] = {S_.h2};
-    RLMD_TRY(fwd(ag, 1, B, H2, H1, true, x2, H1, w2, b2, y2, st));
-    HeadArgs h = head_args(ag, Pa, S_.h2, S_.s, B);
-    h.xsa = S_.xsan;
-    h.logp = S_.logp;
-    h.save = S_.save;
-    h.ctr = &ag->st->learn_cntr;
-    if (sac) {
-      h.mode = 0;
-      h.eps_in = eps_b;
-      h.tag = RLMD_TAG_EPS_CUR;
-    } else {
-      h.mode = 1;  // TD3 actor.forward: tanh(mu) * max_action, no noise
+    QEvalArgs qe{};
+    qe.d = d;
+    qe.co = co;
+    qe.x = S_.xsan;
+    for (int g = 0; g < 2; ++g) {
+      qe.crit[g] = crit[g];
+      qe.e1[g] = S_.e1[g];
+      qe.e2[g] = S_.e2[g];
+      qe.qn[g] = S_.qnpart[g];
     }
-    RLMD_TRY(launch_head(h, st));
-    const float* ex[2] = {S_.xsan, S_.xsan};
-    const float* cw1[2] = {Pc[0] + co.w1, Pc[1] + co.w1};
-    const float* cb1[2] = {Pc[0] + co.b1, Pc[1] + co.b1};
-    RLMD_TRY(fwd(ag, nq, B, H1, X, true, ex, X, cw1, cb1, S_.e1, st));
-    const float* ex2[2] = {S_.e1[0], S_.e1[1]};
-    const float* cw2[2] = {Pc[0] + co.w2, Pc[1] + co.w2};
-    const float* cb2[2] = {Pc[0] + co.b2, Pc[1] + co.b2};
-    const float* hw[2] = {Pc[0] + co.w3, Pc[1] + co.w3};
-    RLMD_TRY(fwd(ag, nq, B, H2, H1, true, ex2, H1, cw2, cb2, S_.e2, st, hw, S_.qnpart));
-    const float* hx[2] = {S_.e2[0], S_.e2[1]};
+    RLMD_TRY(qeval_rows_launch(qe, nq, st));
     ActorLossArgs al{};
     al.qpart[0] = S_.qnpart[0];
     al.qpart[1] = sac ? S_.qnpart[1] : nullptr;
     al.qb[0] = Pc[0] + co.b3;
     al.qb[1] = Pc[1] + co.b3;
-    al.tiles = (H2 + 31) / 32;
+    al.tiles = 1;
     al.logp = sac ? S_.logp : nullptr;
     al.dq[0] = S_.dqn[0];
     al.dq[1] = S_.dqn[1];
@@ -940,57 +939,40 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     al.target_entropy = -(float)A;
     hipLaunchKernelGGL(actor_loss_kernel, dim3(1), dim3(1024), 0, st, al);
     RLMD_LAUNCH_CHECK();
-    // dL/da through the (updated) critics: only the action columns of fc1
-    const float* g3[2] = {S_.dqn[0], S_.dqn[1]};
-    RLMD_TRY(bwd_x(ag, nq, B, H2, 1, g3, 1, hw, H2, hx, S_.de2, st));
-    const float* g2[2] = {S_.de2[0], S_.de2[1]};
-    RLMD_TRY(bwd_x(ag, nq, B, H1, H2, g2, H2, cw2, H1, ex2, S_.de1, st));
-    const float* g1[2] = {S_.de1[0], S_.de1[1]};
-    const float* w1a[2] = {Pc[0] + co.w1 + S, Pc[1] + co.w1 + S};
-    RLMD_TRY(bwd_x(ag, nq, B, A, H1, g1, H1, w1a, X, nullptr, S_.dxa, st));
-    ActorBwdArgs ab{};
-    ab.dxa[0] = S_.dxa[0];
-    ab.dxa[1] = sac ? S_.dxa[1] : nullptr;
+    ABwdArgs ab{};
+    ab.d = d;
+    ab.ao = ao;
+    ab.co = co;
+    ab.smp = smp;
+    ab.nq = nq;
+    for (int g = 0; g < 2; ++g) {
+      ab.crit[g] = crit[g];
+      ab.dqn[g] = S_.dqn[g];
+      ab.e1[g] = S_.e1[g];
+      ab.e2[g] = S_.e2[g];
+    }
+    ab.actor = row_net(ag, SLOT_ACTOR);
     ab.dlogp = S_.dlogp;
     ab.save = S_.save;
-    ab.h2 = S_.h2;
-    ab.params = Pa;
-    ab.off = ao;
+    ab.h1a = S_.h1;
+    ab.h2a = S_.h2;
     ab.gh = S_.gh;
     ab.dh2 = S_.dh2;
-    ab.n = B;
-    ab.A = A;
-    ab.algo = c.algo;
-    ab.max_action = c.max_action;
-    ab.ls_min = c.log_scale_min;
-    ab.ls_max = c.log_scale_max;
-    ab.reparam_noise = c.reparam_noise;
-    hipLaunchKernelGGL(actor_bwd_kernel, dim3((B + 3) / 4), dim3(256), 0, st, ab);
-    RLMD_LAUNCH_CHECK();
-    // head weight gradients (pi and log_scale as two groups)
-    const float* gh[2] = {S_.gh, S_.gh + A};
-    const float* h2x[2] = {S_.h2, S_.h2};
-    float* dwh[2] = {Ga + ao.w3, sac ? Ga + ao.w4 : nullptr};
-    float* dbh[2] = {Ga + ao.b3, sac ? Ga + ao.b4 : nullptr};
-    RLMD_TRY(bwd_w(ag, sac ? 2 : 1, A, H2, B, gh, 2 * A, h2x, H2, dwh, dbh, st));
-    const float* gd2[1] = {S_.dh2};
-    const float* hh1[1] = {S_.h1};
-    float* dw2[1] = {Ga + ao.w2};
-    float* db2[1] = {Ga + ao.b2};
-    RLMD_TRY(bwd_w(ag, 1, H2, H1, B, gd2, H2, hh1, H1, dw2, db2, st));
-    float* dh1[1] = {S_.dh1};
-    RLMD_TRY(bwd_x(ag, 1, B, H1, H2, gd2, H2, w2, H1, hh1, dh1, st));
-    const float* gd1[1] = {S_.dh1};
-    float* dw1[1] = {Ga + ao.w1};
-    float* db1[1] = {Ga + ao.b1};
-    RLMD_TRY(bwd_w(ag, 1, H1, S, B, gd1, H1, x, S, dw1, db1, st));
+    ab.dh1 = S_.dh1;
+    RLMD_TRY(abwd_rows_launch(ab, st));
+    GemmBatch gb{};
+    add_bwd_w(gb, A, H2, B, S_.gh, 2 * A, S_.h2, H2, Ga + ao.w3, Ga + ao.b3);
+    if (sac) add_bwd_w(gb, A, H2, B, S_.gh + A, 2 * A, S_.h2, H2, Ga + ao.w4, Ga + ao.b4);
+    add_bwd_w(gb, H2, H1, B, S_.dh2, H2, S_.h1, H1, Ga + ao.w2, Ga + ao.b2);
+    add_bwd_w(gb, H1, S, B, S_.dh1, H1, S_.s, S, Ga + ao.w1, Ga + ao.b1);
+    RLMD_TRY(launch_bwd_w(ag, gb, st));
     AdamArgs ad{};
-    ad.p = Pa;
+    ad.p = P + ag->off_actor;
     ad.g = Ga;
     ad.split_stride = ag->n_params;
     ad.m = ag->m + ag->off_actor;
     ad.v = ag->v + ag->off_actor;
-    ad.target = sac ? nullptr : Ta;
+    ad.target = sac ? nullptr : T + ag->off_actor;
     ad.n = ao.size;
     ad.lr = c.lr_actor;
     ad.tau = c.tau;
@@ -1001,6 +983,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     ad.lr_temp = c.lr_temp;
     ad.temp_interval = c.temp_update_interval;
     ad.stats = stats;
+    adam_copies(ag, ad, ao, SLOT_ACTOR, 1, !sac);
     RLMD_TRY(adam_launch(ad, st));
   }
   return 0;
@@ -1016,6 +999,7 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
   const int64_t mem = replay_mem_idx(rb);
   const int64_t M = mem < v.capacity ? mem : v.capacity;
   RLMD_CHECK(v.S == c.state_dim && v.A == c.action_dim, "replay / agent dims differ");
+  if (k > 0) RLMD_TRY(refresh_copies(ag, st));
   for (int i = 0; i < k; ++i) {
     Scratch& S_ = ag->sc;
     RLMD_TRY(replay_sample_launch(v, M, c.batch, c.seed ^ 0x5eed5eed5eedull, 0, &ag->st->learn_cntr,
@@ -1029,6 +1013,13 @@ int agent_act(rlmd_agent_s* ag, const float* obs, int64_t n, float* actions, int
               uint64_t noise_ctr, const float* eps, hipStream_t st) {
   const rlmd_agent_cfg& c = ag->cfg;
   if (n <= 0) return 0;
+  RLMD_CHECK(n <= INT32_MAX, "too many rows");
+  static const bool fused_ok = getenv("RLMD_NO_FUSED_ACT") == nullptr;
+  if (fused_ok && fused_act_supported(c)) {
+    if (!ag->act_w2bf) RLMD_HIP(hipMalloc(&ag->act_w2bf, sizeof(unsigned short) * c.h1 * c.h2));
+    return fused_act_launch(c, obs, n, actions, ag->params + ag->off_actor, ag->actor, ag->act_w2bf, mode,
+                            c.seed ^ 0xac7ac7ac7ull, (uint32_t)noise_ctr, eps, st);
+  }
   if (n > ag->act_cap) {
     if (ag->act_h1) {
       RLMD_HIP(hipFree(ag->act_h1));
@@ -1113,10 +1104,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.xsa, B * X);
   RLMD_ALLOC(s.done, B);
   RLMD_ALLOC(s.idx, B);
-  RLMD_ALLOC(s.ha1, B * H1);
-  RLMD_ALLOC(s.ha2, B * H2);
   RLMD_ALLOC(s.logp_next, B);
-  RLMD_ALLOC(s.xs2a2, B * X);
   RLMD_ALLOC(s.y, B);
   RLMD_ALLOC(s.h1, B * H1);
   RLMD_ALLOC(s.h2, B * H2);
@@ -1129,23 +1117,21 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.dh1, B * H1);
   RLMD_ALLOC(s.stats, 16);
   for (int g = 0; g < 2; ++g) {
-    RLMD_ALLOC(s.tc1[g], B * H1);
-    RLMD_ALLOC(s.tc2[g], B * H2);
-    RLMD_ALLOC(s.tpart[g], B * ((H2 + 31) / 32));
+    RLMD_ALLOC(s.tpart[g], B);
     RLMD_ALLOC(s.c1[g], B * H1);
     RLMD_ALLOC(s.c2[g], B * H2);
-    RLMD_ALLOC(s.qpart[g], B * ((H2 + 31) / 32));
+    RLMD_ALLOC(s.qpart[g], B);
     RLMD_ALLOC(s.dq[g], B);
     RLMD_ALLOC(s.dc2[g], B * H2);
     RLMD_ALLOC(s.dc1[g], B * H1);
     RLMD_ALLOC(s.e1[g], B * H1);
     RLMD_ALLOC(s.e2[g], B * H2);
-    RLMD_ALLOC(s.qnpart[g], B * ((H2 + 31) / 32));
+    RLMD_ALLOC(s.qnpart[g], B);
     RLMD_ALLOC(s.dqn[g], B);
-    RLMD_ALLOC(s.de2[g], B * H2);
-    RLMD_ALLOC(s.de1[g], B * H1);
-    RLMD_ALLOC(s.dxa[g], B * A);
   }
+  ag->wcopy_bytes = (size_t)rlmd::pad32(H1) * rlmd::pad32(H2) * (c.precision == RLMD_BF16 ? 2 : 4);
+  RLMD_ALLOC(ag->wcopy, 12 * ag->wcopy_bytes);
+  RLMD_HIP(hipMemset(ag->wcopy, 0, 12 * ag->wcopy_bytes));
   // Zipf-plot x axis (algo_sac.py:157-162): x_j = log((1 + k) / j), centred
   const int k = c.topk;
   std::vector<float> zx(k);
@@ -1179,6 +1165,7 @@ int rlmd_agent_destroy(rlmd_agent_t ag) {
   for (void* p : ag->allocs) (void)hipFree(p);
   if (ag->act_h1) (void)hipFree(ag->act_h1);
   if (ag->act_h2) (void)hipFree(ag->act_h2);
+  if (ag->act_w2bf) (void)hipFree(ag->act_w2bf);
   delete ag;
   return 0;
 }
@@ -1213,6 +1200,7 @@ int rlmd_agent_learn_batch(rlmd_agent_t ag, const float* s, const float* a, cons
                             sizeof(float) * A, B, hipMemcpyDeviceToDevice, st));
   hipLaunchKernelGGL(rlmd::bump_kernel, dim3(1), dim3(1), 0, st, ag->st);
   RLMD_LAUNCH_CHECK();
+  RLMD_TRY(rlmd::refresh_copies(ag, st));
   return rlmd::learn_body(ag, eff, eps_a, eps_b, rlmd::stats_slot(ag, stats, 0), st);
 }
 

@@ -50,4 +50,129 @@ struct HeadArgs {
   int32_t clamp_noise;          // TD3 target: clip noise to +-noise_clip
 };
 
+// ---------------------------------------------------------------------------
+// rows.hip: row-block kernels of the update.  Every per-row chain of learn()
+// (forward of a 2-hidden-layer MLP -> heads -> policy sample -> next MLP, and the
+// data-gradient backward) runs inside one 16-row workgroup: layer 1 on the VALU
+// (K = state/action width is tiny), hidden layers on MFMA with the fc2 weight
+// fragments read straight from a compute copy in HBM/L2, heads as LDS dot
+// products.  Batch-wide reductions (losses, top-k, weight gradients) stay in
+// their own kernels.
+// ---------------------------------------------------------------------------
+constexpr int kRowBlock = 16;
+
+__host__ __device__ inline int pad32(int n) { return (n + 31) & ~31; }
+
+// A net as the row kernels see it: f32 master parameters plus compute copies of
+// fc2.weight in the MFMA operand type (bf16 or f32), zero-padded to 32:
+//   wc [H2p][H1p] (= fc2.weight, forward), wt [H1p][H2p] (transposed, backward).
+struct RowNet {
+  const float* p;
+  const void* wc;
+  const void* wt;
+};
+
+struct RowDims {
+  int32_t S, A, X, H1, H2, H1p, H2p, B, algo, prec;
+};
+
+struct SampleCfg {
+  uint64_t seed;
+  const int32_t* ctr;  // Philox c1 = learn_cntr
+  float max_action, ls_min, ls_max, reparam_noise;
+};
+
+// Phase 1 of an update: y = 0 target path (policy on s2 -> sample -> both target
+// critics), y = 1 + g online critic g on (s, a), y = 3 (with_actor) the policy on
+// s for the actor update (its parameters do not change before the actor step).
+struct FwdRowsArgs {
+  RowDims d;
+  NetOff ao, co;
+  SampleCfg smp;
+  RowNet tactor, tcrit[2];
+  const float* s2;
+  const float* eps_next;  // injected (nullable -> Philox)
+  int32_t t_tag, t_clamp;
+  float t_noise_std, t_noise_clip;
+  float* qt[2];  // [B] target q without the head bias
+  float* logp_next;
+  RowNet crit[2];
+  const float* xsa;
+  float* c1[2];
+  float* c2[2];
+  float* q[2];
+  int32_t with_actor, a_mode, a_tag;
+  RowNet actor;
+  const float* s;
+  const float* eps_cur;
+  float* h1a;
+  float* h2a;
+  float* xsan;
+  float* logp;
+  float* save;  // [B, 5A]
+};
+
+// Critics evaluated on (s, a_new) after their update: y = g.
+struct QEvalArgs {
+  RowDims d;
+  NetOff co;
+  RowNet crit[2];
+  const float* x;
+  float* e1[2];
+  float* e2[2];
+  float* qn[2];
+};
+
+// Critic data-gradients: y = g.  dh2 = dq w3 * [h2 > 0], dh1 = (dh2 W2) * [h1 > 0].
+struct CBwdArgs {
+  RowDims d;
+  NetOff co;
+  RowNet crit[2];
+  const float* dq[2];
+  const float* c1[2];
+  const float* c2[2];
+  float* dc2[2];
+  float* dc1[2];
+};
+
+// Actor data-gradients: dL/da through nq critics, through the sampling, the heads
+// and fc2 of the policy.  Outputs gh [B, 2A], dh2 [B, H2], dh1 [B, H1].
+struct ABwdArgs {
+  RowDims d;
+  NetOff ao, co;
+  SampleCfg smp;
+  int32_t nq;
+  RowNet crit[2];
+  RowNet actor;
+  const float* dqn[2];
+  const float* e1[2];
+  const float* e2[2];
+  const float* dlogp;
+  const float* save;
+  const float* h1a;
+  const float* h2a;
+  float* gh;
+  float* dh2;
+  float* dh1;
+};
+
+size_t rows_lds_bytes(const RowDims& d);
+int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st);
+int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st);
+int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st);
+int abwd_rows_launch(const ABwdArgs& a, hipStream_t st);
+// Compute copies (wc, wt) of fc2.weight for n nets; refresh from the masters.
+struct CopyJob {
+  const float* w2;  // master fc2.weight [H2][H1]
+  void* wc;
+  void* wt;
+};
+int w2_copies_launch(const CopyJob* jobs, int n, const RowDims& d, hipStream_t st);
+
+// act.hip: fused bf16 acting (obs -> actions in one launch) for the headline nets.
+bool fused_act_supported(const rlmd_agent_cfg& c);
+int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float* actions,
+                     const float* actor_params, const NetOff& off, unsigned short* w2bf, int mode,
+                     uint64_t seed, uint32_t ctr, const float* eps, hipStream_t st);
+
 }  // namespace rlmd

@@ -5,7 +5,7 @@
 
 #include "../../include/rlmd_abi.h"
 
-#define RLMD_GEMM_MAX_GROUPS 2
+#define RLMD_GEMM_MAX_PROBS 6
 
 namespace rlmd {
 
@@ -35,14 +35,27 @@ struct GemmShape {
   int32_t M, N, K, relu;
 };
 
+// Up to RLMD_GEMM_MAX_PROBS independent problems of one mode, each with its own
+// shape, share a launch: blockIdx.x runs over the concatenated output tiles of
+// all problems (tile_begin is filled in by gemm_launch), blockIdx.z is the
+// split-K slab.
 struct GemmBatch {
-  GemmShape shape;
-  GemmProblem prob[RLMD_GEMM_MAX_GROUPS];
-  int32_t groups;        // set by gemm_launch
+  GemmShape shape[RLMD_GEMM_MAX_PROBS];
+  GemmProblem prob[RLMD_GEMM_MAX_PROBS];
+  int32_t nprob;
+  int32_t tiles_n[RLMD_GEMM_MAX_PROBS];         // set by gemm_launch
+  int32_t tile_begin[RLMD_GEMM_MAX_PROBS + 1];  // set by gemm_launch
   int32_t splits;        // BWD_W split-K: slabs written at C + s*split_stride (and bias_grad)
   int64_t split_stride;  // floats between slabs
 };
 
-int gemm_launch(int prec, int mode, const GemmBatch& b, int groups, hipStream_t stream);
+// Appends one problem; returns its index.
+inline int gemm_add(GemmBatch& b, const GemmShape& s, const GemmProblem& p) {
+  b.shape[b.nprob] = s;
+  b.prob[b.nprob] = p;
+  return b.nprob++;
+}
+
+int gemm_launch(int prec, int mode, const GemmBatch& b, hipStream_t stream);
 
 }  // namespace rlmd
