@@ -2,18 +2,21 @@
 //
 // learn() (algos/algo_sac.py:300-615, algos/algo_td3.py:302-560) is a chain of
 // small per-row MLP evaluations separated by a few batch-wide reductions.  Every
-// per-row stretch of that chain runs here inside ONE 16-row workgroup (4 waves),
-// so the intermediate activations never round-trip through a kernel boundary:
-//   layer 1      VALU, one thread per hidden unit, x rows broadcast from LDS
-//   layer 2      v_mfma_f32_16x16x32_bf16 (bf16) / v_mfma_f32_16x16x4f32 (fp32):
-//                A = the 16 activation rows in LDS, B = fc2.weight fragments read
-//                16 bytes per lane straight from the zero-padded compute copy
-//                (L2-resident, shared by every workgroup), prefetched a register
-//                group ahead; wave w owns output column blocks w, w+4, ...
-//   heads        LDS dot products, split over up to 64 lanes per dot
-//   sampling     tanh-Gaussian / TD3 noise per row (networks_sac.py:101-178)
+// per-row stretch of that chain runs here inside ONE 16-row workgroup of 8 waves,
+// so intermediate activations never round-trip through a kernel boundary:
+//   layer 1   VALU: thread = (hidden unit, row group), x rows broadcast from LDS
+//   layer 2   v_mfma_f32_16x16x32_bf16 (bf16) / v_mfma_f32_16x16x4f32 (fp32):
+//             A = the 16 activation rows in LDS, B = fc2.weight fragments read
+//             16 bytes per lane straight from the zero-padded compute copy
+//             (L2-resident, shared by every workgroup); wave w owns output column
+//             blocks w, w + 8, ...
+//   heads     reduced from the MFMA accumulators (lane shuffles + one LDS pass)
+//   sampling  tanh-Gaussian / TD3 noise per row (networks_sac.py:101-178)
+// Latency is the whole cost at these sizes (a few MFLOP per workgroup), so every
+// load that does not depend on computed data — both nets' fc2 fragments, biases,
+// head weights, fc1 rows, ReLU masks — is issued in ONE round at kernel start.
 // Backward data paths use the transposed compute copy with the same MFMA loop.
-// Weight gradients (batch reductions) are left to gemm.hip's BWD_W launch.
+// Weight gradients (batch reductions) are gemm.hip's BWD_W launch.
 #include <math.h>
 
 #include "learn_kernels.h"
@@ -24,7 +27,11 @@ namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
-constexpr int R = kRowBlock;
+constexpr int R = kRowBlock;  // rows per workgroup
+constexpr int NT = 512;       // threads per workgroup
+constexpr int NW = NT / 64;   // waves
+constexpr int NHF = 4;        // heads reduced in the MFMA epilogue (more -> LDS dot products)
+constexpr int W1P = 8;        // fc1 inputs preloaded per thread (more -> read in the loop)
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 constexpr int kHeadsMax = 2 * RLMD_MAX_ACTION;
 
@@ -42,7 +49,6 @@ struct CT<RLMD_BF16> {
   using T = unsigned short;
   using Frag = bf16x8;
   static constexpr int KS = 32;  // k covered by one 16-byte fragment per lane
-  static constexpr int PAD = 8;  // LDS row pad (elements): 16-B aligned rows
   __device__ static T cvt(float f) { return to_bf16(f); }
   __device__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
@@ -53,7 +59,6 @@ struct CT<RLMD_FP32> {
   using T = float;
   using Frag = f32x4;
   static constexpr int KS = 16;
-  static constexpr int PAD = 4;
   __device__ static T cvt(float f) { return f; }
   // lane group q = lane >> 4 holds k = k0 + 4q + j in element j: four 16x16x4
   // MFMAs cover k0 .. k0 + 15 (a permutation of the k order, same products)
@@ -65,59 +70,87 @@ struct CT<RLMD_FP32> {
   }
 };
 
+// ---------------------------------------------------------------------------
 // LDS carve-up, identical on host (launch size) and device.
+// ---------------------------------------------------------------------------
 struct Lds {
-  int xs, a1, aT, h2s, h1s, hout, ghs, rowv, total;  // byte offsets
-  int ldx, lda1, ldaT, ldh2, ldh1;                   // row pitches (elements)
+  int xs, a1, aT, h2s, part, hout, ghs, rowv, total;  // byte offsets
+  int ldx, lda1, ldaT, ldh2;                          // row pitches (elements)
 };
 __host__ __device__ inline Lds lds_layout(const RowDims& d) {
   const int ts = d.prec == RLMD_BF16 ? 2 : 4;
-  const int pad = d.prec == RLMD_BF16 ? 8 : 4;
+  const int pad = d.prec == RLMD_BF16 ? 8 : 4;  // rows stay 16-B aligned, banks staggered
+  const int hmax = d.H1p > d.H2p ? d.H1p : d.H2p;
   Lds l{};
   auto up = [](int v) { return (v + 15) & ~15; };
   int o = 0;
   l.ldx = d.X;
   l.xs = o;
   o = up(o + R * d.X * 4);
-  l.lda1 = d.H1p + pad;
+  l.lda1 = hmax + pad;  // A operand of the forward (h1) and backward (dh2) MFMAs
   l.a1 = o;
   o = up(o + R * l.lda1 * ts);
-  l.ldaT = d.H2p + pad;
-  l.aT = o;
-  o = up(o + R * l.ldaT * ts);
-  l.ldh2 = d.H2p + 4;
+  l.ldaT = l.lda1;
+  l.aT = l.a1;
+  l.ldh2 = hmax + 4;  // f32 rows for LDS dot products (many heads / actions)
   l.h2s = o;
   o = up(o + R * l.ldh2 * 4);
-  l.ldh1 = d.H1p + 4;
-  l.h1s = o;
-  o = up(o + R * l.ldh1 * 4);
-  l.hout = o;
+  l.part = o;  // per-wave head partials [NW][R][NHF]
+  o = up(o + NW * R * NHF * 4);
+  l.hout = o;  // [R][kHeadsMax]
   o = up(o + R * kHeadsMax * 4);
-  l.ghs = o;
+  l.ghs = o;  // [R][kHeadsMax]
   o = up(o + R * kHeadsMax * 4);
-  l.rowv = o;
+  l.rowv = o;  // [R][4]
   o = up(o + R * 4 * 4);
   l.total = o;
   return l;
 }
 
-template <int PREC, int NBW, int G>
-__device__ __forceinline__ void frag_load(typename CT<PREC>::Frag (&bf)[G][NBW], const typename CT<PREC>::T* Bg,
-                                          uint32_t boff, int ldb, int s0, int nsteps, int nblk) {
-  const int wave = threadIdx.x >> 6;
+// ---------------------------------------------------------------------------
+// fc2 fragments: Pre holds K-steps [0, G) of one net, issued early; mfma_rows
+// consumes it (and streams the rest in G-step groups when MULTI).
+// ---------------------------------------------------------------------------
+template <int PREC, int NBW, bool MULTI>
+struct Pre {
+  // 16 fragments (64 VGPRs) per lane when one group covers K; 8 per group (two
+  // groups in flight) when the K loop streams
+  static constexpr int G = (MULTI ? 8 : 16) / NBW;
+  typename CT<PREC>::Frag f[G][NBW];
+};
+
+template <int PREC, int NBW, bool MULTI>
+using FragArr = typename CT<PREC>::Frag[Pre<PREC, NBW, MULTI>::G][NBW];
+
+template <int PREC, int NBW, bool MULTI>
+__device__ __forceinline__ void frag_load(FragArr<PREC, NBW, MULTI>& f,
+                                          const typename CT<PREC>::T* Bg, int ldb, int s0, int nsteps, int nblk) {
+  constexpr int G = Pre<PREC, NBW, MULTI>::G;
+  constexpr int EPF = 16 / sizeof(typename CT<PREC>::T);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t base = (uint32_t)((wave * 16 + (lane & 15)) * ldb + EPF * (lane >> 4));
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int i = 0; i < NBW; ++i)
-      if (wave + 4 * i < nblk && s0 + g < nsteps)
-        bf[g][i] = *reinterpret_cast<const typename CT<PREC>::Frag*>(
-            Bg + boff + (uint32_t)(64 * i * ldb) + (uint32_t)((s0 + g) * CT<PREC>::KS));
+      if (wave + NW * i < nblk && s0 + g < nsteps)
+        f[g][i] = *reinterpret_cast<const typename CT<PREC>::Frag*>(
+            Bg + base + (uint32_t)(NW * 16 * i * ldb) + (uint32_t)((s0 + g) * CT<PREC>::KS));
 }
 
-template <int PREC, int NBW, int G>
-__device__ __forceinline__ void frag_mfma(const typename CT<PREC>::Frag (&bf)[G][NBW], const typename CT<PREC>::T* As,
-                                          uint32_t aoff, int s0, int nsteps, int nblk, f32x4 (&acc)[NBW]) {
-  const int wave = threadIdx.x >> 6;
+template <int PREC, int NBW, bool MULTI>
+__device__ __forceinline__ void pre_issue(Pre<PREC, NBW, MULTI>& p, const void* Bg, int ldb, int K, int nblk) {
+  frag_load<PREC, NBW, MULTI>(p.f, static_cast<const typename CT<PREC>::T*>(Bg), ldb, 0, K / CT<PREC>::KS, nblk);
+}
+
+template <int PREC, int NBW, bool MULTI>
+__device__ __forceinline__ void frag_mfma(const FragArr<PREC, NBW, MULTI>& f,
+                                          const typename CT<PREC>::T* As, int lda, int s0, int nsteps, int nblk,
+                                          f32x4 (&acc)[NBW]) {
+  constexpr int G = Pre<PREC, NBW, MULTI>::G;
+  constexpr int EPF = 16 / sizeof(typename CT<PREC>::T);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int aoff = (lane & 15) * lda + EPF * (lane >> 4);
 #pragma unroll
   for (int g = 0; g < G; ++g) {
     if (s0 + g < nsteps) {
@@ -125,108 +158,176 @@ __device__ __forceinline__ void frag_mfma(const typename CT<PREC>::Frag (&bf)[G]
           *reinterpret_cast<const typename CT<PREC>::Frag*>(As + aoff + (s0 + g) * CT<PREC>::KS);
 #pragma unroll
       for (int i = 0; i < NBW; ++i)
-        if (wave + 4 * i < nblk) CT<PREC>::mfma(a, bf[g][i], acc[i]);
+        if (wave + NW * i < nblk) CT<PREC>::mfma(a, f[g][i], acc[i]);
     }
   }
 }
 
-// acc[i] (i < NBW) = A[16 x K] * B^T for output column block nb = wave + 4 i:
-// As: LDS rows of the A operand (pitch lda elements); Bg: compute copy with one
-// row of K elements per output column (pitch ldb), zero-padded.  B fragments are
-// double-buffered in registers, G K-steps (G * NBW 16-byte loads per lane) ahead.
-template <int PREC, int NBW>
-__device__ __forceinline__ void mfma_rows(const typename CT<PREC>::T* As, int lda,
-                                          const typename CT<PREC>::T* Bg, int ldb, int K, int nblk,
-                                          f32x4 (&acc)[NBW]) {
-  using C = CT<PREC>;
-  using Frag = typename C::Frag;
-  constexpr int EPF = 16 / sizeof(typename C::T);
-  constexpr int G = NBW >= 8 ? 1 : 8 / NBW;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int ko = EPF * (lane >> 4);
+// acc[i] = A[16 x K] B^T for output column block nb = wave + 8 i (A: LDS rows of
+// pitch lda; B: compute copy, one row of K elements per output column, pitch ldb).
+template <int PREC, int NBW, bool MULTI>
+__device__ __forceinline__ void mfma_rows(Pre<PREC, NBW, MULTI>& pre, const typename CT<PREC>::T* As, int lda,
+                                          const void* Bv, int ldb, int K, int nblk, f32x4 (&acc)[NBW]) {
+  constexpr int G = Pre<PREC, NBW, MULTI>::G;
+  const auto* Bg = static_cast<const typename CT<PREC>::T*>(Bv);
+  const int nsteps = K / CT<PREC>::KS;
 #pragma unroll
   for (int i = 0; i < NBW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nsteps = K / C::KS;
-  const uint32_t boff = (uint32_t)((wave * 16 + (lane & 15)) * ldb + ko);
-  const uint32_t aoff = (uint32_t)((lane & 15) * lda + ko);
-  Frag b0[G][NBW], b1[G][NBW];
-  frag_load<PREC, NBW, G>(b0, Bg, boff, ldb, 0, nsteps, nblk);
-  for (int s0 = 0; s0 < nsteps; s0 += 2 * G) {
-    frag_load<PREC, NBW, G>(b1, Bg, boff, ldb, s0 + G, nsteps, nblk);
-    frag_mfma<PREC, NBW, G>(b0, As, aoff, s0, nsteps, nblk, acc);
-    frag_load<PREC, NBW, G>(b0, Bg, boff, ldb, s0 + 2 * G, nsteps, nblk);
-    frag_mfma<PREC, NBW, G>(b1, As, aoff, s0 + G, nsteps, nblk, acc);
-  }
-}
-
-// h1 = relu(x W1^T + b1) for the block's rows; x rows in LDS (pitch ldx, first
-// `in` columns).  Writes the MFMA operand copy (T, zero-padded to H1p) and the
-// f32 activations to HBM (nullable) for the weight gradients / masks.
-template <int PREC>
-__device__ void layer1(const float* p, const NetOff& o, const float* xs, int ldx, int in,
-                       typename CT<PREC>::T* a1, int lda1, float* h1_out, int row0, int B) {
-  const int H1 = o.h1, H1p = pad32(H1);
-  for (int c = threadIdx.x; c < H1p; c += blockDim.x) {
-    if (c < H1) {
-      float acc[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = 0.f;
-      const float* w = p + o.w1 + (int64_t)c * in;
-      for (int k = 0; k < in; ++k) {
-        const float wk = w[k];
-#pragma unroll
-        for (int r = 0; r < R; ++r) acc[r] = fmaf(xs[r * ldx + k], wk, acc[r]);
-      }
-      const float bb = p[o.b1 + c];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const float v = fmaxf(acc[r] + bb, 0.f);
-        a1[r * lda1 + c] = CT<PREC>::cvt(v);
-        if (h1_out && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + c] = v;
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) a1[r * lda1 + c] = CT<PREC>::cvt(0.f);
+  if constexpr (!MULTI) {
+    (void)Bg;
+    frag_mfma<PREC, NBW, MULTI>(pre.f, As, lda, 0, nsteps, nblk, acc);
+  } else {
+    FragArr<PREC, NBW, MULTI> b1;
+    for (int s = 0; s < nsteps; s += 2 * G) {
+      frag_load<PREC, NBW, MULTI>(b1, Bg, ldb, s + G, nsteps, nblk);
+      frag_mfma<PREC, NBW, MULTI>(pre.f, As, lda, s, nsteps, nblk, acc);
+      frag_load<PREC, NBW, MULTI>(pre.f, Bg, ldb, s + 2 * G, nsteps, nblk);
+      frag_mfma<PREC, NBW, MULTI>(b1, As, lda, s + G, nsteps, nblk, acc);
     }
   }
 }
 
-// h2 = relu(h1 W2^T + b2) -> LDS f32 rows (zero beyond H2) and HBM (nullable).
-template <int PREC, int NBW>
-__device__ void layer2(const RowNet& net, const NetOff& o, const typename CT<PREC>::T* a1, int lda1,
-                       float* h2s, int ldh2, float* h2_out, int row0, int B) {
-  using T = typename CT<PREC>::T;
-  const int H1p = pad32(o.h1), H2 = o.h2, H2p = pad32(H2);
-  f32x4 acc[NBW];
-  mfma_rows<PREC, NBW>(a1, lda1, static_cast<const T*>(net.wc), H1p, H1p, H2p / 16, acc);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// ---------------------------------------------------------------------------
+// element maps
+// ---------------------------------------------------------------------------
+// [16 x Hp] elementwise work: thread -> (column c, rows [r0, r1))
+struct ElemMap {
+  int c, r0, r1;
+};
+__device__ __forceinline__ ElemMap elem_map(int Hp) {
+  const int tpc = NT / Hp > 0 ? NT / Hp : 1;
+  const int nr = (R + tpc - 1) / tpc;
+  const int grp = threadIdx.x / Hp;
+  ElemMap m;
+  m.c = threadIdx.x % Hp;
+  m.r0 = grp < tpc ? grp * nr : R;
+  m.r1 = m.r0 + nr < R ? m.r0 + nr : R;
+  return m;
+}
+
+// MFMA accumulator element (i, rg) of this lane: column and row
+__device__ __forceinline__ int acc_col(int i) { return ((threadIdx.x >> 6) + NW * i) * 16 + (threadIdx.x & 15); }
+__device__ __forceinline__ int acc_row(int rg) { return 4 * ((threadIdx.x & 63) >> 4) + rg; }
+
+// ---------------------------------------------------------------------------
+// forward pieces
+// ---------------------------------------------------------------------------
+// per-thread constants of one net's forward, loaded before any compute
+template <int NBW>
+struct FwdConst {
+  float w1[W1P], b1;    // fc1 row of this thread's hidden unit
+  float b2[NBW];        // fc2 bias of this lane's accumulator columns
+  float hw[NBW][NHF];   // head weights of those columns (nh <= NHF)
+};
+
+template <int NBW>
+__device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, const NetOff& o, int in, int nh,
+                                          const float* wa, const float* wb, int na) {
+  const ElemMap m = elem_map(pad32(o.h1));
+  const bool own = m.c < o.h1 && m.r0 < R;
+  const float* w = p + o.w1 + (int64_t)m.c * in;
+#pragma unroll
+  for (int j = 0; j < W1P; ++j) k.w1[j] = (own && j < in) ? w[j] : 0.f;
+  k.b1 = own ? p[o.b1 + m.c] : 0.f;
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
-    const int nb = wave + 4 * i;
-    if (nb < H2p / 16) {
-      const int col = nb * 16 + (lane & 15);
-      const bool cin = col < H2;
-      const float bias = cin ? net.p[o.b2 + col] : 0.f;
+    const int col = acc_col(i);
+    const bool cin = col < o.h2;
+    k.b2[i] = cin ? p[o.b2 + col] : 0.f;
 #pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int r = 4 * (lane >> 4) + rg;
-        const float v = cin ? fmaxf(acc[i][rg] + bias, 0.f) : 0.f;
-        h2s[r * ldh2 + col] = v;
-        if (h2_out && cin && row0 + r < B) h2_out[(int64_t)(row0 + r) * H2 + col] = v;
-      }
+    for (int h = 0; h < NHF; ++h) {
+      const float* hwp = h < na ? wa + (int64_t)h * o.h2 : wb + (int64_t)(h - na) * o.h2;
+      k.hw[i][h] = (cin && h < nh) ? hwp[col] : 0.f;
     }
   }
 }
 
-// out[r][h] (+)= sum_c src[r][c] * w_h[c * cstride], h < nh, where w_h = wa + h*ldw
-// for h < na and wb + (h - na)*ldw beyond.  A dot is split over P lanes of one wave.
-__device__ void row_dots(const float* src, int lds, int ncols, int nh, const float* wa, const float* wb,
-                         int na, int64_t ldw, int cstride, float* out, int ldo, bool accumulate) {
+// h1 = relu(x W1^T + b1): A operand (T, zero-padded to H1p) + f32 to HBM (nullable)
+template <int PREC, int NBW>
+__device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, const NetOff& o, const float* xs,
+                                       int ldx, int in, typename CT<PREC>::T* a1, int lda1, float* h1_out, int row0,
+                                       int B) {
+  const int H1 = o.h1;
+  const ElemMap m = elem_map(pad32(H1));
+  const float* w = p + o.w1 + (int64_t)m.c * in;
+  for (int r = m.r0; r < m.r1; ++r) {
+    float v = 0.f;
+    if (m.c < H1) {
+      float acc = 0.f;
+#pragma unroll
+      for (int j = 0; j < W1P; ++j)
+        if (j < in) acc = fmaf(xs[r * ldx + j], k.w1[j], acc);
+      for (int j = W1P; j < in; ++j) acc = fmaf(xs[r * ldx + j], w[j], acc);
+      v = fmaxf(acc + k.b1, 0.f);
+      if (h1_out && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + m.c] = v;
+    }
+    a1[r * lda1 + m.c] = CT<PREC>::cvt(v);
+  }
+}
+
+// relu(acc + b2) -> HBM (nullable), LDS rows (nullable) and the per-wave head
+// partials part[wave][row][h] (nh <= NHF).
+template <int NBW>
+__device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdConst<NBW>& k, const NetOff& o,
+                                             int nh, float* h2_out, float* h2s, int ldh2, float* part, int row0,
+                                             int B) {
+  const int H2 = o.h2, nblk = pad32(H2) / 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float ph[4][NHF];
+#pragma unroll
+  for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+    for (int h = 0; h < NHF; ++h) ph[rg][h] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NBW; ++i) {
+    if (wave + NW * i < nblk) {
+      const int col = acc_col(i);
+      const bool cin = col < H2;
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int r = acc_row(rg);
+        const float v = cin ? fmaxf(acc[i][rg] + k.b2[i], 0.f) : 0.f;
+        if (h2_out && cin && row0 + r < B) h2_out[(int64_t)(row0 + r) * H2 + col] = v;
+        if (h2s) h2s[r * ldh2 + col] = v;
+#pragma unroll
+        for (int h = 0; h < NHF; ++h) ph[rg][h] = fmaf(v, k.hw[i][h], ph[rg][h]);
+      }
+    }
+  }
+  if (nh <= NHF) {
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+      for (int h = 0; h < NHF; ++h) {
+        if (h < nh) {
+          float c = ph[rg][h];
+          c += __shfl_xor(c, 1, 64);
+          c += __shfl_xor(c, 2, 64);
+          c += __shfl_xor(c, 4, 64);
+          c += __shfl_xor(c, 8, 64);
+          if ((lane & 15) == 0) part[(wave * R + acc_row(rg)) * NHF + h] = c;
+        }
+      }
+  }
+}
+
+// sum of the per-wave head partials of row r, head h
+__device__ __forceinline__ float head_sum(const float* part, int r, int h) {
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) s += part[(w * R + r) * NHF + h];
+  return s;
+}
+
+// out[r][h] (+)= sum_c src[r][c] * w_h[c * cstride], h < nh, w_h = wa + h*ldw for
+// h < na, wb + (h - na)*ldw beyond.  A dot is split over P lanes of one wave.
+__device__ void row_dots(const float* src, int lds, int ncols, int nh, const float* wa, const float* wb, int na,
+                         int64_t ldw, int cstride, float* out, int ldo, bool accumulate) {
   const int nd = R * nh;
   int P = 64;
-  while (P > 1 && nd * P > (int)blockDim.x) P >>= 1;
+  while (P > 1 && nd * P > NT) P >>= 1;
   const int part = threadIdx.x % P;
-  for (int d0 = threadIdx.x / P; d0 < nd; d0 += blockDim.x / P) {
+  for (int d0 = threadIdx.x / P; d0 < nd; d0 += NT / P) {
     const int h = d0 / R, r = d0 % R;
     const float* w = h < na ? wa + (int64_t)h * ldw : wb + (int64_t)(h - na) * ldw;
     float acc = 0.f;
@@ -236,241 +337,403 @@ __device__ void row_dots(const float* src, int lds, int ncols, int nh, const flo
   }
 }
 
-// Full critic forward for the block's rows: x in LDS -> q (no head bias).
-template <int PREC, int NBW>
-__device__ void critic_rows(const RowNet& net, const NetOff& co, const float* xs, int ldx, int X,
-                            unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, float* q_out,
-                            int row0, int B) {
+// One 2-hidden-layer MLP forward over the block's rows (x in LDS), heads left in
+// hout[r][h] (no head bias).  pre: this net's fc2 fragments, already issued.
+template <int PREC, int NBW, bool MULTI>
+__device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>& k, Pre<PREC, NBW, MULTI>& pre,
+                         const float* xs, int ldx, int in, int nh, const float* wa, const float* wb, int na,
+                         unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B) {
   using T = typename CT<PREC>::T;
   T* a1 = reinterpret_cast<T*>(smem + L.a1);
-  float* h2s = reinterpret_cast<float*>(smem + L.h2s);
+  float* part = reinterpret_cast<float*>(smem + L.part);
   float* hout = reinterpret_cast<float*>(smem + L.hout);
-  layer1<PREC>(net.p, co, xs, ldx, X, a1, L.lda1, h1_out, row0, B);
-  __syncthreads();
-  layer2<PREC, NBW>(net, co, a1, L.lda1, h2s, L.ldh2, h2_out, row0, B);
-  __syncthreads();
-  row_dots(h2s, L.ldh2, co.h2, 1, net.p + co.w3, nullptr, 1, co.h2, 1, hout, kHeadsMax, false);
-  __syncthreads();
-  if (threadIdx.x < R && row0 + (int)threadIdx.x < B) q_out[row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
-  __syncthreads();
-}
-
-// Policy forward + sample for the block's rows: state in xs[:, :S]; the sampled
-// action is written to xs[:, S:S+A] (the critic input) and to xa_out (nullable).
-// mode 0: stochastic (SAC tanh-Gaussian / TD3 exploration or smoothing noise),
-// mode 1: deterministic.  Same arithmetic as learn.hip's actor_head_kernel.
-template <int PREC, int NBW>
-__device__ void actor_rows(const RowNet& net, const NetOff& ao, const RowDims& d, const SampleCfg& smp,
-                           float* xs, int ldx, unsigned char* smem, const Lds& L, float* h1_out, float* h2_out,
-                           int mode, int tag, const float* eps_in, float noise_std, float noise_clip,
-                           int clamp_noise, float* logp_out, float* save, float* xa_out, int row0, int B) {
-  using T = typename CT<PREC>::T;
-  T* a1 = reinterpret_cast<T*>(smem + L.a1);
   float* h2s = reinterpret_cast<float*>(smem + L.h2s);
-  float* hout = reinterpret_cast<float*>(smem + L.hout);
-  const int S = d.S, A = d.A;
-  const bool sac = d.algo == RLMD_SAC;
-  layer1<PREC>(net.p, ao, xs, ldx, S, a1, L.lda1, h1_out, row0, B);
+  layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, row0, B);
   __syncthreads();
-  layer2<PREC, NBW>(net, ao, a1, L.lda1, h2s, L.ldh2, h2_out, row0, B);
+  f32x4 acc[NBW];
+  const int H1p = pad32(o.h1);
+  mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, pad32(o.h2) / 16, acc);
+  const bool fused = nh <= NHF;
+  fwd_epilogue<NBW>(acc, k, o, nh, h2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B);
   __syncthreads();
-  row_dots(h2s, L.ldh2, ao.h2, sac ? 2 * A : A, net.p + ao.w3, sac ? net.p + ao.w4 : nullptr, A, ao.h2, 1, hout,
-           kHeadsMax, false);
-  __syncthreads();
-  const int r = threadIdx.x;
-  if (r < R) {
-    const int b = row0 + r;
-    const bool valid = b < B;
-    const uint32_t c1 = (uint32_t)*smp.ctr;
-    float logp = 0.f;
-    for (int j = 0; j < A; ++j) {
-      float mu = hout[r * kHeadsMax + j] + net.p[ao.b3 + j];
-      float eps = 0.f;
-      if (mode == 0 && valid) {
-        if (eps_in) {
-          eps = eps_in[(int64_t)b * A + j];
-        } else {
-          double z0, z1;
-          rlmd_normal2(rlmd_philox(smp.seed, (uint32_t)b, c1, (uint32_t)tag, (uint32_t)(j >> 1)), z0, z1);
-          eps = (float)((j & 1) ? z1 : z0);
-        }
-      }
-      float act;
-      if (sac) {
-        const float ls_raw = hout[r * kHeadsMax + A + j] + net.p[ao.b4 + j];
-        const float ls = fminf(fmaxf(ls_raw, smp.ls_min), smp.ls_max);
-        float sigma = expf(ls);
-        if (!isfinite(mu)) mu = 0.f;  // NaN scrub (networks_sac.py:131-134)
-        if (!isfinite(sigma)) sigma = 3.f;
-        if (mode == 1) {
-          act = tanhf(mu) * smp.max_action;
-        } else {
-          const float u = mu + eps * sigma;
-          const float dd = u - mu;
-          const float lpn = -(dd * dd) / (2.f * (sigma * sigma)) - logf(sigma) - kLogSqrt2Pi;
-          act = tanhf(u) * smp.max_action;
-          const float an = act / smp.max_action;
-          logp += lpn - logf(1.f - an * an + smp.reparam_noise);
-          if (save && valid) {
-            float* sv = save + (int64_t)b * 5 * A;
-            sv[j] = mu;
-            sv[A + j] = sigma;
-            sv[2 * A + j] = eps;
-            sv[3 * A + j] = u;
-            sv[4 * A + j] = ls_raw;
-          }
-        }
-      } else {
-        act = tanhf(mu) * smp.max_action;
-        if (mode == 0) {
-          float nz = eps * noise_std;
-          if (clamp_noise) nz = fminf(fmaxf(nz, -noise_clip), noise_clip);
-          act = fminf(fmaxf(act + nz, -smp.max_action), smp.max_action);
-        }
-        if (save && valid) save[(int64_t)b * 5 * A + j] = mu;  // pre-tanh for backward
-      }
-      xs[r * ldx + S + j] = act;
-      if (xa_out && valid) xa_out[(int64_t)b * d.X + S + j] = act;
+  if (fused) {
+    if ((int)threadIdx.x < R * nh) {
+      const int r = threadIdx.x % R, h = threadIdx.x / R;
+      hout[r * kHeadsMax + h] = head_sum(part, r, h);
     }
-    if (logp_out && valid) logp_out[b] = logp;
+  } else {
+    row_dots(h2s, L.ldh2, o.h2, nh, wa, wb, na, o.h2, 1, hout, kHeadsMax, false);
   }
   __syncthreads();
 }
 
+// Policy sample per row from hout (mu | log_scale without biases): writes the
+// action into xs[:, S:S+A] and xa_out (nullable).  Same arithmetic as
+// learn.hip's actor_head_kernel.  mode 0 stochastic, 1 deterministic.
+__device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, const SampleCfg& smp, float* xs,
+                            int ldx, const float* hout, int mode, int tag, const float* eps_in, float noise_std,
+                            float noise_clip, int clamp_noise, float* logp_out, float* save, float* xa_out, int row0,
+                            int B) {
+  const int r = threadIdx.x;
+  if (r >= R) return;
+  const int S = d.S, A = d.A, b = row0 + r;
+  const bool valid = b < B, sac = d.algo == RLMD_SAC;
+  const uint32_t c1 = (uint32_t)*smp.ctr;
+  float logp = 0.f;
+  for (int j = 0; j < A; ++j) {
+    float mu = hout[r * kHeadsMax + j] + p[ao.b3 + j];
+    float eps = 0.f;
+    if (mode == 0 && valid) {
+      if (eps_in) {
+        eps = eps_in[(int64_t)b * A + j];
+      } else {
+        double z0, z1;
+        rlmd_normal2(rlmd_philox(smp.seed, (uint32_t)b, c1, (uint32_t)tag, (uint32_t)(j >> 1)), z0, z1);
+        eps = (float)((j & 1) ? z1 : z0);
+      }
+    }
+    float act;
+    if (sac) {
+      const float ls_raw = hout[r * kHeadsMax + A + j] + p[ao.b4 + j];
+      const float ls = fminf(fmaxf(ls_raw, smp.ls_min), smp.ls_max);
+      float sigma = expf(ls);
+      if (!isfinite(mu)) mu = 0.f;  // NaN scrub (networks_sac.py:131-134)
+      if (!isfinite(sigma)) sigma = 3.f;
+      if (mode == 1) {
+        act = tanhf(mu) * smp.max_action;
+      } else {
+        const float u = mu + eps * sigma;
+        const float dd = u - mu;
+        const float lpn = -(dd * dd) / (2.f * (sigma * sigma)) - logf(sigma) - kLogSqrt2Pi;
+        act = tanhf(u) * smp.max_action;
+        const float an = act / smp.max_action;
+        logp += lpn - logf(1.f - an * an + smp.reparam_noise);
+        if (save && valid) {
+          float* sv = save + (int64_t)b * 5 * A;
+          sv[j] = mu;
+          sv[A + j] = sigma;
+          sv[2 * A + j] = eps;
+          sv[3 * A + j] = u;
+          sv[4 * A + j] = ls_raw;
+        }
+      }
+    } else {
+      act = tanhf(mu) * smp.max_action;
+      if (mode == 0) {
+        float nz = eps * noise_std;
+        if (clamp_noise) nz = fminf(fmaxf(nz, -noise_clip), noise_clip);
+        act = fminf(fmaxf(act + nz, -smp.max_action), smp.max_action);
+      }
+      if (save && valid) save[(int64_t)b * 5 * A + j] = mu;  // pre-tanh for backward
+    }
+    xs[r * ldx + S + j] = act;
+    if (xa_out && valid) xa_out[(int64_t)b * d.X + S + j] = act;
+  }
+  if (logp_out && valid) logp_out[b] = logp;
+}
+
 // Stage rows [row0, row0 + 16) of a [B, in] matrix into xs (pitch ldx), zeros past B.
-__device__ void stage_rows(const float* src, int in, float* xs, int ldx, int row0, int B) {
-  for (int e = threadIdx.x; e < R * in; e += blockDim.x) {
+__device__ __forceinline__ void stage_rows(const float* src, int in, float* xs, int ldx, int row0, int B) {
+  for (int e = threadIdx.x; e < R * in; e += NT) {
     const int r = e / in, k = e % in;
     xs[r * ldx + k] = row0 + r < B ? src[(int64_t)(row0 + r) * in + k] : 0.f;
   }
 }
 
-template <int PREC, int NBW>
-__global__ void __launch_bounds__(256) fwd_rows_kernel(FwdRowsArgs a) {
+template <int NBW>
+__device__ __forceinline__ void actor_const(FwdConst<NBW>& k, const RowNet& n, const NetOff& ao, const RowDims& d) {
+  const bool sac = d.algo == RLMD_SAC;
+  fwd_const<NBW>(k, n.p, ao, d.S, sac ? 2 * d.A : d.A, n.p + ao.w3, sac ? n.p + ao.w4 : n.p + ao.w3, d.A);
+}
+template <int NBW>
+__device__ __forceinline__ void critic_const(FwdConst<NBW>& k, const RowNet& n, const NetOff& co, const RowDims& d) {
+  fwd_const<NBW>(k, n.p, co, d.X, 1, n.p + co.w3, n.p + co.w3, 1);
+}
+
+// y = 0, 1: target path with target critic y (the policy sample is recomputed
+// per critic: same Philox draws, the logp written once); y = 2, 3: online
+// critic y - 2 on (s, a); y = 4: policy on s for the actor step.
+template <int PREC, int NBW, bool MULTI>
+__global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowDims& d = a.d;
   const Lds L = lds_layout(d);
   float* xs = reinterpret_cast<float*>(smem + L.xs);
+  const float* hout = reinterpret_cast<const float*>(smem + L.hout);
   const int row0 = blockIdx.x * R, job = blockIdx.y, B = d.B;
-  if (job == 0) {  // target path (algo_sac.py:300-367 / algo_td3.py:302-361)
+  const bool sac = d.algo == RLMD_SAC;
+  const int H1p = pad32(d.H1), H2p = pad32(d.H2);
+  const int na = sac ? 2 * d.A : d.A;
+  if (job <= 1) {  // target path (algo_sac.py:300-367 / algo_td3.py:302-361)
+    const RowNet& an = a.tactor;
+    const RowNet& cn = a.tcrit[job];
+    Pre<PREC, NBW, MULTI> pa, pc;
+    pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
+    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    FwdConst<NBW> ka, kc;
+    actor_const<NBW>(ka, an, a.ao, d);
+    critic_const<NBW>(kc, cn, a.co, d);
     stage_rows(a.s2, d.S, xs, L.ldx, row0, B);
     __syncthreads();
-    actor_rows<PREC, NBW>(a.tactor, a.ao, d, a.smp, xs, L.ldx, smem, L, nullptr, nullptr, 0, a.t_tag, a.eps_next,
-                          a.t_noise_std, a.t_noise_clip, a.t_clamp, a.logp_next, nullptr, nullptr, row0, B);
-#pragma nounroll
-    for (int g = 0; g < 2; ++g)
-      critic_rows<PREC, NBW>(a.tcrit[g], a.co, xs, L.ldx, d.X, smem, L, nullptr, nullptr, a.qt[g], row0, B);
-  } else if (job <= 2) {  // online critics on (s, a) (algo_sac.py:413-417)
-    const int g = job - 1;
+    mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
+                               d.A, smem, L, nullptr, nullptr, row0, B);
+    sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, 0, a.t_tag, a.eps_next, a.t_noise_std, a.t_noise_clip,
+                a.t_clamp, job == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B);
+    __syncthreads();
+    mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
+                               nullptr, row0, B);
+    if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qt[job][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
+  } else if (job <= 3) {  // online critics on (s, a) (algo_sac.py:413-417)
+    const int g = job - 2;
+    const RowNet& cn = a.crit[g];
+    Pre<PREC, NBW, MULTI> pc;
+    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    FwdConst<NBW> kc;
+    critic_const<NBW>(kc, cn, a.co, d);
     stage_rows(a.xsa, d.X, xs, L.ldx, row0, B);
     __syncthreads();
-    critic_rows<PREC, NBW>(a.crit[g], a.co, xs, L.ldx, d.X, smem, L, a.c1[g], a.c2[g], a.q[g], row0, B);
+    mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.c1[g],
+                               a.c2[g], row0, B);
+    if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)
+    const RowNet& an = a.actor;
+    Pre<PREC, NBW, MULTI> pa;
+    pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
+    FwdConst<NBW> ka;
+    actor_const<NBW>(ka, an, a.ao, d);
     stage_rows(a.s, d.S, xs, L.ldx, row0, B);
     __syncthreads();
-    for (int e = threadIdx.x; e < R * d.S; e += blockDim.x) {
+    for (int e = threadIdx.x; e < R * d.S; e += NT) {
       const int r = e / d.S, k = e % d.S;
       if (row0 + r < B) a.xsan[(int64_t)(row0 + r) * d.X + k] = xs[r * L.ldx + k];
     }
-    actor_rows<PREC, NBW>(a.actor, a.ao, d, a.smp, xs, L.ldx, smem, L, a.h1a, a.h2a, a.a_mode, a.a_tag, a.eps_cur,
-                          0.f, 0.f, 0, a.logp, a.save, a.xsan, row0, B);
+    mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
+                               d.A, smem, L, a.h1a, a.h2a, row0, B);
+    sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, a.a_mode, a.a_tag, a.eps_cur, 0.f, 0.f, 0, a.logp, a.save,
+                a.xsan, row0, B);
   }
 }
 
-template <int PREC, int NBW>
-__global__ void __launch_bounds__(256) qeval_rows_kernel(QEvalArgs a) {
+template <int PREC, int NBW, bool MULTI>
+__global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const Lds L = lds_layout(a.d);
+  const RowDims& d = a.d;
+  const Lds L = lds_layout(d);
   float* xs = reinterpret_cast<float*>(smem + L.xs);
-  const int row0 = blockIdx.x * R, g = blockIdx.y, B = a.d.B;
-  stage_rows(a.x, a.d.X, xs, L.ldx, row0, B);
+  const float* hout = reinterpret_cast<const float*>(smem + L.hout);
+  const int row0 = blockIdx.x * R, g = blockIdx.y, B = d.B;
+  const RowNet& cn = a.crit[g];
+  Pre<PREC, NBW, MULTI> pc;
+  pre_issue<PREC, NBW, MULTI>(pc, cn.wc, pad32(d.H1), pad32(d.H1), pad32(d.H2) / 16);
+  FwdConst<NBW> kc;
+  critic_const<NBW>(kc, cn, a.co, d);
+  stage_rows(a.x, d.X, xs, L.ldx, row0, B);
   __syncthreads();
-  critic_rows<PREC, NBW>(a.crit[g], a.co, xs, L.ldx, a.d.X, smem, L, a.e1[g], a.e2[g], a.qn[g], row0, B);
+  mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.e1[g], a.e2[g],
+                             row0, B);
+  if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qn[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
 }
 
-// dh1 = (dh2 W2) * [h1 > 0] for the block's rows; dh2 already in the aT operand.
-template <int PREC, int NBW>
-__device__ void dh1_rows(const RowNet& net, const NetOff& o, const typename CT<PREC>::T* aT, int ldaT,
-                         const float* h1, float* dh1_out, float* dh1_lds, int ldl, int row0, int B) {
-  using T = typename CT<PREC>::T;
-  const int H1 = o.h1, H1p = pad32(H1), H2p = pad32(o.h2);
-  f32x4 acc[NBW];
-  mfma_rows<PREC, NBW>(aT, ldaT, static_cast<const T*>(net.wt), H2p, H2p, H1p / 16, acc);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+// ---------------------------------------------------------------------------
+// backward pieces
+// ---------------------------------------------------------------------------
+// per-thread ReLU masks of one net's rows: m2 in the elementwise map over H2p
+// (for dh2), m1 in the MFMA accumulator layout over H1p (for dh1)
+// rows per thread of the [16 x H2p] elementwise map: 16 / (512 / H2p) <= 4 NBW
+template <int NBW>
+constexpr int kMR = 4 * NBW < R ? 4 * NBW : R;
+
+template <int NBW>
+struct BwdMask {
+  float m2[kMR<NBW>];
+  float m1[NBW][4];
+  float w3;  // head weight of this thread's dh2 column
+};
+
+template <int NBW>
+__device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const float* h1, const float* h2, const float* w3,
+                                         const NetOff& o, int row0, int B) {
+  const int H1 = o.h1, H2 = o.h2;
+  const ElemMap m = elem_map(pad32(H2));
+  const bool cin = m.c < H2;
+#pragma unroll
+  for (int rr = 0; rr < kMR<NBW>; ++rr) {
+    const int r = m.r0 + rr;
+    k.m2[rr] = (r < m.r1 && cin && row0 + r < B) ? h2[(int64_t)(row0 + r) * H2 + m.c] : 0.f;
+  }
+  k.w3 = (w3 && cin) ? w3[m.c] : 0.f;
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
-    const int nb = wave + 4 * i;
-    if (nb < H1p / 16) {
-      const int col = nb * 16 + (lane & 15);
+    const int col = acc_col(i);
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      const int b = row0 + acc_row(rg);
+      k.m1[i][rg] = (col < H1 && b < B) ? h1[(int64_t)b * H1 + col] : 0.f;
+    }
+  }
+}
+
+// dh2 = dq[r] * w3 * [h2 > 0] -> A operand (T) and HBM (nullable)
+template <int PREC, int NBW>
+__device__ __forceinline__ void dh2_from_q(const BwdMask<NBW>& k, const float* dqr, const NetOff& o,
+                                           typename CT<PREC>::T* aT, int ldaT, float* dh2_out, int row0, int B) {
+  const int H2 = o.h2;
+  const ElemMap m = elem_map(pad32(H2));
+#pragma unroll
+  for (int rr = 0; rr < kMR<NBW>; ++rr) {
+    const int r = m.r0 + rr;
+    if (r < m.r1) {
+      const float v = k.m2[rr] > 0.f ? dqr[r] * k.w3 : 0.f;
+      aT[r * ldaT + m.c] = CT<PREC>::cvt(v);
+      if (dh2_out && m.c < H2 && row0 + r < B) dh2_out[(int64_t)(row0 + r) * H2 + m.c] = v;
+    }
+  }
+}
+
+// dh1 = (dh2 W2) * [h1 > 0] (MFMA with the transposed copy) -> HBM (nullable) and,
+// for the actor path, per-wave partials of dL/da = sum_c dh1[r][c] W1[c][S + j].
+template <int PREC, int NBW, bool MULTI>
+__device__ __forceinline__ void dh1_rows(Pre<PREC, NBW, MULTI>& pre, const RowNet& net, const NetOff& o,
+                                         const BwdMask<NBW>& k, const typename CT<PREC>::T* aT, int ldaT,
+                                         float* dh1_out, const float (*w1a)[NHF], int na, float* part, int row0,
+                                         int B) {
+  const int H1 = o.h1, H1p = pad32(H1), H2p = pad32(o.h2);
+  f32x4 acc[NBW];
+  mfma_rows<PREC, NBW, MULTI>(pre, aT, ldaT, net.wt, H2p, H2p, H1p / 16, acc);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float pd[4][NHF];
+#pragma unroll
+  for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+    for (int j = 0; j < NHF; ++j) pd[rg][j] = 0.f;
+#pragma unroll
+  for (int i = 0; i < NBW; ++i) {
+    if (wave + NW * i < H1p / 16) {
+      const int col = acc_col(i);
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
-        const int r = 4 * (lane >> 4) + rg, b = row0 + r;
-        float v = 0.f;
-        if (col < H1 && b < B) v = h1[(int64_t)b * H1 + col] > 0.f ? acc[i][rg] : 0.f;
+        const int b = row0 + acc_row(rg);
+        const float v = k.m1[i][rg] > 0.f ? acc[i][rg] : 0.f;
         if (dh1_out && col < H1 && b < B) dh1_out[(int64_t)b * H1 + col] = v;
-        if (dh1_lds) dh1_lds[r * ldl + col] = v;
+        if (w1a) {
+#pragma unroll
+          for (int j = 0; j < NHF; ++j) pd[rg][j] = fmaf(v, w1a[i][j], pd[rg][j]);
+        }
       }
     }
   }
-}
-
-// dh2 = dq[b] * w3 * [h2 > 0] -> aT operand (T) and HBM (nullable)
-template <int PREC>
-__device__ void dh2_from_q(const float* p, const NetOff& o, const float* dq, const float* h2,
-                           typename CT<PREC>::T* aT, int ldaT, float* dh2_out, float* rowv, int row0, int B) {
-  const int H2 = o.h2, H2p = pad32(H2);
-  if (threadIdx.x < R) rowv[threadIdx.x] = row0 + (int)threadIdx.x < B ? dq[row0 + threadIdx.x] : 0.f;
-  __syncthreads();
-  for (int c = threadIdx.x; c < H2p; c += blockDim.x) {
-    const float w = c < H2 ? p[o.w3 + c] : 0.f;
+  if (w1a) {
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int b = row0 + r;
-      float v = 0.f;
-      if (c < H2 && b < B) v = h2[(int64_t)b * H2 + c] > 0.f ? rowv[r] * w : 0.f;
-      aT[r * ldaT + c] = CT<PREC>::cvt(v);
-      if (dh2_out && c < H2 && b < B) dh2_out[(int64_t)b * H2 + c] = v;
-    }
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+      for (int j = 0; j < NHF; ++j) {
+        if (j < na) {
+          float c = pd[rg][j];
+          c += __shfl_xor(c, 1, 64);
+          c += __shfl_xor(c, 2, 64);
+          c += __shfl_xor(c, 4, 64);
+          c += __shfl_xor(c, 8, 64);
+          if ((lane & 15) == 0) part[(wave * R + acc_row(rg)) * NHF + j] = c;
+        }
+      }
   }
-  __syncthreads();
 }
 
-template <int PREC, int NBW>
-__global__ void __launch_bounds__(256) cbwd_rows_kernel(CBwdArgs a) {
+template <int PREC, int NBW, bool MULTI>
+__global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
   using T = typename CT<PREC>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Lds L = lds_layout(a.d);
   T* aT = reinterpret_cast<T*>(smem + L.aT);
   float* rowv = reinterpret_cast<float*>(smem + L.rowv);
   const int row0 = blockIdx.x * R, g = blockIdx.y, B = a.d.B;
-  dh2_from_q<PREC>(a.crit[g].p, a.co, a.dq[g], a.c2[g], aT, L.ldaT, a.dc2[g], rowv, row0, B);
-  dh1_rows<PREC, NBW>(a.crit[g], a.co, aT, L.ldaT, a.c1[g], a.dc1[g], nullptr, 0, row0, B);
+  const RowNet& cn = a.crit[g];
+  const int H1p = pad32(a.d.H1), H2p = pad32(a.d.H2);
+  Pre<PREC, NBW, MULTI> pw;
+  pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
+  BwdMask<NBW> k;
+  bwd_mask<NBW>(k, a.c1[g], a.c2[g], cn.p + a.co.w3, a.co, row0, B);
+  if ((int)threadIdx.x < R) rowv[threadIdx.x] = row0 + (int)threadIdx.x < B ? a.dq[g][row0 + threadIdx.x] : 0.f;
+  __syncthreads();
+  dh2_from_q<PREC, NBW>(k, rowv, a.co, aT, L.ldaT, a.dc2[g], row0, B);
+  __syncthreads();
+  dh1_rows<PREC, NBW, MULTI>(pw, cn, a.co, k, aT, L.ldaT, a.dc1[g], nullptr, 0, nullptr, row0, B);
 }
 
 // Actor data-gradients (autograd of algo_sac.py:524-562 through
 // networks_sac.py:163-178; algo_td3.py:507-523 through networks_td3.py:91).
-template <int PREC, int NBW>
-__global__ void __launch_bounds__(256) abwd_rows_kernel(ABwdArgs a) {
+template <int PREC, int NBW, bool MULTI>
+__global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   using T = typename CT<PREC>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowDims& d = a.d;
   const Lds L = lds_layout(d);
   T* aT = reinterpret_cast<T*>(smem + L.aT);
-  float* h1s = reinterpret_cast<float*>(smem + L.h1s);
+  float* h2s = reinterpret_cast<float*>(smem + L.h2s);  // dh1 rows when A > NHF
+  float* part = reinterpret_cast<float*>(smem + L.part);
   float* hout = reinterpret_cast<float*>(smem + L.hout);  // dL/da per row
   float* ghs = reinterpret_cast<float*>(smem + L.ghs);
   float* rowv = reinterpret_cast<float*>(smem + L.rowv);
   const int row0 = blockIdx.x * R, B = d.B, S = d.S, A = d.A, X = d.X;
   const bool sac = d.algo == RLMD_SAC;
-  // dL/da = sum over critics of (dq_g through critic g to its action inputs)
+  const int H1p = pad32(d.H1), H2p = pad32(d.H2);
+  const NetOff& ao = a.ao;
+  const NetOff& co = a.co;
+  const bool fused_da = A <= NHF;
+  // ---- every independent load up front
+  Pre<PREC, NBW, MULTI> p0, p1;
+  pre_issue<PREC, NBW, MULTI>(p0, a.crit[0].wt, H2p, H2p, H1p / 16);
+  if (a.nq > 1) pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
+  BwdMask<NBW> k0, k1, ka;
+  bwd_mask<NBW>(k0, a.e1[0], a.e2[0], a.crit[0].p + co.w3, co, row0, B);
+  if (a.nq > 1) bwd_mask<NBW>(k1, a.e1[1], a.e2[1], a.crit[1].p + co.w3, co, row0, B);
+  bwd_mask<NBW>(ka, a.h1a, a.h2a, nullptr, ao, row0, B);
+  float w1a[2][NBW][NHF];  // W1_g[c][S + j] for this lane's dh1 columns
+#pragma unroll
+  for (int g = 0; g < 2; ++g)
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      const int col = acc_col(i);
+#pragma unroll
+      for (int j = 0; j < NHF; ++j)
+        w1a[g][i][j] = (g < a.nq && col < d.H1 && j < A) ? a.crit[g].p[co.w1 + (int64_t)col * X + S + j] : 0.f;
+    }
+  if ((int)threadIdx.x < 2 * R) {
+    const int g = threadIdx.x / R, r = threadIdx.x % R;
+    rowv[g * R + r] = (g < a.nq && row0 + r < B) ? a.dqn[g][row0 + r] : 0.f;
+  }
+  __syncthreads();
+  // ---- dL/da through each critic: dh2 -> dh1 (MFMA) -> . W1[:, S:S+A]
   for (int g = 0; g < a.nq; ++g) {
-    dh2_from_q<PREC>(a.crit[g].p, a.co, a.dqn[g], a.e2[g], aT, L.ldaT, nullptr, rowv, row0, B);
-    dh1_rows<PREC, NBW>(a.crit[g], a.co, aT, L.ldaT, a.e1[g], nullptr, h1s, L.ldh1, row0, B);
+    const BwdMask<NBW>& k = g == 0 ? k0 : k1;
+    dh2_from_q<PREC, NBW>(k, rowv + g * R, co, aT, L.ldaT, nullptr, row0, B);
     __syncthreads();
-    row_dots(h1s, L.ldh1, d.H1, A, a.crit[g].p + a.co.w1 + S, nullptr, A, 1, X, hout, kHeadsMax, g > 0);
+    if (fused_da) {
+      dh1_rows<PREC, NBW, MULTI>(g == 0 ? p0 : p1, a.crit[g], co, k, aT, L.ldaT, nullptr, w1a[g], A, part, row0, B);
+      __syncthreads();
+      if ((int)threadIdx.x < R * A) {
+        const int r = threadIdx.x % R, j = threadIdx.x / R;
+        const float s = head_sum(part, r, j);
+        hout[r * kHeadsMax + j] = g == 0 ? s : hout[r * kHeadsMax + j] + s;
+      }
+    } else {
+      // many actions: dh1 rows through LDS, then LDS dot products with W1[:, S:]
+      f32x4 acc[NBW];
+      mfma_rows<PREC, NBW, MULTI>(g == 0 ? p0 : p1, aT, L.ldaT, a.crit[g].wt, H2p, H2p, H1p / 16, acc);
+#pragma unroll
+      for (int i = 0; i < NBW; ++i)
+        if (((int)threadIdx.x >> 6) + NW * i < H1p / 16)
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg)
+            h2s[acc_row(rg) * L.ldh2 + acc_col(i)] = k.m1[i][rg] > 0.f ? acc[i][rg] : 0.f;
+      __syncthreads();
+      row_dots(h2s, L.ldh2, d.H1, A, a.crit[g].p + co.w1 + S, nullptr, A, 1, X, hout, kHeadsMax, g > 0);
+    }
     __syncthreads();
   }
-  // through the sampling and the heads
+  // ---- through the sampling and the heads
+  Pre<PREC, NBW, MULTI>& pa = p0;  // reuse the first critic's fragment registers
+  pre_issue<PREC, NBW, MULTI>(pa, a.actor.wt, H2p, H2p, H1p / 16);
   const int r = threadIdx.x;
   if (r < R) {
     const int b = row0 + r;
@@ -489,7 +752,7 @@ __global__ void __launch_bounds__(256) abwd_rows_kernel(ABwdArgs a) {
           const float du = da * a.smp.max_action * om + dlp * dlogp_du;
           const float dmu = du + dlp * (dd / (sigma * sigma));
           const float dsig = du * eps + dlp * ((dd * dd) / (sigma * sigma * sigma) - 1.f / sigma);
-          const bool live = ls_raw >= a.smp.ls_min && ls_raw <= a.smp.ls_max;
+          const bool live = ls_raw >= a.smp.ls_min && ls_raw <= a.smp.ls_max;  // clamp passes [min, max]
           const float dls = live ? dsig * sigma : 0.f;
           ghs[r * kHeadsMax + j] = dmu;
           ghs[r * kHeadsMax + A + j] = dls;
@@ -507,36 +770,30 @@ __global__ void __launch_bounds__(256) abwd_rows_kernel(ABwdArgs a) {
     }
   }
   __syncthreads();
-  // dh2 = (gh . [W_pi; W_ls]) * [h2 > 0]
-  const NetOff& ao = a.ao;
-  const int H2 = ao.h2, H2p = pad32(H2);
-  const float* P = a.actor.p;
-  for (int c = threadIdx.x; c < H2p; c += blockDim.x) {
-    float acc[R];
+  // ---- dh2 = (gh . [W_pi; W_ls]) * [h2 > 0]
+  {
+    const int H2 = ao.h2;
+    const ElemMap m = elem_map(H2p);
+    const float* P = a.actor.p;
 #pragma unroll
-    for (int rr = 0; rr < R; ++rr) acc[rr] = 0.f;
-    if (c < H2) {
-      for (int j = 0; j < A; ++j) {
-        const float wp = P[ao.w3 + (int64_t)j * H2 + c];
-        const float wl = sac ? P[ao.w4 + (int64_t)j * H2 + c] : 0.f;
-#pragma unroll
-        for (int rr = 0; rr < R; ++rr) {
-          acc[rr] = fmaf(ghs[rr * kHeadsMax + j], wp, acc[rr]);
-          if (sac) acc[rr] = fmaf(ghs[rr * kHeadsMax + A + j], wl, acc[rr]);
+    for (int rr = 0; rr < kMR<NBW>; ++rr) {
+      const int rw = m.r0 + rr;
+      if (rw < m.r1) {
+        float acc = 0.f;
+        if (m.c < H2) {
+          for (int j = 0; j < A; ++j) {
+            acc = fmaf(ghs[rw * kHeadsMax + j], P[ao.w3 + (int64_t)j * H2 + m.c], acc);
+            if (sac) acc = fmaf(ghs[rw * kHeadsMax + A + j], P[ao.w4 + (int64_t)j * H2 + m.c], acc);
+          }
         }
+        const float v = ka.m2[rr] > 0.f ? acc : 0.f;
+        aT[rw * L.ldaT + m.c] = CT<PREC>::cvt(v);
+        if (m.c < H2 && row0 + rw < B) a.dh2[(int64_t)(row0 + rw) * H2 + m.c] = v;
       }
-    }
-#pragma unroll
-    for (int rr = 0; rr < R; ++rr) {
-      const int b = row0 + rr;
-      float v = 0.f;
-      if (c < H2 && b < B) v = a.h2a[(int64_t)b * H2 + c] > 0.f ? acc[rr] : 0.f;
-      aT[rr * L.ldaT + c] = CT<PREC>::cvt(v);
-      if (c < H2 && b < B) a.dh2[(int64_t)b * H2 + c] = v;
     }
   }
   __syncthreads();
-  dh1_rows<PREC, NBW>(a.actor, ao, aT, L.ldaT, a.h1a, a.dh1, nullptr, 0, row0, B);
+  dh1_rows<PREC, NBW, MULTI>(pa, a.actor, ao, ka, aT, L.ldaT, a.dh1, nullptr, 0, nullptr, row0, B);
 }
 
 struct CopyJobs {
@@ -558,32 +815,45 @@ __global__ void __launch_bounds__(256) w2_copy_kernel(CopyJobs jobs, int H1, int
   }
 }
 
+template <int PREC, int NBW, bool MULTI>
+void launch_kind(int kind, const void* args, dim3 grid, size_t lds, hipStream_t st) {
+  switch (kind) {
+    case 0:
+      hipLaunchKernelGGL((fwd_rows_kernel<PREC, NBW, MULTI>), grid, dim3(NT), lds, st,
+                         *static_cast<const FwdRowsArgs*>(args));
+      break;
+    case 1:
+      hipLaunchKernelGGL((qeval_rows_kernel<PREC, NBW, MULTI>), grid, dim3(NT), lds, st,
+                         *static_cast<const QEvalArgs*>(args));
+      break;
+    case 2:
+      hipLaunchKernelGGL((cbwd_rows_kernel<PREC, NBW, MULTI>), grid, dim3(NT), lds, st,
+                         *static_cast<const CBwdArgs*>(args));
+      break;
+    default:
+      hipLaunchKernelGGL((abwd_rows_kernel<PREC, NBW, MULTI>), grid, dim3(NT), lds, st,
+                         *static_cast<const ABwdArgs*>(args));
+      break;
+  }
+}
+
+// NBW = column blocks per wave (8 waves x 16 columns each), MULTI when the K
+// loop needs more than the 16 prefetched fragments per lane.
 template <int PREC>
-int launch_all(const RowDims& d, int kind, const void* args, int ny, hipStream_t st) {
+int launch_prec(const RowDims& d, int kind, const void* args, int ny, hipStream_t st) {
   const int H = d.H1p > d.H2p ? d.H1p : d.H2p;
   const dim3 grid((d.B + R - 1) / R, ny);
   const size_t lds = (size_t)lds_layout(d).total;
-#define RLMD_ROWS_CASE(NBW)                                                                                     \
-  switch (kind) {                                                                                               \
-    case 0: hipLaunchKernelGGL((fwd_rows_kernel<PREC, NBW>), grid, dim3(256), lds, st,                          \
-                               *static_cast<const FwdRowsArgs*>(args)); break;                                  \
-    case 1: hipLaunchKernelGGL((qeval_rows_kernel<PREC, NBW>), grid, dim3(256), lds, st,                        \
-                               *static_cast<const QEvalArgs*>(args)); break;                                    \
-    case 2: hipLaunchKernelGGL((cbwd_rows_kernel<PREC, NBW>), grid, dim3(256), lds, st,                         \
-                               *static_cast<const CBwdArgs*>(args)); break;                                     \
-    default: hipLaunchKernelGGL((abwd_rows_kernel<PREC, NBW>), grid, dim3(256), lds, st,                        \
-                                *static_cast<const ABwdArgs*>(args)); break;                                    \
-  }
-  if (H <= 64) {
-    RLMD_ROWS_CASE(1)
-  } else if (H <= 128) {
-    RLMD_ROWS_CASE(2)
+  const int nsteps = H / CT<PREC>::KS;
+  if (H <= 128) {
+    if (nsteps <= 16) launch_kind<PREC, 1, false>(kind, args, grid, lds, st);
+    else launch_kind<PREC, 1, true>(kind, args, grid, lds, st);
   } else if (H <= 256) {
-    RLMD_ROWS_CASE(4)
+    if (nsteps <= 8) launch_kind<PREC, 2, false>(kind, args, grid, lds, st);
+    else launch_kind<PREC, 2, true>(kind, args, grid, lds, st);
   } else {
-    RLMD_ROWS_CASE(8)
+    launch_kind<PREC, 4, true>(kind, args, grid, lds, st);
   }
-#undef RLMD_ROWS_CASE
   RLMD_LAUNCH_CHECK();
   return 0;
 }
@@ -591,9 +861,10 @@ int launch_all(const RowDims& d, int kind, const void* args, int ny, hipStream_t
 int launch_rows(const RowDims& d, int kind, const void* args, int ny, hipStream_t st) {
   RLMD_CHECK(d.H1 <= 512 && d.H2 <= 512, "row kernels: hidden widths up to 512");
   RLMD_CHECK(d.A <= RLMD_MAX_ACTION, "row kernels: too many actions");
+  RLMD_CHECK(lds_layout(d).total <= 160 * 1024, "row kernels: LDS budget exceeded");
   if (d.B <= 0) return 0;
-  return d.prec == RLMD_BF16 ? launch_all<RLMD_BF16>(d, kind, args, ny, st)
-                             : launch_all<RLMD_FP32>(d, kind, args, ny, st);
+  return d.prec == RLMD_BF16 ? launch_prec<RLMD_BF16>(d, kind, args, ny, st)
+                             : launch_prec<RLMD_FP32>(d, kind, args, ny, st);
 }
 
 }  // namespace
@@ -601,7 +872,7 @@ int launch_rows(const RowDims& d, int kind, const void* args, int ny, hipStream_
 size_t rows_lds_bytes(const RowDims& d) { return (size_t)lds_layout(d).total; }
 
 int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st) {
-  return launch_rows(a.d, 0, &a, a.with_actor ? 4 : 3, st);
+  return launch_rows(a.d, 0, &a, a.with_actor ? 5 : 4, st);
 }
 int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st) { return launch_rows(a.d, 1, &a, nq, st); }
 int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st) { return launch_rows(a.d, 2, &a, 2, st); }
