@@ -38,55 +38,22 @@ __device__ __forceinline__ uint32_t f2key(float f) {
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
-// deterministic block reduction (fixed tree) of one float per thread
-__device__ float block_sum(float v, float* red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  v = wave_sum(v);
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  float t = 0.f;
-  if (threadIdx.x < 64) {
-    t = threadIdx.x < nw ? red[threadIdx.x] : 0.f;
-    t = wave_sum(t);
-    if (threadIdx.x == 0) red[32] = t;
-  }
-  __syncthreads();
-  return red[32];
-}
-
-__device__ float block_max(float v, float* red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  __syncthreads();
-  if (lane == 0) red[w] = v;
-  __syncthreads();
-  if (threadIdx.x < 64) {
-    float t = threadIdx.x < nw ? red[threadIdx.x] : -INFINITY;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) t = fmaxf(t, __shfl_xor(t, o, 64));
-    if (threadIdx.x == 0) red[32] = t;
-  }
-  __syncthreads();
-  return red[32];
-}
-
-__device__ float block_min(float v, float* red) { return -block_max(-v, red); }
-
-// Block all-reduce of NS sums and NM maxima at once (2 barriers).  Each wave
-// reduces with shuffles; every thread then combines the per-wave partials in
-// wave order (deterministic).  red: >= 16 * (NS + NM) floats.
+// Block all-reduce of NS sums and NM maxima at once (3 barriers).  Each wave
+// reduces with shuffles and parks its partial in red[v][16]; lanes of the first
+// waves fold the per-wave partials of one value each (a fixed tree, so the
+// result is deterministic) and every thread reads the NS + NM results back.
+// red: 16 * (NS + NM) + 16 floats.
 template <int NS, int NM>
-__device__ void block_allreduce(float* sm, float* mx, float* red) {
+__device__ __forceinline__ void block_allreduce(float* sm, float* mx, float* red) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  constexpr int NV = NS + NM;
+  float* res = red + 16 * NV;
 #pragma unroll
   for (int v = 0; v < NS; ++v) sm[v] = wave_sum(sm[v]);
 #pragma unroll
   for (int v = 0; v < NM; ++v)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx[v] = fmaxf(mx[v], __shfl_xor(mx[v], o, 64));
-  __syncthreads();
   if (lane == 0) {
 #pragma unroll
     for (int v = 0; v < NS; ++v) red[v * 16 + w] = sm[v];
@@ -94,18 +61,66 @@ __device__ void block_allreduce(float* sm, float* mx, float* red) {
     for (int v = 0; v < NM; ++v) red[(NS + v) * 16 + w] = mx[v];
   }
   __syncthreads();
+  if ((int)threadIdx.x < 16 * NV) {
+    const int v = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const bool is_sum = v < NS;
+    float t = q < nw ? red[threadIdx.x] : (is_sum ? 0.f : -INFINITY);
 #pragma unroll
-  for (int v = 0; v < NS; ++v) {
-    float t = 0.f;
-    for (int q = 0; q < nw; ++q) t += red[v * 16 + q];
-    sm[v] = t;
+    for (int o = 1; o < 16; o <<= 1) {
+      const float u = __shfl_xor(t, o, 64);
+      t = is_sum ? t + u : fmaxf(t, u);
+    }
+    if (q == 0) res[v] = t;
   }
+  __syncthreads();
 #pragma unroll
-  for (int v = 0; v < NM; ++v) {
-    float t = -INFINITY;
-    for (int q = 0; q < nw; ++q) t = fmaxf(t, red[(NS + v) * 16 + q]);
-    mx[v] = t;
+  for (int v = 0; v < NS; ++v) sm[v] = res[v];
+#pragma unroll
+  for (int v = 0; v < NM; ++v) mx[v] = res[NS + v];
+  __syncthreads();  // red / res reusable
+}
+
+// Ascending bitonic sort of one 64-bit key per lane across the wave (registers).
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t key) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint64_t other = rlmd_shfl_xor_u64(key, j);
+      const bool up = (l & k) == 0 || k == 64;
+      const bool keep_min = ((l & j) == 0) == up;
+      key = keep_min ? (key < other ? key : other) : (key < other ? other : key);
+    }
+  return key;
+}
+
+// Ranks of distinct 64-bit keys across the block (ascending; key ~0 = absent):
+// each wave sorts its 64 keys in registers, parks the sorted run in LDS, and the
+// key at lane l of run w gets rank l + sum over the other runs of a binary
+// search (6 probes over the first 63 entries + the last entry).  The rank is scattered to out[key & 0xffffffff] (the caller's
+// index in the low word) and read back by the key's owner after the barrier.
+// runs: LDS [blockDim.x] uint64; out: LDS int [blockDim.x].
+__device__ __forceinline__ void block_rank(uint64_t key, uint64_t* runs, int* out) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t sk = wave_sort64(key);
+  runs[threadIdx.x] = sk;
+  __syncthreads();
+  if (sk != ~0ull) {
+    int rank = l;
+    for (int v = 0; v < nw; ++v) {
+      if (v == w) continue;
+      const uint64_t* run = runs + 64 * v;
+      // 6 probes count the smaller keys among run[0..62]; run[63] separately
+      int pos = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (run[pos + st - 1] < sk) pos += st;
+      rank += pos + (run[63] < sk ? 1 : 0);
+    }
+    out[(int)(sk & 0xffffffffu)] = rank;
   }
+  __syncthreads();
 }
 
 // ---------------------------------------------------------------------------
@@ -251,14 +266,28 @@ __device__ __forceinline__ void loss_and_grad(int lt, float q, float t, float c,
 // Bootstrapped target (algo_sac.py:347-365 / algo_td3.py:346-359) + critic loss,
 // top-k, tail index, CIM kernel and Nagy scale (tools/critic_loss.py:26-453,
 // algo_sac.py:413-473).  One workgroup; thread b owns mini-batch row b.
-__global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
-  __shared__ uint64_t keys[1024];
-  __shared__ float red[16 * 12];
-  __shared__ float lsel[2][1024];
-  __shared__ int rank_of[1024];
+#ifdef RLMD_TIMING
+// experiment builds only (tools/ts_probe.py): thread-0 s_memtime checkpoints
+__device__ unsigned long long g_ts[64];
+#define RLMD_TS(i)                                                   \
+  do {                                                               \
+    if (threadIdx.x == 0) g_ts[i] = __builtin_amdgcn_s_memtime();    \
+  } while (0)
+#else
+#define RLMD_TS(i) \
+  do {             \
+  } while (0)
+#endif
+
+template <int NTH>
+__global__ void __launch_bounds__(NTH) critic_loss_kernel(LossArgs a) {
+  __shared__ __attribute__((aligned(16))) uint64_t runs[NTH];
+  __shared__ int rank_of[3][NTH];
+  __shared__ float red[16 * 9];
   const int b = threadIdx.x, B = a.B, T = a.tiles;
   const bool in = b < B;
   LearnState* st = a.st;
+  RLMD_TS(0);
   // -- target and current q from the fused-head partials
   float y = 0.f, q[2] = {0.f, 0.f};
   if (in) {
@@ -279,6 +308,7 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
     else y = a.r[b] + ge * m;
     if (a.y_out) a.y_out[b] = y;
   }
+  RLMD_TS(1);
   const float scale[2] = {st->cauchy[0], st->cauchy[1]};
   // -- R1: means of (t - q)^2 (CIM kernel), of y, q (TCAU), Nagy terms; NaN flag
   const float e0 = (y - q[0]) * (y - q[0]), e1 = (y - q[1]) * (y - q[1]);
@@ -286,7 +316,9 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
   float s1[7] = {in ? e0 : 0.f, in ? e1 : 0.f, in ? y : 0.f, in ? q[0] : 0.f, in ? q[1] : 0.f,
                  in ? 1.f / (1.f + z0 * z0) : 0.f, in ? 1.f / (1.f + z1 * z1) : 0.f};
   float m1[1] = {(in && (isnan(q[0]) || isnan(q[1]) || isnan(y))) ? 1.f : 0.f};
+  RLMD_TS(2);
   block_allreduce<7, 1>(s1, m1, red);
+  RLMD_TS(3);
   const float me0 = s1[0] / B, me1 = s1[1] / B, my = s1[2] / B, mq0 = s1[3] / B, mq1 = s1[4] / B;
   // -- R2: population variances (two-pass, like torch.std(unbiased=False))
   float s2[5] = {in ? (e0 - me0) * (e0 - me0) : 0.f, in ? (e1 - me1) * (e1 - me1) : 0.f,
@@ -294,6 +326,7 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
                  in ? (q[1] - mq1) * (q[1] - mq1) : 0.f};
   float m2[1] = {-INFINITY};
   block_allreduce<5, 0>(s2, m2, red);
+  RLMD_TS(4);
   const float kern[2] = {sqrtf(s2[0] / B), sqrtf(s2[1] / B)};
   // TCAU 3-sigma truncation (critic_loss.py:26-50)
   float yt[2] = {y, y}, qt_[2] = {q[0], q[1]};
@@ -312,51 +345,40 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
     loss_and_grad(a.loss_type, qt_[g], yt[g], scale[g], kern[g], l[g], dl[g]);
     if (qtr[g]) dl[g] = 0.f;
   }
-  // -- top-k rows by l1 + l2, descending (critic_loss.py:438-441)
+  // -- top-k rows by l1 + l2, descending (critic_loss.py:438-441); ties by row
   const int k = B > a.k ? a.k : B;
-  int npow = 1;
-  while (npow < B) npow <<= 1;
   bool sel = in;
   int rank = b;
+  RLMD_TS(5);
   if (B > a.k) {
-    const uint64_t key = in ? ((uint64_t)(~f2key(l[0] + l[1])) << 32) | (uint32_t)b : ~0ull;
-    const uint64_t sk = rlmd_block_bitonic(key, npow, keys);
-    __syncthreads();
-    if (b < B) rank_of[(int)(sk & 0xffffffffu)] = b;
-    __syncthreads();
-    rank = in ? rank_of[b] : B;
+    block_rank(in ? ((uint64_t)(~f2key(l[0] + l[1])) << 32) | (uint32_t)b : ~0ull, runs, rank_of[0]);
+    rank = in ? rank_of[0][b] : B;
     sel = in && rank < k;
   }
+  RLMD_TS(6);
+  RLMD_TS(7);
   // -- R3: mean / min / max of the selected losses per critic
   float s3[2] = {sel ? l[0] : 0.f, sel ? l[1] : 0.f};
   float m3[4] = {sel ? l[0] : -INFINITY, sel ? l[1] : -INFINITY, sel ? -l[0] : -INFINITY,
                  sel ? -l[1] : -INFINITY};
   block_allreduce<2, 4>(s3, m3, red);
+  RLMD_TS(8);
   // -- Zipf-plot tail index of the selected losses' order statistics
-  //    (critic_loss.py:238-266): both critics sorted in one pass, critic g in
-  //    the g-th kp-aligned thread segment
-  int kp = 1;
-  while (kp < k) kp <<= 1;
-  __syncthreads();
-  if (sel) {
-    lsel[0][rank] = l[0];
-    lsel[1][rank] = l[1];
-  }
-  __syncthreads();
-  const int g_seg = b / kp, slot = b % kp;
-  uint64_t key = ~0ull;
-  if (g_seg < 2 && slot < k) key = ((uint64_t)(~f2key(lsel[g_seg][slot])) << 32) | (uint32_t)slot;
-  const uint64_t sk = rlmd_block_bitonic(key, kp, keys);
-  float lg = 0.f;
-  const bool zin = g_seg < 2 && slot < k;
-  if (zin) lg = logf(lsel[g_seg][(int)(sk & 0xffffffffu)] + a.log_noise);
-  float s4[2] = {zin && g_seg == 0 ? lg : 0.f, zin && g_seg == 1 ? lg : 0.f};
+  //    (critic_loss.py:238-266): each critic's selected losses ranked among
+  //    themselves, descending, ties by selection rank; that rank is the slot
+  RLMD_TS(9);
+  block_rank(sel ? ((uint64_t)(~f2key(l[0])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of[1]);
+  block_rank(sel ? ((uint64_t)(~f2key(l[1])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of[2]);
+  const int rz0 = sel ? rank_of[1][rank] : 0, rz1 = sel ? rank_of[2][rank] : 0;
+  RLMD_TS(10);
+  const float lg0 = sel ? logf(l[0] + a.log_noise) : 0.f;
+  const float lg1 = sel ? logf(l[1] + a.log_noise) : 0.f;
+  float s4[2] = {lg0, lg1};
   float m4[1] = {-INFINITY};
   block_allreduce<2, 0>(s4, m4, red);
-  const float lmean = zin ? s4[g_seg] / k : 0.f;
-  const float zx = zin ? a.zipf_x[slot] : 0.f;
-  float s5[2] = {zin && g_seg == 0 ? zx * (lg - lmean) : 0.f, zin && g_seg == 1 ? zx * (lg - lmean) : 0.f};
+  float s5[2] = {sel ? a.zipf_x[rz0] * (lg0 - s4[0] / k) : 0.f, sel ? a.zipf_x[rz1] * (lg1 - s4[1] / k) : 0.f};
   block_allreduce<2, 0>(s5, m4, red);
+  RLMD_TS(11);
   // -- gradients of grad_scale * (mean(l1[sel]) + mean(l2[sel])) w.r.t. q
   if (in) {
     a.dq[0][b] = sel ? a.grad_scale * dl[0] / (float)k : 0.f;
@@ -385,6 +407,7 @@ __global__ void __launch_bounds__(1024) critic_loss_kernel(LossArgs a) {
     a.stats[14] = kern[0];
     a.stats[15] = kern[1];
   }
+  RLMD_TS(12);
 }
 
 // ---------------------------------------------------------------------------
@@ -405,10 +428,11 @@ struct ActorLossArgs {
   float target_entropy;
 };
 
-__global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
-  __shared__ uint64_t keys[1024];
+template <int NTH>
+__global__ void __launch_bounds__(NTH) actor_loss_kernel(ActorLossArgs a) {
+  __shared__ __attribute__((aligned(16))) uint64_t runs[NTH];
+  __shared__ int rank_of[NTH];
   __shared__ float red[16 * 4];
-  __shared__ int rank_of[1024];
   const int b = threadIdx.x, B = a.B;
   const bool in = b < B;
   LearnState* st = a.st;
@@ -427,16 +451,11 @@ __global__ void __launch_bounds__(1024) actor_loss_kernel(ActorLossArgs a) {
   const float lp = (in && a.logp) ? a.logp[b] : 0.f;
   const float v = a.algo == RLMD_SAC ? fminf(q1, q2) - alpha * lp : q1;
   const int k = a.topk ? (B < a.k ? B : a.k) : B;
-  int npow = 1;
-  while (npow < B) npow <<= 1;
   bool sel = in;
   if (a.topk) {
     // SAC sorts descending, TD3 ascending
     const uint64_t key = in ? ((uint64_t)(a.algo == RLMD_SAC ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)b : ~0ull;
-    const uint64_t sk = rlmd_block_bitonic(key, npow, keys);
-    __syncthreads();
-    if (b < B) rank_of[(int)(sk & 0xffffffffu)] = b;
-    __syncthreads();
+    block_rank(key, runs, rank_of);
     sel = in && rank_of[b] < k;
   }
   float sm[2] = {sel ? v : 0.f, in ? -(lp + a.target_entropy) : 0.f};
@@ -866,7 +885,10 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     la.algo = c.algo;
     la.log_noise = c.log_noise;
     la.grad_scale = sac ? 0.5f : 1.0f;  // SAC: 0.5 (q1_loss + q2_loss)
-    hipLaunchKernelGGL(critic_loss_kernel, dim3(1), dim3(1024), 0, st, la);
+    if (B <= 512)
+      hipLaunchKernelGGL(critic_loss_kernel<512>, dim3(1), dim3(512), 0, st, la);
+    else
+      hipLaunchKernelGGL(critic_loss_kernel<1024>, dim3(1), dim3(1024), 0, st, la);
     RLMD_LAUNCH_CHECK();
   }
   // ---- critic backward: data gradients per row, then all weight gradients
@@ -937,7 +959,10 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     al.algo = c.algo;
     al.topk = c.actor_topk;
     al.target_entropy = -(float)A;
-    hipLaunchKernelGGL(actor_loss_kernel, dim3(1), dim3(1024), 0, st, al);
+    if (B <= 512)
+      hipLaunchKernelGGL(actor_loss_kernel<512>, dim3(1), dim3(512), 0, st, al);
+    else
+      hipLaunchKernelGGL(actor_loss_kernel<1024>, dim3(1), dim3(1024), 0, st, al);
     RLMD_LAUNCH_CHECK();
     ABwdArgs ab{};
     ab.d = d;
@@ -1203,6 +1228,14 @@ int rlmd_agent_learn_batch(rlmd_agent_t ag, const float* s, const float* a, cons
   RLMD_TRY(rlmd::refresh_copies(ag, st));
   return rlmd::learn_body(ag, eff, eps_a, eps_b, rlmd::stats_slot(ag, stats, 0), st);
 }
+
+#ifdef RLMD_TIMING
+int rlmd_debug_ts(unsigned long long* out) {
+  RLMD_HIP(hipDeviceSynchronize());
+  RLMD_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(rlmd::g_ts), sizeof(unsigned long long) * 64));
+  return 0;
+}
+#endif
 
 int rlmd_agent_scalars(rlmd_agent_t ag, double* out) {
   RLMD_CHECK(ag && out, "null argument");
