@@ -20,6 +20,7 @@ Output: ONE JSON line on rank 0 (see the harness contract), with
   cpu_baseline  the CPU oracle port of the same loop on the host cores.
 """
 import argparse
+import glob
 import json
 import math
 import os
@@ -110,13 +111,37 @@ def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
 
 
 def load_traffic():
-    path = os.path.join(ROOT, "profiles", "pmc_env_kernel.json")
-    if not os.path.exists(path):
+    """HBM bytes per env_train_kernel launch from the newest committed PMC summary
+    (profiles/<round>_pmc_env.json, written by tools/pmc_summary.py from separate
+    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same bench command)."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_env.json")))
+    if not paths:
         return None
     try:
-        return json.load(open(path))
+        return json.load(open(paths[-1]))
     except Exception:
         return None
+
+
+def reduce_ranks(elapsed, ep_stats, steps, world, device):
+    """Logging-time exchange across ranks (the only collective of the run): the
+    max-over-ranks wall time, and one all_gather of every rank's log slab
+    [episodes, sum final reward, sum length, steps seen, env steps timed].
+    RCCL ("nccl") on the GPU box; tests/test_multirank_cpu.py runs it on gloo."""
+    import torch
+    import torch.distributed as dist
+
+    el_t = torch.tensor([elapsed], dtype=torch.float64, device=device)
+    slab = torch.cat([ep_stats.to(device=device, dtype=torch.float64),
+                      torch.tensor([steps], dtype=torch.float64, device=device)])
+    if world > 1:
+        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
+        gathered = [torch.empty_like(slab) for _ in range(world)]
+        dist.all_gather(gathered, slab)
+        slab_all = torch.stack(gathered)
+    else:
+        slab_all = slab[None]
+    return float(el_t.item()), slab_all
 
 
 def main():
@@ -172,17 +197,7 @@ def main():
     cnt = (C.c_int64 * 3)()
     _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
     _abi.check(_abi.lib().rlmd_profile_enable(0))
-    el_t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    # logging-time exchange: one RCCL all_gather of each rank's episode-log slab
-    slab = torch.cat([tr.ep_stats.double(), torch.tensor([float(N * args.steps)], dtype=torch.float64, device=dev)])
-    if world > 1:
-        dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
-        gathered = [torch.empty_like(slab) for _ in range(world)]
-        dist.all_gather(gathered, slab)
-        slab_all = torch.stack(gathered)
-    else:
-        slab_all = slab[None]
-    t_max = float(el_t.item())
+    t_max, slab_all = reduce_ranks(elapsed, tr.ep_stats.double(), float(N * args.steps), world, dev)
     total_steps = float(slab_all[:, 4].sum().item())
     value = total_steps / t_max
 

@@ -366,7 +366,7 @@ __device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st)
   }
 }
 
-__global__ void env_reset_kernel(EnvParams P, const uint8_t* mask, double* state) {
+__global__ void __launch_bounds__(256) env_reset_kernel(EnvParams P, const uint8_t* mask, double* state) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= P.n_lanes) return;
   if (mask && !mask[lane]) return;
@@ -375,7 +375,7 @@ __global__ void env_reset_kernel(EnvParams P, const uint8_t* mask, double* state
   });
 }
 
-__global__ void env_step_kernel(EnvParams P, uint32_t step, const float* __restrict__ actions,
+__global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t step, const float* __restrict__ actions,
                                 const double* __restrict__ draws, double* next_state,
                                 double* reward, uint8_t* done, double* risk) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -405,14 +405,16 @@ __global__ void env_step_kernel(EnvParams P, uint32_t step, const float* __restr
 // fused training step: action (warm-up draw | policy) -> action_window clip ->
 // env step -> replay insert (s, a, r, s', learn_done) -> auto reset.
 // ---------------------------------------------------------------------------
-__global__ void env_train_kernel(EnvParams P, uint32_t step, float* actions, int random_actions,
+__global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t step, float* actions, int random_actions,
                                  int abs_actions, float clip_lo, float clip_hi, float* obs,
                                  rlmd::ReplayView rb, int64_t ring_base, double* ep_stats) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lane >= P.n_lanes) return;
+  double st_n = 0.0, st_r = 0.0, st_t = 0.0;  // finished-episode stats of this lane
+  if (lane < P.n_lanes) {
   const int S = P.state_dim, A = P.action_dim;
-  float a[RLMD_MAX_ACTION];
-  for (int i = 0; i < A; ++i) {
+  // action i: warm-up Philox draw (|.| unless GBM/market) or the policy's, then the
+  // smoothing-window clip; recomputed per use (no per-lane array -> no scratch)
+  auto act = [&](int i) -> float {
     float v;
     if (random_actions) {
       const rlmd_u32x4 w = rlmd_philox(P.seed, lane, step, RLMD_TAG_WARMUP_ACTION, (uint32_t)(i >> 1));
@@ -422,19 +424,19 @@ __global__ void env_train_kernel(EnvParams P, uint32_t step, float* actions, int
     } else {
       v = actions[(int64_t)lane * A + i];
     }
-    a[i] = fminf(fmaxf(v, clip_lo), clip_hi);
-  }
+    return fminf(fmaxf(v, clip_lo), clip_hi);
+  };
   const int64_t row = (ring_base + lane) % rb.capacity;
   // s (current obs) goes to the ring unchanged
   for (int k = 0; k < S; ++k) rb.state[row * S + k] = obs[(int64_t)lane * S + k];
-  for (int i = 0; i < A; ++i) rb.action[row * A + i] = a[i];
+  for (int i = 0; i < A; ++i) rb.action[row * A + i] = act(i);
 
   const double w0 = P.wealth[lane];
   const int t = P.time[lane];
   const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
   const uint32_t ep = P.episode[lane];
   StepOut o = env_step_lane(
-      P, lane, w0, t, start, ep, [&](int i) { return a[i]; },
+      P, lane, w0, t, start, ep, act,
       [&](int j) { return philox_draw(P, lane, step, j); },
       [&](int k, double v) {
         const float f = (float)v;
@@ -445,19 +447,32 @@ __global__ void env_train_kernel(EnvParams P, uint32_t step, float* actions, int
   rb.reward[row] = (float)o.reward;  // max(reward, r_abs_zero = -inf)
   rb.done[row] = o.learn_done;
   if (o.done) {
-    if (ep_stats) {
-      atomicAdd(&ep_stats[0], 1.0);
-      atomicAdd(&ep_stats[1], o.reward);
-      atomicAdd(&ep_stats[2], (double)t);
-    }
+    st_n = 1.0;
+    st_r = o.reward;
+    st_t = (double)t;
     env_reset_lane(P, lane, [&](int k, double v) { obs[(int64_t)lane * S + k] = (float)v; });
   } else {
     P.wealth[lane] = o.W;
     P.time[lane] = t + 1;
   }
+  }
+  // episode statistics: one wave-reduced atomic per wave instead of one per lane
+  if (ep_stats) {
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+      st_n += __shfl_xor(st_n, m, 64);
+      st_r += __shfl_xor(st_r, m, 64);
+      st_t += __shfl_xor(st_t, m, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && st_n > 0.0) {
+      atomicAdd(&ep_stats[0], st_n);
+      atomicAdd(&ep_stats[1], st_r);
+      atomicAdd(&ep_stats[2], st_t);
+    }
+  }
 }
 
-__global__ void env_obs_reset_kernel(EnvParams P, float* obs) {
+__global__ void __launch_bounds__(256) env_obs_reset_kernel(EnvParams P, float* obs) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= P.n_lanes) return;
   env_reset_lane(P, lane, [&](int k, double v) { obs[(int64_t)lane * P.state_dim + k] = (float)v; });

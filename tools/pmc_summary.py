@@ -1,0 +1,62 @@
+"""Turn one round's rocprofv3 outputs (tools/profile_round.sh) into profiles/.
+
+  python tools/pmc_summary.py r01
+
+writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, per kernel),
+profiles/<tag>_kernel_summary.txt (top kernels, per-dispatch averages) and
+profiles/<tag>_pmc_env.json: HBM bytes per env_train_kernel launch from the
+separate FETCH_SIZE and WRITE_SIZE passes.  Units and gfx950 corrections
+(MI355X_MICROARCH.md, HBM section): both counters are KiB; FETCH_SIZE counts
+half the bytes of wide coalesced reads on gfx950, so it is doubled.
+"""
+import csv
+import json
+import os
+import shutil
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def counter(path, name, kernel="env_train_kernel"):
+    vals, grids = [], set()
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel in row["Kernel_Name"] and row["Counter_Name"] == name:
+                vals.append(float(row["Counter_Value"]))
+                grids.add(int(row["Grid_Size"]))
+    return vals, grids
+
+
+def main(tag):
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    dst = os.path.join(ROOT, "profiles")
+    os.makedirs(dst, exist_ok=True)
+    stats = os.path.join(src, "trace", "trace_kernel_stats.csv")
+    shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    rows = list(csv.DictReader(open(stats)))
+    tot = sum(float(r["TotalDurationNs"]) for r in rows)
+    lines = [f"rocprofv3 --kernel-trace --stats: python bench.py --no-cpu-baseline --steps 25 --warmup 5 "
+             f"(C2, 65,536 GBM lanes, SAC 256/256 bf16, K=8)", "",
+             f"{'calls':>6} {'avg_us':>9} {'total_ms':>9} {'pct':>6}  kernel"]
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+        n, t = int(r["Calls"]), float(r["TotalDurationNs"])
+        lines.append(f"{n:6d} {t / n / 1e3:9.2f} {t / 1e6:9.3f} {100 * t / tot:6.2f}  {r['Name'][:120]}")
+    open(os.path.join(dst, f"{tag}_kernel_summary.txt"), "w").write("\n".join(lines) + "\n")
+    fetch, g1 = counter(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write, g2 = counter(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
+    fetch_b = 2.0 * 1024.0 * statistics.median(fetch)
+    write_b = 1024.0 * statistics.median(write)
+    out = {"kernel": "env_train_kernel", "lanes": sorted(g1 | g2)[0], "launches": [len(fetch), len(write)],
+           "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
+           "hbm_bytes_per_launch": fetch_b + write_b,
+           "method": "median over launches of separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes; KiB x 1024; "
+                     "FETCH_SIZE doubled (gfx950 half-count of wide coalesced reads)"}
+    json.dump(out, open(os.path.join(dst, f"{tag}_pmc_env.json"), "w"), indent=1)
+    print(json.dumps(out, indent=1))
+    print("\n".join(lines[:14]))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
