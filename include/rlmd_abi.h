@@ -91,12 +91,26 @@ int rlmd_replay_insert(rlmd_replay_t rb, int64_t n, const float* s_dev, const fl
                        const float* r_dev, const float* s2_dev, const uint8_t* done_dev,
                        void* stream);
 int rlmd_replay_mem_idx(rlmd_replay_t rb, int64_t* mem_idx);
-/* Replaces sample_exp (tools/replay_torch.py:360-412): B DISTINCT uniform indices
- * in [0, min(mem_idx, capacity)) drawn with Philox(seed, (slot, draw_ctr, TAG, round))
- * and gathered; idx_dev i64 [B]; s/s2 f32 [B,S], a [B,A], r [B], done u8 [B]. */
+/* Replaces the multi_steps > 1 path of tools/replay.py (ReplayBuffer
+ * _episode_history :93-141 and the history sampling :176-332): `lanes`
+ * independent transition streams (transition p of lane l at row
+ * (p * lanes + l) % capacity), n-step returns summed (additive != 0, dynamics
+ * "A") or multiplied (dynamics "M") with discount gamma.  Call before the first
+ * insert; capacity must be a multiple of lanes.  n_steps <= 1 = single-step. */
+int rlmd_replay_set_multistep(rlmd_replay_t rb, int32_t lanes, int32_t n_steps, int32_t additive,
+                              double gamma);
+/* Replaces sample_exp (tools/replay_torch.py:360-412 / tools/replay.py:334-376): B
+ * DISTINCT uniform indices in [0, min(mem_idx, capacity)) drawn with
+ * Philox(seed, (slot, draw_ctr, TAG, round)) and gathered; idx_dev i64 [B];
+ * s/s2 f32 [B,S], a [B,A], r [B], done u8 [B], eff i32 [B] (nullable).  In
+ * multi-step mode s/a/r are the history's initial state/action and n-step
+ * return and eff the effective length (the target bootstraps with gamma^eff). */
 int rlmd_replay_sample(rlmd_replay_t rb, int32_t batch, uint64_t seed, uint64_t draw_ctr,
                        int64_t* idx_dev, float* s_dev, float* a_dev, float* r_dev, float* s2_dev,
-                       uint8_t* done_dev, void* stream);
+                       uint8_t* done_dev, int32_t* eff_dev, void* stream);
+/* The gather half of sample_exp for caller-chosen rows (rows_dev i64 [n]). */
+int rlmd_replay_gather(rlmd_replay_t rb, int32_t n, const int64_t* rows_dev, float* s_dev, float* a_dev,
+                       float* r_dev, float* s2_dev, uint8_t* done_dev, int32_t* eff_dev, void* stream);
 
 /* ------------------------------------------------------------------- agent */
 enum { RLMD_SAC = 0, RLMD_TD3 = 1 };

@@ -71,7 +71,9 @@ SIGNATURES = {
     "rlmd_replay_insert": (C.c_int, [P, I64, P, P, P, P, P, P]),
     "rlmd_replay_mem_idx": (C.c_int, [P, C.POINTER(I64)]),
     "rlmd_replay_read": (C.c_int, [P, I64, I64, P, P, P, P, P, P]),
-    "rlmd_replay_sample": (C.c_int, [P, I32, U64, U64, P, P, P, P, P, P, P]),
+    "rlmd_replay_sample": (C.c_int, [P, I32, U64, U64, P, P, P, P, P, P, P, P]),
+    "rlmd_replay_set_multistep": (C.c_int, [P, I32, I32, I32, C.c_double]),
+    "rlmd_replay_gather": (C.c_int, [P, I32, P, P, P, P, P, P, P, P]),
     "rlmd_agent_layout": (C.c_int, [C.POINTER(AgentCfg), C.POINTER(I64), C.POINTER(I64),
                                     C.POINTER(I64), C.POINTER(I64)]),
     "rlmd_agent_create": (C.c_int, [C.POINTER(AgentCfg), P, P, P, P, P, C.POINTER(P)]),

@@ -176,12 +176,20 @@ class DeviceAgent:
 
 
 class ReplayMemory:
-    """On-device ring (rlmd_replay_*) with the reference's mem_idx attribute."""
+    """On-device ring (rlmd_replay_*) with the reference's mem_idx attribute.
 
-    def __init__(self, capacity, S, A, device="cuda:0"):
+    multi_steps > 1 selects the n-step history sampling of tools/replay.py
+    (:93-332) over `lanes` independent transition streams; dynamics "A" sums the
+    discounted rewards, anything else multiplies them (replay.py:280-283)."""
+
+    def __init__(self, capacity, S, A, device="cuda:0", multi_steps=1, lanes=1, dynamics="A", gamma=0.99):
         h = C.c_void_p()
         check(_abi.lib().rlmd_replay_create(int(capacity), S, A, C.byref(h)))
         self.h, self.capacity, self.S, self.A, self.device = h, int(capacity), S, A, torch.device(device)
+        self.multi_steps = int(multi_steps)
+        if self.multi_steps > 1:
+            check(_abi.lib().rlmd_replay_set_multistep(h, int(lanes), self.multi_steps,
+                                                       1 if str(dynamics) == "A" else 0, float(gamma)))
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -204,6 +212,18 @@ class ReplayMemory:
         r = torch.as_tensor(np.asarray(reward, dtype=np.float32).reshape(n), device=dev)
         d = torch.as_tensor(np.asarray(done, dtype=np.uint8).reshape(n), device=dev)
         check(_abi.lib().rlmd_replay_insert(self.h, n, ptr(s), ptr(a), ptr(r), ptr(s2), ptr(d), stream_ptr()))
+
+    def gather(self, rows):
+        """sample_exp's gather for given ring rows: (s, a, r, s', done, eff)."""
+        dev = self.device
+        rows = torch.as_tensor(rows, dtype=torch.int64, device=dev)
+        n = rows.numel()
+        s, s2 = torch.empty(n, self.S, device=dev), torch.empty(n, self.S, device=dev)
+        a, r = torch.empty(n, self.A, device=dev), torch.empty(n, device=dev)
+        d, eff = torch.empty(n, dtype=torch.uint8, device=dev), torch.empty(n, dtype=torch.int32, device=dev)
+        check(_abi.lib().rlmd_replay_gather(self.h, n, ptr(rows), ptr(s), ptr(a), ptr(r), ptr(s2), ptr(d), ptr(eff),
+                                            stream_ptr()))
+        return s, a, r, s2, d.bool(), eff
 
 
 def _loss_code(name):
@@ -252,7 +272,8 @@ class _Agent:
         self.dev = DeviceAgent(self.algo, S, A, h1, h2, self.batch_size, self.optimise_count,
                                loss=inputs["loss_fn"], precision=precision, seed=seed, device=device, **kw)
         buf = int(min(inputs["buffer"], inputs["n_cumsteps"]))  # replay.py:75-78
-        self.memory = ReplayMemory(buf, S, A, device=device)
+        self.memory = ReplayMemory(buf, S, A, device=device, multi_steps=int(inputs.get("multi_steps", 1)),
+                                   dynamics=inputs.get("dynamics", "A"), gamma=float(inputs["discount"]))
         self._act_ctr = 0
         self.file_prefix = None
 

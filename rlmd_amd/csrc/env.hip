@@ -446,6 +446,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
       [&](int, double) {});
   rb.reward[row] = (float)o.reward;  // max(reward, r_abs_zero = -inf)
   rb.done[row] = o.learn_done;
+  if (rb.n_steps > 1) rlmd::ms_record(rb, lane, row, o.learn_done);
   if (o.done) {
     st_n = 1.0;
     st_r = o.reward;

@@ -619,6 +619,7 @@ struct Scratch {
   float *s, *a, *r, *s2, *xsa;
   uint8_t* done;
   int64_t* idx;
+  int32_t* eff;  // multi-step effective lengths
   // target path: target q per row (no head bias), logp of the next actions
   float *logp_next, *tpart[2], *y;
   // critic path
@@ -1027,9 +1028,10 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
   if (k > 0) RLMD_TRY(refresh_copies(ag, st));
   for (int i = 0; i < k; ++i) {
     Scratch& S_ = ag->sc;
+    int32_t* eff = v.n_steps > 1 ? S_.eff : nullptr;
     RLMD_TRY(replay_sample_launch(v, M, c.batch, c.seed ^ 0x5eed5eed5eedull, 0, &ag->st->learn_cntr,
-                                  S_.idx, S_.s, S_.a, S_.r, S_.s2, S_.done, S_.xsa, st));
-    RLMD_TRY(learn_body(ag, nullptr, nullptr, nullptr, stats_slot(ag, stats, i), st));
+                                  S_.idx, S_.s, S_.a, S_.r, S_.s2, S_.done, S_.xsa, eff, st));
+    RLMD_TRY(learn_body(ag, eff, nullptr, nullptr, stats_slot(ag, stats, i), st));
   }
   return 0;
 }
@@ -1129,6 +1131,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.xsa, B * X);
   RLMD_ALLOC(s.done, B);
   RLMD_ALLOC(s.idx, B);
+  RLMD_ALLOC(s.eff, B);
   RLMD_ALLOC(s.logp_next, B);
   RLMD_ALLOC(s.y, B);
   RLMD_ALLOC(s.h1, B * H1);
@@ -1302,6 +1305,8 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   hipStream_t st = (hipStream_t)stream;
   const int N = rlmd::env_lanes(env);
   const rlmd::ReplayView v = rlmd::replay_view(rb);
+  RLMD_CHECK(v.n_steps <= 1 || (v.lanes == N && rlmd::replay_mem_idx(rb) % N == 0),
+             "multi-step replay: its lane count must equal the env's lanes");
   RLMD_CHECK(v.S == rlmd::env_state_dim(env) && v.A == rlmd::env_action_dim(env),
              "replay / env dims differ");
   const int64_t cs = cfg->cum_step;

@@ -14,9 +14,16 @@
 //              already appeared at a smaller slot (found through an LDS hash
 //              table whose entries keep the minimum owning slot), repeat
 //              (collision rate <= B/M <= 1/8 per round).
+// Multi-step mode (tools/replay.py:93-332): rows carry (position, episode,
+// episode start) tags and every lane its episode bookkeeping, so the reference's
+// history slicing — including its one-step-ahead slices of finished episodes and
+// the episode-0 fallback of in-progress ones — is O(1) per
+// sampled row; the n-step return, initial (next) state and action, and eff are
+// gathered in the same kernel (restated in oracle/replay.py MultiStepRing).
 #include <string.h>
 
 #include <string>
+#include <vector>
 
 #include "rlmd_common.h"
 #include "rlmd_internal.h"
@@ -29,13 +36,74 @@ struct rlmd_replay_s {
 namespace {
 
 constexpr int kSampleThreads = RLMD_MAX_BATCH;
+
+__device__ __forceinline__ int64_t ms_row(const rlmd::ReplayView& rb, int lane, int64_t pos) {
+  return (pos * rb.lanes + lane) % rb.capacity;
+}
+
+// Gather row `row` into output slot i: single-step copies the row; multi-step
+// follows MultiStepRing.gather (oracle/replay.py).
+__device__ void gather_row(const rlmd::ReplayView& rb, int64_t row, int i, float* s, float* a, float* r,
+                           float* s2, uint8_t* done, float* xsa, int32_t* eff) {
+  const int S = rb.S, A = rb.A;
+  int64_t src = row;  // row supplying the (initial) state and action
+  float rew = rb.reward[row];
+  int e = 1;
+  if (rb.n_steps > 1) {
+    const int lane = (int)(row % rb.lanes);
+    const int32_t* t = rb.tag + 3 * row;
+    const int32_t* ls = rb.lane + 4 * (int64_t)lane;
+    const int64_t sp = t[0], j = t[1], aj = t[2], m = ls[1], d0 = ls[3];
+    int64_t lo, b;
+    if (j == 0) {
+      lo = 0;
+      b = sp;
+    } else if (j < m) {
+      lo = aj;
+      b = rb.done[row] ? sp : sp + 1;
+    } else {
+      lo = 0;
+      b = sp - aj + 1 < d0 ? sp - aj + 1 : d0;
+    }
+    e = (int)(b - lo + 1 < rb.n_steps ? b - lo + 1 : rb.n_steps);
+    const int64_t f = b - e + 1;
+    double acc = rb.additive ? 0.0 : 1.0;
+    for (int k = 0; k < e - 1; ++k) {
+      const double term = pow(rb.gamma, (double)k) * (double)rb.reward[ms_row(rb, lane, f + k)];
+      acc = rb.additive ? acc + term : acc * term;
+    }
+    rew = (float)acc;
+    src = ms_row(rb, lane, f);
+    for (int k = 0; k < S; ++k) {
+      const float v = rb.next_state[src * S + k];  // histories hold next states
+      if (s) s[(int64_t)i * S + k] = v;
+      if (xsa) xsa[(int64_t)i * (S + A) + k] = v;
+    }
+  } else {
+    for (int k = 0; k < S; ++k) {
+      const float v = rb.state[row * S + k];
+      if (s) s[(int64_t)i * S + k] = v;
+      if (xsa) xsa[(int64_t)i * (S + A) + k] = v;
+    }
+  }
+  for (int k = 0; k < S; ++k)
+    if (s2) s2[(int64_t)i * S + k] = rb.next_state[row * S + k];
+  for (int k = 0; k < A; ++k) {
+    const float v = rb.action[src * A + k];
+    if (a) a[(int64_t)i * A + k] = v;
+    if (xsa) xsa[(int64_t)i * (S + A) + S + k] = v;
+  }
+  if (r) r[i] = rew;
+  if (done) done[i] = rb.done[row];
+  if (eff) eff[i] = e;
+}
 constexpr int kMaxRounds = 64;
 constexpr int kSortPopulation = 8192;  // M at or below: sort-based subset
 
 __global__ void __launch_bounds__(kSampleThreads)
     replay_sample_kernel(rlmd::ReplayView rb, int64_t M, int B, uint64_t seed, uint32_t ctr_lo,
                          uint32_t ctr_hi, int32_t* dev_ctr, int64_t* idx_out, float* s, float* a,
-                         float* r, float* s2, uint8_t* done, float* xsa) {
+                         float* r, float* s2, uint8_t* done, float* xsa, int32_t* eff) {
   __shared__ uint64_t keys[kSortPopulation];
   __shared__ int64_t cand[kSampleThreads];
   __shared__ int any_dup;
@@ -113,21 +181,14 @@ __global__ void __launch_bounds__(kSampleThreads)
   if (dev_ctr && i == 0) *dev_ctr = (int32_t)ctr_lo + 1;
   if (i >= B) return;
   const int64_t row = cand[i];
-  const int S = rb.S, A = rb.A;
   if (idx_out) idx_out[i] = row;
-  for (int k = 0; k < S; ++k) {
-    const float v = rb.state[row * S + k];
-    if (s) s[(int64_t)i * S + k] = v;
-    if (xsa) xsa[(int64_t)i * (S + A) + k] = v;
-    if (s2) s2[(int64_t)i * S + k] = rb.next_state[row * S + k];
-  }
-  for (int k = 0; k < A; ++k) {
-    const float v = rb.action[row * A + k];
-    if (a) a[(int64_t)i * A + k] = v;
-    if (xsa) xsa[(int64_t)i * (S + A) + S + k] = v;
-  }
-  if (r) r[i] = rb.reward[row];
-  if (done) done[i] = rb.done[row];
+  gather_row(rb, row, i, s, a, r, s2, done, xsa, eff);
+}
+
+__global__ void replay_gather_kernel(rlmd::ReplayView rb, int n, const int64_t* rows, float* s, float* a,
+                                     float* r, float* s2, uint8_t* done, int32_t* eff) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) gather_row(rb, rows[i], i, s, a, r, s2, done, nullptr, eff);
 }
 
 __global__ void replay_insert_kernel(rlmd::ReplayView rb, int64_t base, int64_t n, const float* s,
@@ -143,6 +204,7 @@ __global__ void replay_insert_kernel(rlmd::ReplayView rb, int64_t base, int64_t 
   for (int k = 0; k < rb.A; ++k) rb.action[row * rb.A + k] = a[i * rb.A + k];
   rb.reward[row] = r[i];
   rb.done[row] = d[i];
+  if (rb.n_steps > 1) rlmd::ms_record(rb, (int)((base + i) % rb.lanes), row, d[i] != 0);
 }
 
 __global__ void replay_read_kernel(rlmd::ReplayView rb, int64_t start, int64_t n, float* s, float* a,
@@ -170,12 +232,12 @@ void replay_advance(rlmd_replay_t rb, int64_t n) { rb->mem_idx += n; }
 
 int replay_sample_launch(const ReplayView& rb, int64_t M, int B, uint64_t seed, uint64_t ctr,
                          int32_t* dev_ctr, int64_t* idx, float* s, float* a, float* r, float* s2,
-                         uint8_t* done, float* xsa, hipStream_t stream) {
+                         uint8_t* done, float* xsa, int32_t* eff, hipStream_t stream) {
   RLMD_CHECK(B >= 1 && B <= RLMD_MAX_BATCH, "batch must be in [1, 1024]");
   RLMD_CHECK(M >= B, "replay holds fewer transitions than the mini-batch");
   RLMD_CHECK(M <= (int64_t)1 << 52, "replay too large");
   hipLaunchKernelGGL(replay_sample_kernel, dim3(1), dim3(kSampleThreads), 0, stream, rb, M, B, seed,
-                     (uint32_t)ctr, (uint32_t)(ctr >> 32), dev_ctr, idx, s, a, r, s2, done, xsa);
+                     (uint32_t)ctr, (uint32_t)(ctr >> 32), dev_ctr, idx, s, a, r, s2, done, xsa, eff);
   RLMD_LAUNCH_CHECK();
   return 0;
 }
@@ -195,7 +257,32 @@ int rlmd_replay_create(int64_t capacity, int32_t S, int32_t A, rlmd_replay_t* ou
   RLMD_HIP(hipMalloc(&rb->v.action, sizeof(float) * capacity * A));
   RLMD_HIP(hipMalloc(&rb->v.reward, sizeof(float) * capacity));
   RLMD_HIP(hipMalloc(&rb->v.done, capacity));
+  rb->v.n_steps = 1;
+  rb->v.lanes = 1;
+  rb->v.additive = 1;
+  rb->v.gamma = 0.99;
   *out = rb;
+  return 0;
+}
+
+int rlmd_replay_set_multistep(rlmd_replay_t rb, int32_t lanes, int32_t n_steps, int32_t additive,
+                              double gamma) {
+  RLMD_CHECK(rb, "null replay");
+  RLMD_CHECK(rb->mem_idx == 0, "multi-step mode must be set before the first insert");
+  RLMD_CHECK(lanes >= 1 && rb->v.capacity % lanes == 0, "capacity must be a multiple of the lane count");
+  RLMD_CHECK(n_steps >= 1, "multi_steps must be >= 1");
+  rb->v.n_steps = n_steps;
+  rb->v.lanes = lanes;
+  rb->v.additive = additive ? 1 : 0;
+  rb->v.gamma = gamma;
+  if (n_steps > 1) {
+    if (!rb->v.tag) RLMD_HIP(hipMalloc(&rb->v.tag, sizeof(int32_t) * 3 * rb->v.capacity));
+    if (rb->v.lane) RLMD_HIP(hipFree(rb->v.lane));
+    RLMD_HIP(hipMalloc(&rb->v.lane, sizeof(int32_t) * 4 * lanes));
+    std::vector<int32_t> init(4 * (size_t)lanes, 0);
+    for (int32_t l = 0; l < lanes; ++l) init[4 * l + 3] = -1;
+    RLMD_HIP(hipMemcpy(rb->v.lane, init.data(), sizeof(int32_t) * init.size(), hipMemcpyHostToDevice));
+  }
   return 0;
 }
 
@@ -206,6 +293,8 @@ int rlmd_replay_destroy(rlmd_replay_t rb) {
   (void)hipFree(rb->v.action);
   (void)hipFree(rb->v.reward);
   (void)hipFree(rb->v.done);
+  if (rb->v.tag) (void)hipFree(rb->v.tag);
+  if (rb->v.lane) (void)hipFree(rb->v.lane);
   delete rb;
   return 0;
 }
@@ -214,6 +303,7 @@ int rlmd_replay_insert(rlmd_replay_t rb, int64_t n, const float* s, const float*
                        const float* s2, const uint8_t* d, void* stream) {
   RLMD_CHECK(rb && s && a && r && s2 && d, "null argument");
   if (n <= 0) return 0;
+  RLMD_CHECK(rb->v.n_steps <= 1 || n <= rb->v.lanes, "multi-step insert: at most one transition per lane per call");
   hipLaunchKernelGGL(replay_insert_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
                      (hipStream_t)stream, rb->v, rb->mem_idx, n, s, a, r, s2, d);
   RLMD_LAUNCH_CHECK();
@@ -238,11 +328,21 @@ int rlmd_replay_mem_idx(rlmd_replay_t rb, int64_t* m) {
 }
 
 int rlmd_replay_sample(rlmd_replay_t rb, int32_t B, uint64_t seed, uint64_t ctr, int64_t* idx,
-                       float* s, float* a, float* r, float* s2, uint8_t* done, void* stream) {
+                       float* s, float* a, float* r, float* s2, uint8_t* done, int32_t* eff, void* stream) {
   RLMD_CHECK(rb, "null replay");
   const int64_t M = rb->mem_idx < rb->v.capacity ? rb->mem_idx : rb->v.capacity;
-  return rlmd::replay_sample_launch(rb->v, M, B, seed, ctr, nullptr, idx, s, a, r, s2, done, nullptr,
+  return rlmd::replay_sample_launch(rb->v, M, B, seed, ctr, nullptr, idx, s, a, r, s2, done, nullptr, eff,
                                     (hipStream_t)stream);
+}
+
+int rlmd_replay_gather(rlmd_replay_t rb, int32_t n, const int64_t* rows, float* s, float* a, float* r,
+                       float* s2, uint8_t* done, int32_t* eff, void* stream) {
+  RLMD_CHECK(rb && rows, "null argument");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(replay_gather_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     rb->v, n, rows, s, a, r, s2, done, eff);
+  RLMD_LAUNCH_CHECK();
+  return 0;
 }
 
 }  // extern "C"

@@ -11,7 +11,9 @@
 
 namespace rlmd {
 
-// Device view of the replay ring (SoA, f32; done as u8).
+// Device view of the replay ring (SoA, f32; done as u8).  Multi-step mode
+// (n_steps > 1, tools/replay.py:93-332) adds per-row tags and per-lane episode
+// bookkeeping; transition p of lane l sits at row (p * lanes + l) % capacity.
 struct ReplayView {
   float* state;       // [capacity, S]
   float* action;      // [capacity, A]
@@ -20,7 +22,30 @@ struct ReplayView {
   uint8_t* done;      // [capacity]
   int64_t capacity;
   int32_t S, A;
+  int32_t n_steps;    // <= 1: single-step
+  int32_t lanes;      // independent transition streams
+  int32_t additive;   // 1: dynamics "A" (sum), 0: product
+  double gamma;
+  int32_t* tag;       // [capacity, 3]: lane-local position, episode ordinal, episode start
+  int32_t* lane;      // [lanes, 4]: next position, finished episodes, in-progress start, end of episode 0
 };
+
+// Record the multi-step tags of a transition just written to `row` by lane `l`
+// (one writer per lane per launch) and advance that lane's episode bookkeeping.
+__device__ inline void ms_record(const ReplayView& rb, int l, int64_t row, bool done) {
+  int32_t* ls = rb.lane + 4 * (int64_t)l;
+  const int32_t p = ls[0];
+  int32_t* t = rb.tag + 3 * row;
+  t[0] = p;
+  t[1] = ls[1];
+  t[2] = ls[2];
+  if (done) {
+    if (ls[1] == 0) ls[3] = p;
+    ls[1] += 1;
+    ls[2] = p + 1;
+  }
+  ls[0] = p + 1;
+}
 
 ReplayView replay_view(rlmd_replay_t rb);
 int64_t replay_mem_idx(rlmd_replay_t rb);
@@ -37,8 +62,10 @@ int env_action_dim(rlmd_env_t env);
 // the critic input [s | a] as xsa [B, S+A].
 // dev_ctr (nullable): device counter used as the draw counter instead of ctr and
 // incremented by the kernel (the learner's learn_step_cntr).
+// Multi-step mode: s / a are the history's initial next-state / action, r the
+// n-step return, eff [B] the effective length (nullable); see oracle/replay.py.
 int replay_sample_launch(const ReplayView& rb, int64_t M, int B, uint64_t seed, uint64_t ctr,
                          int32_t* dev_ctr, int64_t* idx, float* s, float* a, float* r, float* s2,
-                         uint8_t* done, float* xsa, hipStream_t stream);
+                         uint8_t* done, float* xsa, int32_t* eff, hipStream_t stream);
 
 }  // namespace rlmd

@@ -398,6 +398,57 @@ def shadow_fixtures():
 
 
 # ----------------------------------------------------------------------------
+# F4: multi-step replay histories (tools/replay.py:93-332)
+# ----------------------------------------------------------------------------
+MS_STREAMS = {"a": (30, [4, 9, 13, 22]), "b": (26, [12, 14, 15, 20]), "c": (16, [0, 1, 5, 6, 7])}
+MS_CHECKPOINTS = (1, 2, 3, 5, 6, 8, 11, 13, 14, 16, 20, 23, 26, 30)
+
+
+def multistep_fixtures():
+    """Scripted single-stream transitions stored with the reference ReplayBuffer
+    (NumPy, the default buffer_gpu=False); after every checkpoint prefix, the
+    multi-step (reward, initial state, initial action, eff) of EVERY stored step
+    from its own history logic (_episode_rewards_states_actions +
+    _multi_step_batch, i.e. sample_exp without the random index draw).
+    terminal_memory is zero-filled after construction, as the reference's 1e6-row
+    np.empty is in practice (fresh zero pages); the store sequence is learn_done
+    as a Python bool, as scripts/rl_multiplicative.py:218-220 passes it."""
+    from tools.replay import ReplayBuffer
+
+    S, A = 2, 1
+    out = {}
+    for name, (L, dones) in MS_STREAMS.items():
+        idx = np.arange(L)
+        st = np.stack([idx - 1.0, 0.5 - idx], 1)
+        s2 = np.stack([idx * 1.0, -0.5 - idx], 1)
+        act = (0.05 * idx - 0.5)[:, None].astype(np.float32)
+        rew = 1.0 + 0.013 * idx + 0.001 * (idx % 3)
+        done = np.isin(idx, dones)
+        out.update({f"{name}/state": st, f"{name}/action": act, f"{name}/reward": rew,
+                    f"{name}/next_state": s2, f"{name}/done": done})
+        for n in (3, 5, 7):
+            for dyn in ("A", "M"):
+                inputs = {"input_dims": [S], "num_actions": A, "mini_batch_size": 1, "discount": 0.99,
+                          "multi_steps": n, "r_abs_zero": None, "dynamics": dyn, "buffer": 4096,
+                          "n_cumsteps": 4096}
+                rb = ReplayBuffer(inputs)
+                rb.terminal_memory[:] = False
+                for t in range(L):
+                    rb.store_exp(st[t], act[t], rew[t], s2[t], bool(done[t]))
+                    T = t + 1
+                    if T in MS_CHECKPOINTS:
+                        rb.batch_size = T
+                        hist = rb._episode_rewards_states_actions(list(range(T)))
+                        R, Sx, Ax, eff = rb._multi_step_batch(*hist)
+                        key = f"{name}/n{n}{dyn}/T{T}"
+                        out[key + "/reward"] = np.asarray(R, dtype=np.float64)
+                        out[key + "/state"] = np.asarray(Sx, dtype=np.float64)
+                        out[key + "/action"] = np.asarray(Ax, dtype=np.float64)
+                        out[key + "/eff"] = np.asarray(eff, dtype=np.int64)
+    return out
+
+
+# ----------------------------------------------------------------------------
 # F5: learn() steps for SAC and TD3
 # ----------------------------------------------------------------------------
 def _inputs(algo, S, A, hidden, loss_fn="MSE", B=None, k=None):
@@ -544,6 +595,7 @@ def main():
         "market_env.npz": market_env_traces,
         "critic_loss.npz": critic_loss_fixtures,
         "shadow.npz": shadow_fixtures,
+        "multistep.npz": multistep_fixtures,
         "learn.npz": learn_fixtures,
     }
     only = sys.argv[1:]

@@ -108,7 +108,7 @@ def test_replay_ring_and_distinct_sampling(dev, cap, inserts):
         s2 = torch.empty(B, S, device=dev)
         d = torch.empty(B, dtype=torch.uint8, device=dev)
         P = _abi.ptr
-        _abi.check(_abi.lib().rlmd_replay_sample(h, B, 42, ctr, P(idx), P(s), P(a), P(r), P(s2), P(d),
+        _abi.check(_abi.lib().rlmd_replay_sample(h, B, 42, ctr, P(idx), P(s), P(a), P(r), P(s2), P(d), None,
                                                  _abi.stream_ptr()))
         got = idx.cpu().numpy()
         assert len(set(got.tolist())) == B  # without replacement
@@ -137,7 +137,7 @@ def test_replay_tiny_population_forces_duplicate_rounds(dev):
     _abi.check(_abi.lib().rlmd_replay_insert(h, M, P(z), P(za), P(zr), P(z), P(zd), _abi.stream_ptr()))
     idx = torch.empty(B, dtype=torch.int64, device=dev)
     r = torch.empty(B, device=dev)
-    _abi.check(_abi.lib().rlmd_replay_sample(h, B, 9, 1, P(idx), None, None, P(r), None, None, _abi.stream_ptr()))
+    _abi.check(_abi.lib().rlmd_replay_sample(h, B, 9, 1, P(idx), None, None, P(r), None, None, None, _abi.stream_ptr()))
     got = idx.cpu().numpy()
     ref = orp.sample_indices(9, 1, M, B)
     assert len(set(got.tolist())) == B

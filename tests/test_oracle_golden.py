@@ -140,3 +140,31 @@ def test_market_env_episode_matches_reference(golden, key):
         np.testing.assert_allclose(risk[0], g[key + "/risk"][t], rtol=RTOL, equal_nan=True)
         state = ns
     assert g[key + "/done"][-1][0]  # the episode ran to its done flag
+
+
+# ---------------------------------------------------------------- F4 multi-step
+@pytest.mark.parametrize("stream", ["a", "b", "c"])
+@pytest.mark.parametrize("n", [3, 5, 7])
+@pytest.mark.parametrize("dyn", ["A", "M"])
+def test_multistep_history_matches_reference(golden, stream, n, dyn):
+    """oracle.replay.MultiStepRing (one lane) vs the reference ReplayBuffer's
+    multi-step reward / initial state / initial action / eff for every stored
+    step after every checkpoint (tools/replay.py:93-332)."""
+    from oracle.replay import MultiStepRing
+
+    g = golden("multistep.npz")
+    st, act, rew, s2, done = (g[f"{stream}/{k}"] for k in ("state", "action", "reward", "next_state", "done"))
+    ring = MultiStepRing(4096, 2, 1, 1, n, dyn, 0.99)
+    checked = 0
+    for t in range(len(rew)):
+        ring.insert(st[t], act[t], rew[t], s2[t], done[t])
+        key = f"{stream}/n{n}{dyn}/T{t + 1}"
+        if key + "/eff" not in g:
+            continue
+        R, S0, A0, S2, D, eff = ring.gather(np.arange(t + 1))
+        np.testing.assert_array_equal(eff, g[key + "/eff"], err_msg=key)
+        np.testing.assert_allclose(R, g[key + "/reward"], rtol=1e-15, atol=0, err_msg=key)
+        np.testing.assert_array_equal(S0, g[key + "/state"], err_msg=key)
+        np.testing.assert_array_equal(A0, g[key + "/action"].astype(np.float32).astype(np.float64), err_msg=key)
+        checked += 1
+    assert checked >= 8
