@@ -74,6 +74,14 @@ int rlmd_env_step(rlmd_env_t env, const float* actions_dev, const double* draws_
                   double* next_state_dev, double* reward_dev, uint8_t* done_dev, double* risk_dev,
                   void* stream);
 
+/* The same step with FLOAT64 actions [N, A]: what the reference's env.step
+ * receives inside the smoothing window (utils.action_window's np.clip with
+ * np.float64 bounds promotes under NumPy 2, tools/utils.py:345-373), where every
+ * action-derived quantity is float64. */
+int rlmd_env_step_f64(rlmd_env_t env, const double* actions_dev, const double* draws_dev,
+                      double* next_state_dev, double* reward_dev, uint8_t* done_dev, double* risk_dev,
+                      void* stream);
+
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
 

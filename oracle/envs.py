@@ -180,9 +180,17 @@ class OracleVecEnv:
         return px.uniform_draws(self.seed, lanes, step, px.TAG_ENV_DRAW, self.D)
 
     def step(self, actions, draws=None):
-        """actions f32 [N, A]; draws [N, D] (None: Philox at the step counter)."""
-        a32 = np.asarray(actions, dtype=np.float32).reshape(self.N, self.A)
+        """actions [N, A] (f32 from the policy / warm-up sampler, or f64 inside the
+        smoothing window, where np.clip with np.float64 bounds promotes them —
+        utils.py:345-373); draws [N, D] (None: Philox at the step counter)."""
+        arr = np.asarray(actions)
+        AT = np.float64 if arr.dtype == np.float64 else np.float32  # dtype the env receives
+        a32 = arr.astype(AT).reshape(self.N, self.A)
         a = a32.astype(np.float64)
+
+        def hs(x):  # (a + MAX_ABS_ACTION) / 2 in the action dtype (Python floats weak)
+            return (x + AT(MAX_ABS_ACTION)) / AT(2)
+
         if draws is None and self.f != MARKET:
             draws = self.philox_draws()
         self.step_ctr += 1
@@ -197,21 +205,21 @@ class OracleVecEnv:
         if f == DICE_SH:
             idx = choice_index(draws[:, 0], DICE_P)
             r = DICE_VALS[idx]
-            r_sh32 = np.where(idx == 2, F32(SH_MID_R), np.where(idx == 0, F32(SH_UP_R), F32(SH_DOWN_R)))
+            r_sh32 = np.where(idx == 2, AT(SH_MID_R), np.where(idx == 0, AT(SH_UP_R), AT(SH_DOWN_R)))
             if inv == INV_INSURED:
-                lev32 = a32[:, 0] * F32(SH_I_LEV)  # f32 * Python float
+                lev32 = a32[:, 0] * AT(SH_I_LEV)  # action * Python float
                 lev = lev32.astype(np.float64)
-                lev_sh32 = F32(1) - lev32
+                lev_sh32 = AT(1) - lev32
                 lev_max = np.abs(lev) == MAX_ABS_ACTION * LF
-                lev_min = np.abs(lev32) < F32(MIN_WEIGHT)
+                lev_min = np.abs(lev32) < AT(MIN_WEIGHT)
             else:
                 off = {INV_A: 0, INV_B: 1, INV_C: 2}[inv]
                 if inv in (INV_B, INV_C):
-                    sl32 = half_shift32(a32[:, 0])
+                    sl32 = hs(a32[:, 0])
                 if inv == INV_C:
-                    ret32 = half_shift32(a32[:, 1])
+                    ret32 = hs(a32[:, 1])
                 lev = a[:, off] * LF
-                lev_sh32 = half_shift32(a32[:, off + 1]) * F32(1)
+                lev_sh32 = hs(a32[:, off + 1]) * AT(1)
                 lev_max = np.abs(lev) == MAX_ABS_ACTION * LF
                 lev_min = np.abs(lev) < MIN_WEIGHT
             R = lev * r + (lev_sh32 * r_sh32).astype(np.float64)
@@ -222,10 +230,10 @@ class OracleVecEnv:
         else:
             off = {INV_A: 0, INV_B: 1, INV_C: 2}[inv]
             if inv == INV_B:
-                sl32 = np.abs(a32[:, 0]) if f == COIN else half_shift32(a32[:, 0])  # Q1
+                sl32 = np.abs(a32[:, 0]) if f == COIN else hs(a32[:, 0])  # Q1
             elif inv == INV_C:
-                sl32 = half_shift32(a32[:, 0])
-                ret32 = half_shift32(a32[:, 1])
+                sl32 = hs(a32[:, 0])
+                ret32 = hs(a32[:, 1])
             if f == COIN:
                 rets = COIN_VALS[choice_index(draws, COIN_P)]
             elif f == DICE:
@@ -235,18 +243,20 @@ class OracleVecEnv:
             else:
                 rets = np.stack([self.market_obs(l, t[l])[:n] / self.market_obs(l, 0)[:n] - 1
                                  for l in range(self.N)])
-            if f in (GBM, MARKET):  # f32 leverages (f32 action * Python int)
+            use_all = f in (GBM, MARKET)  # lev_max uses np.all (Q4)
+            f32lev = use_all and AT is np.float32  # f32 action * Python int stays f32
+            if f32lev:
                 lev32 = a32[:, off:off + n] * F32(LF)
                 levs = lev32.astype(np.float64)
                 lev_max = np.all(np.abs(lev32) == F32(MAX_ABS_ACTION * LF), 1)
                 lev_min = np.all(np.abs(lev32) < F32(MIN_WEIGHT), 1)
             else:
                 levs = a[:, off:off + n] * LF
-                lev_max = np.any(np.abs(levs) == MAX_ABS_ACTION * LF, 1)
+                lev_max = (np.all if use_all else np.any)(np.abs(levs) == MAX_ABS_ACTION * LF, 1)
                 lev_min = np.all(np.abs(levs) < MIN_WEIGHT, 1)
             R = np.sum(levs * rets, 1)
             # np.mean(lev): float32 pairwise mean for the f32 leverages of GBM / market
-            lev_mean = (np.mean(lev32, 1) if f in (GBM, MARKET) else np.mean(levs, 1)).astype(np.float64)
+            lev_mean = (np.mean(lev32, 1) if f32lev else np.mean(levs, 1)).astype(np.float64)
         if inv in (INV_B, INV_C):
             sl = sl32.astype(np.float64)
         if inv == INV_C:
@@ -264,12 +274,12 @@ class OracleVecEnv:
             W = np.clip(w0 * g, MIN_VALUE, mv)
             done_active = np.zeros(self.N, bool)
         else:
-            mw32 = np.maximum(F32(INITIAL_VALUE) * sl32, F32(MIN_VALUE))  # f32 (Python floats weak)
+            mw32 = np.maximum(AT(INITIAL_VALUE) * sl32, AT(MIN_VALUE))  # action dtype (Python floats weak)
             mw = mw32.astype(np.float64)
             if inv == INV_C:
                 mw = np.where(w0 <= INITIAL_VALUE, mw, INITIAL_VALUE + (w0 - INITIAL_VALUE) * ret)
             # first step of an episode: wealth is the Python float 1e4 -> f32 subtraction
-            active32 = np.maximum(F32(INITIAL_VALUE) - mw32, F32(0)).astype(np.float64)
+            active32 = np.maximum(AT(INITIAL_VALUE) - mw32, AT(0)).astype(np.float64)
             active = np.where(t == 1, active32, np.maximum(w0 - mw, 0))
             W = np.clip(mw + active * g, mw, mv)
             done_active = active == 0

@@ -65,6 +65,7 @@ SIGNATURES = {
     "rlmd_env_dims": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)]),
     "rlmd_env_reset": (C.c_int, [P, P, P, P]),
     "rlmd_env_step": (C.c_int, [P, P, P, P, P, P, P, P]),
+    "rlmd_env_step_f64": (C.c_int, [P, P, P, P, P, P, P, P]),
     "rlmd_env_lane_state": (C.c_int, [P, P, P]),
     "rlmd_replay_create": (C.c_int, [I64, I32, I32, C.POINTER(P)]),
     "rlmd_replay_destroy": (C.c_int, [P]),

@@ -153,27 +153,34 @@ __device__ inline T np_mean(int n, GetF get) {
   return np_sum<T>(n, get) / (T)n;
 }
 
-__device__ inline float half_shift32(float a) { return (a + (float)kMaxAbsAction) / 2.f; }
 
 struct StepOut {
   double W, reward;
   bool done, learn_done;
 };
 
-// One env step for one lane.  `act(i)` yields action i (f32), `draw(j)` the
+// One env step for one lane.  `act(i)` yields action i as AT, `draw(j)` the
 // j-th uniform/normal.  Writes state element k through st(k, v) and risk
 // element k through rk(k, v).
-template <typename ActF, typename DrawF, typename StF, typename RkF>
+// AT is the dtype of the action array the reference's env.step receives: f32
+// from the policy / warm-up sampler, f64 inside the smoothing window (np.clip
+// with np.float64 bounds promotes, utils.py:345-373).  Every action-derived
+// quantity follows NumPy 2's promotion from it: with f32 actions, GBM/market
+// leverage (x Python int) and the half-shifted stop-loss / retention / safe-haven
+// weights stay f32; with f64 actions everything is f64.
+template <typename AT, typename ActF, typename DrawF, typename StF, typename RkF>
 __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, double w0, int t,
                                         int start, uint32_t ep, ActF act, DrawF draw, StF st,
                                         RkF rk) {
   const FamConst C = fam_const(P.fam);
   const int fam = P.fam, inv = P.inv, n = P.n;
-  const bool f32lev = (fam == RLMD_GBM || fam == RLMD_MARKET);
+  const bool use_all = (fam == RLMD_GBM || fam == RLMD_MARKET);  // lev_max: np.all (Q4)
+  const bool f32lev = use_all && sizeof(AT) == 4;                // lev = f32 action * int
   const double lev_cap64 = kMaxAbsAction * C.lev_factor;
   const float lev_cap32 = (float)lev_cap64;
+  auto half_shift = [](AT a) -> AT { return (a + (AT)kMaxAbsAction) / (AT)2; };
 
-  float sl32 = NAN, ret32 = NAN, lev_sh32 = NAN;
+  AT sl32 = (AT)NAN, ret32 = (AT)NAN, lev_sh32 = (AT)NAN;
   double R = 0.0, lev_mean = 0.0, lev0 = 0.0, r_sh = 0.0, r_die = 0.0;
   bool lev_max_any = false, lev_max_all = true, lev_min_all = true;
   int lev_off = 0;
@@ -184,29 +191,29 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
     r_sh = idx == 2 ? -0.99 : (idx == 0 ? -0.99 : 5.0);  // MID, UP -> -0.99 ; DOWN -> 5
     double lev;
     if (inv == RLMD_INV_INSURED) {
-      const float lev32 = act(0) * (float)kShILev;  // f32 * Python float
+      const AT lev32 = act(0) * (AT)kShILev;  // action * Python float
       lev = (double)lev32;
-      lev_sh32 = 1.f - lev32;
-      lev_min_all = fabsf(lev32) < (float)kMinWeight;
+      lev_sh32 = (AT)1 - lev32;
+      lev_min_all = fabs(lev32) < (AT)kMinWeight;
     } else {
       const int ai = inv == RLMD_INV_A ? 0 : (inv == RLMD_INV_B ? 1 : 2);
-      if (inv != RLMD_INV_A) sl32 = half_shift32(act(0));
-      if (inv == RLMD_INV_C) ret32 = half_shift32(act(1));
+      if (inv != RLMD_INV_A) sl32 = half_shift(act(0));
+      if (inv == RLMD_INV_C) ret32 = half_shift(act(1));
       lev = (double)act(ai) * C.lev_factor;
-      lev_sh32 = half_shift32(act(ai + 1)) * 1.f;
+      lev_sh32 = half_shift(act(ai + 1)) * (AT)1;
       lev_min_all = fabs(lev) < kMinWeight;
     }
     lev_max_any = fabs(lev) == lev_cap64;
-    R = lev * r_die + (double)(lev_sh32 * (float)r_sh);
+    R = lev * r_die + (double)(lev_sh32 * (AT)r_sh);
     lev_mean = lev;
     lev0 = lev;
   } else {
     if (inv == RLMD_INV_B) {
-      sl32 = fam == RLMD_COIN ? fabsf(act(0)) : half_shift32(act(0));  // Coin_InvB: |a0| (Q1)
+      sl32 = fam == RLMD_COIN ? (AT)fabs(act(0)) : half_shift(act(0));  // Coin_InvB: |a0| (Q1)
       lev_off = 1;
     } else if (inv == RLMD_INV_C) {
-      sl32 = half_shift32(act(0));
-      ret32 = half_shift32(act(1));
+      sl32 = half_shift(act(0));
+      ret32 = half_shift(act(1));
       lev_off = 2;
     }
     auto ret_of = [&](int j) -> double {
@@ -216,25 +223,26 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
       return market_obs(P, lane, start, ep, t, j) / market_obs(P, lane, start, ep, 0, j) - 1.0;
     };
     auto lev_of = [&](int j) -> double {
-      const float a = act(lev_off + j);
-      return f32lev ? (double)(a * (float)C.lev_factor) : (double)a * C.lev_factor;
+      const AT a = act(lev_off + j);
+      return f32lev ? (double)((float)a * (float)C.lev_factor) : (double)a * C.lev_factor;
     };
     R = np_sum<double>(n, [&](int j) { return lev_of(j) * ret_of(j); });  // np.sum(lev * r)
     for (int j = 0; j < n; ++j) {
-      const float a = act(lev_off + j);
+      const AT a = act(lev_off + j);
       if (f32lev) {
-        const float l32 = a * (float)C.lev_factor;
+        const float l32 = (float)a * (float)C.lev_factor;
         lev_max_all &= fabsf(l32) == lev_cap32;
         lev_min_all &= fabsf(l32) < (float)kMinWeight;
       } else {
         const double lev = (double)a * C.lev_factor;
+        lev_max_all &= fabs(lev) == lev_cap64;
         lev_max_any |= fabs(lev) == lev_cap64;
         lev_min_all &= fabs(lev) < kMinWeight;
       }
     }
     lev0 = lev_of(0);
     if (f32lev)
-      lev_mean = (double)np_mean<float>(n, [&](int j) { return act(lev_off + j) * (float)C.lev_factor; });
+      lev_mean = (double)np_mean<float>(n, [&](int j) { return (float)act(lev_off + j) * (float)C.lev_factor; });
     else
       lev_mean = np_mean<double>(n, [&](int j) { return (double)act(lev_off + j) * C.lev_factor; });
   }
@@ -255,13 +263,13 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
     mw = kMinValue;
     W = fmin(fmax(w0 * g, kMinValue), C.max_value);
   } else {
-    const float mw32 = fmaxf((float)kInitialValue * sl32, (float)kMinValue);
+    const AT mw32 = fmax((AT)kInitialValue * sl32, (AT)kMinValue);
     if (inv == RLMD_INV_C && w0 > kInitialValue)
       mw = kInitialValue + (w0 - kInitialValue) * (double)ret32;
     else
       mw = (double)mw32;
     // episode's first step: wealth is still the Python float 1e4 -> f32 subtraction
-    const double active = t == 1 ? (double)fmaxf((float)kInitialValue - mw32, 0.f) : fmax(w0 - mw, 0.0);
+    const double active = t == 1 ? (double)fmax((AT)kInitialValue - mw32, (AT)0) : fmax(w0 - mw, 0.0);
     W = fmin(fmax(mw + active * g, mw), C.max_value);
     done_active = active == 0.0;
   }
@@ -296,7 +304,7 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
     }
   }
 
-  const bool lev_max = f32lev ? lev_max_all : lev_max_any;
+  const bool lev_max = use_all ? lev_max_all : lev_max_any;
   const bool done_time = fam == RLMD_MARKET &&
                          t == (P.obs_days == 1 ? P.time_length : P.time_length - P.obs_days + 1);
   const bool done = done_time || W == mw || reward < C.min_reward || R == C.min_return || lev_max ||
@@ -323,8 +331,8 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
     if (inv == RLMD_INV_C) rk(k++, (double)ret32);
     if (n > 1) {
       for (int j = 0; j < n; ++j) {
-        const float a = act(lev_off + j);
-        rk(k + j, f32lev ? (double)(a * (float)C.lev_factor) : (double)a * C.lev_factor);
+        const AT a = act(lev_off + j);
+        rk(k + j, f32lev ? (double)((float)a * (float)C.lev_factor) : (double)a * C.lev_factor);
       }
     }
   }
@@ -375,17 +383,18 @@ __global__ void __launch_bounds__(256) env_reset_kernel(EnvParams P, const uint8
   });
 }
 
-__global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t step, const float* __restrict__ actions,
+template <typename AT>
+__global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t step, const AT* __restrict__ actions,
                                 const double* __restrict__ draws, double* next_state,
                                 double* reward, uint8_t* done, double* risk) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= P.n_lanes) return;
-  const float* a = actions + (int64_t)lane * P.action_dim;
+  const AT* a = actions + (int64_t)lane * P.action_dim;
   const double w0 = P.wealth[lane];
   const int t = P.time[lane];
   const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
   const uint32_t ep = P.episode[lane];
-  StepOut o = env_step_lane(
+  StepOut o = env_step_lane<AT>(
       P, lane, w0, t, start, ep, [&](int i) { return a[i]; },
       [&](int j) {
         return draws ? draws[(int64_t)lane * P.draw_dim + j] : philox_draw(P, lane, step, j);
@@ -405,8 +414,12 @@ __global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t ste
 // fused training step: action (warm-up draw | policy) -> action_window clip ->
 // env step -> replay insert (s, a, r, s', learn_done) -> auto reset.
 // ---------------------------------------------------------------------------
+// AT = float outside the smoothing window; double inside it, where the clipped
+// action array is float64 (np.clip with np.float64 bounds, utils.py:345-373) and
+// is stored to the replay as the f32 cast of that value.
+template <typename AT>
 __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t step, float* actions, int random_actions,
-                                 int abs_actions, float clip_lo, float clip_hi, float* obs,
+                                 int abs_actions, double clip_lo, double clip_hi, float* obs,
                                  rlmd::ReplayView rb, int64_t ring_base, double* ep_stats) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   double st_n = 0.0, st_r = 0.0, st_t = 0.0;  // finished-episode stats of this lane
@@ -414,7 +427,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
   const int S = P.state_dim, A = P.action_dim;
   // action i: warm-up Philox draw (|.| unless GBM/market) or the policy's, then the
   // smoothing-window clip; recomputed per use (no per-lane array -> no scratch)
-  auto act = [&](int i) -> float {
+  auto act = [&](int i) -> AT {
     float v;
     if (random_actions) {
       const rlmd_u32x4 w = rlmd_philox(P.seed, lane, step, RLMD_TAG_WARMUP_ACTION, (uint32_t)(i >> 1));
@@ -424,18 +437,19 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
     } else {
       v = actions[(int64_t)lane * A + i];
     }
-    return fminf(fmaxf(v, clip_lo), clip_hi);
+    if (sizeof(AT) == 4) return (AT)v;
+    return (AT)fmin(fmax((double)v, clip_lo), clip_hi);
   };
   const int64_t row = (ring_base + lane) % rb.capacity;
   // s (current obs) goes to the ring unchanged
   for (int k = 0; k < S; ++k) rb.state[row * S + k] = obs[(int64_t)lane * S + k];
-  for (int i = 0; i < A; ++i) rb.action[row * A + i] = act(i);
+  for (int i = 0; i < A; ++i) rb.action[row * A + i] = (float)act(i);
 
   const double w0 = P.wealth[lane];
   const int t = P.time[lane];
   const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
   const uint32_t ep = P.episode[lane];
-  StepOut o = env_step_lane(
+  StepOut o = env_step_lane<AT>(
       P, lane, w0, t, start, ep, act,
       [&](int j) { return philox_draw(P, lane, step, j); },
       [&](int k, double v) {
@@ -519,12 +533,16 @@ int env_dims_for(const rlmd_env_cfg& c, int& S, int& A, int& R, int& D) {
 void env_train_launch_params(rlmd_env_t env, EnvParams*& P);
 
 int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uint32_t step,
-              float* actions, int random_actions, int abs_actions, float clip_lo, float clip_hi,
+              float* actions, int random_actions, int abs_actions, int window, double clip_lo, double clip_hi,
               float* obs, double* ep_stats, hipStream_t stream) {
   const int N = env->P.n_lanes;
-  hipLaunchKernelGGL(env_train_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, env->P, step,
-                     actions, random_actions, abs_actions, clip_lo, clip_hi, obs, rb, ring_base,
-                     ep_stats);
+  const dim3 grid((N + 255) / 256), block(256);
+  if (window)
+    hipLaunchKernelGGL(env_train_kernel<double>, grid, block, 0, stream, env->P, step, actions, random_actions,
+                       abs_actions, clip_lo, clip_hi, obs, rb, ring_base, ep_stats);
+  else
+    hipLaunchKernelGGL(env_train_kernel<float>, grid, block, 0, stream, env->P, step, actions, random_actions,
+                       abs_actions, clip_lo, clip_hi, obs, rb, ring_base, ep_stats);
   RLMD_LAUNCH_CHECK();
   return 0;
 }
@@ -629,7 +647,18 @@ int rlmd_env_step(rlmd_env_t env, const float* actions, const double* draws, dou
                   double* reward, uint8_t* done, double* risk, void* stream) {
   RLMD_CHECK(env && actions && next_state && reward && done, "null argument");
   const int N = env->P.n_lanes;
-  hipLaunchKernelGGL(env_step_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(env_step_kernel<float>, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
+                     env->P, env->step_ctr, actions, draws, next_state, reward, done, risk);
+  RLMD_LAUNCH_CHECK();
+  env->step_ctr++;
+  return 0;
+}
+
+int rlmd_env_step_f64(rlmd_env_t env, const double* actions, const double* draws, double* next_state,
+                      double* reward, uint8_t* done, double* risk, void* stream) {
+  RLMD_CHECK(env && actions && next_state && reward && done, "null argument");
+  const int N = env->P.n_lanes;
+  hipLaunchKernelGGL(env_step_kernel<double>, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
                      env->P, env->step_ctr, actions, draws, next_state, reward, done, risk);
   RLMD_LAUNCH_CHECK();
   env->step_ctr++;

@@ -1318,17 +1318,18 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
     RLMD_TRY(g_prof.record(0, 1, st));
   }
   // action_window (tools/utils.py:345-373): only warmup < cum_step <= smoothing_window
-  float lo = -INFINITY, hi = INFINITY;
-  if (cs <= cfg->smoothing_window && cs > cfg->warmup_steps) {
+  double lo = -INFINITY, hi = INFINITY;
+  const bool window = cs <= cfg->smoothing_window && cs > cfg->warmup_steps;
+  if (window) {
     const double ratio = (double)cs / (double)cfg->smoothing_window;
     const double width = (sin(M_PI * (ratio - 0.5)) + 1.0) / 2.0;
-    lo = (float)(width * -0.99);
-    hi = (float)(width * 0.99);
+    lo = width * -0.99;
+    hi = width * 0.99;
   }
   const int64_t base = rlmd::replay_mem_idx(rb);
   RLMD_TRY(g_prof.record(1, 0, st));
-  RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, lo,
-                           hi, obs, ep_stats, st));
+  RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, window ? 1 : 0,
+                           lo, hi, obs, ep_stats, st));
   RLMD_TRY(g_prof.record(1, 1, st));
   rlmd::replay_advance(rb, N);
   if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch) {

@@ -67,15 +67,19 @@ class VecEnv:
         return self.state
 
     def step(self, actions, draws=None, risk=True):
-        """actions f32 [N, A] (device); draws f64 [N, D] to inject (None: Philox)."""
-        a = actions.to(device=self.device, dtype=torch.float32).contiguous()
+        """actions [N, A] (device): f32, or f64 as inside the reference's smoothing
+        window (every action-derived quantity then f64); draws f64 [N, D] to inject
+        (None: Philox)."""
+        f64 = actions.dtype == torch.float64
+        a = actions.to(device=self.device, dtype=torch.float64 if f64 else torch.float32).contiguous()
         assert a.shape == (self.n_lanes, self.action_dim), a.shape
         d = None
         if draws is not None:
             d = draws.to(device=self.device, dtype=torch.float64).contiguous()
             assert d.shape == (self.n_lanes, self.draw_dim), d.shape
-        check(_abi.lib().rlmd_env_step(self.h, ptr(a), ptr(d), ptr(self.next_state), ptr(self.reward),
-                                       ptr(self.done), ptr(self.risk) if risk else None, stream_ptr()))
+        fn = _abi.lib().rlmd_env_step_f64 if f64 else _abi.lib().rlmd_env_step
+        check(fn(self.h, ptr(a), ptr(d), ptr(self.next_state), ptr(self.reward), ptr(self.done),
+                 ptr(self.risk) if risk else None, stream_ptr()))
         return self.next_state, self.reward, self.done, self.risk
 
     def lane_state(self):
@@ -117,7 +121,8 @@ class _SingleEnv:
         return self._v.reset()[0].cpu().numpy().copy()
 
     def step(self, action):
-        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, -1))
+        arr = np.asarray(action)
+        a = torch.as_tensor(arr.astype(np.float64 if arr.dtype == np.float64 else np.float32).reshape(1, -1))
         ns, r, d, risk = self._v.step(a)
         d = d[0].cpu().numpy()
         return (ns[0].cpu().numpy().copy(), np.float64(r[0].item()), [bool(d[0]), bool(d[1])],

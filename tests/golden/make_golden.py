@@ -159,13 +159,25 @@ EDGE_SPECS = [  # all-favourable draws so wealth reaches MAX_VALUE (done_state)
 ]
 
 
+def _window_actions(acts, t0=1000, sw=2000):
+    """The smoothing-window clip of scripts/rl_multiplicative.py:203-211 applied as
+    the reference applies it (tools/utils.py:345-373): np.clip with np.float64
+    bounds, so the env receives FLOAT64 actions (NumPy 2 promotion)."""
+    import tools.utils as ut
+
+    return np.stack([ut.action_window(acts[t], 0.99, -0.99, t0 + 1 + 7 * t, sw, t0) for t in range(len(acts))])
+
+
 def env_traces(n_steps=240, seed=7):
     import importlib
 
     out = {}
     rng = np.random.default_rng(seed)
-    specs = [(s, False) for s in ENV_SPECS] + [(s, True) for s in EDGE_SPECS]
-    for (fam, modname, cls, inv, n), edge in specs:
+    rng_w = np.random.default_rng(seed + 1000)
+    specs = ([(s, False, False) for s in ENV_SPECS] + [(s, True, False) for s in EDGE_SPECS]
+             + [(s, False, True) for s in ENV_SPECS])
+    for (fam, modname, cls, inv, n), edge, win in specs:
+        r_ = rng_w if win else rng
         mod = importlib.import_module("envs." + modname)
         rnd = _InjectedRandom()
         saved = mod.np
@@ -174,14 +186,17 @@ def env_traces(n_steps=240, seed=7):
             env = getattr(mod, cls)() if fam == "sh" else getattr(mod, cls)(n)
             a_dim = env.action_space.shape[0]
             s_dim = env.observation_space.shape[0]
-            acts = _action_schedule(rng, n_steps, a_dim)
+            acts = _action_schedule(r_, n_steps, a_dim)
             n_draw = 1 if fam == "sh" else n
             if fam == "gbm":
-                draws = rng.standard_normal((n_steps, n_draw))
+                draws = r_.standard_normal((n_steps, n_draw))
                 # fat left tail occasionally so MIN_RETURN clipping is exercised
                 draws[::29] -= 8.0
             else:
-                draws = rng.random((n_steps, n_draw))
+                draws = r_.random((n_steps, n_draw))
+            if win:
+                acts = _window_actions(acts)
+                assert acts.dtype == np.float64
             if edge:
                 acts = np.full((n_steps, a_dim), np.float32(0.7), dtype=np.float32)
                 if fam == "sh":
@@ -206,7 +221,7 @@ def env_traces(n_steps=240, seed=7):
                 if done[0]:
                     state = env.reset().copy()
             risk_dim = RISK[0].size
-            key = f"{cls}_n{n}" + ("_edge" if edge else "")
+            key = f"{cls}_n{n}" + ("_edge" if edge else "") + ("_win" if win else "")
             out[key + "/actions"] = acts
             out[key + "/draws"] = draws
             out[key + "/state"] = S

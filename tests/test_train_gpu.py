@@ -158,13 +158,55 @@ def test_policy_steps_apply_action_window_and_learn(dev):
         if cs >= 3:  # policy acted: tr.actions holds the raw policy actions
             raw = tr.actions.cpu().numpy()
             _, stored, _, _, _ = read_ring(tr, (t * N) % (N * 16), N)
-            if 3 < cs <= 8:
+            if 3 < cs <= 8:  # utils.action_window: np.clip with np.float64 bounds -> f64, stored as f32
                 w = (math.sin(math.pi * (cs / 8 - 0.5)) + 1) / 2
-                lo, hi = np.float32(w * -0.99), np.float32(w * 0.99)
-                np.testing.assert_array_equal(stored, np.clip(raw, lo, hi))
+                np.testing.assert_array_equal(stored, np.clip(raw.astype(np.float64), w * -0.99, w * 0.99).astype(np.float32))
             else:
                 np.testing.assert_array_equal(stored, raw)
     st = tr.last_stats()
     assert np.all(np.isfinite(st[[0, 1, 2, 3, 4, 5, 8, 9, 10, 11, 12, 13, 14, 15]])), st
     assert tr.agent.scalars()["learn_step_cntr"] == 2 * 12
     assert tr.agent.scalars()["nan_flag"] == 0
+
+
+@pytest.mark.parametrize("env,inv,fam,oinv", [("gbm", "A", oe.GBM, oe.INV_A), ("dice_sh", "B", oe.DICE_SH, oe.INV_B)])
+def test_window_steps_feed_the_env_float64_actions(dev, env, inv, fam, oinv):
+    """Inside the smoothing window the reference env receives FLOAT64 actions
+    (np.clip with np.float64 bounds): GBM leverage, stop-loss and safe-haven
+    weights are then f64, not f32.  The fused step must follow, bit for bit with
+    the oracle driven by the same clipped f64 actions and Philox draws."""
+    from rlmd_amd.trainer import VecTrainer
+
+    N, T, seed, warm, sw = 512, 14, 29, 3, 2000
+    tr = VecTrainer(env=env, investor=inv, n_lanes=N, algo="SAC", k_updates=0, seed=seed, warmup_steps=warm,
+                    smoothing_window=sw, replay_capacity=N * T, precision="fp32", device=dev)
+    ora = oe.OracleVecEnv(fam, oinv, N, 1, seed=seed)
+    obs = ora.reset()
+    for t in range(T):
+        tr.step()
+        if t < warm:
+            a = np.empty((N, ora.A), dtype=np.float32)
+            for i in range(ora.A):
+                v = px.philox(seed, np.arange(N), t, px.TAG_WARMUP_ACTION, i >> 1)
+                u = px.u01(v[0], v[1]) if i % 2 == 0 else px.u01(v[2], v[3])
+                a[:, i] = (-0.99 + 2 * 0.99 * u).astype(np.float32)
+            if fam != oe.GBM:
+                a = np.abs(a)
+        else:
+            raw = tr.actions.cpu().numpy()
+            w = (math.sin(math.pi * (t / sw - 0.5)) + 1) / 2 if t > warm else None
+            a = raw if w is None else np.clip(raw.astype(np.float64), w * -0.99, w * 0.99)
+        ns, r, d, _ = ora.step(a)
+        _, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
+        np.testing.assert_array_equal(a_r, a.astype(np.float32), err_msg=f"t={t} actions")
+        np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s2")
+        np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6, err_msg=f"t={t} r")
+        np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
+        w_gpu = tr.env.lane_state()[0]
+        live = ~d[:, 0]
+        # GBM draws go through Box-Muller (libm ulps, see test_env_gpu.py): 1e-12
+        np.testing.assert_allclose(w_gpu[live], ora.wealth[live], rtol=1e-12, atol=0, err_msg=f"t={t} wealth")
+        obs = ns.copy()
+        m = d[:, 0]
+        if m.any():
+            obs[m] = ora.reset(m)[m]
