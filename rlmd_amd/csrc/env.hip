@@ -414,9 +414,11 @@ __global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t ste
 // fused training step: action (warm-up draw | policy) -> action_window clip ->
 // env step -> replay insert (s, a, r, s', learn_done) -> auto reset.
 // ---------------------------------------------------------------------------
-// AT = float outside the smoothing window; double inside it, where the clipped
-// action array is float64 (np.clip with np.float64 bounds, utils.py:345-373) and
-// is stored to the replay as the f32 cast of that value.
+// AT = the dtype of the action array the reference's env.step receives:
+// float64 during warm-up (action_space.sample() of the float64 Box) and inside
+// the smoothing window (np.clip with np.float64 bounds, utils.py:345-373);
+// float32 for policy actions afterwards.  The replay stores the f32 cast, as the
+// reference's float64 buffer does when it batches to torch.float.
 template <typename AT>
 __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t step, float* actions, int random_actions,
                                  int abs_actions, double clip_lo, double clip_hi, float* obs,
@@ -428,17 +430,17 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
   // action i: warm-up Philox draw (|.| unless GBM/market) or the policy's, then the
   // smoothing-window clip; recomputed per use (no per-lane array -> no scratch)
   auto act = [&](int i) -> AT {
-    float v;
-    if (random_actions) {
+    double v;
+    if (random_actions) {  // Box(-0.99, 0.99, float64).sample() = low + (high - low) * random_sample()
       const rlmd_u32x4 w = rlmd_philox(P.seed, lane, step, RLMD_TAG_WARMUP_ACTION, (uint32_t)(i >> 1));
       const double u = (i & 1) ? rlmd_u01(w.z, w.w) : rlmd_u01(w.x, w.y);
-      v = (float)(-kMaxAbsAction + 2.0 * kMaxAbsAction * u);
-      if (abs_actions) v = fabsf(v);
+      v = -kMaxAbsAction + 2.0 * kMaxAbsAction * u;
+      if (abs_actions) v = fabs(v);
     } else {
-      v = actions[(int64_t)lane * A + i];
+      v = (double)actions[(int64_t)lane * A + i];
     }
-    if (sizeof(AT) == 4) return (AT)v;
-    return (AT)fmin(fmax((double)v, clip_lo), clip_hi);
+    if (sizeof(AT) == 4) return (AT)v;  // policy action outside the window: exact f32
+    return (AT)fmin(fmax(v, clip_lo), clip_hi);
   };
   const int64_t row = (ring_base + lane) % rb.capacity;
   // s (current obs) goes to the ring unchanged
@@ -537,7 +539,7 @@ int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uin
               float* obs, double* ep_stats, hipStream_t stream) {
   const int N = env->P.n_lanes;
   const dim3 grid((N + 255) / 256), block(256);
-  if (window)
+  if (window || random_actions)
     hipLaunchKernelGGL(env_train_kernel<double>, grid, block, 0, stream, env->P, step, actions, random_actions,
                        abs_actions, clip_lo, clip_hi, obs, rb, ring_base, ep_stats);
   else

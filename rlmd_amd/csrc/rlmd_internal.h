@@ -51,8 +51,9 @@ ReplayView replay_view(rlmd_replay_t rb);
 int64_t replay_mem_idx(rlmd_replay_t rb);
 void replay_advance(rlmd_replay_t rb, int64_t n);
 
-// window != 0: the smoothing-window clip [clip_lo, clip_hi] applies and the env
-// sees float64 actions (utils.py:345-373 under NumPy 2).
+// window != 0: the smoothing-window clip [clip_lo, clip_hi] applies.  Warm-up
+// (random_actions) and window steps hand the env float64 actions, as the
+// reference's float64 action space and np.clip with np.float64 bounds do.
 int env_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step,
               float* actions, int random_actions, int abs_actions, int window, double clip_lo, double clip_hi,
               float* obs, double* ep_stats, hipStream_t stream);

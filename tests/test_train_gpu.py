@@ -28,6 +28,17 @@ def read_ring(tr, start, n):
     return [x.cpu().numpy() for x in (s, a, r, s2, d)]
 
 
+def warmup_actions(seed, N, A, t, absw):
+    """Warm-up actions of step t: gym Box(-0.99, 0.99, float64).sample() =
+    low + (high - low) * random_sample() on the Philox uniforms (np.abs unless GBM)."""
+    a = np.empty((N, A), dtype=np.float64)
+    for i in range(A):
+        v = px.philox(seed, np.arange(N), t, px.TAG_WARMUP_ACTION, i >> 1)
+        u = px.u01(v[0], v[1]) if i % 2 == 0 else px.u01(v[2], v[3])
+        a[:, i] = -0.99 + 2 * 0.99 * u
+    return np.abs(a) if absw else a
+
+
 @pytest.mark.parametrize("env,inv,fam,oinv,n", [("gbm", "A", oe.GBM, oe.INV_A, 1), ("coin", "B", oe.COIN, oe.INV_B, 2),
                                                 ("dice_sh", "C", oe.DICE_SH, oe.INV_C, 1)])
 def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
@@ -42,16 +53,10 @@ def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
     absw = fam != oe.GBM
     for t in range(T):
         tr.step()
-        a = np.empty((N, ora.A), dtype=np.float32)
-        for i in range(ora.A):
-            v = px.philox(seed, np.arange(N), t, px.TAG_WARMUP_ACTION, i >> 1)
-            u = px.u01(v[0], v[1]) if i % 2 == 0 else px.u01(v[2], v[3])
-            a[:, i] = (-0.99 + 2 * 0.99 * u).astype(np.float32)
-        if absw:
-            a = np.abs(a)
-        ns, r, d, _ = ora.step(a)
+        a = warmup_actions(seed, N, ora.A, t, absw)
+        ns, r, d, _ = ora.step(a)  # float64 actions, as action_space.sample() gives
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
-        np.testing.assert_array_equal(a_r, a, err_msg=f"t={t} actions")
+        np.testing.assert_array_equal(a_r, a.astype(np.float32), err_msg=f"t={t} actions")
         np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s")
         np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s2")
         np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6)
@@ -171,10 +176,11 @@ def test_policy_steps_apply_action_window_and_learn(dev):
 
 @pytest.mark.parametrize("env,inv,fam,oinv", [("gbm", "A", oe.GBM, oe.INV_A), ("dice_sh", "B", oe.DICE_SH, oe.INV_B)])
 def test_window_steps_feed_the_env_float64_actions(dev, env, inv, fam, oinv):
-    """Inside the smoothing window the reference env receives FLOAT64 actions
-    (np.clip with np.float64 bounds): GBM leverage, stop-loss and safe-haven
-    weights are then f64, not f32.  The fused step must follow, bit for bit with
-    the oracle driven by the same clipped f64 actions and Philox draws."""
+    """During warm-up (float64 action space sample) and inside the smoothing window
+    (np.clip with np.float64 bounds) the reference env receives FLOAT64 actions:
+    GBM leverage, stop-loss and safe-haven weights are then f64, not f32; policy
+    actions after the window are f32.  The fused step must follow, against the
+    oracle driven by the same actions and Philox draws."""
     from rlmd_amd.trainer import VecTrainer
 
     N, T, seed, warm, sw = 512, 14, 29, 3, 2000
@@ -185,13 +191,7 @@ def test_window_steps_feed_the_env_float64_actions(dev, env, inv, fam, oinv):
     for t in range(T):
         tr.step()
         if t < warm:
-            a = np.empty((N, ora.A), dtype=np.float32)
-            for i in range(ora.A):
-                v = px.philox(seed, np.arange(N), t, px.TAG_WARMUP_ACTION, i >> 1)
-                u = px.u01(v[0], v[1]) if i % 2 == 0 else px.u01(v[2], v[3])
-                a[:, i] = (-0.99 + 2 * 0.99 * u).astype(np.float32)
-            if fam != oe.GBM:
-                a = np.abs(a)
+            a = warmup_actions(seed, N, ora.A, t, fam != oe.GBM)
         else:
             raw = tr.actions.cpu().numpy()
             w = (math.sin(math.pi * (t / sw - 0.5)) + 1) / 2 if t > warm else None
