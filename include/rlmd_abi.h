@@ -82,6 +82,23 @@ int rlmd_env_step_f64(rlmd_env_t env, const double* actions_dev, const double* d
                       double* next_state_dev, double* reward_dev, uint8_t* done_dev, double* risk_dev,
                       void* stream);
 
+/* Replaces the episode loop of eval_multiplicative (tools/eval_episodes.py:
+ * 231-274): every lane of `env` (reset by the caller) is one evaluation episode
+ * run with the constant action actions_dev f32 [N, A] (eval_next_action of the
+ * reset state), after the action window when warmup_steps < cum_step <=
+ * smoothing_window (float64 actions then), until done or max_steps.  Outputs the
+ * last reward f64 [N], the step count i32 [N] and the last risk vector f64 [N, R]
+ * (nullable).  draws_dev: injected draws f64 [N, max_steps, D] or NULL (Philox). */
+int rlmd_eval_rollout(rlmd_env_t env, const float* actions_dev, int32_t max_steps, int64_t cum_step,
+                      int32_t warmup_steps, int32_t smoothing_window, const double* draws_dev,
+                      double* reward_dev, int32_t* steps_dev, double* risk_dev, void* stream);
+/* The summary of eval_episodes.py:289-330 with NumPy's arithmetic (pairwise means,
+ * std ddof 0, median_unbiased percentiles) over n <= 1024 episodes: stats_dev f64
+ * [17] = l%, g% mean/med/5%/mad/std, V$ mean/med/5%/mad, steps mean/med/5%/mad/std,
+ * mean stop-loss and mean retention (NaN unless InvB / InvC). */
+int rlmd_eval_stats(const double* reward_dev, const int32_t* steps_dev, const double* risk_dev, int32_t n,
+                    int32_t risk_dim, int32_t investor, double* stats_dev, void* stream);
+
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
 

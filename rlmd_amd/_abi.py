@@ -67,6 +67,8 @@ SIGNATURES = {
     "rlmd_env_step": (C.c_int, [P, P, P, P, P, P, P, P]),
     "rlmd_env_step_f64": (C.c_int, [P, P, P, P, P, P, P, P]),
     "rlmd_env_lane_state": (C.c_int, [P, P, P]),
+    "rlmd_eval_rollout": (C.c_int, [P, P, I32, I64, I32, I32, P, P, P, P, P]),
+    "rlmd_eval_stats": (C.c_int, [P, P, P, I32, I32, I32, P, P]),
     "rlmd_replay_create": (C.c_int, [I64, I32, I32, C.POINTER(P)]),
     "rlmd_replay_destroy": (C.c_int, [P]),
     "rlmd_replay_insert": (C.c_int, [P, I64, P, P, P, P, P, P]),

@@ -489,6 +489,55 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
   }
 }
 
+// ---------------------------------------------------------------------------
+// evaluation episodes (tools/eval_episodes.py:176-399): every lane is one eval
+// episode from its reset state, the policy's action held constant for the whole
+// episode (action_window applied first when warmup < cum_step <= smoothing:
+// float64 actions then), stepped until done or max_steps; the last step's
+// reward, the step count and the last risk vector are kept.  Draws: injected
+// [N, max_steps, D] or Philox at (lane, step_base + k).
+// ---------------------------------------------------------------------------
+template <typename AT>
+__global__ void __launch_bounds__(256) eval_rollout_kernel(EnvParams P, uint32_t step_base, const float* actions,
+                                                           int max_steps, double clip_lo, double clip_hi,
+                                                           const double* draws, double* reward_out,
+                                                           int32_t* steps_out, double* risk_out) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= P.n_lanes) return;
+  const int A = P.action_dim, D = P.draw_dim, R = P.risk_dim;
+  auto act = [&](int i) -> AT {
+    const double v = (double)actions[(int64_t)lane * A + i];
+    if (sizeof(AT) == 4) return (AT)v;
+    return (AT)fmin(fmax(v, clip_lo), clip_hi);
+  };
+  double w = P.wealth[lane];
+  int t = P.time[lane];
+  const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
+  const uint32_t ep = P.episode[lane];
+  double run_reward = 0.0;
+  int k = 0;
+  while (k < max_steps) {
+    const StepOut o = env_step_lane<AT>(
+        P, lane, w, t, start, ep, act,
+        [&](int j) {
+          return draws ? draws[((int64_t)lane * max_steps + k) * D + j] : philox_draw(P, lane, step_base + k, j);
+        },
+        [&](int, double) {},
+        [&](int r, double v) {
+          if (risk_out) risk_out[(int64_t)lane * R + r] = v;
+        });
+    run_reward = o.reward;
+    ++k;
+    if (o.done) break;
+    w = o.W;
+    ++t;
+  }
+  P.wealth[lane] = w;
+  P.time[lane] = t;
+  reward_out[lane] = run_reward;
+  steps_out[lane] = k;
+}
+
 __global__ void __launch_bounds__(256) env_obs_reset_kernel(EnvParams P, float* obs) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= P.n_lanes) return;
@@ -664,6 +713,33 @@ int rlmd_env_step_f64(rlmd_env_t env, const double* actions, const double* draws
                      env->P, env->step_ctr, actions, draws, next_state, reward, done, risk);
   RLMD_LAUNCH_CHECK();
   env->step_ctr++;
+  return 0;
+}
+
+int rlmd_eval_rollout(rlmd_env_t env, const float* actions, int32_t max_steps, int64_t cum_step,
+                      int32_t warmup_steps, int32_t smoothing_window, const double* draws, double* reward,
+                      int32_t* steps, double* risk, void* stream) {
+  RLMD_CHECK(env && actions && reward && steps, "null argument");
+  RLMD_CHECK(max_steps >= 1, "max_steps must be >= 1");
+  const int N = env->P.n_lanes;
+  // eval_episodes.py:240-248: action_window when cum_steps <= smoothing_window,
+  // which clips only past the warm-up (utils.py:366-371)
+  const bool window = cum_step <= smoothing_window && cum_step > warmup_steps;
+  double lo = -INFINITY, hi = INFINITY;
+  if (window) {
+    const double width = (sin(M_PI * ((double)cum_step / (double)smoothing_window - 0.5)) + 1.0) / 2.0;
+    lo = width * -0.99;
+    hi = width * 0.99;
+  }
+  const dim3 grid((N + 255) / 256), block(256);
+  if (window)
+    hipLaunchKernelGGL(eval_rollout_kernel<double>, grid, block, 0, (hipStream_t)stream, env->P, env->step_ctr,
+                       actions, max_steps, lo, hi, draws, reward, steps, risk);
+  else
+    hipLaunchKernelGGL(eval_rollout_kernel<float>, grid, block, 0, (hipStream_t)stream, env->P, env->step_ctr,
+                       actions, max_steps, lo, hi, draws, reward, steps, risk);
+  RLMD_LAUNCH_CHECK();
+  env->step_ctr += (uint32_t)max_steps;
   return 0;
 }
 

@@ -32,6 +32,9 @@ class VecEnv:
         self.family = FAMILY[family] if isinstance(family, str) else family
         self.investor = INVESTOR[investor] if isinstance(investor, str) else investor
         self.n_lanes, self.n_gambles, self.device = n_lanes, n_gambles, torch.device(device)
+        self.seed = seed
+        self.make_kw = dict(prices=prices, obs_days=obs_days, time_length=time_length, action_days=action_days,
+                            shuffle_days=shuffle_days, sample_days=sample_days)
         cfg = _abi.EnvCfg(self.family, self.investor, n_lanes, n_gambles, obs_days, time_length,
                           action_days, shuffle_days, sample_days, 0, seed)
         self._prices = None

@@ -77,6 +77,34 @@ class VecTrainer:
         """loss[11] | logtemp | loss_params[4] of the last update (numpy f64)."""
         return self.stats[max(self.cfg.k_updates, 1) - 1].double().cpu().numpy()
 
+    def evaluate(self, n_eval=100, max_steps=100):
+        """eval_multiplicative (tools/eval_episodes.py:176-399) on the device: n_eval
+        episodes of a separate env (its own seed), each from the reset state with
+        the deterministic policy action held constant, the action window applied
+        as the reference does at this cum_step; returns the per-episode last
+        reward / steps / risk and the 17-entry summary (rlmd_eval_stats)."""
+        env = getattr(self, "_eval_env", None)
+        if env is None or env.n_lanes != n_eval:
+            kw = dict(self.env.make_kw, shuffle_days=3)  # eval shuffles market rows in blocks of 3 (E8)
+            env = VecEnv(self.env.family, self.env.investor, n_eval, self.env.n_gambles, seed=self.env.seed + 10007,
+                         device=self.device, **kw)
+            self._eval_env = env
+        obs = env.reset().float()
+        actions = self.agent.act(obs, mode=1)
+        dev = self.device
+        reward = torch.empty(n_eval, dtype=torch.float64, device=dev)
+        steps = torch.empty(n_eval, dtype=torch.int32, device=dev)
+        risk = torch.empty(n_eval, env.risk_dim, dtype=torch.float64, device=dev)
+        stats = torch.empty(17, dtype=torch.float64, device=dev)
+        lib = _abi.lib()
+        check(lib.rlmd_eval_rollout(env.h, ptr(actions), int(max_steps), int(self.cfg.cum_step),
+                                    int(self.cfg.warmup_steps), int(self.cfg.smoothing_window), None, ptr(reward),
+                                    ptr(steps), ptr(risk), stream_ptr()))
+        check(lib.rlmd_eval_stats(ptr(reward), ptr(steps), ptr(risk), n_eval, env.risk_dim, env.investor,
+                                  ptr(stats), stream_ptr()))
+        return {"reward": reward.cpu().numpy(), "steps": steps.cpu().numpy(), "risk": risk.cpu().numpy(),
+                "stats": stats.cpu().numpy()}
+
     def episode_stats(self):
         n, rsum, lsum, _ = self.ep_stats.cpu().numpy()
         return {"episodes": int(n), "mean_final_reward": rsum / max(n, 1), "mean_length": lsum / max(n, 1)}

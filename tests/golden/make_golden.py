@@ -464,6 +464,86 @@ def multistep_fixtures():
 
 
 # ----------------------------------------------------------------------------
+# F7: evaluation episodes (tools/eval_episodes.py:176-399)
+# ----------------------------------------------------------------------------
+EVAL_CASES = [  # (module, class, n_gambles, action, cum_steps, warmup, smoothing)
+    ("gbm_envs", "GBM_InvA", 1, [0.35], 5000, 1000, 2000),
+    ("gbm_envs", "GBM_InvA", 1, [0.35], 1500, 1000, 2000),  # inside the smoothing window
+    ("gbm_envs", "GBM_InvB", 1, [0.2, 0.6], 800, 1000, 2000),  # before warm-up ends: no window
+    ("coin_flip_envs", "Coin_InvA", 1, [0.125], 5000, 1000, 2000),
+    ("coin_flip_envs", "Coin_InvC", 2, [0.5, 0.3, 0.2, -0.1], 1700, 1000, 2000),
+    ("dice_roll_envs", "Dice_InvB", 1, [0.1, 0.19], 5000, 1000, 2000),
+    ("dice_roll_sh_envs", "Dice_SH_InvA", 1, [0.9, -0.6], 5000, 1000, 2000),
+    ("dice_roll_sh_envs", "Dice_SH_INSURED", 1, [0.83], 1200, 1000, 2000),
+    ("gbm_envs", "GBM_InvA", 3, [0.97, -0.95, 0.9], 5000, 1000, 2000),  # high leverage: early dones
+    ("coin_flip_envs", "Coin_InvB", 1, [0.4, 0.98], 5000, 1000, 2000),
+]
+
+
+class _FixedAgent:
+    """eval_next_action stub: the deterministic policy output (f32, as the
+    reference agent's torch->numpy action) for the episode's reset state."""
+
+    def __init__(self, action):
+        self.action = np.asarray(action, dtype=np.float32)
+
+    def eval_next_action(self, state):
+        return self.action.copy()
+
+
+def eval_fixtures(seed=21, n_eval=24, max_steps=100):
+    import importlib
+
+    import tools.eval_episodes as ev
+
+    out = {}
+    rng = np.random.default_rng(seed)
+    for ci, (modname, cls, n, action, cum, warm, sw) in enumerate(EVAL_CASES):
+        mod = importlib.import_module("envs." + modname)
+        rnd = _InjectedRandom()
+        saved = mod.np
+        mod.np = _NpProxy(rnd, flatten_array=True)
+        try:
+            sh = modname == "dice_roll_sh_envs"
+            D = 1 if sh else n
+            if modname == "gbm_envs":
+                pool = rng.standard_normal(n_eval * max_steps * D)
+            else:
+                pool = rng.random(n_eval * max_steps * D)
+            rnd.queue, rnd.log = list(pool), []
+            inputs = {"ENV_KEY": 0, "algo": "SAC", "s_dist": "N", "loss_fn": "MSE", "n_eval": n_eval,
+                      "smoothing_window": sw, "max_action": np.float64(0.99), "min_action": np.float64(-0.99),
+                      "random": warm, "max_eval_steps": max_steps,
+                      "env_gym": f"{modname}.{cls}()" if sh else f"{modname}.{cls}(n_gambles)", "env_id": cls}
+            eval_log = np.zeros((1, 1, n_eval, 20))
+            risk_w = 7 if sh else (4 + (1 if cls.endswith("InvB") else 2 if cls.endswith("InvC") else 0)
+                                   + (n if n > 1 else 0))
+            eval_risk = np.zeros((1, 1, n_eval, risk_w))
+            ev.eval_multiplicative(n, _FixedAgent(action), inputs, eval_log, eval_risk, 1, cum, 0, 0,
+                                   [0.0] * 11, 0.0, [0.0] * 4)
+            steps = eval_log[0, 0, :, 2].astype(np.int64)
+            used = np.array(rnd.log)
+            assert used.size == steps.sum() * D
+            draws = np.zeros((n_eval, max_steps, D))
+            pos = 0
+            for e in range(n_eval):
+                k = steps[e] * D
+                draws[e, : steps[e]] = used[pos: pos + k].reshape(steps[e], D)
+                pos += k
+            key = f"case{ci}"
+            out[key + "/spec"] = np.array([modname, cls])
+            out[key + "/params"] = np.array([n, cum, warm, sw, n_eval, max_steps], dtype=np.int64)
+            out[key + "/action"] = np.asarray(action, np.float32)
+            out[key + "/draws"] = draws
+            out[key + "/reward"] = eval_log[0, 0, :, 1]
+            out[key + "/steps"] = steps
+            out[key + "/risk"] = eval_risk[0, 0]
+        finally:
+            mod.np = saved
+    return out
+
+
+# ----------------------------------------------------------------------------
 # F5: learn() steps for SAC and TD3
 # ----------------------------------------------------------------------------
 def _inputs(algo, S, A, hidden, loss_fn="MSE", B=None, k=None):
@@ -611,6 +691,7 @@ def main():
         "critic_loss.npz": critic_loss_fixtures,
         "shadow.npz": shadow_fixtures,
         "multistep.npz": multistep_fixtures,
+        "eval.npz": eval_fixtures,
         "learn.npz": learn_fixtures,
     }
     only = sys.argv[1:]

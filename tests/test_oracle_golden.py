@@ -168,3 +168,28 @@ def test_multistep_history_matches_reference(golden, stream, n, dyn):
         np.testing.assert_array_equal(A0, g[key + "/action"].astype(np.float32).astype(np.float64), err_msg=key)
         checked += 1
     assert checked >= 8
+
+
+# ---------------------------------------------------------------- F7 evaluation
+def _eval_case(g, c):
+    modname, cls = (str(x) for x in g[f"case{c}/spec"])
+    n, cum, warm, sw, n_eval, max_steps = (int(x) for x in g[f"case{c}/params"])
+    fam, inv, _ = parse_env_key(f"{cls}_n{n}")
+    return fam, inv, n, cum, warm, sw, n_eval, max_steps
+
+
+@pytest.mark.parametrize("c", range(10))
+def test_eval_rollout_matches_reference(golden, c):
+    """oracle.eval.rollout vs the reference's eval_multiplicative on the same
+    injected draws: last reward, steps and last risk vector of every episode."""
+    from oracle import eval as oev
+
+    g = golden("eval.npz")
+    fam, inv, n, cum, warm, sw, n_eval, max_steps = _eval_case(g, c)
+    rew, steps, risk = oev.rollout(fam, inv, n, g[f"case{c}/action"], cum, warm, sw, n_eval, max_steps,
+                                   g[f"case{c}/draws"])
+    np.testing.assert_array_equal(steps, g[f"case{c}/steps"])
+    np.testing.assert_allclose(rew, g[f"case{c}/reward"], rtol=RTOL, atol=0)
+    np.testing.assert_allclose(risk, g[f"case{c}/risk"], rtol=RTOL, atol=0, equal_nan=True)
+    st = oev.summary(rew, steps, risk, inv)
+    assert np.isfinite(st[:15]).all()
