@@ -494,6 +494,7 @@ struct AdamArgs {
   float* target;  // Polyak target (nullable)
   int64_t n;
   float lr, tau;
+  int32_t cnt;             // learn_step_cntr of this update (written back to LearnState)
   int32_t interval;        // Adam step count t = learn_cntr / interval
   int32_t polyak_interval; // Polyak when learn_cntr % polyak_interval == 0 (0 = never)
   LearnState* st;
@@ -523,7 +524,8 @@ __device__ __forceinline__ void store_copy(void* base, int64_t i, float v, int b
 }
 
 __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
-  const int cnt = a.st->learn_cntr;
+  const int cnt = a.cnt;
+  if (blockIdx.x == 0 && threadIdx.x == 0) a.st->learn_cntr = cnt;
   const int t = cnt / a.interval;
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
   const double bc1 = 1.0 - pow(0.9, (double)t);
@@ -580,7 +582,6 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
   }
 }
 
-__global__ void bump_kernel(LearnState* st) { st->learn_cntr += 1; }
 
 }  // namespace
 }  // namespace rlmd
@@ -618,8 +619,6 @@ struct Scratch {
   // mini-batch
   float *s, *a, *r, *s2, *xsa;
   uint8_t* done;
-  int64_t* idx;
-  int32_t* eff;  // multi-step effective lengths
   // target path: target q per row (no head bias), logp of the next actions
   float *logp_next, *tpart[2], *y;
   // critic path
@@ -647,6 +646,12 @@ struct rlmd_agent_s {
   // fc2.weight compute copies (rows.hip RowNet), slot x {wc, wt}:
   // 0 actor, 1 target actor, 2/3 critics, 4/5 target critics
   unsigned char* wcopy = nullptr;
+  // K mini-batches sampled by one launch (agent_learn_k)
+  int kcap = 0;
+  float *kb_s = nullptr, *kb_a = nullptr, *kb_r = nullptr, *kb_s2 = nullptr, *kb_xsa = nullptr;
+  uint8_t* kb_done = nullptr;
+  int64_t* kb_idx = nullptr;
+  int32_t* kb_eff = nullptr;
   size_t wcopy_bytes = 0;  // per copy
   float *act_h1 = nullptr, *act_h2 = nullptr;
   unsigned short* act_w2bf = nullptr;  // fused acting: bf16 copy of the actor's fc2.weight
@@ -795,8 +800,16 @@ void adam_copies(rlmd_agent_s* ag, AdamArgs& ad, const NetOff& o, int slot0, int
 // Launches (SAC, actor step): fwd rows | critic loss | critic bwd rows | critic
 // dW | Adam critics | q rows on (s, a_new) | actor loss | actor bwd rows |
 // actor dW | Adam actor (+ temperature).
-int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const float* eps_b,
-               float* stats, hipStream_t st) {
+// One mini-batch (device): s, s' [B, S], r [B], done [B], critic input
+// xsa = [s | a] [B, S+A], eff [B] (nullable = 1).
+struct Batch {
+  const float *s, *r, *s2, *xsa;
+  const uint8_t* done;
+  const int32_t* eff;
+};
+
+int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const float* eps_b, float* stats,
+               hipStream_t st) {
   const rlmd_agent_cfg& c = ag->cfg;
   Scratch& S_ = ag->sc;
   const int B = c.batch, S = c.state_dim, A = c.action_dim, X = S + A, H1 = c.h1, H2 = c.h2;
@@ -810,7 +823,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
   const bool actor_step = cntr % c.actor_update_interval == 0;
   const int nq = sac ? 2 : 1;
   const RowDims d = row_dims(ag);
-  const SampleCfg smp{c.seed, &ag->st->learn_cntr, c.max_action, c.log_scale_min, c.log_scale_max,
+  const SampleCfg smp{c.seed, (uint32_t)cntr, c.max_action, c.log_scale_min, c.log_scale_max,
                       c.reparam_noise};
   float* Pc[2] = {P + ag->off_c[0], P + ag->off_c[1]};
   float* Tc[2] = {T + ag->off_c[0], T + ag->off_c[1]};
@@ -829,7 +842,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     f.tactor = row_net(ag, sac ? SLOT_ACTOR : SLOT_TACTOR);  // SAC samples next actions from the online actor
     f.tcrit[0] = row_net(ag, SLOT_TC0);
     f.tcrit[1] = row_net(ag, SLOT_TC0 + 1);
-    f.s2 = S_.s2;
+    f.s2 = mb.s2;
     f.eps_next = eps_a;
     f.t_tag = sac ? RLMD_TAG_EPS_NEXT : RLMD_TAG_TD3_TARGET;
     f.t_clamp = sac ? 0 : 1;
@@ -843,12 +856,12 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
       f.c2[g] = S_.c2[g];
       f.q[g] = S_.qpart[g];
     }
-    f.xsa = S_.xsa;
+    f.xsa = mb.xsa;
     f.with_actor = actor_step ? 1 : 0;
     f.a_mode = sac ? 0 : 1;  // TD3 actor.forward: tanh(mu) * max_action, no noise
     f.a_tag = RLMD_TAG_EPS_CUR;
     f.actor = row_net(ag, SLOT_ACTOR);
-    f.s = S_.s;
+    f.s = mb.s;
     f.eps_cur = eps_b;
     f.h1a = S_.h1;
     f.h2a = S_.h2;
@@ -867,9 +880,9 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
       la.tb[g] = Tc[g] + co.b3;
     }
     la.tiles = 1;
-    la.r = S_.r;
-    la.done = S_.done;
-    la.eff = eff;
+    la.r = mb.r;
+    la.done = mb.done;
+    la.eff = mb.eff;
     la.logp_next = S_.logp_next;
     la.gamma = c.gamma;
     la.reward_scale = c.reward_scale;
@@ -910,7 +923,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     for (int g = 0; g < 2; ++g) {
       add_bwd_w(gb, 1, H2, B, S_.dq[g], 1, S_.c2[g], H2, Gc[g] + co.w3, Gc[g] + co.b3);
       add_bwd_w(gb, H2, H1, B, S_.dc2[g], H2, S_.c1[g], H1, Gc[g] + co.w2, Gc[g] + co.b2);
-      add_bwd_w(gb, H1, X, B, S_.dc1[g], H1, S_.xsa, X, Gc[g] + co.w1, Gc[g] + co.b1);
+      add_bwd_w(gb, H1, X, B, S_.dc1[g], H1, mb.xsa, X, Gc[g] + co.w1, Gc[g] + co.b1);
     }
     RLMD_TRY(launch_bwd_w(ag, gb, st));
     AdamArgs ad{};
@@ -923,6 +936,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     ad.n = 2 * co.size;
     ad.lr = c.lr_critic;
     ad.tau = c.tau;
+    ad.cnt = (int32_t)cntr;
     ad.interval = 1;
     ad.polyak_interval = c.target_critic_update;
     ad.st = ag->st;
@@ -990,7 +1004,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     add_bwd_w(gb, A, H2, B, S_.gh, 2 * A, S_.h2, H2, Ga + ao.w3, Ga + ao.b3);
     if (sac) add_bwd_w(gb, A, H2, B, S_.gh + A, 2 * A, S_.h2, H2, Ga + ao.w4, Ga + ao.b4);
     add_bwd_w(gb, H2, H1, B, S_.dh2, H2, S_.h1, H1, Ga + ao.w2, Ga + ao.b2);
-    add_bwd_w(gb, H1, S, B, S_.dh1, H1, S_.s, S, Ga + ao.w1, Ga + ao.b1);
+    add_bwd_w(gb, H1, S, B, S_.dh1, H1, mb.s, S, Ga + ao.w1, Ga + ao.b1);
     RLMD_TRY(launch_bwd_w(ag, gb, st));
     AdamArgs ad{};
     ad.p = P + ag->off_actor;
@@ -1002,6 +1016,7 @@ int learn_body(rlmd_agent_s* ag, const int32_t* eff, const float* eps_a, const f
     ad.n = ao.size;
     ad.lr = c.lr_actor;
     ad.tau = c.tau;
+    ad.cnt = (int32_t)cntr;
     ad.interval = c.actor_update_interval;
     ad.polyak_interval = sac ? 0 : c.target_actor_update;
     ad.st = ag->st;
@@ -1025,13 +1040,35 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
   const int64_t mem = replay_mem_idx(rb);
   const int64_t M = mem < v.capacity ? mem : v.capacity;
   RLMD_CHECK(v.S == c.state_dim && v.A == c.action_dim, "replay / agent dims differ");
-  if (k > 0) RLMD_TRY(refresh_copies(ag, st));
+  if (k <= 0) return 0;
+  const int B = c.batch, S = c.state_dim, A = c.action_dim;
+  if (k > ag->kcap) {  // K mini-batches of scratch, grown on demand
+    for (void* p : {(void*)ag->kb_s, (void*)ag->kb_a, (void*)ag->kb_r, (void*)ag->kb_s2, (void*)ag->kb_xsa,
+                    (void*)ag->kb_done, (void*)ag->kb_idx, (void*)ag->kb_eff})
+      if (p) RLMD_HIP(hipFree(p));
+    const size_t KB = (size_t)k * B;
+    RLMD_HIP(hipMalloc(&ag->kb_s, sizeof(float) * KB * S));
+    RLMD_HIP(hipMalloc(&ag->kb_a, sizeof(float) * KB * A));
+    RLMD_HIP(hipMalloc(&ag->kb_r, sizeof(float) * KB));
+    RLMD_HIP(hipMalloc(&ag->kb_s2, sizeof(float) * KB * S));
+    RLMD_HIP(hipMalloc(&ag->kb_xsa, sizeof(float) * KB * (S + A)));
+    RLMD_HIP(hipMalloc(&ag->kb_done, KB));
+    RLMD_HIP(hipMalloc(&ag->kb_idx, sizeof(int64_t) * KB));
+    RLMD_HIP(hipMalloc(&ag->kb_eff, sizeof(int32_t) * KB));
+    ag->kcap = k;
+  }
+  RLMD_TRY(refresh_copies(ag, st));
+  // all K mini-batches at once: the ring does not change during the K updates;
+  // batch i draws with counter learn_step_cntr + i (as K single draws would)
+  const bool ms = v.n_steps > 1;
+  RLMD_TRY(replay_sample_launch(v, M, B, k, c.seed ^ 0x5eed5eed5eedull, (uint64_t)ag->host_cntr, ag->kb_idx,
+                                ag->kb_s, ag->kb_a, ag->kb_r, ag->kb_s2, ag->kb_done, ag->kb_xsa,
+                                ms ? ag->kb_eff : nullptr, st));
   for (int i = 0; i < k; ++i) {
-    Scratch& S_ = ag->sc;
-    int32_t* eff = v.n_steps > 1 ? S_.eff : nullptr;
-    RLMD_TRY(replay_sample_launch(v, M, c.batch, c.seed ^ 0x5eed5eed5eedull, 0, &ag->st->learn_cntr,
-                                  S_.idx, S_.s, S_.a, S_.r, S_.s2, S_.done, S_.xsa, eff, st));
-    RLMD_TRY(learn_body(ag, eff, nullptr, nullptr, stats_slot(ag, stats, i), st));
+    const size_t o = (size_t)i * B;
+    const Batch mb{ag->kb_s + o * S, ag->kb_r + o, ag->kb_s2 + o * S, ag->kb_xsa + o * (S + A), ag->kb_done + o,
+                   ms ? ag->kb_eff + o : nullptr};
+    RLMD_TRY(learn_body(ag, mb, nullptr, nullptr, stats_slot(ag, stats, i), st));
   }
   return 0;
 }
@@ -1130,8 +1167,6 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.s2, B * S);
   RLMD_ALLOC(s.xsa, B * X);
   RLMD_ALLOC(s.done, B);
-  RLMD_ALLOC(s.idx, B);
-  RLMD_ALLOC(s.eff, B);
   RLMD_ALLOC(s.logp_next, B);
   RLMD_ALLOC(s.y, B);
   RLMD_ALLOC(s.h1, B * H1);
@@ -1194,6 +1229,9 @@ int rlmd_agent_destroy(rlmd_agent_t ag) {
   if (ag->act_h1) (void)hipFree(ag->act_h1);
   if (ag->act_h2) (void)hipFree(ag->act_h2);
   if (ag->act_w2bf) (void)hipFree(ag->act_w2bf);
+  for (void* p : {(void*)ag->kb_s, (void*)ag->kb_a, (void*)ag->kb_r, (void*)ag->kb_s2, (void*)ag->kb_xsa,
+                  (void*)ag->kb_done, (void*)ag->kb_idx, (void*)ag->kb_eff})
+    if (p) (void)hipFree(p);
   delete ag;
   return 0;
 }
@@ -1226,10 +1264,9 @@ int rlmd_agent_learn_batch(rlmd_agent_t ag, const float* s, const float* a, cons
                             B, hipMemcpyDeviceToDevice, st));
   RLMD_HIP(hipMemcpy2DAsync(S_.xsa + S, sizeof(float) * (S + A), a, sizeof(float) * A,
                             sizeof(float) * A, B, hipMemcpyDeviceToDevice, st));
-  hipLaunchKernelGGL(rlmd::bump_kernel, dim3(1), dim3(1), 0, st, ag->st);
-  RLMD_LAUNCH_CHECK();
   RLMD_TRY(rlmd::refresh_copies(ag, st));
-  return rlmd::learn_body(ag, eff, eps_a, eps_b, rlmd::stats_slot(ag, stats, 0), st);
+  const rlmd::Batch mb{S_.s, S_.r, S_.s2, S_.xsa, S_.done, eff};
+  return rlmd::learn_body(ag, mb, eps_a, eps_b, rlmd::stats_slot(ag, stats, 0), st);
 }
 
 #ifdef RLMD_TIMING

@@ -78,7 +78,7 @@ struct RowDims {
 
 struct SampleCfg {
   uint64_t seed;
-  const int32_t* ctr;  // Philox c1 = learn_cntr
+  uint32_t ctr;  // Philox c1 = learn_step_cntr of this update
   float max_action, ls_min, ls_max, reparam_noise;
 };
 

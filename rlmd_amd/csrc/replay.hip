@@ -102,15 +102,29 @@ constexpr int kSortPopulation = 8192;  // M at or below: sort-based subset
 
 __global__ void __launch_bounds__(kSampleThreads)
     replay_sample_kernel(rlmd::ReplayView rb, int64_t M, int B, uint64_t seed, uint32_t ctr_lo,
-                         uint32_t ctr_hi, int32_t* dev_ctr, int64_t* idx_out, float* s, float* a,
+                         uint32_t ctr_hi, int64_t* idx_out, float* s, float* a,
                          float* r, float* s2, uint8_t* done, float* xsa, int32_t* eff) {
   __shared__ uint64_t keys[kSortPopulation];
   __shared__ int64_t cand[kSampleThreads];
   __shared__ int any_dup;
   const int i = threadIdx.x;
-  // learner path: the draw counter is the device learn counter, bumped here
-  // (every thread reads it before the first barrier; thread 0 writes after the last)
-  if (dev_ctr) ctr_lo = (uint32_t)*dev_ctr;
+  // workgroup k of a K-batch launch draws mini-batch k with counter ctr + k and
+  // writes it at offset k (one independent sample per workgroup)
+  {
+    const int k = blockIdx.x;
+    const uint64_t ctr = ((uint64_t)ctr_hi << 32 | ctr_lo) + (uint64_t)k;
+    ctr_lo = (uint32_t)ctr;
+    ctr_hi = (uint32_t)(ctr >> 32);
+    const int S = rb.S, A = rb.A;
+    if (idx_out) idx_out += (int64_t)k * B;
+    if (s) s += (int64_t)k * B * S;
+    if (a) a += (int64_t)k * B * A;
+    if (r) r += (int64_t)k * B;
+    if (s2) s2 += (int64_t)k * B * S;
+    if (done) done += (int64_t)k * B;
+    if (xsa) xsa += (int64_t)k * B * (S + A);
+    if (eff) eff += (int64_t)k * B;
+  }
   const uint32_t c2 = RLMD_TAG_REPLAY_IDX | (ctr_hi << 8);
   if (M <= kSortPopulation) {
     int npow = 1;
@@ -178,7 +192,6 @@ __global__ void __launch_bounds__(kSampleThreads)
     }
   }
   __syncthreads();
-  if (dev_ctr && i == 0) *dev_ctr = (int32_t)ctr_lo + 1;
   if (i >= B) return;
   const int64_t row = cand[i];
   if (idx_out) idx_out[i] = row;
@@ -230,14 +243,15 @@ ReplayView replay_view(rlmd_replay_t rb) { return rb->v; }
 int64_t replay_mem_idx(rlmd_replay_t rb) { return rb->mem_idx; }
 void replay_advance(rlmd_replay_t rb, int64_t n) { rb->mem_idx += n; }
 
-int replay_sample_launch(const ReplayView& rb, int64_t M, int B, uint64_t seed, uint64_t ctr,
-                         int32_t* dev_ctr, int64_t* idx, float* s, float* a, float* r, float* s2,
-                         uint8_t* done, float* xsa, int32_t* eff, hipStream_t stream) {
+int replay_sample_launch(const ReplayView& rb, int64_t M, int B, int K, uint64_t seed, uint64_t ctr,
+                         int64_t* idx, float* s, float* a, float* r, float* s2, uint8_t* done, float* xsa,
+                         int32_t* eff, hipStream_t stream) {
   RLMD_CHECK(B >= 1 && B <= RLMD_MAX_BATCH, "batch must be in [1, 1024]");
+  RLMD_CHECK(K >= 1, "need at least one mini-batch");
   RLMD_CHECK(M >= B, "replay holds fewer transitions than the mini-batch");
   RLMD_CHECK(M <= (int64_t)1 << 52, "replay too large");
-  hipLaunchKernelGGL(replay_sample_kernel, dim3(1), dim3(kSampleThreads), 0, stream, rb, M, B, seed,
-                     (uint32_t)ctr, (uint32_t)(ctr >> 32), dev_ctr, idx, s, a, r, s2, done, xsa, eff);
+  hipLaunchKernelGGL(replay_sample_kernel, dim3(K), dim3(kSampleThreads), 0, stream, rb, M, B, seed,
+                     (uint32_t)ctr, (uint32_t)(ctr >> 32), idx, s, a, r, s2, done, xsa, eff);
   RLMD_LAUNCH_CHECK();
   return 0;
 }
@@ -331,7 +345,7 @@ int rlmd_replay_sample(rlmd_replay_t rb, int32_t B, uint64_t seed, uint64_t ctr,
                        float* s, float* a, float* r, float* s2, uint8_t* done, int32_t* eff, void* stream) {
   RLMD_CHECK(rb, "null replay");
   const int64_t M = rb->mem_idx < rb->v.capacity ? rb->mem_idx : rb->v.capacity;
-  return rlmd::replay_sample_launch(rb->v, M, B, seed, ctr, nullptr, idx, s, a, r, s2, done, nullptr, eff,
+  return rlmd::replay_sample_launch(rb->v, M, B, 1, seed, ctr, idx, s, a, r, s2, done, nullptr, eff,
                                     (hipStream_t)stream);
 }
 

@@ -61,14 +61,14 @@ int env_lanes(rlmd_env_t env);
 int env_state_dim(rlmd_env_t env);
 int env_action_dim(rlmd_env_t env);
 
-// mini-batch sampler: B distinct indices in [0, M) + gather; optionally writes
-// the critic input [s | a] as xsa [B, S+A].
-// dev_ctr (nullable): device counter used as the draw counter instead of ctr and
-// incremented by the kernel (the learner's learn_step_cntr).
-// Multi-step mode: s / a are the history's initial next-state / action, r the
-// n-step return, eff [B] the effective length (nullable); see oracle/replay.py.
-int replay_sample_launch(const ReplayView& rb, int64_t M, int B, uint64_t seed, uint64_t ctr,
-                         int32_t* dev_ctr, int64_t* idx, float* s, float* a, float* r, float* s2,
-                         uint8_t* done, float* xsa, int32_t* eff, hipStream_t stream);
+// mini-batch sampler: K independent mini-batches in one launch (one workgroup
+// each), batch k = B distinct indices in [0, M) drawn with counter ctr + k, then
+// gathered to offset k of every output; optionally writes the critic input
+// [s | a] as xsa [K, B, S+A].  Multi-step mode: s / a are the history's initial
+// next-state / action, r the n-step return, eff [K, B] the effective length
+// (nullable); see oracle/replay.py.
+int replay_sample_launch(const ReplayView& rb, int64_t M, int B, int K, uint64_t seed, uint64_t ctr,
+                         int64_t* idx, float* s, float* a, float* r, float* s2, uint8_t* done, float* xsa,
+                         int32_t* eff, hipStream_t stream);
 
 }  // namespace rlmd

@@ -378,7 +378,7 @@ __device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, 
   if (r >= R) return;
   const int S = d.S, A = d.A, b = row0 + r;
   const bool valid = b < B, sac = d.algo == RLMD_SAC;
-  const uint32_t c1 = (uint32_t)*smp.ctr;
+  const uint32_t c1 = smp.ctr;
   float logp = 0.f;
   for (int j = 0; j < A; ++j) {
     float mu = hout[r * kHeadsMax + j] + p[ao.b3 + j];
