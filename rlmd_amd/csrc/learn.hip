@@ -19,109 +19,13 @@
 #include <vector>
 
 #include "learn_kernels.h"
+#include "rlmd_block.h"
 #include "rlmd_gemm.h"
 
 namespace rlmd {
 namespace {
 
 constexpr float kLog2Pi_half = 0.91893853320467274178f;  // log(sqrt(2*pi))
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// orderable key of a float (ascending unsigned order == ascending float order)
-__device__ __forceinline__ uint32_t f2key(float f) {
-  const uint32_t u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-
-// Block all-reduce of NS sums and NM maxima at once (3 barriers).  Each wave
-// reduces with shuffles and parks its partial in red[v][16]; lanes of the first
-// waves fold the per-wave partials of one value each (a fixed tree, so the
-// result is deterministic) and every thread reads the NS + NM results back.
-// red: 16 * (NS + NM) + 16 floats.
-template <int NS, int NM>
-__device__ __forceinline__ void block_allreduce(float* sm, float* mx, float* red) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  constexpr int NV = NS + NM;
-  float* res = red + 16 * NV;
-#pragma unroll
-  for (int v = 0; v < NS; ++v) sm[v] = wave_sum(sm[v]);
-#pragma unroll
-  for (int v = 0; v < NM; ++v)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx[v] = fmaxf(mx[v], __shfl_xor(mx[v], o, 64));
-  if (lane == 0) {
-#pragma unroll
-    for (int v = 0; v < NS; ++v) red[v * 16 + w] = sm[v];
-#pragma unroll
-    for (int v = 0; v < NM; ++v) red[(NS + v) * 16 + w] = mx[v];
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < 16 * NV) {
-    const int v = threadIdx.x >> 4, q = threadIdx.x & 15;
-    const bool is_sum = v < NS;
-    float t = q < nw ? red[threadIdx.x] : (is_sum ? 0.f : -INFINITY);
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const float u = __shfl_xor(t, o, 64);
-      t = is_sum ? t + u : fmaxf(t, u);
-    }
-    if (q == 0) res[v] = t;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int v = 0; v < NS; ++v) sm[v] = res[v];
-#pragma unroll
-  for (int v = 0; v < NM; ++v) mx[v] = res[NS + v];
-  __syncthreads();  // red / res reusable
-}
-
-// Ascending bitonic sort of one 64-bit key per lane across the wave (registers).
-__device__ __forceinline__ uint64_t wave_sort64(uint64_t key) {
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1)
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const uint64_t other = rlmd_shfl_xor_u64(key, j);
-      const bool up = (l & k) == 0 || k == 64;
-      const bool keep_min = ((l & j) == 0) == up;
-      key = keep_min ? (key < other ? key : other) : (key < other ? other : key);
-    }
-  return key;
-}
-
-// Ranks of distinct 64-bit keys across the block (ascending; key ~0 = absent):
-// each wave sorts its 64 keys in registers, parks the sorted run in LDS, and the
-// key at lane l of run w gets rank l + sum over the other runs of a binary
-// search (6 probes over the first 63 entries + the last entry).  The rank is scattered to out[key & 0xffffffff] (the caller's
-// index in the low word) and read back by the key's owner after the barrier.
-// runs: LDS [blockDim.x] uint64; out: LDS int [blockDim.x].
-__device__ __forceinline__ void block_rank(uint64_t key, uint64_t* runs, int* out) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const uint64_t sk = wave_sort64(key);
-  runs[threadIdx.x] = sk;
-  __syncthreads();
-  if (sk != ~0ull) {
-    int rank = l;
-    for (int v = 0; v < nw; ++v) {
-      if (v == w) continue;
-      const uint64_t* run = runs + 64 * v;
-      // 6 probes count the smaller keys among run[0..62]; run[63] separately
-      int pos = 0;
-#pragma unroll
-      for (int st = 32; st > 0; st >>= 1)
-        if (run[pos + st - 1] < sk) pos += st;
-      rank += pos + (run[63] < sk ? 1 : 0);
-    }
-    out[(int)(sk & 0xffffffffu)] = rank;
-  }
-  __syncthreads();
-}
 
 // ---------------------------------------------------------------------------
 // actor heads + policy sampling (networks_sac.py:101-178, :268-285;
@@ -210,11 +114,10 @@ __global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
 // One workgroup of 1024 threads; thread b owns mini-batch row b.
 // ---------------------------------------------------------------------------
 struct LossArgs {
-  const float* qpart[2];  // online critics' fused-head partials [tiles][B]
+  const float* qpart[2];  // online critics' q per row without the head bias [B]
   const float* qb[2];     // q_value.bias (online)
-  const float* tpart[2];  // target critics' partials [tiles][B]
+  const float* tpart[2];  // target critics' q per row without the head bias [B]
   const float* tb[2];     // q_value.bias (target)
-  int32_t tiles;
   const float* r;
   const uint8_t* done;
   const int32_t* eff;
@@ -284,29 +187,39 @@ __global__ void __launch_bounds__(NTH) critic_loss_kernel(LossArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t runs[NTH];
   __shared__ int rank_of[3][NTH];
   __shared__ float red[16 * 9];
-  const int b = threadIdx.x, B = a.B, T = a.tiles;
+  const int b = threadIdx.x, B = a.B;
   const bool in = b < B;
   LearnState* st = a.st;
   RLMD_TS(0);
-  // -- target and current q from the fused-head partials
-  float y = 0.f, q[2] = {0.f, 0.f};
+  // -- target and current q (row kernels' head outputs + biases).  Every row's
+  //    loads are issued unconditionally (range-checked buffer loads), so the
+  //    whole prologue is one memory round trip
+  const int64_t nB = (int64_t)B * 4;
+  float qt[2], q[2] = {0.f, 0.f};
+  for (int g = 0; g < 2; ++g) {
+    qt[g] = rlmd_ldf(rlmd_rsrc(a.tpart[g], nB), b, in);
+    q[g] = rlmd_ldf(rlmd_rsrc(a.qpart[g], nB), b, in);
+  }
+  const float rw = rlmd_ldf(rlmd_rsrc(a.r, nB), b, in);
+  const float lpn = a.logp_next ? rlmd_ldf(rlmd_rsrc(a.logp_next, nB), b, in) : 0.f;
+  const uint8_t dn = __builtin_amdgcn_raw_buffer_load_b8(rlmd_rsrc(a.done, B), in ? b : 0x7fffffff, 0, 0);
+  const int eff = a.eff ? (int)__builtin_bit_cast(
+                              int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, nB), in ? b * 4 : 0x7fffffff, 0, 0))
+                        : 1;
+  float y = 0.f;
+  for (int g = 0; g < 2; ++g) {
+    qt[g] += a.tb[g][0];
+    q[g] += a.qb[g][0];
+  }
   if (in) {
-    float qt[2];
-    for (int g = 0; g < 2; ++g) {
-      float t = 0.f, c = 0.f;
-      for (int u = 0; u < T; ++u) {
-        t += a.tpart[g][(int64_t)u * B + b];
-        c += a.qpart[g][(int64_t)u * B + b];
-      }
-      qt[g] = t + a.tb[g][0];
-      q[g] = c + a.qb[g][0];
-    }
-    if (a.done[b]) qt[0] = qt[1] = 0.f;
+    if (dn) qt[0] = qt[1] = 0.f;
     const float m = fminf(qt[0], qt[1]);
-    const float ge = powf(a.gamma, (float)(a.eff ? a.eff[b] : 1));
-    if (a.algo == RLMD_SAC) y = (a.reward_scale * a.r[b] + ge * m) - expf(st->log_alpha) * a.logp_next[b];
-    else y = a.r[b] + ge * m;
+    const float ge = powf(a.gamma, (float)eff);
+    if (a.algo == RLMD_SAC) y = (a.reward_scale * rw + ge * m) - expf(st->log_alpha) * lpn;
+    else y = rw + ge * m;
     if (a.y_out) a.y_out[b] = y;
+  } else {
+    q[0] = q[1] = 0.f;
   }
   RLMD_TS(1);
   const float scale[2] = {st->cauchy[0], st->cauchy[1]};
@@ -416,9 +329,8 @@ __global__ void __launch_bounds__(NTH) critic_loss_kernel(LossArgs a) {
 // dL/dlogp per row.
 // ---------------------------------------------------------------------------
 struct ActorLossArgs {
-  const float* qpart[2];  // fused-head partials [tiles][B]; qpart[1] null for TD3
+  const float* qpart[2];  // q per row without the head bias [B]; qpart[1] null for TD3
   const float* qb[2];
-  int32_t tiles;
   const float* logp;  // SAC
   float* dq[2];
   float* dlogp;
@@ -437,18 +349,11 @@ __global__ void __launch_bounds__(NTH) actor_loss_kernel(ActorLossArgs a) {
   const bool in = b < B;
   LearnState* st = a.st;
   const float alpha = a.algo == RLMD_SAC ? expf(st->log_alpha) : 0.f;
-  float q1 = 0.f, q2 = 0.f;
-  if (in) {
-    for (int u = 0; u < a.tiles; ++u) q1 += a.qpart[0][(int64_t)u * B + b];
-    q1 += a.qb[0][0];
-    if (a.qpart[1]) {
-      for (int u = 0; u < a.tiles; ++u) q2 += a.qpart[1][(int64_t)u * B + b];
-      q2 += a.qb[1][0];
-    } else {
-      q2 = q1;
-    }
-  }
-  const float lp = (in && a.logp) ? a.logp[b] : 0.f;
+  const int64_t nB = (int64_t)B * 4;
+  float q1 = rlmd_ldf(rlmd_rsrc(a.qpart[0], nB), b, in) + a.qb[0][0];
+  float q2 = a.qpart[1] ? rlmd_ldf(rlmd_rsrc(a.qpart[1], nB), b, in) + a.qb[1][0] : q1;
+  if (!in) q1 = q2 = 0.f;
+  const float lp = a.logp ? rlmd_ldf(rlmd_rsrc(a.logp, nB), b, in) : 0.f;
   const float v = a.algo == RLMD_SAC ? fminf(q1, q2) - alpha * lp : q1;
   const int k = a.topk ? (B < a.k ? B : a.k) : B;
   bool sel = in;
@@ -496,6 +401,8 @@ struct AdamArgs {
   float lr, tau;
   int32_t cnt;             // learn_step_cntr of this update (written back to LearnState)
   int32_t interval;        // Adam step count t = learn_cntr / interval
+  float step_size, bc2_sqrt;            // lr / (1 - b1^t), sqrt(1 - b2^t): host-side, as torch's Python floats
+  float temp_step_size, temp_bc2_sqrt;  // the same for the temperature step
   int32_t polyak_interval; // Polyak when learn_cntr % polyak_interval == 0 (0 = never)
   LearnState* st;
   int32_t temp;            // thread 0 also steps log_alpha (SAC)
@@ -526,12 +433,8 @@ __device__ __forceinline__ void store_copy(void* base, int64_t i, float v, int b
 __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
   const int cnt = a.cnt;
   if (blockIdx.x == 0 && threadIdx.x == 0) a.st->learn_cntr = cnt;
-  const int t = cnt / a.interval;
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
-  const double bc1 = 1.0 - pow(0.9, (double)t);
-  const double bc2 = 1.0 - pow(0.999, (double)t);
-  const float step_size = (float)(a.lr / bc1);
-  const float bc2_sqrt = (float)sqrt(bc2);
+  const float step_size = a.step_size, bc2_sqrt = a.bc2_sqrt;
   const bool polyak = a.target && a.polyak_interval > 0 && (cnt % a.polyak_interval) == 0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -552,10 +455,11 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
       a.target[i] = tv;
     }
     if (a.ncopy) {
-      const int net = (int)(i / a.net_size);
-      const int64_t j = i - net * a.net_size - a.w2_off;
-      if (net < a.ncopy && j >= 0 && j < (int64_t)a.H1 * a.H2) {
-        const int n = (int)(j / a.H1), k = (int)(j - (int64_t)n * a.H1);
+      const int i32 = (int)i, ns = (int)a.net_size;
+      const int net = i32 / ns;
+      const int j = i32 - net * ns - (int)a.w2_off;
+      if (net < a.ncopy && j >= 0 && j < a.H1 * a.H2) {
+        const int n = j / a.H1, k = j - n * a.H1;
         store_copy(a.wc[net], (int64_t)n * a.H1p + k, p, a.bf16);
         store_copy(a.wt[net], (int64_t)k * a.H2p + n, p, a.bf16);
         if (polyak && a.twc[net]) {
@@ -568,15 +472,13 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
   if (a.temp && blockIdx.x == 0 && threadIdx.x == 0) {
     LearnState* st = a.st;
     if (cnt % a.temp_interval == 0) {
-      const int tt = cnt / a.temp_interval;
-      const double c1 = 1.0 - pow(0.9, (double)tt), c2 = 1.0 - pow(0.999, (double)tt);
       const float g = st->pad_temp_grad;
       float m = st->temp_m + (1.f - b1) * (g - st->temp_m);
       float v = st->temp_v * b2 + (1.f - b2) * g * g;
       st->temp_m = m;
       st->temp_v = v;
-      const float denom = sqrtf(v) / (float)sqrt(c2) + eps;
-      st->log_alpha = st->log_alpha - (float)(a.lr_temp / c1) * (m / denom);
+      const float denom = sqrtf(v) / a.temp_bc2_sqrt + eps;
+      st->log_alpha = st->log_alpha - a.temp_step_size * (m / denom);
     }
     if (a.stats) a.stats[11] = st->log_alpha;
   }
@@ -730,7 +632,19 @@ int launch_head(const HeadArgs& h, hipStream_t s) {
   return 0;
 }
 
-int adam_launch(const AdamArgs& a, hipStream_t s) {
+// torch.optim.Adam's bias corrections for step t, evaluated in double on the
+// host as torch evaluates them in Python floats, handed over as f32 scalars.
+void adam_scalars(double lr, int t, float& step_size, float& bc2_sqrt) {
+  const double bc1 = 1.0 - pow(0.9, (double)t), bc2 = 1.0 - pow(0.999, (double)t);
+  step_size = (float)(lr / bc1);
+  bc2_sqrt = (float)sqrt(bc2);
+}
+
+int adam_launch(const AdamArgs& a_in, hipStream_t s) {
+  AdamArgs a = a_in;
+  adam_scalars(a.lr, a.cnt / a.interval, a.step_size, a.bc2_sqrt);
+  if (a.temp && a.cnt % a.temp_interval == 0)
+    adam_scalars(a.lr_temp, a.cnt / a.temp_interval, a.temp_step_size, a.temp_bc2_sqrt);
   const int64_t blocks = std::min<int64_t>((a.n + 255) / 256, 1024);
   hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, a);
   RLMD_LAUNCH_CHECK();
@@ -879,7 +793,6 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       la.tpart[g] = S_.tpart[g];
       la.tb[g] = Tc[g] + co.b3;
     }
-    la.tiles = 1;
     la.r = mb.r;
     la.done = mb.done;
     la.eff = mb.eff;
@@ -957,28 +870,29 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       qe.qn[g] = S_.qnpart[g];
     }
     RLMD_TRY(qeval_rows_launch(qe, nq, st));
-    ActorLossArgs al{};
-    al.qpart[0] = S_.qnpart[0];
-    al.qpart[1] = sac ? S_.qnpart[1] : nullptr;
-    al.qb[0] = Pc[0] + co.b3;
-    al.qb[1] = Pc[1] + co.b3;
-    al.tiles = 1;
-    al.logp = sac ? S_.logp : nullptr;
-    al.dq[0] = S_.dqn[0];
-    al.dq[1] = S_.dqn[1];
-    al.dlogp = S_.dlogp;
-    al.st = ag->st;
-    al.stats = stats;
-    al.B = B;
-    al.k = c.topk;
-    al.algo = c.algo;
-    al.topk = c.actor_topk;
-    al.target_entropy = -(float)A;
-    if (B <= 512)
-      hipLaunchKernelGGL(actor_loss_kernel<512>, dim3(1), dim3(512), 0, st, al);
-    else
+    // B <= 512: the actor loss is fused into abwd_rows (row ranks + a loss
+    // workgroup); larger mini-batches use the one-workgroup loss kernel
+    const bool fused_loss = B <= 512;
+    if (!fused_loss) {
+      ActorLossArgs al{};
+      al.qpart[0] = S_.qnpart[0];
+      al.qpart[1] = sac ? S_.qnpart[1] : nullptr;
+      al.qb[0] = Pc[0] + co.b3;
+      al.qb[1] = Pc[1] + co.b3;
+      al.logp = sac ? S_.logp : nullptr;
+      al.dq[0] = S_.dqn[0];
+      al.dq[1] = S_.dqn[1];
+      al.dlogp = S_.dlogp;
+      al.st = ag->st;
+      al.stats = stats;
+      al.B = B;
+      al.k = c.topk;
+      al.algo = c.algo;
+      al.topk = c.actor_topk;
+      al.target_entropy = -(float)A;
       hipLaunchKernelGGL(actor_loss_kernel<1024>, dim3(1), dim3(1024), 0, st, al);
-    RLMD_LAUNCH_CHECK();
+      RLMD_LAUNCH_CHECK();
+    }
     ABwdArgs ab{};
     ab.d = d;
     ab.ao = ao;
@@ -987,15 +901,22 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     ab.nq = nq;
     for (int g = 0; g < 2; ++g) {
       ab.crit[g] = crit[g];
-      ab.dqn[g] = S_.dqn[g];
+      ab.qn[g] = S_.qnpart[g];
       ab.e1[g] = S_.e1[g];
       ab.e2[g] = S_.e2[g];
+      ab.dqn_ext[g] = fused_loss ? nullptr : S_.dqn[g];
     }
+    ab.dlogp_ext = fused_loss ? nullptr : S_.dlogp;
     ab.actor = row_net(ag, SLOT_ACTOR);
-    ab.dlogp = S_.dlogp;
+    ab.logp = S_.logp;
     ab.save = S_.save;
     ab.h1a = S_.h1;
     ab.h2a = S_.h2;
+    ab.st = ag->st;
+    ab.stats = stats;
+    ab.k = c.topk;
+    ab.topk = c.actor_topk;
+    ab.target_entropy = -(float)A;
     ab.gh = S_.gh;
     ab.dh2 = S_.dh2;
     ab.dh1 = S_.dh1;

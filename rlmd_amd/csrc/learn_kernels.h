@@ -135,8 +135,12 @@ struct CBwdArgs {
   float* dc1[2];
 };
 
-// Actor data-gradients: dL/da through nq critics, through the sampling, the heads
-// and fc2 of the policy.  Outputs gh [B, 2A], dh2 [B, H2], dh1 [B, H1].
+// Actor loss + data-gradients.  Row workgroups rank their own rows' objective
+// v = min(q1, q2) - alpha logp (SAC, descending) / q1 (TD3, ascending) against
+// all B (algo_sac.py:546-562 / algo_td3.py:507-523), form dL/dq and dL/dlogp,
+// and back-propagate through nq critics, the sampling, the heads and fc2 of the
+// policy.  One extra workgroup computes the loss value and the temperature
+// gradient (algo_sac.py:580-587).  Outputs gh [B, 2A], dh2 [B, H2], dh1 [B, H1].
 struct ABwdArgs {
   RowDims d;
   NetOff ao, co;
@@ -144,13 +148,20 @@ struct ABwdArgs {
   int32_t nq;
   RowNet crit[2];
   RowNet actor;
-  const float* dqn[2];
+  const float* qn[2];  // updated critics on (s, a_new), no head bias [B]
+  const float* logp;   // SAC
   const float* e1[2];
   const float* e2[2];
-  const float* dlogp;
   const float* save;
   const float* h1a;
   const float* h2a;
+  LearnState* st;
+  float* stats;
+  int32_t k, topk;
+  float target_entropy;
+  // B > 512: the loss comes from actor_loss_kernel (learn.hip) instead
+  const float* dqn_ext[2];
+  const float* dlogp_ext;
   float* gh;
   float* dh2;
   float* dh1;

@@ -1,0 +1,111 @@
+// rlmd_block.h — workgroup-level building blocks shared by the loss kernels
+// (learn.hip) and the row kernels (rows.hip): wave sums, orderable float keys,
+// deterministic block all-reduces and block-wide ranks of distinct 64-bit keys.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rlmd_common.h"
+
+namespace rlmd {
+namespace {
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// orderable key of a float (ascending unsigned order == ascending float order)
+__device__ __forceinline__ uint32_t f2key(float f) {
+  const uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Block all-reduce of NS sums and NM maxima at once (3 barriers).  Each wave
+// reduces with shuffles and parks its partial in red[v][16]; lanes of the first
+// waves fold the per-wave partials of one value each (a fixed tree, so the
+// result is deterministic) and every thread reads the NS + NM results back.
+// red: 16 * (NS + NM) + 16 floats.
+template <int NS, int NM>
+__device__ __forceinline__ void block_allreduce(float* sm, float* mx, float* red) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  constexpr int NV = NS + NM;
+  float* res = red + 16 * NV;
+#pragma unroll
+  for (int v = 0; v < NS; ++v) sm[v] = wave_sum(sm[v]);
+#pragma unroll
+  for (int v = 0; v < NM; ++v)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx[v] = fmaxf(mx[v], __shfl_xor(mx[v], o, 64));
+  if (lane == 0) {
+#pragma unroll
+    for (int v = 0; v < NS; ++v) red[v * 16 + w] = sm[v];
+#pragma unroll
+    for (int v = 0; v < NM; ++v) red[(NS + v) * 16 + w] = mx[v];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < 16 * NV) {
+    const int v = threadIdx.x >> 4, q = threadIdx.x & 15;
+    const bool is_sum = v < NS;
+    float t = q < nw ? red[threadIdx.x] : (is_sum ? 0.f : -INFINITY);
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      const float u = __shfl_xor(t, o, 64);
+      t = is_sum ? t + u : fmaxf(t, u);
+    }
+    if (q == 0) res[v] = t;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int v = 0; v < NS; ++v) sm[v] = res[v];
+#pragma unroll
+  for (int v = 0; v < NM; ++v) mx[v] = res[NS + v];
+  __syncthreads();  // red / res reusable
+}
+
+// Ascending bitonic sort of one 64-bit key per lane across the wave (registers).
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t key) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const uint64_t other = rlmd_shfl_xor_u64(key, j);
+      const bool up = (l & k) == 0 || k == 64;
+      const bool keep_min = ((l & j) == 0) == up;
+      key = keep_min ? (key < other ? key : other) : (key < other ? other : key);
+    }
+  return key;
+}
+
+// Ranks of distinct 64-bit keys across the block (ascending; key ~0 = absent):
+// each wave sorts its 64 keys in registers, parks the sorted run in LDS, and the
+// key at lane l of run w gets rank l + sum over the other runs of a binary
+// search (6 probes over the first 63 entries + the last entry).  The rank is scattered to out[key & 0xffffffff] (the caller's
+// index in the low word) and read back by the key's owner after the barrier.
+// runs: LDS [blockDim.x] uint64; out: LDS int [blockDim.x].
+__device__ __forceinline__ void block_rank(uint64_t key, uint64_t* runs, int* out) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint64_t sk = wave_sort64(key);
+  runs[threadIdx.x] = sk;
+  __syncthreads();
+  if (sk != ~0ull) {
+    int rank = l;
+    for (int v = 0; v < nw; ++v) {
+      if (v == w) continue;
+      const uint64_t* run = runs + 64 * v;
+      // 6 probes count the smaller keys among run[0..62]; run[63] separately
+      int pos = 0;
+#pragma unroll
+      for (int st = 32; st > 0; st >>= 1)
+        if (run[pos + st - 1] < sk) pos += st;
+      rank += pos + (run[63] < sk ? 1 : 0);
+    }
+    out[(int)(sk & 0xffffffffu)] = rank;
+  }
+  __syncthreads();
+}
+
+}  // namespace
+}  // namespace rlmd

@@ -91,6 +91,17 @@ __device__ __forceinline__ uint64_t rlmd_shfl_xor_u64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// Range-checked buffer loads: an element load is always issued (no exec-masked
+// branch, whose s_waitcnt vmcnt(0) would serialise a run of conditional loads);
+// ok == false turns the byte offset out of range and the hardware returns 0.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rlmd_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
+                                           (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+}
+__device__ __forceinline__ float rlmd_ldf(__amdgpu_buffer_rsrc_t r, int64_t idx, bool ok) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? (int)(idx * 4) : 0x7fffffff, 0, 0));
+}
+
 __device__ inline uint64_t rlmd_block_bitonic(uint64_t key, int n, uint64_t* lds) {
   const int i = threadIdx.x;
   for (int k = 2; k <= n; k <<= 1) {

@@ -20,6 +20,7 @@
 #include <math.h>
 
 #include "learn_kernels.h"
+#include "rlmd_block.h"
 #include "rlmd_common.h"
 
 namespace rlmd {
@@ -34,6 +35,20 @@ constexpr int NHF = 4;        // heads reduced in the MFMA epilogue (more -> LDS
 constexpr int W1P = 8;        // fc1 inputs preloaded per thread (more -> read in the loop)
 constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 constexpr int kHeadsMax = 2 * RLMD_MAX_ACTION;
+
+#ifdef RLMD_TIMING
+// experiment builds only (tools/ts_probe.py): thread-0 s_memtime checkpoints of
+// workgroup (0, y) — slots [16 y, 16 y + 16) for fwd jobs, 96.. for abwd
+__device__ unsigned long long g_ts_rows[128];
+#define RLMD_TSR(i)                                                                      \
+  do {                                                                                   \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_ts_rows[i] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define RLMD_TSR(i) \
+  do {              \
+  } while (0)
+#endif
 
 __device__ __forceinline__ unsigned short to_bf16(float f) {
   unsigned u = __float_as_uint(f);
@@ -74,7 +89,7 @@ struct CT<RLMD_FP32> {
 // LDS carve-up, identical on host (launch size) and device.
 // ---------------------------------------------------------------------------
 struct Lds {
-  int xs, a1, aT, h2s, part, hout, ghs, rowv, total;  // byte offsets
+  int xs, a1, aT, h2s, part, hout, ghs, rowv, vkey, vval, total;  // byte offsets
   int ldx, lda1, ldaT, ldh2;                          // row pitches (elements)
 };
 __host__ __device__ inline Lds lds_layout(const RowDims& d) {
@@ -103,6 +118,10 @@ __host__ __device__ inline Lds lds_layout(const RowDims& d) {
   o = up(o + R * kHeadsMax * 4);
   l.rowv = o;  // [R][4]
   o = up(o + R * 4 * 4);
+  l.vkey = o;  // actor loss: every row's ranking key [B] (abwd)
+  o = up(o + d.B * 8);
+  l.vval = o;  // and its objective v [B]
+  o = up(o + d.B * 4);
   l.total = o;
   return l;
 }
@@ -127,15 +146,20 @@ __device__ __forceinline__ void frag_load(FragArr<PREC, NBW, MULTI>& f,
                                           const typename CT<PREC>::T* Bg, int ldb, int s0, int nsteps, int nblk) {
   constexpr int G = Pre<PREC, NBW, MULTI>::G;
   constexpr int EPF = 16 / sizeof(typename CT<PREC>::T);
+  constexpr int TS = sizeof(typename CT<PREC>::T);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint32_t base = (uint32_t)((wave * 16 + (lane & 15)) * ldb + EPF * (lane >> 4));
+  // the copy is [nblk * 16 rows][ldb]; fragments past it read 0 (never used)
+  const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(Bg, (int64_t)nblk * 16 * ldb * TS);
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int i = 0; i < NBW; ++i)
-      if (wave + NW * i < nblk && s0 + g < nsteps)
-        f[g][i] = *reinterpret_cast<const typename CT<PREC>::Frag*>(
-            Bg + base + (uint32_t)(NW * 16 * i * ldb) + (uint32_t)((s0 + g) * CT<PREC>::KS));
+    for (int i = 0; i < NBW; ++i) {
+      const bool ok = wave + NW * i < nblk && s0 + g < nsteps;
+      const uint32_t e = base + (uint32_t)(NW * 16 * i * ldb) + (uint32_t)((s0 + g) * CT<PREC>::KS);
+      f[g][i] = __builtin_bit_cast(typename CT<PREC>::Frag,
+                                   __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (int)(e * TS) : 0x7fffffff, 0, 0));
+    }
 }
 
 template <int PREC, int NBW, bool MULTI>
@@ -225,19 +249,20 @@ __device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, cons
                                           const float* wa, const float* wb, int na) {
   const ElemMap m = elem_map(pad32(o.h1));
   const bool own = m.c < o.h1 && m.r0 < R;
-  const float* w = p + o.w1 + (int64_t)m.c * in;
+  const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(p, o.size * 4);
 #pragma unroll
-  for (int j = 0; j < W1P; ++j) k.w1[j] = (own && j < in) ? w[j] : 0.f;
-  k.b1 = own ? p[o.b1 + m.c] : 0.f;
+  for (int j = 0; j < W1P; ++j) k.w1[j] = rlmd_ldf(rp, o.w1 + (int64_t)m.c * in + j, own && j < in);
+  k.b1 = rlmd_ldf(rp, o.b1 + m.c, own);
+  const int64_t oa = wa - p, ob = (wb ? wb : wa) - p;  // head rows relative to p
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
     const int col = acc_col(i);
     const bool cin = col < o.h2;
-    k.b2[i] = cin ? p[o.b2 + col] : 0.f;
+    k.b2[i] = rlmd_ldf(rp, o.b2 + col, cin);
 #pragma unroll
     for (int h = 0; h < NHF; ++h) {
-      const float* hwp = h < na ? wa + (int64_t)h * o.h2 : wb + (int64_t)(h - na) * o.h2;
-      k.hw[i][h] = (cin && h < nh) ? hwp[col] : 0.f;
+      const int64_t row = h < na ? oa + (int64_t)h * o.h2 : ob + (int64_t)(h - na) * o.h2;
+      k.hw[i][h] = rlmd_ldf(rp, row + col, cin && h < nh);
     }
   }
 }
@@ -350,12 +375,16 @@ __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>
   float* h2s = reinterpret_cast<float*>(smem + L.h2s);
   layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, row0, B);
   __syncthreads();
+  if (blockIdx.y == 2) RLMD_TSR(64);
   f32x4 acc[NBW];
   const int H1p = pad32(o.h1);
   mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, pad32(o.h2) / 16, acc);
+  if (blockIdx.y == 2) RLMD_TSR(65);
   const bool fused = nh <= NHF;
   fwd_epilogue<NBW>(acc, k, o, nh, h2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B);
+  if (blockIdx.y == 2) RLMD_TSR(66);
   __syncthreads();
+  if (blockIdx.y == 2) RLMD_TSR(67);
   if (fused) {
     if ((int)threadIdx.x < R * nh) {
       const int r = threadIdx.x % R, h = threadIdx.x / R;
@@ -434,9 +463,10 @@ __device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, 
 
 // Stage rows [row0, row0 + 16) of a [B, in] matrix into xs (pitch ldx), zeros past B.
 __device__ __forceinline__ void stage_rows(const float* src, int in, float* xs, int ldx, int row0, int B) {
+  const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(src, (int64_t)B * in * 4);
   for (int e = threadIdx.x; e < R * in; e += NT) {
     const int r = e / in, k = e % in;
-    xs[r * ldx + k] = row0 + r < B ? src[(int64_t)(row0 + r) * in + k] : 0.f;
+    xs[r * ldx + k] = rlmd_ldf(rs, (int64_t)(row0 + r) * in + k, row0 + r < B);
   }
 }
 
@@ -465,6 +495,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
   const int H1p = pad32(d.H1), H2p = pad32(d.H2);
   const int na = sac ? 2 * d.A : d.A;
   if (job <= 1) {  // target path (algo_sac.py:300-367 / algo_td3.py:302-361)
+    RLMD_TSR(16 * job + 0);
     const RowNet& an = a.tactor;
     const RowNet& cn = a.tcrit[job];
     Pre<PREC, NBW, MULTI> pa, pc;
@@ -473,17 +504,23 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     FwdConst<NBW> ka, kc;
     actor_const<NBW>(ka, an, a.ao, d);
     critic_const<NBW>(kc, cn, a.co, d);
+    RLMD_TSR(16 * job + 1);
     stage_rows(a.s2, d.S, xs, L.ldx, row0, B);
     __syncthreads();
+    RLMD_TSR(16 * job + 2);
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
                                d.A, smem, L, nullptr, nullptr, row0, B);
+    RLMD_TSR(16 * job + 3);
     sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, 0, a.t_tag, a.eps_next, a.t_noise_std, a.t_noise_clip,
                 a.t_clamp, job == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B);
     __syncthreads();
+    RLMD_TSR(16 * job + 4);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
                                nullptr, row0, B);
+    RLMD_TSR(16 * job + 5);
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qt[job][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else if (job <= 3) {  // online critics on (s, a) (algo_sac.py:413-417)
+    if (job == 2) RLMD_TSR(60);
     const int g = job - 2;
     const RowNet& cn = a.crit[g];
     Pre<PREC, NBW, MULTI> pc;
@@ -492,8 +529,10 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     critic_const<NBW>(kc, cn, a.co, d);
     stage_rows(a.xsa, d.X, xs, L.ldx, row0, B);
     __syncthreads();
+    if (job == 2) RLMD_TSR(61);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.c1[g],
                                a.c2[g], row0, B);
+    if (job == 2) RLMD_TSR(62);
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)
     const RowNet& an = a.actor;
@@ -556,19 +595,20 @@ __device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const float* h1, const
   const int H1 = o.h1, H2 = o.h2;
   const ElemMap m = elem_map(pad32(H2));
   const bool cin = m.c < H2;
+  const __amdgpu_buffer_rsrc_t r1 = rlmd_rsrc(h1, (int64_t)B * H1 * 4), r2 = rlmd_rsrc(h2, (int64_t)B * H2 * 4);
 #pragma unroll
   for (int rr = 0; rr < kMR<NBW>; ++rr) {
     const int r = m.r0 + rr;
-    k.m2[rr] = (r < m.r1 && cin && row0 + r < B) ? h2[(int64_t)(row0 + r) * H2 + m.c] : 0.f;
+    k.m2[rr] = rlmd_ldf(r2, (int64_t)(row0 + r) * H2 + m.c, r < m.r1 && cin && row0 + r < B);
   }
-  k.w3 = (w3 && cin) ? w3[m.c] : 0.f;
+  k.w3 = w3 ? rlmd_ldf(rlmd_rsrc(w3, (int64_t)H2 * 4), m.c, cin) : 0.f;
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
     const int col = acc_col(i);
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
       const int b = row0 + acc_row(rg);
-      k.m1[i][rg] = (col < H1 && b < B) ? h1[(int64_t)b * H1 + col] : 0.f;
+      k.m1[i][rg] = rlmd_ldf(r1, (int64_t)b * H1 + col, col < H1 && b < B);
     }
   }
 }
@@ -653,7 +693,8 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
   pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
   BwdMask<NBW> k;
   bwd_mask<NBW>(k, a.c1[g], a.c2[g], cn.p + a.co.w3, a.co, row0, B);
-  if ((int)threadIdx.x < R) rowv[threadIdx.x] = row0 + (int)threadIdx.x < B ? a.dq[g][row0 + threadIdx.x] : 0.f;
+  if ((int)threadIdx.x < R)
+    rowv[threadIdx.x] = rlmd_ldf(rlmd_rsrc(a.dq[g], (int64_t)B * 4), row0 + threadIdx.x, row0 + (int)threadIdx.x < B);
   __syncthreads();
   dh2_from_q<PREC, NBW>(k, rowv, a.co, aT, L.ldaT, a.dc2[g], row0, B);
   __syncthreads();
@@ -680,6 +721,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const NetOff& ao = a.ao;
   const NetOff& co = a.co;
   const bool fused_da = A <= NHF;
+  RLMD_TSR(96);
   // ---- every independent load up front
   Pre<PREC, NBW, MULTI> p0, p1;
   pre_issue<PREC, NBW, MULTI>(p0, a.crit[0].wt, H2p, H2p, H1p / 16);
@@ -690,17 +732,89 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   bwd_mask<NBW>(ka, a.h1a, a.h2a, nullptr, ao, row0, B);
   float w1a[2][NBW][NHF];  // W1_g[c][S + j] for this lane's dh1 columns
 #pragma unroll
-  for (int g = 0; g < 2; ++g)
+  for (int g = 0; g < 2; ++g) {
+    const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(a.crit[g < a.nq ? g : 0].p, co.size * 4);
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
       const int col = acc_col(i);
 #pragma unroll
       for (int j = 0; j < NHF; ++j)
-        w1a[g][i][j] = (g < a.nq && col < d.H1 && j < A) ? a.crit[g].p[co.w1 + (int64_t)col * X + S + j] : 0.f;
+        w1a[g][i][j] = rlmd_ldf(rp, co.w1 + (int64_t)col * X + S + j, g < a.nq && col < d.H1 && j < A);
     }
-  if ((int)threadIdx.x < 2 * R) {
-    const int g = threadIdx.x / R, r = threadIdx.x % R;
-    rowv[g * R + r] = (g < a.nq && row0 + r < B) ? a.dqn[g][row0 + r] : 0.f;
+  }
+  // ---- actor loss (algo_sac.py:546-562 / algo_td3.py:507-523): every row's
+  //      objective and ranking key (SAC sorts descending, TD3 ascending, Q5)
+  uint64_t* vkey = reinterpret_cast<uint64_t*>(smem + L.vkey);
+  float* vval = reinterpret_cast<float*>(smem + L.vval);
+  int* rank16 = reinterpret_cast<int*>(part);  // [R] (part is free until the first dh1)
+  const float alpha = sac ? expf(a.st->log_alpha) : 0.f;
+  const float qb0 = a.crit[0].p[co.b3], qb1 = a.nq > 1 ? a.crit[1].p[co.b3] : 0.f;
+  for (int j = threadIdx.x; j < B; j += NT) {
+    const float q1 = a.qn[0][j] + qb0;
+    const float q2 = a.nq > 1 ? a.qn[1][j] + qb1 : q1;
+    const float v = sac ? fminf(q1, q2) - alpha * a.logp[j] : q1;
+    vval[j] = v;
+    vkey[j] = ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)j;
+  }
+  if ((int)threadIdx.x < R) rank16[threadIdx.x] = 0;
+  const int kk = a.topk ? (B < a.k ? B : a.k) : B;
+  const bool ext = a.dqn_ext[0] != nullptr;  // loss from actor_loss_kernel (B > 512)
+  __syncthreads();
+  if (!ext && blockIdx.x == gridDim.x - 1) {
+    // the loss workgroup: selection over all rows -> loss value, temperature gradient
+    uint64_t* runs = reinterpret_cast<uint64_t*>(smem + L.a1);
+    int* rank_of = reinterpret_cast<int*>(smem + L.h2s);
+    const int t = threadIdx.x;
+    bool sel = t < B;
+    if (a.topk) {
+      block_rank(t < B ? vkey[t] : ~0ull, runs, rank_of);
+      sel = t < B && rank_of[t] < kk;
+    }
+    float sm[2] = {sel ? vval[t] : 0.f, (t < B && sac) ? -(a.logp[t] + a.target_entropy) : 0.f};
+    float mx[1] = {-INFINITY};
+    block_allreduce<2, 0>(sm, mx, hout);
+    if (t == 0) {
+      if (sac) a.st->pad_temp_grad = sm[1] / B * alpha;
+      a.stats[10] = -sm[0] / kk;
+    }
+    return;
+  }
+  // rank of this block's rows among all B (32 partial counts per row)
+  {
+    const int r = threadIdx.x & (R - 1), prt = threadIdx.x / R;
+    constexpr int NP = NT / R;
+    const uint64_t mine = row0 + r < B ? vkey[row0 + r] : ~0ull;
+    int c = 0;
+    if (!ext)
+      for (int j = prt; j < B; j += NP) c += vkey[j] < mine;
+    atomicAdd(&rank16[r], c);
+  }
+  __syncthreads();
+  float* dlogp_r = rowv + 2 * R;  // [R]
+  if ((int)threadIdx.x < R) {
+    const int r = threadIdx.x, b = row0 + r;
+    float dq0 = 0.f, dq1 = 0.f, dlp = 0.f;
+    if (ext && b < B) {
+      dq0 = a.dqn_ext[0][b];
+      dq1 = a.nq > 1 ? a.dqn_ext[1][b] : 0.f;
+      dlp = sac ? a.dlogp_ext[b] : 0.f;
+    } else if (b < B) {
+      const bool sel = !a.topk || rank16[r] < kk;
+      const float dv = sel ? -1.f / (float)kk : 0.f;
+      if (sac) {
+        // d min(q1, q2): ties split evenly (torch.minimum backward)
+        const float q1 = a.qn[0][b] + qb0, q2 = a.qn[1][b] + qb1;
+        const float g1 = q1 < q2 ? 1.f : (q1 > q2 ? 0.f : 0.5f);
+        dq0 = dv * g1;
+        dq1 = dv * (1.f - g1);
+        dlp = -alpha * dv;
+      } else {
+        dq0 = dv;
+      }
+    }
+    rowv[r] = dq0;
+    rowv[R + r] = dq1;
+    dlogp_r[r] = dlp;
   }
   __syncthreads();
   // ---- dL/da through each critic: dh2 -> dh1 (MFMA) -> . W1[:, S:S+A]
@@ -708,9 +822,12 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     const BwdMask<NBW>& k = g == 0 ? k0 : k1;
     dh2_from_q<PREC, NBW>(k, rowv + g * R, co, aT, L.ldaT, nullptr, row0, B);
     __syncthreads();
+    RLMD_TSR(99 + 4 * g);
     if (fused_da) {
       dh1_rows<PREC, NBW, MULTI>(g == 0 ? p0 : p1, a.crit[g], co, k, aT, L.ldaT, nullptr, w1a[g], A, part, row0, B);
+      RLMD_TSR(100 + 4 * g);
       __syncthreads();
+      RLMD_TSR(101 + 4 * g);
       if ((int)threadIdx.x < R * A) {
         const int r = threadIdx.x % R, j = threadIdx.x / R;
         const float s = head_sum(part, r, j);
@@ -731,6 +848,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     }
     __syncthreads();
   }
+  RLMD_TSR(108);
   // ---- through the sampling and the heads
   Pre<PREC, NBW, MULTI>& pa = p0;  // reuse the first critic's fragment registers
   pre_issue<PREC, NBW, MULTI>(pa, a.actor.wt, H2p, H2p, H1p / 16);
@@ -744,7 +862,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
         if (sac) {
           const float mu = sv[j], sigma = sv[A + j], eps = sv[2 * A + j], u = sv[3 * A + j];
           const float ls_raw = sv[4 * A + j];
-          const float dlp = a.dlogp[b];
+          const float dlp = dlogp_r[r];
           const float t = tanhf(u);
           const float om = 1.f - t * t;
           const float dd = u - mu;
@@ -770,6 +888,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     }
   }
   __syncthreads();
+  RLMD_TSR(109);
   // ---- dh2 = (gh . [W_pi; W_ls]) * [h2 > 0]
   {
     const int H2 = ao.h2;
@@ -793,7 +912,9 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     }
   }
   __syncthreads();
+  RLMD_TSR(110);
   dh1_rows<PREC, NBW, MULTI>(pa, a.actor, ao, ka, aT, L.ldaT, a.dh1, nullptr, 0, nullptr, row0, B);
+  RLMD_TSR(111);
 }
 
 struct CopyJobs {
@@ -840,9 +961,9 @@ void launch_kind(int kind, const void* args, dim3 grid, size_t lds, hipStream_t 
 // NBW = column blocks per wave (8 waves x 16 columns each), MULTI when the K
 // loop needs more than the 16 prefetched fragments per lane.
 template <int PREC>
-int launch_prec(const RowDims& d, int kind, const void* args, int ny, hipStream_t st) {
+int launch_prec(const RowDims& d, int kind, const void* args, int ny, hipStream_t st, int extra_x) {
   const int H = d.H1p > d.H2p ? d.H1p : d.H2p;
-  const dim3 grid((d.B + R - 1) / R, ny);
+  const dim3 grid((d.B + R - 1) / R + extra_x, ny);
   const size_t lds = (size_t)lds_layout(d).total;
   const int nsteps = H / CT<PREC>::KS;
   if (H <= 128) {
@@ -858,25 +979,40 @@ int launch_prec(const RowDims& d, int kind, const void* args, int ny, hipStream_
   return 0;
 }
 
-int launch_rows(const RowDims& d, int kind, const void* args, int ny, hipStream_t st) {
+int launch_rows(const RowDims& d, int kind, const void* args, int ny, hipStream_t st, int extra_x = 0) {
   RLMD_CHECK(d.H1 <= 512 && d.H2 <= 512, "row kernels: hidden widths up to 512");
   RLMD_CHECK(d.A <= RLMD_MAX_ACTION, "row kernels: too many actions");
   RLMD_CHECK(lds_layout(d).total <= 160 * 1024, "row kernels: LDS budget exceeded");
   if (d.B <= 0) return 0;
-  return d.prec == RLMD_BF16 ? launch_prec<RLMD_BF16>(d, kind, args, ny, st)
-                             : launch_prec<RLMD_FP32>(d, kind, args, ny, st);
+  return d.prec == RLMD_BF16 ? launch_prec<RLMD_BF16>(d, kind, args, ny, st, extra_x)
+                             : launch_prec<RLMD_FP32>(d, kind, args, ny, st, extra_x);
 }
 
 }  // namespace
 
 size_t rows_lds_bytes(const RowDims& d) { return (size_t)lds_layout(d).total; }
 
+}  // namespace rlmd
+
+#ifdef RLMD_TIMING
+extern "C" int rlmd_debug_ts_rows(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rlmd::g_ts_rows), sizeof(unsigned long long) * 128) == hipSuccess ? 0 : 2;
+}
+#endif
+
+namespace rlmd {
+
 int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st) {
   return launch_rows(a.d, 0, &a, a.with_actor ? 5 : 4, st);
 }
 int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st) { return launch_rows(a.d, 1, &a, nq, st); }
 int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st) { return launch_rows(a.d, 2, &a, 2, st); }
-int abwd_rows_launch(const ABwdArgs& a, hipStream_t st) { return launch_rows(a.d, 3, &a, 1, st); }
+int abwd_rows_launch(const ABwdArgs& a, hipStream_t st) {
+  const bool ext = a.dqn_ext[0] != nullptr;
+  RLMD_CHECK(ext || a.d.B <= NT, "fused actor loss: mini-batch up to 512 rows");
+  return launch_rows(a.d, 3, &a, 1, st, ext ? 0 : 1);  // + the loss workgroup
+}
 
 int w2_copies_launch(const CopyJob* jobs, int n, const RowDims& d, hipStream_t st) {
   RLMD_CHECK(n >= 1 && n <= 6, "bad copy job count");

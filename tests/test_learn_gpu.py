@@ -60,11 +60,14 @@ def test_learn_matches_reference_golden(golden, dev, case):
         np.testing.assert_allclose(ag.target.cpu().numpy(), ref_t, rtol=0, atol=2e-6, err_msg=f"step {s} targets")
 
 
-def assert_params_close(got, ref, lr, msg):
+def assert_params_close(got, ref, lr, msg, max_lr_frac=0.1):
+    # Adam divides by sqrt(v): a near-zero gradient whose fp32 summation order
+    # differs can move one element by a visible fraction of lr, so the bound on
+    # the worst element is a fraction of lr and the bulk must agree to 2e-6.
     diff = np.abs(got - ref)
     frac = np.mean(diff <= 2e-6)
     assert frac >= 0.999, f"{msg}: only {frac:.6f} within 2e-6 (max {diff.max():.3g})"
-    assert diff.max() <= 0.1 * lr, f"{msg}: max diff {diff.max():.3g} > 10% of lr"
+    assert diff.max() <= max_lr_frac * lr, f"{msg}: max diff {diff.max():.3g} > {max_lr_frac:.0%} of lr"
 
 
 FULL = [("SAC", 5, 1, 256, 256, 512, 256), ("TD3", 6, 2, 400, 300, 200, 100), ("SAC", 6, 2, 256, 256, 512, 256)]
@@ -81,7 +84,7 @@ def _random_batch(rng, B, S, A):
 
 @pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL)
 @pytest.mark.parametrize("loss", ["MSE", "HUB", "MAE", "HSC"])
-def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss):
+def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_lr_frac=0.1):
     from rlmd_amd.agent import reference_init
 
     init = reference_init(algo, S, A, h1, h2, seed=11)
@@ -102,13 +105,20 @@ def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss):
         np.testing.assert_allclose(st[:11], loss_o, rtol=2e-4, atol=1e-6, equal_nan=True, err_msg=f"step {step}")
         np.testing.assert_allclose(st[12:16], lp_o, rtol=2e-4, atol=1e-6)
         lr = 3e-4 if algo == "SAC" else 1e-3
-        assert_params_close(ag.params.cpu().numpy(), ora.P.numpy(), lr, f"step {step} params")
-        assert_params_close(ag.target.cpu().numpy(), ora.T.numpy(), lr, f"step {step} targets")
+        assert_params_close(ag.params.cpu().numpy(), ora.P.numpy(), lr, f"step {step} params", max_lr_frac)
+        assert_params_close(ag.target.cpu().numpy(), ora.T.numpy(), lr, f"step {step} targets", max_lr_frac)
 
 
 @pytest.mark.parametrize("loss", ["CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"])
 def test_remaining_losses_fp32(dev, loss):
     test_full_size_fp32_matches_oracle(dev, "SAC", 5, 1, 256, 256, 512, 256, loss)
+
+
+@pytest.mark.parametrize("algo", ["SAC", "TD3"])
+def test_batch_1024_separate_actor_loss(dev, algo):
+    """B > 512 routes the actor loss through actor_loss_kernel instead of abwd_rows."""
+    # 1024-row sums: twice the reduction length of the 512-row cases
+    test_full_size_fp32_matches_oracle(dev, algo, 5, 1, 256, 256, 1024, 512, "MSE", max_lr_frac=0.2)
 
 
 @pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL[:2])

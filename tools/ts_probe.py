@@ -21,10 +21,15 @@ def build():
 
     b.build()
     os.makedirs(OUT, exist_ok=True)
-    obj = os.path.join(OUT, "learn_ts.o")
-    subprocess.check_call([b.HIPCC, *b.FLAGS, "-DRLMD_TIMING", "-c", os.path.join(b.CSRC, "learn.hip"), "-o", obj])
-    objs = [os.path.join(b.BUILD, os.path.splitext(s)[0] + ".o") for s in b.SOURCES if s != "learn.hip"]
-    subprocess.check_call([b.HIPCC, "-shared", f"--offload-arch={b.ARCH}", "-o", LIB, obj, *objs])
+    timed = ("learn.hip", "rows.hip")
+    tobjs = []
+    for src in timed:
+        obj = os.path.join(OUT, src.replace(".hip", "_ts.o"))
+        subprocess.check_call([b.HIPCC, *b.FLAGS, *b.PER_FILE.get(src, b.DEFAULT_EXTRA), "-DRLMD_TIMING", "-c",
+                               os.path.join(b.CSRC, src), "-o", obj])
+        tobjs.append(obj)
+    objs = [os.path.join(b.BUILD, os.path.splitext(s)[0] + ".o") for s in b.SOURCES if s not in timed]
+    subprocess.check_call([b.HIPCC, "-shared", f"--offload-arch={b.ARCH}", "-o", LIB, *tobjs, *objs])
     print("built", LIB)
 
 
@@ -36,8 +41,9 @@ def run():
 
     _abi._LIB = _abi.load(LIB)
     lib = _abi._LIB
-    lib.rlmd_debug_ts.restype = C.c_int
-    lib.rlmd_debug_ts.argtypes = [C.POINTER(C.c_ulonglong)]
+    for fn in ("rlmd_debug_ts", "rlmd_debug_ts_rows"):
+        getattr(lib, fn).restype = C.c_int
+        getattr(lib, fn).argtypes = [C.POINTER(C.c_ulonglong)]
     from rlmd_amd.trainer import VecTrainer
 
     tr = VecTrainer("gbm", "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
@@ -45,19 +51,32 @@ def run():
     for _ in range(20):
         tr.step()
     torch.cuda.synchronize()
-    rows = []
+    rows, rrows = [], []
     buf = (C.c_ulonglong * 64)()
+    rbuf = (C.c_ulonglong * 128)()
     for _ in range(30):
         tr.step()
         torch.cuda.synchronize()
         lib.rlmd_debug_ts(buf)
+        lib.rlmd_debug_ts_rows(rbuf)
         rows.append(np.array(buf[:16], dtype=np.int64))
+        rrows.append(np.array(rbuf[:128], dtype=np.int64))
     a = np.stack(rows)
     d = np.diff(a[:, :13], axis=1)
     med = np.median(d, axis=0)
+    print("critic_loss_kernel:")
     for i, v in enumerate(med):
-        print(f"ts{i}->ts{i + 1}: {v:10.0f} cycles")
-    print("total", np.median(a[:, 12] - a[:, 0]))
+        print(f"  ts{i}->ts{i + 1}: {v:10.0f} cycles")
+    print("  total", np.median(a[:, 12] - a[:, 0]))
+    r = np.stack(rrows)
+    def seq(name, idx):
+        print(name + ":")
+        for i, j in zip(idx[:-1], idx[1:]):
+            print(f"  {i}->{j}: {np.median(r[:, j] - r[:, i]):10.0f} cycles")
+        print("  total", np.median(r[:, idx[-1]] - r[:, idx[0]]))
+    seq("fwd_rows target job 0", [0, 1, 2, 3, 4, 5])
+    seq("fwd_rows critic job 2", [60, 61, 64, 65, 66, 67, 62])
+    seq("abwd_rows", [96, 97, 98, 99, 100, 101, 103, 104, 105, 108, 109, 110, 111])
 
 
 if __name__ == "__main__":
