@@ -20,6 +20,7 @@
 
 #include "learn_kernels.h"
 #include "rlmd_block.h"
+#include "rlmd_loss.h"
 #include "rlmd_gemm.h"
 
 namespace rlmd {
@@ -109,66 +110,10 @@ __global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
 }
 
 // ---------------------------------------------------------------------------
-// Critic loss, top-k, tail index, CIM kernel, Nagy scale
-// (tools/critic_loss.py:26-341, loss_function :344-453; algo_sac.py:419-473).
-// One workgroup of 1024 threads; thread b owns mini-batch row b.
+// Critic loss, top-k, tail index, CIM kernel, Nagy scale as one workgroup
+// (rlmd_loss.h).  Launched for B > 512 (dq + statistics) and, on updates
+// without an actor step, for the statistics alone (cbwd_rows forms dq).
 // ---------------------------------------------------------------------------
-struct LossArgs {
-  const float* qpart[2];  // online critics' q per row without the head bias [B]
-  const float* qb[2];     // q_value.bias (online)
-  const float* tpart[2];  // target critics' q per row without the head bias [B]
-  const float* tb[2];     // q_value.bias (target)
-  const float* r;
-  const uint8_t* done;
-  const int32_t* eff;
-  const float* logp_next;  // SAC
-  float gamma, reward_scale;
-  float* dq[2];
-  float* y_out;  // nullable
-  const float* zipf_x;
-  float zipf_x2;
-  LearnState* st;
-  float* stats;  // [16]
-  int32_t B, k, loss_type, algo;
-  float log_noise, grad_scale;
-};
-
-__device__ __forceinline__ void loss_and_grad(int lt, float q, float t, float c, float kern,
-                                              float& l, float& dl) {
-  const float d = t - q;
-  switch (lt) {
-    case RLMD_LOSS_MSE: l = d * d; dl = -2.f * d; break;
-    case RLMD_LOSS_MSE2: l = d * d * d * d; dl = -4.f * d * d * d; break;
-    case RLMD_LOSS_MSE4: { const float d2 = d * d; l = d2 * d2 * d2; dl = -6.f * d2 * d2 * d; break; }
-    case RLMD_LOSS_MSE6: { const float d2 = d * d; l = d2 * d2 * d2 * d2; dl = -8.f * d2 * d2 * d2 * d; break; }
-    case RLMD_LOSS_MAE: l = fabsf(d); dl = d > 0.f ? -1.f : (d < 0.f ? 1.f : 0.f); break;
-    case RLMD_LOSS_HUB: {
-      const float ad = fabsf(d);
-      const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
-      if (ad < 1.f) { l = 0.5f * ad * ad; dl = -ad * sg; }
-      else { l = ad - 0.5f; dl = -sg; }
-      break;
-    }
-    case RLMD_LOSS_HSC: { const float s = sqrtf(1.f + d * d); l = s - 1.f; dl = -d / s; break; }
-    case RLMD_LOSS_CAU:
-    case RLMD_LOSS_TCAU: {
-      const float z = d / c;
-      l = logf(1.f + z * z);
-      dl = -(2.f * z / c) / (1.f + z * z);
-      break;
-    }
-    default: {  // CIM
-      const float e = expf(-(d * d) / (2.f * kern * kern)) / sqrtf(2.f * 3.14159265358979323846f * kern);
-      l = 1.f - e;
-      dl = -e * d / (kern * kern);
-      break;
-    }
-  }
-}
-
-// Bootstrapped target (algo_sac.py:347-365 / algo_td3.py:346-359) + critic loss,
-// top-k, tail index, CIM kernel and Nagy scale (tools/critic_loss.py:26-453,
-// algo_sac.py:413-473).  One workgroup; thread b owns mini-batch row b.
 #ifdef RLMD_TIMING
 // experiment builds only (tools/ts_probe.py): thread-0 s_memtime checkpoints
 __device__ unsigned long long g_ts[64];
@@ -187,140 +132,7 @@ __global__ void __launch_bounds__(NTH) critic_loss_kernel(LossArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t runs[NTH];
   __shared__ int rank_of[3][NTH];
   __shared__ float red[16 * 9];
-  const int b = threadIdx.x, B = a.B;
-  const bool in = b < B;
-  LearnState* st = a.st;
-  RLMD_TS(0);
-  // -- target and current q (row kernels' head outputs + biases).  Every row's
-  //    loads are issued unconditionally (range-checked buffer loads), so the
-  //    whole prologue is one memory round trip
-  const int64_t nB = (int64_t)B * 4;
-  float qt[2], q[2] = {0.f, 0.f};
-  for (int g = 0; g < 2; ++g) {
-    qt[g] = rlmd_ldf(rlmd_rsrc(a.tpart[g], nB), b, in);
-    q[g] = rlmd_ldf(rlmd_rsrc(a.qpart[g], nB), b, in);
-  }
-  const float rw = rlmd_ldf(rlmd_rsrc(a.r, nB), b, in);
-  const float lpn = a.logp_next ? rlmd_ldf(rlmd_rsrc(a.logp_next, nB), b, in) : 0.f;
-  const uint8_t dn = __builtin_amdgcn_raw_buffer_load_b8(rlmd_rsrc(a.done, B), in ? b : 0x7fffffff, 0, 0);
-  const int eff = a.eff ? (int)__builtin_bit_cast(
-                              int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, nB), in ? b * 4 : 0x7fffffff, 0, 0))
-                        : 1;
-  float y = 0.f;
-  for (int g = 0; g < 2; ++g) {
-    qt[g] += a.tb[g][0];
-    q[g] += a.qb[g][0];
-  }
-  if (in) {
-    if (dn) qt[0] = qt[1] = 0.f;
-    const float m = fminf(qt[0], qt[1]);
-    const float ge = powf(a.gamma, (float)eff);
-    if (a.algo == RLMD_SAC) y = (a.reward_scale * rw + ge * m) - expf(st->log_alpha) * lpn;
-    else y = rw + ge * m;
-    if (a.y_out) a.y_out[b] = y;
-  } else {
-    q[0] = q[1] = 0.f;
-  }
-  RLMD_TS(1);
-  const float scale[2] = {st->cauchy[0], st->cauchy[1]};
-  // -- R1: means of (t - q)^2 (CIM kernel), of y, q (TCAU), Nagy terms; NaN flag
-  const float e0 = (y - q[0]) * (y - q[0]), e1 = (y - q[1]) * (y - q[1]);
-  const float z0 = (y - q[0]) / scale[0], z1 = (y - q[1]) / scale[1];
-  float s1[7] = {in ? e0 : 0.f, in ? e1 : 0.f, in ? y : 0.f, in ? q[0] : 0.f, in ? q[1] : 0.f,
-                 in ? 1.f / (1.f + z0 * z0) : 0.f, in ? 1.f / (1.f + z1 * z1) : 0.f};
-  float m1[1] = {(in && (isnan(q[0]) || isnan(q[1]) || isnan(y))) ? 1.f : 0.f};
-  RLMD_TS(2);
-  block_allreduce<7, 1>(s1, m1, red);
-  RLMD_TS(3);
-  const float me0 = s1[0] / B, me1 = s1[1] / B, my = s1[2] / B, mq0 = s1[3] / B, mq1 = s1[4] / B;
-  // -- R2: population variances (two-pass, like torch.std(unbiased=False))
-  float s2[5] = {in ? (e0 - me0) * (e0 - me0) : 0.f, in ? (e1 - me1) * (e1 - me1) : 0.f,
-                 in ? (y - my) * (y - my) : 0.f, in ? (q[0] - mq0) * (q[0] - mq0) : 0.f,
-                 in ? (q[1] - mq1) * (q[1] - mq1) : 0.f};
-  float m2[1] = {-INFINITY};
-  block_allreduce<5, 0>(s2, m2, red);
-  RLMD_TS(4);
-  const float kern[2] = {sqrtf(s2[0] / B), sqrtf(s2[1] / B)};
-  // TCAU 3-sigma truncation (critic_loss.py:26-50)
-  float yt[2] = {y, y}, qt_[2] = {q[0], q[1]};
-  bool qtr[2] = {false, false};
-  if (a.loss_type == RLMD_LOSS_TCAU) {
-    const bool ytr = fabsf(y - my) > 3.f * sqrtf(s2[2] / B);
-    const float mq[2] = {mq0, mq1}, sq[2] = {sqrtf(s2[3] / B), sqrtf(s2[4] / B)};
-    for (int g = 0; g < 2; ++g) {
-      qtr[g] = fabsf(q[g] - mq[g]) > 3.f * sq[g];
-      qt_[g] = qtr[g] ? 0.f : q[g];
-      yt[g] = ytr ? 0.f : y;
-    }
-  }
-  float l[2], dl[2];
-  for (int g = 0; g < 2; ++g) {
-    loss_and_grad(a.loss_type, qt_[g], yt[g], scale[g], kern[g], l[g], dl[g]);
-    if (qtr[g]) dl[g] = 0.f;
-  }
-  // -- top-k rows by l1 + l2, descending (critic_loss.py:438-441); ties by row
-  const int k = B > a.k ? a.k : B;
-  bool sel = in;
-  int rank = b;
-  RLMD_TS(5);
-  if (B > a.k) {
-    block_rank(in ? ((uint64_t)(~f2key(l[0] + l[1])) << 32) | (uint32_t)b : ~0ull, runs, rank_of[0]);
-    rank = in ? rank_of[0][b] : B;
-    sel = in && rank < k;
-  }
-  RLMD_TS(6);
-  RLMD_TS(7);
-  // -- R3: mean / min / max of the selected losses per critic
-  float s3[2] = {sel ? l[0] : 0.f, sel ? l[1] : 0.f};
-  float m3[4] = {sel ? l[0] : -INFINITY, sel ? l[1] : -INFINITY, sel ? -l[0] : -INFINITY,
-                 sel ? -l[1] : -INFINITY};
-  block_allreduce<2, 4>(s3, m3, red);
-  RLMD_TS(8);
-  // -- Zipf-plot tail index of the selected losses' order statistics
-  //    (critic_loss.py:238-266): each critic's selected losses ranked among
-  //    themselves, descending, ties by selection rank; that rank is the slot
-  RLMD_TS(9);
-  block_rank(sel ? ((uint64_t)(~f2key(l[0])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of[1]);
-  block_rank(sel ? ((uint64_t)(~f2key(l[1])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of[2]);
-  const int rz0 = sel ? rank_of[1][rank] : 0, rz1 = sel ? rank_of[2][rank] : 0;
-  RLMD_TS(10);
-  const float lg0 = sel ? logf(l[0] + a.log_noise) : 0.f;
-  const float lg1 = sel ? logf(l[1] + a.log_noise) : 0.f;
-  float s4[2] = {lg0, lg1};
-  float m4[1] = {-INFINITY};
-  block_allreduce<2, 0>(s4, m4, red);
-  float s5[2] = {sel ? a.zipf_x[rz0] * (lg0 - s4[0] / k) : 0.f, sel ? a.zipf_x[rz1] * (lg1 - s4[1] / k) : 0.f};
-  block_allreduce<2, 0>(s5, m4, red);
-  RLMD_TS(11);
-  // -- gradients of grad_scale * (mean(l1[sel]) + mean(l2[sel])) w.r.t. q
-  if (in) {
-    a.dq[0][b] = sel ? a.grad_scale * dl[0] / (float)k : 0.f;
-    a.dq[1][b] = sel ? a.grad_scale * dl[1] / (float)k : 0.f;
-  }
-  if (b == 0) {
-    float newc[2];
-    for (int g = 0; g < 2; ++g) {  // Nagy Cauchy-scale update (critic_loss.py:74-101)
-      const float ie = 1.f / (s1[5 + g] / B);
-      newc[g] = ie > 1.f ? scale[g] * sqrtf(ie - 1.f) : scale[g];
-      a.stats[0 + g] = s3[g] / k;
-      a.stats[2 + g] = -m3[2 + g];
-      a.stats[4 + g] = m3[g];
-      a.stats[6 + g] = NAN;
-      a.stats[8 + g] = 1.f / (s5[g] / a.zipf_x2);
-    }
-    st->cauchy[0] = newc[0];
-    st->cauchy[1] = newc[1];
-    st->kernel[0] = kern[0];
-    st->kernel[1] = kern[1];
-    if (m1[0] > 0.f) st->nan_flag = 1;
-    a.stats[10] = NAN;
-    a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
-    a.stats[12] = newc[0];
-    a.stats[13] = newc[1];
-    a.stats[14] = kern[0];
-    a.stats[15] = kern[1];
-  }
-  RLMD_TS(12);
+  critic_loss_block(a, runs, &rank_of[0][0], red);
 }
 
 // ---------------------------------------------------------------------------
@@ -523,6 +335,7 @@ struct Scratch {
   uint8_t* done;
   // target path: target q per row (no head bias), logp of the next actions
   float *logp_next, *tpart[2], *y;
+  float* qbias;  // [4] q_value.bias of the online, then target critics at loss time
   // critic path
   float *c1[2], *c2[2], *qpart[2], *dq[2], *dc2[2], *dc1[2];
   // actor path
@@ -785,6 +598,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     RLMD_TRY(fwd_rows_launch(f, st));
   }
   // ---- critic loss (algo_sac.py:413-465)
+  LossArgs loss_fused{}, loss_stats{};  // B == 0: not used
   {
     LossArgs la{};
     for (int g = 0; g < 2; ++g) {
@@ -812,11 +626,22 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     la.algo = c.algo;
     la.log_noise = c.log_noise;
     la.grad_scale = sac ? 0.5f : 1.0f;  // SAC: 0.5 (q1_loss + q2_loss)
-    if (B <= 512)
-      hipLaunchKernelGGL(critic_loss_kernel<512>, dim3(1), dim3(512), 0, st, la);
-    else
+    if (B > 512) {
       hipLaunchKernelGGL(critic_loss_kernel<1024>, dim3(1), dim3(1024), 0, st, la);
-    RLMD_LAUNCH_CHECK();
+      RLMD_LAUNCH_CHECK();
+    } else {
+      // B <= 512: cbwd_rows forms dq per row workgroup; the statistics come
+      // from a workgroup of abwd_rows (actor step) or a kernel after cbwd
+      // the statistics run after the critic Adam step has moved the heads'
+      // biases: they read the loss-time biases cbwd_rows saved
+      loss_fused = la;
+      loss_stats = la;
+      loss_stats.dq[0] = loss_stats.dq[1] = nullptr;
+      for (int g = 0; g < 2; ++g) {
+        loss_stats.qb[g] = S_.qbias + g;
+        loss_stats.tb[g] = S_.qbias + 2 + g;
+      }
+    }
   }
   // ---- critic backward: data gradients per row, then all weight gradients
   {
@@ -831,7 +656,13 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       cb.dc2[g] = S_.dc2[g];
       cb.dc1[g] = S_.dc1[g];
     }
+    cb.loss = loss_fused;
+    cb.bias_out = S_.qbias;
     RLMD_TRY(cbwd_rows_launch(cb, st));
+    if (loss_stats.B > 0 && !actor_step) {
+      hipLaunchKernelGGL(critic_loss_kernel<512>, dim3(1), dim3(512), 0, st, loss_stats);
+      RLMD_LAUNCH_CHECK();
+    }
     GemmBatch gb{};
     for (int g = 0; g < 2; ++g) {
       add_bwd_w(gb, 1, H2, B, S_.dq[g], 1, S_.c2[g], H2, Gc[g] + co.w3, Gc[g] + co.b3);
@@ -920,6 +751,8 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     ab.gh = S_.gh;
     ab.dh2 = S_.dh2;
     ab.dh1 = S_.dh1;
+    ab.cstats = loss_stats;
+    ab.cstats.keep_actor_slot = 1;  // stats[10] belongs to the actor-loss workgroup
     RLMD_TRY(abwd_rows_launch(ab, st));
     GemmBatch gb{};
     add_bwd_w(gb, A, H2, B, S_.gh, 2 * A, S_.h2, H2, Ga + ao.w3, Ga + ao.b3);
@@ -1100,6 +933,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.dh2, B * H2);
   RLMD_ALLOC(s.dh1, B * H1);
   RLMD_ALLOC(s.stats, 16);
+  RLMD_ALLOC(s.qbias, 4);
   for (int g = 0; g < 2; ++g) {
     RLMD_ALLOC(s.tpart[g], B);
     RLMD_ALLOC(s.c1[g], B * H1);

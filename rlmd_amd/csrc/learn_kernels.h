@@ -124,6 +124,31 @@ struct QEvalArgs {
 };
 
 // Critic data-gradients: y = g.  dh2 = dq w3 * [h2 > 0], dh1 = (dh2 W2) * [h1 > 0].
+// Critic loss inputs (tools/critic_loss.py:26-453, algo_sac.py:413-473).  Used
+// by critic_loss_kernel (learn.hip), by cbwd_rows (every row workgroup forms the
+// per-row loss gradients of its rows) and by the critic-statistics workgroup of
+// abwd_rows (rows.hip).
+struct LossArgs {
+  const float* qpart[2];  // online critics' q per row without the head bias [B]
+  const float* qb[2];     // q_value.bias (online)
+  const float* tpart[2];  // target critics' q per row without the head bias [B]
+  const float* tb[2];     // q_value.bias (target)
+  const float* r;
+  const uint8_t* done;
+  const int32_t* eff;
+  const float* logp_next;  // SAC
+  float gamma, reward_scale;
+  float* dq[2];
+  float* y_out;  // nullable
+  const float* zipf_x;
+  float zipf_x2;
+  LearnState* st;
+  float* stats;  // [16]
+  int32_t B, k, loss_type, algo;
+  float log_noise, grad_scale;
+  int32_t keep_actor_slot;  // 1: leave stats[10] (actor loss) alone
+};
+
 struct CBwdArgs {
   RowDims d;
   NetOff co;
@@ -133,6 +158,10 @@ struct CBwdArgs {
   const float* c2[2];
   float* dc2[2];
   float* dc1[2];
+  // B <= 512: the row workgroups form dq from the loss inputs themselves
+  // (dq then written, not read); loss.B == 0: dq comes from critic_loss_kernel
+  LossArgs loss;
+  float* bias_out;  // [4] loss-time head biases (online 0/1, target 0/1) for the statistics
 };
 
 // Actor loss + data-gradients.  Row workgroups rank their own rows' objective
@@ -165,6 +194,9 @@ struct ABwdArgs {
   float* gh;
   float* dh2;
   float* dh1;
+  // critic statistics workgroup (stats, Cauchy scales, CIM kernel, NaN flag of
+  // this update's critic loss) when cstats.B > 0
+  LossArgs cstats;
 };
 
 size_t rows_lds_bytes(const RowDims& d);

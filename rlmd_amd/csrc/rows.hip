@@ -21,6 +21,7 @@
 
 #include "learn_kernels.h"
 #include "rlmd_block.h"
+#include "rlmd_loss.h"
 #include "rlmd_common.h"
 
 namespace rlmd {
@@ -89,7 +90,7 @@ struct CT<RLMD_FP32> {
 // LDS carve-up, identical on host (launch size) and device.
 // ---------------------------------------------------------------------------
 struct Lds {
-  int xs, a1, aT, h2s, part, hout, ghs, rowv, vkey, vval, total;  // byte offsets
+  int xs, a1, aT, h2s, part, hout, ghs, rowv, vkey, vval, runs, rank, red, total;  // byte offsets
   int ldx, lda1, ldaT, ldh2;                          // row pitches (elements)
 };
 __host__ __device__ inline Lds lds_layout(const RowDims& d) {
@@ -122,6 +123,12 @@ __host__ __device__ inline Lds lds_layout(const RowDims& d) {
   o = up(o + d.B * 8);
   l.vval = o;  // and its objective v [B]
   o = up(o + d.B * 4);
+  l.runs = o;  // loss workgroups: block_rank runs [NT], ranks [3][NT], reductions
+  o = up(o + NT * 8);
+  l.rank = o;
+  o = up(o + 3 * NT * 4);
+  l.red = o;
+  o = up(o + 16 * 9 * 4);
   l.total = o;
   return l;
 }
@@ -693,8 +700,42 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
   pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
   BwdMask<NBW> k;
   bwd_mask<NBW>(k, a.c1[g], a.c2[g], cn.p + a.co.w3, a.co, row0, B);
-  if ((int)threadIdx.x < R)
+  if (a.loss.B > 0) {
+    // critic loss gradient of this block's rows (rlmd_loss.h): every row's loss,
+    // then the rows' top-k ranks counted against all B keys
+    uint64_t* vkey = reinterpret_cast<uint64_t*>(smem + L.vkey);
+    float* red = reinterpret_cast<float*>(smem + L.red);
+    int* rank16 = reinterpret_cast<int*>(smem + L.part);
+    float* dl16 = reinterpret_cast<float*>(smem + L.part) + R;
+    CriticRow o;
+    critic_row_loss(a.loss, red, o);
+    const int t = threadIdx.x;
+    if (a.bias_out && blockIdx.x == 0 && g == 0 && t < 4)
+      a.bias_out[t] = t < 2 ? a.loss.qb[t][0] : a.loss.tb[t - 2][0];
+    if (t < B) vkey[t] = critic_sel_key(o);
+    if (t < R) rank16[t] = 0;
+    if (t >= row0 && t < row0 + R) dl16[t - row0] = g == 0 ? o.dl[0] : o.dl[1];
+    __syncthreads();
+    const bool topk = B > a.loss.k;
+    if (topk) {
+      const int r = t & (R - 1), prt = t / R;
+      constexpr int NP = NT / R;
+      const uint64_t mine = vkey[row0 + r < B ? row0 + r : 0];
+      int c = 0;
+      for (int j = prt; j < B; j += NP) c += vkey[j] < mine;
+      atomicAdd(&rank16[r], c);
+      __syncthreads();
+    }
+    if (t < R) {
+      const int b = row0 + t, kk = topk ? a.loss.k : B;
+      const bool sel = b < B && (!topk || rank16[t] < kk);
+      const float dq = sel ? a.loss.grad_scale * dl16[t] / (float)kk : 0.f;
+      rowv[t] = dq;
+      if (b < B) a.loss.dq[g][b] = dq;
+    }
+  } else if ((int)threadIdx.x < R) {
     rowv[threadIdx.x] = rlmd_ldf(rlmd_rsrc(a.dq[g], (int64_t)B * 4), row0 + threadIdx.x, row0 + (int)threadIdx.x < B);
+  }
   __syncthreads();
   dh2_from_q<PREC, NBW>(k, rowv, a.co, aT, L.ldaT, a.dc2[g], row0, B);
   __syncthreads();
@@ -721,6 +762,12 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const NetOff& ao = a.ao;
   const NetOff& co = a.co;
   const bool fused_da = A <= NHF;
+  if (a.cstats.B > 0 && blockIdx.x == gridDim.x - 1) {
+    // this update's critic statistics (rlmd_loss.h), off the critical path
+    critic_loss_block(a.cstats, reinterpret_cast<uint64_t*>(smem + L.runs), reinterpret_cast<int*>(smem + L.rank),
+                      reinterpret_cast<float*>(smem + L.red));
+    return;
+  }
   RLMD_TSR(96);
   // ---- every independent load up front
   Pre<PREC, NBW, MULTI> p0, p1;
@@ -760,10 +807,10 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const int kk = a.topk ? (B < a.k ? B : a.k) : B;
   const bool ext = a.dqn_ext[0] != nullptr;  // loss from actor_loss_kernel (B > 512)
   __syncthreads();
-  if (!ext && blockIdx.x == gridDim.x - 1) {
+  if (!ext && blockIdx.x == gridDim.x - 1 - (a.cstats.B > 0 ? 1 : 0)) {
     // the loss workgroup: selection over all rows -> loss value, temperature gradient
-    uint64_t* runs = reinterpret_cast<uint64_t*>(smem + L.a1);
-    int* rank_of = reinterpret_cast<int*>(smem + L.h2s);
+    uint64_t* runs = reinterpret_cast<uint64_t*>(smem + L.runs);
+    int* rank_of = reinterpret_cast<int*>(smem + L.rank);
     const int t = threadIdx.x;
     bool sel = t < B;
     if (a.topk) {
@@ -772,7 +819,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     }
     float sm[2] = {sel ? vval[t] : 0.f, (t < B && sac) ? -(a.logp[t] + a.target_entropy) : 0.f};
     float mx[1] = {-INFINITY};
-    block_allreduce<2, 0>(sm, mx, hout);
+    block_allreduce<2, 0>(sm, mx, reinterpret_cast<float*>(smem + L.red));
     if (t == 0) {
       if (sac) a.st->pad_temp_grad = sm[1] / B * alpha;
       a.stats[10] = -sm[0] / kk;
@@ -1011,7 +1058,9 @@ int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st) { return launch_rows(a.d
 int abwd_rows_launch(const ABwdArgs& a, hipStream_t st) {
   const bool ext = a.dqn_ext[0] != nullptr;
   RLMD_CHECK(ext || a.d.B <= NT, "fused actor loss: mini-batch up to 512 rows");
-  return launch_rows(a.d, 3, &a, 1, st, ext ? 0 : 1);  // + the loss workgroup
+  RLMD_CHECK(a.cstats.B <= NT, "critic statistics workgroup: mini-batch up to 512 rows");
+  // + the actor-loss workgroup, + the critic-statistics workgroup
+  return launch_rows(a.d, 3, &a, 1, st, (ext ? 0 : 1) + (a.cstats.B > 0 ? 1 : 0));
 }
 
 int w2_copies_launch(const CopyJob* jobs, int n, const RowDims& d, hipStream_t st) {
