@@ -145,6 +145,8 @@ enum {
   RLMD_LOSS_TCAU = 5, RLMD_LOSS_CIM = 6, RLMD_LOSS_MSE2 = 7, RLMD_LOSS_MSE4 = 8, RLMD_LOSS_MSE6 = 9
 };
 enum { RLMD_FP32 = 0, RLMD_BF16 = 1 }; /* MLP GEMM operand precision (fp32 accumulate) */
+/* SAC policy sampler, inputs["s_dist"] (algo_sac.py:207-218): "N", "L", "MVN" */
+enum { RLMD_DIST_N = 0, RLMD_DIST_L = 1, RLMD_DIST_MVN = 2 };
 
 typedef struct rlmd_agent_s* rlmd_agent_t;
 
@@ -156,6 +158,7 @@ typedef struct {
   int32_t precision;   /* RLMD_FP32 | RLMD_BF16 */
   int32_t actor_update_interval, target_critic_update, target_actor_update, temp_update_interval;
   int32_t actor_topk;  /* 1: actor percentile != 100 (sort + top-k), 0: plain mean */
+  int32_t policy_dist; /* RLMD_DIST_* (SAC; ignored by TD3) */
   float gamma, tau, lr_actor, lr_critic, lr_temp, reward_scale, max_action;
   float log_scale_min, log_scale_max, reparam_noise, log_noise, cauchy_scale, initial_logtemp;
   float policy_noise, target_policy_noise, target_policy_clip; /* already x max_action */

@@ -2,7 +2,8 @@
 
 (see oracle/__init__.py).  Restates majidsina/rlmd:
   SAC  algos/algo_sac.py:300-367 (_multi_step_target), :369-595 (learn), :597-615 (Polyak)
-       algos/networks_sac.py:101-178 (forward, stochastic_uv_gaussian), :346-362 (critic)
+       algos/networks_sac.py:101-178 (forward, stochastic_uv_gaussian), :180-220
+       (stochastic_uv_laplace), :222-258 (stochastic_mv_gaussian), :346-362 (critic)
   TD3  algos/algo_td3.py:302-361, :363-531, :533-563; algos/networks_td3.py:76-91, :152-168
   losses tools/critic_loss.py:26-453 (per-sample losses, top-k, aggregator_fast, zipf_plot,
        cim_size, nagy_algo)
@@ -152,8 +153,9 @@ class OracleLearner:
                  max_action=0.99, ls_min=-20.0, ls_max=2.0, reparam_noise=1e-6, log_noise=1e-6,
                  cauchy=1.0, logtemp=0.0, policy_noise=0.1, target_noise=0.2, target_clip=0.5,
                  actor_interval=None, target_critic_update=None, target_actor_update=2,
-                 temp_interval=1, actor_topk=True):
+                 temp_interval=1, actor_topk=True, s_dist="N"):
         sac = algo == "SAC"
+        self.s_dist = s_dist
         self.algo, self.S, self.A, self.B, self.k, self.lt = algo, S, A, B, k, loss_type
         self.lay, self.n = layout(algo, S, A, h1, h2)
         self.P = torch.tensor(params, dtype=torch.float32).clone()
@@ -187,7 +189,9 @@ class OracleLearner:
         return views(flat, self.lay)
 
     def policy(self, p, s, eps, stochastic=True):
-        """SAC stochastic_uv_gaussian / deterministic_policy; TD3 forward."""
+        """SAC stochastic_uv_gaussian / _uv_laplace / _mv_gaussian (s_dist N / L / MVN)
+        or deterministic_policy; TD3 forward.  eps: the injected noise (Laplace: the
+        uniform w of Laplace.rsample)."""
         h, mu = mlp(p, s, "pi" if self.algo == "SAC" else "mu")
         if self.algo == "TD3":
             return torch.tanh(mu) * self.max_action, None
@@ -196,8 +200,17 @@ class OracleLearner:
         ls = F.linear(h, p["log_scale.weight"], p["log_scale.bias"])
         ls = torch.clamp(ls, self.ls_min, self.ls_max)
         scale = ls.exp()
-        u = mu + eps * scale
-        lp = (-((u - mu) ** 2) / (2 * scale**2) - torch.log(scale) - math.log(math.sqrt(2 * math.pi))).sum(1)
+        if self.s_dist == "L":  # torch Laplace: loc - scale sign(w) log1p(-|w|)
+            u = mu - scale * eps.sign() * torch.log1p(-eps.abs())
+            lp = (-torch.log(2 * scale) - torch.abs(u - mu) / scale).sum(1)
+        elif self.s_dist == "MVN":  # scale used as the variance: L = cholesky(diag) = sqrt
+            sd = torch.sqrt(scale)
+            u = mu + sd * eps
+            z = (u - mu) / sd
+            lp = -0.5 * (self.A * math.log(2 * math.pi) + (z * z).sum(1)) - torch.log(sd).sum(1)
+        else:
+            u = mu + eps * scale
+            lp = (-((u - mu) ** 2) / (2 * scale**2) - torch.log(scale) - math.log(math.sqrt(2 * math.pi))).sum(1)
         a = torch.tanh(u) * self.max_action
         lp = lp - torch.log(1 - (a / self.max_action) ** 2 + self.reparam_noise).sum(1)
         return a, lp

@@ -16,6 +16,7 @@ COIN, DICE, GBM, DICE_SH, MARKET = range(5)
 INV_A, INV_B, INV_C, INV_INSURED = range(4)
 SAC, TD3 = 0, 1
 FP32, BF16 = 0, 1
+DIST_N, DIST_L, DIST_MVN = 0, 1, 2
 LOSSES = ["MSE", "HUB", "MAE", "HSC", "CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"]
 GEMM_FWD, GEMM_BWD_X, GEMM_BWD_W = 0, 1, 2
 GRAD_SPLITS = 4  # RLMD_GRAD_SPLITS
@@ -38,7 +39,7 @@ class AgentCfg(C.Structure):
                 ("loss_type", C.c_int32), ("precision", C.c_int32),
                 ("actor_update_interval", C.c_int32), ("target_critic_update", C.c_int32),
                 ("target_actor_update", C.c_int32), ("temp_update_interval", C.c_int32),
-                ("actor_topk", C.c_int32),
+                ("actor_topk", C.c_int32), ("policy_dist", C.c_int32),
                 ("gamma", C.c_float), ("tau", C.c_float), ("lr_actor", C.c_float),
                 ("lr_critic", C.c_float), ("lr_temp", C.c_float), ("reward_scale", C.c_float),
                 ("max_action", C.c_float), ("log_scale_min", C.c_float),

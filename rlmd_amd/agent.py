@@ -65,6 +65,10 @@ def reference_init(algo, S, A, h1, h2, seed=None):
     return out
 
 
+# inputs["s_dist"] (algo_sac.py:100, :207-218): the SAC policy's sampler
+POLICY_DIST = {"N": _abi.DIST_N, "L": _abi.DIST_L, "MVN": _abi.DIST_MVN}
+
+
 class DeviceAgent:
     """The learner state on the device + its librlmd_amd handle."""
 
@@ -74,7 +78,7 @@ class DeviceAgent:
                  log_noise=1e-6, cauchy_scale=1.0, initial_logtemp=0.0, policy_noise=0.1,
                  target_policy_noise=0.2, target_policy_clip=0.5, actor_update_interval=None,
                  target_critic_update=None, target_actor_update=2, temp_update_interval=1,
-                 actor_topk=True, init=None, init_seed=None, device="cuda:0"):
+                 actor_topk=True, policy_dist="N", init=None, init_seed=None, device="cuda:0"):
         sac = algo == "SAC"
         self.algo, self.S, self.A, self.h1, self.h2 = algo, S, A, h1, h2
         self.batch, self.topk, self.device = batch, topk, torch.device(device)
@@ -89,6 +93,7 @@ class DeviceAgent:
         cfg.target_actor_update = target_actor_update
         cfg.temp_update_interval = temp_update_interval
         cfg.actor_topk = 1 if actor_topk else 0
+        cfg.policy_dist = POLICY_DIST[policy_dist]
         cfg.gamma, cfg.tau = gamma, tau
         cfg.lr_actor = lr_actor or (3e-4 if sac else 1e-3)
         cfg.lr_critic = lr_critic or (3e-4 if sac else 1e-3)
@@ -256,7 +261,7 @@ class _Agent:
                       lr_critic=inputs["sac_critic_learn_rate"], lr_temp=inputs["sac_temp_learn_rate"],
                       reward_scale=float(inputs["reward_scale"]),
                       log_scale_min=float(inputs["log_scale_min"]), log_scale_max=float(inputs["log_scale_max"]),
-                      reparam_noise=float(inputs["reparam_noise"]),
+                      reparam_noise=float(inputs["reparam_noise"]), policy_dist=str(inputs.get("s_dist", "N")),
                       initial_logtemp=float(inputs["initial_logtemp"]),
                       actor_update_interval=int(inputs["sac_actor_step_update"]),
                       temp_update_interval=int(inputs["sac_temp_step_update"]),

@@ -16,6 +16,7 @@
 
 #include "learn_kernels.h"
 #include "rlmd_common.h"
+#include "rlmd_policy.h"
 
 namespace rlmd {
 namespace {
@@ -50,6 +51,7 @@ struct FusedActArgs {
   uint32_t tag, ctr;
   const float* eps_in;          // injected noise [n, A] (nullable)
   float max_action, ls_min, ls_max, noise_std;
+  int32_t dist;  // SAC sampler (rlmd_policy.h)
 };
 
 template <int H1>
@@ -164,26 +166,17 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
         ls_raw = a.params[o.b4 + j];
         for (int w = 0; w < 4; ++w) ls_raw += part[(w * kRows + r) * 2 * kMaxA + A + j];
       }
-      float eps = 0.f;
-      if (a.mode == 0) {
-        if (a.eps_in) {
-          eps = a.eps_in[(int64_t)b * A + j];
-        } else {
-          double z0, z1;
-          rlmd_normal2(rlmd_philox(a.seed, (uint32_t)b, a.ctr, a.tag, (uint32_t)(j >> 1)), z0, z1);
-          eps = (float)((j & 1) ? z1 : z0);
-        }
-      }
+      float noise = 0.f;
+      if (a.mode == 0)
+        noise = a.eps_in ? a.eps_in[(int64_t)b * A + j]
+                         : policy_draw(a.algo == RLMD_SAC ? a.dist : RLMD_DIST_N, a.seed, (uint32_t)b, a.ctr, a.tag, j);
       float act;
       if (a.algo == RLMD_SAC) {
-        const float ls = fminf(fmaxf(ls_raw, a.ls_min), a.ls_max);
-        float sigma = expf(ls);
-        if (!isfinite(mu)) mu = 0.f;
-        if (!isfinite(sigma)) sigma = 3.f;
-        act = a.mode == 1 ? tanhf(mu) * a.max_action : tanhf(mu + eps * sigma) * a.max_action;
+        const PolicyComp pc = policy_comp(a.dist, mu, ls_raw, noise, a.ls_min, a.ls_max);
+        act = tanhf(a.mode == 1 ? pc.mu : pc.u) * a.max_action;
       } else {
         act = tanhf(mu) * a.max_action;
-        if (a.mode == 0) act = fminf(fmaxf(act + eps * a.noise_std, -a.max_action), a.max_action);
+        if (a.mode == 0) act = fminf(fmaxf(act + noise * a.noise_std, -a.max_action), a.max_action);
       }
       a.actions[(int64_t)b * A + j] = act;
     }
@@ -223,6 +216,7 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
   a.ls_min = c.log_scale_min;
   a.ls_max = c.log_scale_max;
   a.noise_std = c.policy_noise;
+  a.dist = c.policy_dist;
   const dim3 grid((unsigned)((n + kRows - 1) / kRows));
   const size_t lds_bytes = (size_t)kRows * (c.h1 + 8) * 2 + 4 * kRows * 2 * kMaxA * 4 +
                            ((size_t)c.h1 * c.state_dim + c.h1 + kRows * c.state_dim) * 4;

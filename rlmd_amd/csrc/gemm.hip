@@ -82,27 +82,59 @@ __device__ __forceinline__ float store_c(const rlmd::GemmProblem& p, const rlmd:
 
 
 // Register stage of one (A, B) tile pair: issue all global loads of a K-step.
+// BWD_W operands are both [K rows][cols] with cols contiguous: each thread takes
+// groups of 4 adjacent columns of one row, read as one 16-B buffer load when the
+// operand's pitch, width and base allow it (4x fewer memory instructions), else
+// as 4 dword loads.  FWD / BWD_X keep one element per load.
 template <int MODE, int BM, int BK>
 struct TileRegs {
   static constexpr int BN = BM;
   static constexpr int kPerThread = (BM * BK) / 256;  // elements of each operand tile per thread
+  static constexpr int kG = BM / 4;                   // BWD_W: 4-column groups per K row
   float a[kPerThread], b[kPerThread];
+
+  // BWD_W: 4 adjacent elements (row gr, columns gc .. gc+3) of a [K][ncols] operand
+  __device__ __forceinline__ static void load4(__amdgpu_buffer_rsrc_t rs, bool vec, int ld, int ncols, int gr,
+                                               int gc, bool row_ok, float* out) {
+    if (vec) {
+      const bool ok = row_ok && gc < ncols;  // ncols % 4 == 0: the group is all in or all out
+      const f32x4 v = __builtin_bit_cast(
+          f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (gr * ld + gc) * 4 : kOutOfRange, 0, 0));
+      out[0] = v[0];
+      out[1] = v[1];
+      out[2] = v[2];
+      out[3] = v[3];
+    } else {
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        out[c] = buf_load(rs, (row_ok && gc + c < ncols) ? (gr * ld + gc + c) * 4 : kOutOfRange);
+    }
+  }
 
   __device__ __forceinline__ void load(const rlmd::GemmProblem& p, const rlmd::GemmShape& s,
                                        __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb, int i0,
                                        int j0, int r0, int r_end) {
     const int tid = threadIdx.x;
+    if constexpr (MODE == rlmd::GEMM_BWD_W) {
+      const bool va = (p.lda & 3) == 0 && (s.M & 3) == 0 && ((uintptr_t)p.A & 15) == 0;
+      const bool vb = (p.ldb & 3) == 0 && (s.N & 3) == 0 && ((uintptr_t)p.B & 15) == 0;
+#pragma unroll
+      for (int e = 0; e < kPerThread / 4; ++e) {
+        const int g = e * 256 + tid, c4 = (g % kG) * 4, rr = g / kG;
+        const int gr = r0 + rr;
+        load4(ra, va, p.lda, s.M, gr, i0 + c4, gr < r_end, &a[4 * e]);
+        load4(rb, vb, p.ldb, s.N, gr, j0 + c4, gr < r_end, &b[4 * e]);
+        if (p.bias_grad)  // ones column -> db
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            if (j0 + c4 + c == s.N && gr < r_end) b[4 * e + c] = 1.f;
+      }
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < kPerThread; ++e) {
       const int idx = e * 256 + tid;
-      int ii, rr;
-      if (MODE == rlmd::GEMM_BWD_W) {  // A element (i, r) at A[r*lda + i]: i fastest
-        ii = idx % BM;
-        rr = idx / BM;
-      } else {
-        rr = idx % BK;
-        ii = idx / BK;
-      }
+      const int rr = idx % BK, ii = idx / BK;
       const int gi = i0 + ii, gr = r0 + rr;
       const bool ok = gi < s.M && gr < r_end;
       a[e] = buf_load(ra, ok ? (int)(a_off<MODE>(p, gi, gr) * 4) : kOutOfRange);
@@ -120,20 +152,34 @@ struct TileRegs {
       }
       const int gj = j0 + jj, gr = r0 + rr;
       const bool ok = gj < s.N && gr < r_end;
-      float v = buf_load(rb, ok ? (int)(b_off<MODE>(p, gr, gj) * 4) : kOutOfRange);
-      if (MODE == rlmd::GEMM_BWD_W && p.bias_grad) v = (gj == s.N && gr < r_end) ? 1.f : v;  // ones column -> db
-      b[e] = v;
+      b[e] = buf_load(rb, ok ? (int)(b_off<MODE>(p, gr, gj) * 4) : kOutOfRange);
     }
   }
 
   template <typename T, int LD>
   __device__ __forceinline__ void store(T (*As)[LD], T (*Bs)[LD]) const {
     const int tid = threadIdx.x;
+    if constexpr (MODE == rlmd::GEMM_BWD_W) {
+#pragma unroll
+      for (int e = 0; e < kPerThread / 4; ++e) {
+        const int g = e * 256 + tid, c4 = (g % kG) * 4, rr = g / kG;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if constexpr (sizeof(T) == 4) {
+            As[c4 + c][rr] = a[4 * e + c];
+            Bs[c4 + c][rr] = b[4 * e + c];
+          } else {
+            As[c4 + c][rr] = f2bf(a[4 * e + c]);
+            Bs[c4 + c][rr] = f2bf(b[4 * e + c]);
+          }
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int e = 0; e < kPerThread; ++e) {
       const int idx = e * 256 + tid;
-      const int ii = MODE == rlmd::GEMM_BWD_W ? idx % BM : idx / BK;
-      const int rr = MODE == rlmd::GEMM_BWD_W ? idx / BM : idx % BK;
+      const int ii = idx / BK, rr = idx % BK;
       if constexpr (sizeof(T) == 4) As[ii][rr] = a[e];
       else As[ii][rr] = f2bf(a[e]);
     }
@@ -152,31 +198,43 @@ template <int PREC, int MODE, int BM, int BK>
 __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
   constexpr int BN = BM;
   constexpr int MB = BM / 32;  // 16x16 MFMA blocks per wave per dimension (waves are 2 x 2)
-  const int split = blockIdx.z;
   int pi = 0;
   while (pi + 1 < batch.nprob && (int)blockIdx.x >= batch.tile_begin[pi + 1]) ++pi;
   rlmd::GemmProblem p = batch.prob[pi];
   const rlmd::GemmShape s = batch.shape[pi];
   const int tile = (int)blockIdx.x - batch.tile_begin[pi];
   const int tile_x = tile % batch.tiles_n[pi], tile_y = tile / batch.tiles_n[pi];
-  // split-K (weight gradients): split `split` reduces rows [r_beg, r_end) of the
-  // batch and writes its own partial slab; the optimiser sums the slabs in order
+  // split-K (weight gradients): split `sp` reduces rows [sp*chunk, min(K, (sp+1)*chunk))
+  // of the batch.  Unfused: blockIdx.z is the split and writes its own partial
+  // slab (the optimiser sums the slabs in order).  Fused: the block runs every
+  // split in order, keeping each split's sum in its own accumulator and adding
+  // them slab by slab, as the optimiser would.
+  const bool fused = MODE == rlmd::GEMM_BWD_W && batch.fuse_adam;
   const int chunk = (s.K + batch.splits - 1) / batch.splits;
-  const int r_beg = split * chunk, r_end = min(s.K, r_beg + chunk);
-  if (split) {
-    p.C += (int64_t)split * batch.split_stride;
-    if (p.bias_grad) p.bias_grad += (int64_t)split * batch.split_stride;
+  const int sp0 = fused ? 0 : (int)blockIdx.z, nsp = fused ? batch.splits : 1;
+  if (!fused && sp0) {
+    p.C += (int64_t)sp0 * batch.split_stride;
+    if (p.bias_grad) p.bias_grad += (int64_t)sp0 * batch.split_stride;
   }
   const int i0 = tile_y * BM, j0 = tile_x * BN;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wr = wave >> 1, wc = wave & 1;
-  f32x4 acc[MB][MB];
+  f32x4 acc[MB][MB], tot[MB][MB];
 #pragma unroll
   for (int a = 0; a < MB; ++a)
 #pragma unroll
-    for (int b = 0; b < MB; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < MB; ++b) acc[a][b] = tot[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = r_end > r_beg ? (r_end - r_beg + BK - 1) / BK : 0;
+  // K-steps per split (every split gets the same count; steps past a split's
+  // end read zeros through the range check and add exact zeros)
+  const int nkc = (chunk + BK - 1) / BK;
+  const int nq = s.K > 0 ? nsp * nkc : 0;
+  auto step_rows = [&](int q, int& r0, int& r1) {
+    const int sp = sp0 + q / nkc, t = q % nkc;
+    const int rb = sp * chunk;
+    r0 = rb + t * BK;
+    r1 = min(s.K, rb + chunk);
+  };
   // operand extents in bytes (range-checked buffer resources)
   const int64_t a_rows = MODE == rlmd::GEMM_BWD_W ? s.K : s.M;
   const int64_t a_cols = MODE == rlmd::GEMM_BWD_W ? s.M : s.K;
@@ -186,17 +244,69 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
       (void*)p.A, (short)0, (int)(((a_rows - 1) * p.lda + a_cols) * 4), 0x00020000);
   const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
       (void*)p.B, (short)0, (int)(((b_rows - 1) * p.ldb + b_cols) * 4), 0x00020000);
-  TileRegs<MODE, BM, BK> regs;
-  if (nk) regs.load(p, s, ra, rb, i0, j0, r_beg, r_end);
+  // K-steps in flight: D register stages.  One: every split-K workgroup has a
+  // single K-step at B <= 512, and a deeper ring (4: a fused tile's whole
+  // reduction at once) doubles the VGPRs and halves the resident waves.
+  constexpr int D = 1;
+  TileRegs<MODE, BM, BK> regs[D];
+#pragma unroll
+  for (int u = 0; u < D; ++u)
+    if (u < nq) {
+      int r0, r1;
+      step_rows(u, r0, r1);
+      regs[u].load(p, s, ra, rb, i0, j0, r0, r1);
+    }
   const int row0 = MB * 16 * wr, col0 = MB * 16 * wc;
+  // fused optimiser: this thread's parameters and their state, loaded now
+  int pidx[MB][MB][4];
+  rlmd::AdamIn ain[MB][MB][4];
+  bool polyak = false;
+  if constexpr (MODE == rlmd::GEMM_BWD_W) {
+    if (fused) {
+      const rlmd::AdamArgs& ad = batch.adam;
+      polyak = rlmd::adam_polyak(ad);
+      const int offc = (int)(p.C - ad.g), offb = p.bias_grad ? (int)(p.bias_grad - ad.g) : 0;
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MB; ++ni)
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            const int i = i0 + row0 + 16 * mi + 4 * (lane >> 4) + rg;
+            const int j = j0 + col0 + 16 * ni + (lane & 15);
+            pidx[mi][ni][rg] = (i < s.M && j < s.N) ? offc + i * p.ldc + j
+                                                    : ((i < s.M && j == s.N && p.bias_grad) ? offb + i : -1);
+            ain[mi][ni][rg] = rlmd::adam_load(ad, pidx[mi][ni][rg], polyak);
+          }
+    }
+  }
+  // end of K-step q: fold the split's accumulator into the total when its last step is done
+  auto close_step = [&](int q) {
+    if (q % nkc != nkc - 1) return;
+#pragma unroll
+    for (int a = 0; a < MB; ++a)
+#pragma unroll
+      for (int b = 0; b < MB; ++b) {
+        tot[a][b] = q == nkc - 1 ? acc[a][b] : tot[a][b] + acc[a][b];
+        acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+  };
   if constexpr (PREC == RLMD_FP32) {
     __shared__ float As[BM][BK + PAD_F32];
     __shared__ float Bs[BN][BK + PAD_F32];
-    for (int t = 0; t < nk; ++t) {
+    for (int q0 = 0; q0 < nq; q0 += D)
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int q = q0 + u;
+      if (q >= nq) break;
       __syncthreads();
-      regs.store(As, Bs);
+      regs[u].store(As, Bs);
       __syncthreads();
-      if (t + 1 < nk) regs.load(p, s, ra, rb, i0, j0, r_beg + (t + 1) * BK, r_end);  // next K-step in flight
+      if (q + D < nq) {  // the stage refills D steps ahead
+        int r0, r1;
+        step_rows(q + D, r0, r1);
+        regs[u].load(p, s, ra, rb, i0, j0, r0, r1);
+      }
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 4) {
         const int kr = kk + (lane >> 4);
@@ -212,15 +322,24 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
           for (int n = 0; n < MB; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[m], bv[n], acc[m][n], 0, 0, 0);
       }
+      close_step(q);
     }
   } else {
     __shared__ __attribute__((aligned(16))) unsigned short As[BM][BK + PAD_BF];
     __shared__ __attribute__((aligned(16))) unsigned short Bs[BN][BK + PAD_BF];
-    for (int t = 0; t < nk; ++t) {
+    for (int q0 = 0; q0 < nq; q0 += D)
+#pragma unroll
+    for (int u = 0; u < D; ++u) {
+      const int q = q0 + u;
+      if (q >= nq) break;
       __syncthreads();
-      regs.store(As, Bs);
+      regs[u].store(As, Bs);
       __syncthreads();
-      if (t + 1 < nk) regs.load(p, s, ra, rb, i0, j0, r_beg + (t + 1) * BK, r_end);
+      if (q + D < nq) {
+        int r0, r1;
+        step_rows(q + D, r0, r1);
+        regs[u].load(p, s, ra, rb, i0, j0, r0, r1);
+      }
 #pragma unroll
       for (int kk = 0; kk < BK; kk += 32) {
         const int kr = kk + 8 * (lane >> 4);
@@ -236,8 +355,30 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
           for (int n = 0; n < MB; ++n)
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[m], bv[n], acc[m][n], 0, 0, 0);
       }
+      close_step(q);
     }
   }
+  if constexpr (MODE == rlmd::GEMM_BWD_W) {
+    if (fused) {
+      // optimiser epilogue: this block's dW elements (and db when the tile holds
+      // the ones column), then the per-step scalars once
+      const rlmd::AdamArgs& ad = batch.adam;
+#pragma unroll
+      for (int mi = 0; mi < MB; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < MB; ++ni)
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg)
+            if (pidx[mi][ni][rg] >= 0)
+              rlmd::adam_apply(ad, pidx[mi][ni][rg], tot[mi][ni][rg], ain[mi][ni][rg], polyak);
+      if (blockIdx.x == 0 && threadIdx.x == 0) rlmd::adam_scalar_step(ad);
+      return;
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < MB; ++a)
+#pragma unroll
+    for (int b = 0; b < MB; ++b) acc[a][b] = tot[a][b];
   // C/D map (16x16 MFMA, every dtype): col = lane & 15, row = 4*(lane >> 4) + reg
   __amdgpu_buffer_rsrc_t rx = ra;
   if (MODE == rlmd::GEMM_FWD && p.bias)
@@ -287,6 +428,7 @@ int gemm_launch(int prec, int mode, const GemmBatch& b_in, hipStream_t stream) {
   GemmBatch b = b_in;
   if (b.splits < 1) b.splits = 1;
   RLMD_CHECK(mode == GEMM_BWD_W || b.splits == 1, "split-K only for weight gradients");
+  RLMD_CHECK(mode == GEMM_BWD_W || !b.fuse_adam, "the optimiser epilogue is for weight gradients");
   bool big = false;
   for (int i = 0; i < b.nprob; ++i) big = big || b.shape[i].M > 1024;
   const int T = big ? 64 : 32;
@@ -301,7 +443,7 @@ int gemm_launch(int prec, int mode, const GemmBatch& b_in, hipStream_t stream) {
   }
   b.tile_begin[b.nprob] = tiles;
   if (tiles == 0) return 0;
-  dim3 grid(tiles, 1, b.splits);
+  dim3 grid(tiles, 1, b.fuse_adam ? 1 : b.splits);
 #define RLMD_GEMM_CASE(P, M)                                                                  \
   if (prec == P && mode == M) {                                                               \
     if (big) hipLaunchKernelGGL((gemm_kernel<P, M, 64, 64>), grid, dim3(256), 0, stream, b);  \

@@ -21,12 +21,13 @@
 #include "learn_kernels.h"
 #include "rlmd_block.h"
 #include "rlmd_loss.h"
+#include "rlmd_policy.h"
+#include "rlmd_adam.h"
 #include "rlmd_gemm.h"
 
 namespace rlmd {
 namespace {
 
-constexpr float kLog2Pi_half = 0.91893853320467274178f;  // log(sqrt(2*pi))
 
 // ---------------------------------------------------------------------------
 // actor heads + policy sampling (networks_sac.py:101-178, :268-285;
@@ -42,7 +43,7 @@ __global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
   const uint32_t c1 = h.ctr ? (uint32_t)*h.ctr : h.ctr_host;
   if (h.xsa)
     for (int k = lane; k < h.S; k += 64) h.xsa[(int64_t)b * (h.S + A) + k] = h.state[(int64_t)b * h.S + k];
-  float logp = 0.f;
+  float lp_sum = 0.f, m2_sum = 0.f, hld_sum = 0.f, jac_sum = 0.f;
   for (int j = 0; j < A; ++j) {
     float dm = 0.f, dl = 0.f;
     const float* wm = h.params + o.w3 + (int64_t)j * H;
@@ -55,41 +56,32 @@ __global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
     dm = wave_sum(dm);
     if (h.algo == RLMD_SAC) dl = wave_sum(dl);
     if (lane != 0) continue;
-    float mu = dm + h.params[o.b3 + j];
+    const float mu = dm + h.params[o.b3 + j];
     float a;
-    float eps = 0.f;
+    float noise = 0.f;
     if (h.mode == 0 || h.algo == RLMD_TD3) {
-      if (h.eps_in) {
-        eps = h.eps_in[(int64_t)b * A + j];
-      } else if (h.mode == 0) {
-        double z0, z1;
-        rlmd_normal2(rlmd_philox(h.seed, (uint32_t)b, c1, h.tag, (uint32_t)(j >> 1)), z0, z1);
-        eps = (float)((j & 1) ? z1 : z0);
-      }
+      if (h.eps_in) noise = h.eps_in[(int64_t)b * A + j];
+      else if (h.mode == 0)
+        noise = policy_draw(h.algo == RLMD_SAC ? h.dist : RLMD_DIST_N, h.seed, (uint32_t)b, c1, h.tag, j);
     }
     if (h.algo == RLMD_SAC) {
       const float ls_raw = dl + h.params[o.b4 + j];
-      const float ls = fminf(fmaxf(ls_raw, h.ls_min), h.ls_max);
-      float sigma = expf(ls);
-      // NaN scrub (networks_sac.py:131-134), applied per element
-      if (!isfinite(mu)) mu = 0.f;
-      if (!isfinite(sigma)) sigma = 3.f;
+      const PolicyComp pc = policy_comp(h.dist, mu, ls_raw, noise, h.ls_min, h.ls_max);
       if (h.mode == 1) {
-        a = tanhf(mu) * h.max_action;
+        a = tanhf(pc.mu) * h.max_action;
       } else {
-        const float u = mu + eps * sigma;
-        const float d = u - mu;
-        const float lpn = -(d * d) / (2.f * (sigma * sigma)) - logf(sigma) - kLog2Pi_half;
-        const float t = tanhf(u);
-        a = t * h.max_action;
+        a = tanhf(pc.u) * h.max_action;
         const float an = a / h.max_action;
-        logp += lpn - logf(1.f - an * an + h.reparam_noise);
+        lp_sum += pc.lp;
+        m2_sum += pc.m2;
+        hld_sum += pc.hld;
+        jac_sum += logf(1.f - an * an + h.reparam_noise);
         if (h.save) {
           float* sv = h.save + (int64_t)b * 5 * A;
-          sv[j] = mu;
-          sv[A + j] = sigma;
-          sv[2 * A + j] = eps;
-          sv[3 * A + j] = u;
+          sv[j] = pc.mu;
+          sv[A + j] = pc.sigma;
+          sv[2 * A + j] = pc.c;
+          sv[3 * A + j] = pc.u;
           sv[4 * A + j] = ls_raw;
         }
       }
@@ -97,7 +89,7 @@ __global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
       const float t = tanhf(mu);
       a = t * h.max_action;
       if (h.mode == 0) {
-        float nz = eps * h.noise_std;
+        float nz = noise * h.noise_std;
         if (h.clamp_noise) nz = fminf(fmaxf(nz, -h.noise_clip), h.noise_clip);
         a = fminf(fmaxf(a + nz, -h.max_action), h.max_action);
       }
@@ -106,7 +98,7 @@ __global__ void __launch_bounds__(256) actor_head_kernel(HeadArgs h) {
     if (h.actions) h.actions[(int64_t)b * A + j] = a;
     if (h.xsa) h.xsa[(int64_t)b * (h.S + A) + h.S + j] = a;
   }
-  if (lane == 0 && h.logp) h.logp[b] = logp;
+  if (lane == 0 && h.logp) h.logp[b] = policy_logp(h.dist, A, lp_sum, m2_sum, hld_sum, jac_sum);
 }
 
 // ---------------------------------------------------------------------------
@@ -197,105 +189,6 @@ __global__ void __launch_bounds__(NTH) actor_loss_kernel(ActorLossArgs a) {
     a.stats[10] = loss;
   }
 }
-
-// ---------------------------------------------------------------------------
-// Adam (torch.optim.Adam defaults, _single_tensor_adam) + optional Polyak
-// target update (algo_sac.py:597-615) + optional temperature Adam.
-// ---------------------------------------------------------------------------
-struct AdamArgs {
-  float* p;
-  const float* g;          // RLMD_GRAD_SPLITS partial-gradient slabs, split_stride apart
-  int64_t split_stride;
-  float* m;
-  float* v;
-  float* target;  // Polyak target (nullable)
-  int64_t n;
-  float lr, tau;
-  int32_t cnt;             // learn_step_cntr of this update (written back to LearnState)
-  int32_t interval;        // Adam step count t = learn_cntr / interval
-  float step_size, bc2_sqrt;            // lr / (1 - b1^t), sqrt(1 - b2^t): host-side, as torch's Python floats
-  float temp_step_size, temp_bc2_sqrt;  // the same for the temperature step
-  int32_t polyak_interval; // Polyak when learn_cntr % polyak_interval == 0 (0 = never)
-  LearnState* st;
-  int32_t temp;            // thread 0 also steps log_alpha (SAC)
-  float lr_temp;
-  int32_t temp_interval;
-  float* stats;
-  // compute copies of fc2.weight (rows.hip RowNet) refreshed for the updated
-  // nets: net = i / net_size (ncopy nets), element (n, k) of its fc2.weight
-  int32_t ncopy, bf16;
-  int64_t net_size, w2_off;
-  int32_t H1, H2, H1p, H2p;
-  void* wc[2];
-  void* wt[2];
-  void* twc[2];  // Polyak targets' copies (nullable)
-  void* twt[2];
-};
-
-__device__ __forceinline__ void store_copy(void* base, int64_t i, float v, int bf16) {
-  if (bf16) {
-    unsigned u = __float_as_uint(v);
-    u += 0x7fffu + ((u >> 16) & 1u);  // RNE (finite weights)
-    static_cast<unsigned short*>(base)[i] = (unsigned short)(u >> 16);
-  } else {
-    static_cast<float*>(base)[i] = v;
-  }
-}
-
-__global__ void __launch_bounds__(256) adam_kernel(AdamArgs a) {
-  const int cnt = a.cnt;
-  if (blockIdx.x == 0 && threadIdx.x == 0) a.st->learn_cntr = cnt;
-  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
-  const float step_size = a.step_size, bc2_sqrt = a.bc2_sqrt;
-  const bool polyak = a.target && a.polyak_interval > 0 && (cnt % a.polyak_interval) == 0;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n;
-       i += (int64_t)gridDim.x * blockDim.x) {
-    float g = a.g[i];
-#pragma unroll
-    for (int sp = 1; sp < RLMD_GRAD_SPLITS; ++sp) g += a.g[i + sp * a.split_stride];
-    float m = a.m[i], v = a.v[i];
-    m = m + (1.f - b1) * (g - m);
-    v = v * b2 + (1.f - b2) * g * g;
-    a.m[i] = m;
-    a.v[i] = v;
-    const float denom = sqrtf(v) / bc2_sqrt + eps;
-    const float p = a.p[i] - step_size * (m / denom);
-    a.p[i] = p;
-    float tv = 0.f;
-    if (polyak) {
-      tv = a.tau * p + (1.f - a.tau) * a.target[i];
-      a.target[i] = tv;
-    }
-    if (a.ncopy) {
-      const int i32 = (int)i, ns = (int)a.net_size;
-      const int net = i32 / ns;
-      const int j = i32 - net * ns - (int)a.w2_off;
-      if (net < a.ncopy && j >= 0 && j < a.H1 * a.H2) {
-        const int n = j / a.H1, k = j - n * a.H1;
-        store_copy(a.wc[net], (int64_t)n * a.H1p + k, p, a.bf16);
-        store_copy(a.wt[net], (int64_t)k * a.H2p + n, p, a.bf16);
-        if (polyak && a.twc[net]) {
-          store_copy(a.twc[net], (int64_t)n * a.H1p + k, tv, a.bf16);
-          store_copy(a.twt[net], (int64_t)k * a.H2p + n, tv, a.bf16);
-        }
-      }
-    }
-  }
-  if (a.temp && blockIdx.x == 0 && threadIdx.x == 0) {
-    LearnState* st = a.st;
-    if (cnt % a.temp_interval == 0) {
-      const float g = st->pad_temp_grad;
-      float m = st->temp_m + (1.f - b1) * (g - st->temp_m);
-      float v = st->temp_v * b2 + (1.f - b2) * g * g;
-      st->temp_m = m;
-      st->temp_v = v;
-      const float denom = sqrtf(v) / a.temp_bc2_sqrt + eps;
-      st->log_alpha = st->log_alpha - a.temp_step_size * (m / denom);
-    }
-    if (a.stats) a.stats[11] = st->log_alpha;
-  }
-}
-
 
 }  // namespace
 }  // namespace rlmd
@@ -408,11 +301,6 @@ void add_bwd_w(GemmBatch& b, int M, int N, int K, const float* G, int ldg, const
   gemm_add(b, {M, N, K, 0}, {G, ldg, X, ldx, nullptr, DW, N, nullptr, 0, DB, nullptr, nullptr});
 }
 
-int launch_bwd_w(rlmd_agent_s* ag, GemmBatch& b, hipStream_t s) {
-  b.splits = RLMD_GRAD_SPLITS;  // batch reduction split 4 ways; Adam sums the slabs
-  b.split_stride = ag->n_params;
-  return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, s);
-}
 
 #define RLMD_TRY(x)         \
   do {                      \
@@ -436,6 +324,7 @@ HeadArgs head_args(rlmd_agent_s* ag, const float* params, const float* h2, const
   h.ls_min = c.log_scale_min;
   h.ls_max = c.log_scale_max;
   h.reparam_noise = c.reparam_noise;
+  h.dist = c.policy_dist;
   return h;
 }
 
@@ -453,13 +342,43 @@ void adam_scalars(double lr, int t, float& step_size, float& bc2_sqrt) {
   bc2_sqrt = (float)sqrt(bc2);
 }
 
-int adam_launch(const AdamArgs& a_in, hipStream_t s) {
-  AdamArgs a = a_in;
+// Adam over the nets of one phase: sums the RLMD_GRAD_SPLITS weight-gradient
+// slabs in slab order, then steps, Polyak-averages and refreshes the compute
+// copies (rlmd_adam.h).  Block 0 also steps the temperature.
+__global__ void __launch_bounds__(256) adam_kernel(AdamArgs a, int64_t split_stride) {
+  const bool polyak = adam_polyak(a);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < (int)a.n; i += gridDim.x * blockDim.x) {
+    const AdamIn in = adam_load(a, i, polyak);
+    float g = a.g[i];
+#pragma unroll
+    for (int sp = 1; sp < RLMD_GRAD_SPLITS; ++sp) g += a.g[i + sp * split_stride];
+    adam_apply(a, i, g, in, polyak);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) adam_scalar_step(a);
+}
+
+// Weight gradients of one phase, then the optimiser step.  Two launches: the
+// split-K GEMM writes RLMD_GRAD_SPLITS slabs over 4x the workgroups, and
+// adam_kernel reduces them.  (Folding the reduction and Adam into the GEMM's
+// epilogue, GemmBatch::fuse_adam, runs each tile's splits serially in one
+// workgroup and measured slower at these sizes: 18.3 vs 8.4 + 6.4 us.)
+int launch_bwd_w_adam(rlmd_agent_s* ag, GemmBatch& b, const AdamArgs& ad_in, hipStream_t s) {
+  b.splits = RLMD_GRAD_SPLITS;
+  b.split_stride = ag->n_params;
+  AdamArgs a = ad_in;
   adam_scalars(a.lr, a.cnt / a.interval, a.step_size, a.bc2_sqrt);
   if (a.temp && a.cnt % a.temp_interval == 0)
     adam_scalars(a.lr_temp, a.cnt / a.temp_interval, a.temp_step_size, a.temp_bc2_sqrt);
+  constexpr bool kFuse = false;
+  if (kFuse) {
+    b.fuse_adam = 1;
+    b.adam = a;
+    return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, s);
+  }
+  RLMD_TRY(gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, s));
   const int64_t blocks = std::min<int64_t>((a.n + 255) / 256, 1024);
-  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(adam_kernel, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, a,
+                     (int64_t)ag->n_params);
   RLMD_LAUNCH_CHECK();
   return 0;
 }
@@ -551,7 +470,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
   const int nq = sac ? 2 : 1;
   const RowDims d = row_dims(ag);
   const SampleCfg smp{c.seed, (uint32_t)cntr, c.max_action, c.log_scale_min, c.log_scale_max,
-                      c.reparam_noise};
+                      c.reparam_noise, c.algo == RLMD_SAC ? c.policy_dist : RLMD_DIST_N};
   float* Pc[2] = {P + ag->off_c[0], P + ag->off_c[1]};
   float* Tc[2] = {T + ag->off_c[0], T + ag->off_c[1]};
   float* Gc[2] = {G + ag->off_c[0], G + ag->off_c[1]};
@@ -669,11 +588,9 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       add_bwd_w(gb, H2, H1, B, S_.dc2[g], H2, S_.c1[g], H1, Gc[g] + co.w2, Gc[g] + co.b2);
       add_bwd_w(gb, H1, X, B, S_.dc1[g], H1, mb.xsa, X, Gc[g] + co.w1, Gc[g] + co.b1);
     }
-    RLMD_TRY(launch_bwd_w(ag, gb, st));
     AdamArgs ad{};
     ad.p = Pc[0];
     ad.g = Gc[0];
-    ad.split_stride = ag->n_params;
     ad.m = ag->m + ag->off_c[0];
     ad.v = ag->v + ag->off_c[0];
     ad.target = Tc[0];
@@ -685,7 +602,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     ad.polyak_interval = c.target_critic_update;
     ad.st = ag->st;
     adam_copies(ag, ad, co, SLOT_C0, 2, true);
-    RLMD_TRY(adam_launch(ad, st));
+    RLMD_TRY(launch_bwd_w_adam(ag, gb, ad, st));
   }
   // ---- actor (+ temperature) update every actor_update_interval
   if (!actor_step) return 0;
@@ -759,11 +676,9 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     if (sac) add_bwd_w(gb, A, H2, B, S_.gh + A, 2 * A, S_.h2, H2, Ga + ao.w4, Ga + ao.b4);
     add_bwd_w(gb, H2, H1, B, S_.dh2, H2, S_.h1, H1, Ga + ao.w2, Ga + ao.b2);
     add_bwd_w(gb, H1, S, B, S_.dh1, H1, mb.s, S, Ga + ao.w1, Ga + ao.b1);
-    RLMD_TRY(launch_bwd_w(ag, gb, st));
     AdamArgs ad{};
     ad.p = P + ag->off_actor;
     ad.g = Ga;
-    ad.split_stride = ag->n_params;
     ad.m = ag->m + ag->off_actor;
     ad.v = ag->v + ag->off_actor;
     ad.target = sac ? nullptr : T + ag->off_actor;
@@ -779,7 +694,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     ad.temp_interval = c.temp_update_interval;
     ad.stats = stats;
     adam_copies(ag, ad, ao, SLOT_ACTOR, 1, !sac);
-    RLMD_TRY(adam_launch(ad, st));
+    RLMD_TRY(launch_bwd_w_adam(ag, gb, ad, st));
   }
   return 0;
 }

@@ -38,7 +38,7 @@ struct HeadArgs {
   float* xsa;           // [n, S+A] critic input (nullable)
   float* actions;       // [n, A] (nullable)
   float* logp;          // [n] (nullable)
-  float* save;          // [n, 5A]: mu, sigma, eps, u, ls_raw for backward (nullable)
+  float* save;          // [n, 5A]: mu, sigma, noise multiplier c, u, ls_raw for backward (nullable)
   const float* eps_in;  // injected eps [n, A] (nullable -> Philox)
   uint64_t seed;
   uint32_t tag;         // Philox tag for the eps draws
@@ -48,6 +48,7 @@ struct HeadArgs {
   float max_action, ls_min, ls_max, reparam_noise;
   float noise_std, noise_clip;  // TD3: policy / target smoothing noise (already x max_action)
   int32_t clamp_noise;          // TD3 target: clip noise to +-noise_clip
+  int32_t dist;                 // SAC sampler, RLMD_DIST_*
 };
 
 // ---------------------------------------------------------------------------
@@ -80,6 +81,7 @@ struct SampleCfg {
   uint64_t seed;
   uint32_t ctr;  // Philox c1 = learn_step_cntr of this update
   float max_action, ls_min, ls_max, reparam_noise;
+  int32_t dist;  // RLMD_DIST_* (rlmd_policy.h)
 };
 
 // Phase 1 of an update: y = 0 target path (policy on s2 -> sample -> both target

@@ -1,0 +1,138 @@
+// rlmd_adam.h — the optimiser step as per-element device code, applied in the
+// epilogue of the weight-gradient GEMM (gemm.hip): the workgroup that owns an
+// output tile of dW / db has the whole mini-batch reduction in registers and
+// steps those parameters in place.
+//
+// Restates torch.optim.Adam defaults (_single_tensor_adam: betas .9/.999,
+// eps 1e-8, bias corrections from Python floats), the Polyak target update
+// (algo_sac.py:597-615 / algo_td3.py:533-563) and the SAC temperature step
+// (algo_sac.py:580-595), plus the bf16/f32 compute copies of fc2.weight that
+// the row kernels read (rows.hip RowNet: wc [H2p][H1p], wt [H1p][H2p]).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "learn_kernels.h"
+
+namespace rlmd {
+
+struct AdamArgs {
+  float* p;        // parameters of the stepped nets (index 0 = first element)
+  const float* g;  // gradient slab 0 at the same index (locates GEMM outputs)
+  float* m;
+  float* v;
+  float* target;  // Polyak target (nullable)
+  int64_t n;
+  float lr, tau;
+  int32_t cnt;             // learn_step_cntr of this update (written back to LearnState)
+  int32_t interval;        // Adam step count t = learn_cntr / interval
+  float step_size, bc2_sqrt;            // lr / (1 - b1^t), sqrt(1 - b2^t): host-side, as torch's Python floats
+  float temp_step_size, temp_bc2_sqrt;  // the same for the temperature step
+  int32_t polyak_interval; // Polyak when learn_cntr % polyak_interval == 0 (0 = never)
+  LearnState* st;
+  int32_t temp;            // also step log_alpha (SAC)
+  float lr_temp;
+  int32_t temp_interval;
+  float* stats;
+  // compute copies of fc2.weight (rows.hip RowNet) refreshed for the updated
+  // nets: net = i / net_size (ncopy nets), element (n, k) of its fc2.weight
+  int32_t ncopy, bf16;
+  int64_t net_size, w2_off;
+  int32_t H1, H2, H1p, H2p;
+  void* wc[2];
+  void* wt[2];
+  void* twc[2];  // Polyak targets' copies (nullable)
+  void* twt[2];
+};
+
+namespace {
+
+__device__ __forceinline__ void store_copy(void* base, int64_t i, float v, int bf16) {
+  if (bf16) {
+    unsigned u = __float_as_uint(v);
+    u += 0x7fffu + ((u >> 16) & 1u);  // RNE (finite weights)
+    static_cast<unsigned short*>(base)[i] = (unsigned short)(u >> 16);
+  } else {
+    static_cast<float*>(base)[i] = v;
+  }
+}
+
+__device__ __forceinline__ bool adam_polyak(const AdamArgs& a) {
+  return a.target && a.polyak_interval > 0 && (a.cnt % a.polyak_interval) == 0;
+}
+
+// One parameter's optimiser state, loaded ahead of its gradient (range-checked
+// buffer loads: an element index < 0 reads zeros and is never stored).
+struct AdamIn {
+  float m, v, p, t;
+};
+
+__device__ __forceinline__ AdamIn adam_load(const AdamArgs& a, int i, bool polyak) {
+  const int n4 = (int)(a.n * 4), off = i >= 0 ? i * 4 : 0x7fffffff;
+  AdamIn o;
+  o.m = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                     __builtin_amdgcn_make_buffer_rsrc(a.m, (short)0, n4, 0x00020000), off, 0, 0));
+  o.v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                     __builtin_amdgcn_make_buffer_rsrc(a.v, (short)0, n4, 0x00020000), off, 0, 0));
+  o.p = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                     __builtin_amdgcn_make_buffer_rsrc(a.p, (short)0, n4, 0x00020000), off, 0, 0));
+  o.t = polyak ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                               __builtin_amdgcn_make_buffer_rsrc(a.target, (short)0, n4, 0x00020000),
+                                               off, 0, 0))
+               : 0.f;
+  return o;
+}
+
+// One parameter: Adam with gradient g, then Polyak and the compute copies.
+__device__ __forceinline__ void adam_apply(const AdamArgs& a, int i, float g, const AdamIn& in, bool polyak) {
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+  float m = in.m, v = in.v;
+  m = m + (1.f - b1) * (g - m);
+  v = v * b2 + (1.f - b2) * g * g;
+  a.m[i] = m;
+  a.v[i] = v;
+  const float denom = sqrtf(v) / a.bc2_sqrt + eps;
+  const float p = in.p - a.step_size * (m / denom);
+  a.p[i] = p;
+  float tv = 0.f;
+  if (polyak) {
+    tv = a.tau * p + (1.f - a.tau) * in.t;
+    a.target[i] = tv;
+  }
+  if (a.ncopy) {
+    const int ns = (int)a.net_size;
+    const int net = i / ns;
+    const int j = i - net * ns - (int)a.w2_off;
+    if (net < a.ncopy && j >= 0 && j < a.H1 * a.H2) {
+      const int n = j / a.H1, k = j - n * a.H1;
+      store_copy(a.wc[net], (int64_t)n * a.H1p + k, p, a.bf16);
+      store_copy(a.wt[net], (int64_t)k * a.H2p + n, p, a.bf16);
+      if (polyak && a.twc[net]) {
+        store_copy(a.twc[net], (int64_t)n * a.H1p + k, tv, a.bf16);
+        store_copy(a.twt[net], (int64_t)k * a.H2p + n, tv, a.bf16);
+      }
+    }
+  }
+}
+
+// Once per step (one thread): the learner counter and the temperature Adam.
+__device__ __forceinline__ void adam_scalar_step(const AdamArgs& a) {
+  LearnState* st = a.st;
+  st->learn_cntr = a.cnt;
+  if (!a.temp) return;
+  if (a.cnt % a.temp_interval == 0) {
+    const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
+    const float g = st->pad_temp_grad;
+    const float m = st->temp_m + (1.f - b1) * (g - st->temp_m);
+    const float v = st->temp_v * b2 + (1.f - b2) * g * g;
+    st->temp_m = m;
+    st->temp_v = v;
+    const float denom = sqrtf(v) / a.temp_bc2_sqrt + eps;
+    st->log_alpha = st->log_alpha - a.temp_step_size * (m / denom);
+  }
+  if (a.stats) a.stats[11] = st->log_alpha;
+}
+
+}  // namespace
+}  // namespace rlmd

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/rlmd_abi.h"
+#include "rlmd_adam.h"
 
 #define RLMD_GEMM_MAX_PROBS 6
 
@@ -47,6 +48,12 @@ struct GemmBatch {
   int32_t tile_begin[RLMD_GEMM_MAX_PROBS + 1];  // set by gemm_launch
   int32_t splits;        // BWD_W split-K: slabs written at C + s*split_stride (and bias_grad)
   int64_t split_stride;  // floats between slabs
+  // BWD_W with fuse_adam: each workgroup reduces all `splits` slabs of its tile
+  // itself (same slab order and rounding as separate slabs summed by Adam) and
+  // steps the parameters it covers (rlmd_adam.h) instead of storing gradients.
+  // Parameter index = (C or bias_grad) - adam.g + element offset.
+  int32_t fuse_adam;
+  AdamArgs adam;
 };
 
 // Appends one problem; returns its index.

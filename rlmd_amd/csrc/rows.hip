@@ -11,7 +11,7 @@
 //             (L2-resident, shared by every workgroup); wave w owns output column
 //             blocks w, w + 8, ...
 //   heads     reduced from the MFMA accumulators (lane shuffles + one LDS pass)
-//   sampling  tanh-Gaussian / TD3 noise per row (networks_sac.py:101-178)
+//   sampling  tanh-squashed N / Laplace / MVN policy, TD3 noise per row (rlmd_policy.h)
 // Latency is the whole cost at these sizes (a few MFLOP per workgroup), so every
 // load that does not depend on computed data — both nets' fc2 fragments, biases,
 // head weights, fc1 rows, ReLU masks — is issued in ONE round at kernel start.
@@ -22,6 +22,7 @@
 #include "learn_kernels.h"
 #include "rlmd_block.h"
 #include "rlmd_loss.h"
+#include "rlmd_policy.h"
 #include "rlmd_common.h"
 
 namespace rlmd {
@@ -34,7 +35,6 @@ constexpr int NT = 512;       // threads per workgroup
 constexpr int NW = NT / 64;   // waves
 constexpr int NHF = 4;        // heads reduced in the MFMA epilogue (more -> LDS dot products)
 constexpr int W1P = 8;        // fc1 inputs preloaded per thread (more -> read in the loop)
-constexpr float kLogSqrt2Pi = 0.91893853320467274178f;
 constexpr int kHeadsMax = 2 * RLMD_MAX_ACTION;
 
 #ifdef RLMD_TIMING
@@ -415,48 +415,38 @@ __device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, 
   const int S = d.S, A = d.A, b = row0 + r;
   const bool valid = b < B, sac = d.algo == RLMD_SAC;
   const uint32_t c1 = smp.ctr;
-  float logp = 0.f;
+  float lp_sum = 0.f, m2_sum = 0.f, hld_sum = 0.f, jac_sum = 0.f;
   for (int j = 0; j < A; ++j) {
-    float mu = hout[r * kHeadsMax + j] + p[ao.b3 + j];
-    float eps = 0.f;
-    if (mode == 0 && valid) {
-      if (eps_in) {
-        eps = eps_in[(int64_t)b * A + j];
-      } else {
-        double z0, z1;
-        rlmd_normal2(rlmd_philox(smp.seed, (uint32_t)b, c1, (uint32_t)tag, (uint32_t)(j >> 1)), z0, z1);
-        eps = (float)((j & 1) ? z1 : z0);
-      }
-    }
+    const float mu = hout[r * kHeadsMax + j] + p[ao.b3 + j];
+    float noise = 0.f;
+    if (mode == 0 && valid)
+      noise = eps_in ? eps_in[(int64_t)b * A + j] : policy_draw(smp.dist, smp.seed, (uint32_t)b, c1, (uint32_t)tag, j);
     float act;
     if (sac) {
       const float ls_raw = hout[r * kHeadsMax + A + j] + p[ao.b4 + j];
-      const float ls = fminf(fmaxf(ls_raw, smp.ls_min), smp.ls_max);
-      float sigma = expf(ls);
-      if (!isfinite(mu)) mu = 0.f;  // NaN scrub (networks_sac.py:131-134)
-      if (!isfinite(sigma)) sigma = 3.f;
+      const PolicyComp pc = policy_comp(smp.dist, mu, ls_raw, noise, smp.ls_min, smp.ls_max);
       if (mode == 1) {
-        act = tanhf(mu) * smp.max_action;
+        act = tanhf(pc.mu) * smp.max_action;
       } else {
-        const float u = mu + eps * sigma;
-        const float dd = u - mu;
-        const float lpn = -(dd * dd) / (2.f * (sigma * sigma)) - logf(sigma) - kLogSqrt2Pi;
-        act = tanhf(u) * smp.max_action;
+        act = tanhf(pc.u) * smp.max_action;
         const float an = act / smp.max_action;
-        logp += lpn - logf(1.f - an * an + smp.reparam_noise);
+        lp_sum += pc.lp;
+        m2_sum += pc.m2;
+        hld_sum += pc.hld;
+        jac_sum += logf(1.f - an * an + smp.reparam_noise);
         if (save && valid) {
           float* sv = save + (int64_t)b * 5 * A;
-          sv[j] = mu;
-          sv[A + j] = sigma;
-          sv[2 * A + j] = eps;
-          sv[3 * A + j] = u;
+          sv[j] = pc.mu;
+          sv[A + j] = pc.sigma;
+          sv[2 * A + j] = pc.c;
+          sv[3 * A + j] = pc.u;
           sv[4 * A + j] = ls_raw;
         }
       }
     } else {
       act = tanhf(mu) * smp.max_action;
       if (mode == 0) {
-        float nz = eps * noise_std;
+        float nz = noise * noise_std;
         if (clamp_noise) nz = fminf(fmaxf(nz, -noise_clip), noise_clip);
         act = fminf(fmaxf(act + nz, -smp.max_action), smp.max_action);
       }
@@ -465,7 +455,7 @@ __device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, 
     xs[r * ldx + S + j] = act;
     if (xa_out && valid) xa_out[(int64_t)b * d.X + S + j] = act;
   }
-  if (logp_out && valid) logp_out[b] = logp;
+  if (logp_out && valid) logp_out[b] = policy_logp(smp.dist, A, lp_sum, m2_sum, hld_sum, jac_sum);
 }
 
 // Stage rows [row0, row0 + 16) of a [B, in] matrix into xs (pitch ldx), zeros past B.
@@ -907,18 +897,9 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       for (int j = 0; j < A; ++j) {
         const float da = hout[r * kHeadsMax + j];
         if (sac) {
-          const float mu = sv[j], sigma = sv[A + j], eps = sv[2 * A + j], u = sv[3 * A + j];
-          const float ls_raw = sv[4 * A + j];
-          const float dlp = dlogp_r[r];
-          const float t = tanhf(u);
-          const float om = 1.f - t * t;
-          const float dd = u - mu;
-          const float dlogp_du = -dd / (sigma * sigma) + 2.f * t * om / (om + a.smp.reparam_noise);
-          const float du = da * a.smp.max_action * om + dlp * dlogp_du;
-          const float dmu = du + dlp * (dd / (sigma * sigma));
-          const float dsig = du * eps + dlp * ((dd * dd) / (sigma * sigma * sigma) - 1.f / sigma);
-          const bool live = ls_raw >= a.smp.ls_min && ls_raw <= a.smp.ls_max;  // clamp passes [min, max]
-          const float dls = live ? dsig * sigma : 0.f;
+          float dmu, dls;
+          policy_comp_bwd(a.smp.dist, sv[j], sv[A + j], sv[2 * A + j], sv[3 * A + j], sv[4 * A + j], da,
+                          dlogp_r[r], a.smp.max_action, a.smp.reparam_noise, a.smp.ls_min, a.smp.ls_max, dmu, dls);
           ghs[r * kHeadsMax + j] = dmu;
           ghs[r * kHeadsMax + A + j] = dls;
           a.gh[(int64_t)b * 2 * A + j] = dmu;

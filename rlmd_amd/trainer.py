@@ -31,7 +31,7 @@ class VecTrainer:
                  k_updates=1, replay_capacity=1 << 20, seed=0, warmup_steps=1000,
                  smoothing_window=2000, precision="bf16", hidden=None, batch=None, topk=None,
                  prices=None, obs_days=1, time_length=0, shuffle_days=5, sample_days=0,
-                 device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99):
+                 device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99, s_dist="N"):
         self.device = torch.device(device)
         self.env = VecEnv(env, investor, n_lanes, n_gambles, seed=seed, prices=prices, obs_days=obs_days,
                           time_length=time_length, shuffle_days=shuffle_days, sample_days=sample_days,
@@ -42,7 +42,7 @@ class VecTrainer:
         self.topk = topk or d["topk"]
         S, A = self.env.state_dim, self.env.action_dim
         self.agent = DeviceAgent(algo, S, A, h1, h2, self.batch, self.topk, loss=loss, precision=precision,
-                                 seed=seed, init_seed=init_seed, device=device)
+                                 seed=seed, init_seed=init_seed, policy_dist=s_dist, device=device)
         self.replay = ReplayMemory(replay_capacity, S, A, device=device, multi_steps=multi_steps, lanes=n_lanes,
                                    dynamics=dynamics, gamma=gamma)
         self.n_lanes, self.k_updates = n_lanes, k_updates

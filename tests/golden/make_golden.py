@@ -546,11 +546,11 @@ def eval_fixtures(seed=21, n_eval=24, max_steps=100):
 # ----------------------------------------------------------------------------
 # F5: learn() steps for SAC and TD3
 # ----------------------------------------------------------------------------
-def _inputs(algo, S, A, hidden, loss_fn="MSE", B=None, k=None):
+def _inputs(algo, S, A, hidden, loss_fn="MSE", B=None, k=None, s_dist="N"):
     inputs = {
         "test_agent": True, "ENV_KEY": 14, "env_id": "GOLDEN_n1", "dynamics": "M",
         "input_dims": (S,), "num_actions": A, "max_action": 0.99, "min_action": -0.99,
-        "algo": algo, "s_dist": "N", "loss_fn": loss_fn, "multi_steps": 1,
+        "algo": algo, "s_dist": s_dist, "loss_fn": loss_fn, "multi_steps": 1,
         "n_trials": 1, "trial": 1, "n_cumsteps": 5e4, "buffer": 1e6,
         "mini_batch_size": B, "actor_percentile": 50, "critic_percentile": 50,
         "batch_size": {"SAC": k, "TD3": k}, "discount": 0.99, "r_abs_zero": None,
@@ -581,17 +581,23 @@ def learn_fixtures(seed=5):
     import tools.replay as rp
 
     out = {}
+    # (algo, S, A, hidden, B, k, loss, s_dist): cases 4-6 cover the Laplace and
+    # MVN samplers (networks_sac.py:180-258); their noise is injected as the
+    # uniform w of Laplace.rsample / the eps of MultivariateNormal.rsample
     cases = [
-        ("SAC", 5, 1, (64, 64), 512, 256, "MSE"),
-        ("SAC", 6, 2, (64, 48), 512, 256, "HUB"),
-        ("TD3", 6, 2, (64, 48), 200, 100, "MSE"),
-        ("TD3", 5, 1, (40, 32), 200, 100, "HSC"),
+        ("SAC", 5, 1, (64, 64), 512, 256, "MSE", "N"),
+        ("SAC", 6, 2, (64, 48), 512, 256, "HUB", "N"),
+        ("TD3", 6, 2, (64, 48), 200, 100, "MSE", "N"),
+        ("TD3", 5, 1, (40, 32), 200, 100, "HSC", "N"),
+        ("SAC", 5, 1, (64, 64), 512, 256, "MSE", "L"),
+        ("SAC", 6, 3, (64, 48), 512, 256, "HUB", "L"),
+        ("SAC", 6, 3, (64, 48), 512, 256, "MSE", "MVN"),
     ]
     n_steps = 4
-    for ci, (algo, S, A, hid, B, k, lt) in enumerate(cases):
+    for ci, (algo, S, A, hid, B, k, lt, sd) in enumerate(cases):
         T.manual_seed(seed + ci)
         rng = np.random.default_rng(seed + ci)
-        inputs = _inputs(algo, S, A, hid, lt, B, k)
+        inputs = _inputs(algo, S, A, hid, lt, B, k, sd)
         agent = asac.Agent_sac(inputs) if algo == "SAC" else atd3.Agent_td3(inputs)
         nets = _net_names(algo)
         init = {}
@@ -628,6 +634,23 @@ def learn_fixtures(seed=5):
             return self.loc + e * self.scale
 
         Normal.rsample = _rsample
+        from torch.distributions import Laplace, MultivariateNormal
+        from torch.distributions.multivariate_normal import _batch_mv
+
+        saved_lrs, saved_mrs = Laplace.rsample, MultivariateNormal.rsample
+
+        def _lrsample(self, sample_shape=T.Size()):  # torch's formula with the uniform injected
+            w = eps_q.pop(0)
+            assert tuple(w.shape) == tuple(self.loc.shape)
+            return self.loc - self.scale * w.sign() * T.log1p(-w.abs())
+
+        def _mrsample(self, sample_shape=T.Size()):
+            e = eps_q.pop(0)
+            assert tuple(e.shape) == tuple(self.loc.shape)
+            return self.loc + _batch_mv(self._unbroadcasted_scale_tril, e)
+
+        Laplace.rsample = _lrsample
+        MultivariateNormal.rsample = _mrsample
         saved_normal_ = T.Tensor.normal_
 
         def _normal_(self, mean=0.0, std=1.0, generator=None):
@@ -643,7 +666,14 @@ def learn_fixtures(seed=5):
             for s in range(n_steps):
                 idx = rng.choice(M, size=B, replace=False)
                 idx_q.append(idx)
-                if algo == "SAC":
+                if algo == "SAC" and sd == "L":  # U(eps - 1, 1) as Laplace.rsample draws
+                    lo = float(np.finfo(np.float32).eps) - 1.0
+                    e1 = T.from_numpy(rng.uniform(lo, 1.0, (B, A)).astype(np.float32))
+                    e2 = T.from_numpy(rng.uniform(lo, 1.0, (B, A)).astype(np.float32))
+                    eps_q.extend([e1, e2])
+                    out[f"{key}/step{s}/eps_next"] = e1.numpy()
+                    out[f"{key}/step{s}/eps_cur"] = e2.numpy()
+                elif algo == "SAC":
                     e1 = T.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
                     e2 = T.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
                     eps_q.extend([e1, e2])
@@ -665,9 +695,11 @@ def learn_fixtures(seed=5):
         finally:
             rp.np = saved_np
             Normal.rsample = saved_rs
+            Laplace.rsample, MultivariateNormal.rsample = saved_lrs, saved_mrs
             T.Tensor.normal_ = saved_normal_
         out[f"{key}/algo"] = np.array(algo)
         out[f"{key}/loss_fn"] = np.array(lt)
+        out[f"{key}/s_dist"] = np.array(sd)
         out[f"{key}/dims"] = np.array([S, A, hid[0], hid[1], B, k], dtype=np.int64)
         out[f"{key}/n_steps"] = np.int64(n_steps)
         for kk, v in init.items():

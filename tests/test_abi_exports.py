@@ -48,7 +48,7 @@ def test_struct_sizes():
     assert C.sizeof(_abi.EnvCfg) == 48
     assert C.sizeof(_abi.TrainCfg) == 24
     # rlmd_agent_cfg: 13 x i32, 16 x f32, (pad) u64
-    assert C.sizeof(_abi.AgentCfg) == 13 * 4 + 16 * 4 + 4 + 8
+    assert C.sizeof(_abi.AgentCfg) == 15 * 4 + 16 * 4 + 4 + 8  # 15 int32, 16 f32, pad, u64 seed
 
 
 def test_layout_is_host_only_and_matches_torch_order(lib):

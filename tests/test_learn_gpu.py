@@ -34,12 +34,12 @@ def golden_init(g, case):
     return out
 
 
-@pytest.mark.parametrize("case", ["case0", "case1", "case2", "case3"])
+@pytest.mark.parametrize("case", ["case0", "case1", "case2", "case3", "case4", "case5", "case6"])
 def test_learn_matches_reference_golden(golden, dev, case):
     g = golden("learn.npz")
     algo, (S, A, h1, h2, B, k), lay, n, _, _ = build(g, case)
     lt = str(g[case + "/loss_fn"])
-    ag = device_agent(algo, S, A, h1, h2, B, k, lt, golden_init(g, case))
+    ag = device_agent(algo, S, A, h1, h2, B, k, lt, golden_init(g, case), policy_dist=str(g[case + "/s_dist"]))
     rep = {x: torch.from_numpy(g[f"{case}/replay/{x}"]) for x in ("state", "action", "reward", "next_state", "done")}
     for s in range(int(g[case + "/n_steps"])):
         idx = torch.from_numpy(g[f"{case}/step{s}/idx"])
@@ -84,7 +84,7 @@ def _random_batch(rng, B, S, A):
 
 @pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL)
 @pytest.mark.parametrize("loss", ["MSE", "HUB", "MAE", "HSC"])
-def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_lr_frac=0.1):
+def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_lr_frac=0.1, s_dist="N"):
     from rlmd_amd.agent import reference_init
 
     init = reference_init(algo, S, A, h1, h2, seed=11)
@@ -92,13 +92,15 @@ def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_
     p = ol.flatten({nm: dict(zip([x[0] for x in lay[nm]], [t.numpy() for t in init[nm]])) for nm in NETS}, lay, n)
     t = ol.flatten({nm: dict(zip([x[0] for x in lay[nm]], [t.numpy() for t in init[tn]]))
                     for nm, tn in zip(NETS, TNETS)}, lay, n)
-    ora = ol.OracleLearner(algo, S, A, h1, h2, B, k, loss, p, t)
-    ag = device_agent(algo, S, A, h1, h2, B, k, loss, init)
+    ora = ol.OracleLearner(algo, S, A, h1, h2, B, k, loss, p, t, s_dist=s_dist)
+    ag = device_agent(algo, S, A, h1, h2, B, k, loss, init, policy_dist=s_dist)
     rng = np.random.default_rng(3)
+    lo = np.finfo(np.float32).eps - 1.0
+    draw = (lambda: rng.uniform(lo, 1.0, (B, A))) if s_dist == "L" else (lambda: rng.standard_normal((B, A)))
     for step in range(4):
         s, a, r, s2, d = _random_batch(rng, B, S, A)
-        ea = torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
-        eb = torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32))
+        ea = torch.from_numpy(draw().astype(np.float32))
+        eb = torch.from_numpy(draw().astype(np.float32))
         st = ag.learn_batch(s, a, r, s2, d, ea, eb if algo == "SAC" else None).double().cpu().numpy()
         loss_o, lt_o, lp_o = ora.learn(s.numpy(), a.numpy(), r.numpy(), s2.numpy(), d.numpy(), ea.numpy(),
                                        eb.numpy() if algo == "SAC" else None)
@@ -112,6 +114,12 @@ def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_
 @pytest.mark.parametrize("loss", ["CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"])
 def test_remaining_losses_fp32(dev, loss):
     test_full_size_fp32_matches_oracle(dev, "SAC", 5, 1, 256, 256, 512, 256, loss)
+
+
+@pytest.mark.parametrize("s_dist", ["L", "MVN"])
+def test_full_size_policy_dists(dev, s_dist):
+    """Laplace / MVN samplers through the whole update at full size (SAC 256/256)."""
+    test_full_size_fp32_matches_oracle(dev, "SAC", 6, 2, 256, 256, 512, 256, "MSE", s_dist=s_dist)
 
 
 @pytest.mark.parametrize("algo", ["SAC", "TD3"])

@@ -32,12 +32,12 @@ def build(g, c):
     return algo, (S, A, h1, h2, B, k), lay, n, p, t
 
 
-@pytest.mark.parametrize("case", ["case0", "case1", "case2", "case3"])
+@pytest.mark.parametrize("case", ["case0", "case1", "case2", "case3", "case4", "case5", "case6"])
 def test_learn_steps_match_reference(golden, case):
     g = golden("learn.npz")
     algo, (S, A, h1, h2, B, k), lay, n, p, t = build(g, case)
     lt = str(g[case + "/loss_fn"])
-    L = ol.OracleLearner(algo, S, A, h1, h2, B, k, lt, p, t)
+    L = ol.OracleLearner(algo, S, A, h1, h2, B, k, lt, p, t, s_dist=str(g[case + "/s_dist"]))
     rep = {x: g[f"{case}/replay/{x}"] for x in ("state", "action", "reward", "next_state", "done")}
     for s in range(int(g[case + "/n_steps"])):
         idx = g[f"{case}/step{s}/idx"]

@@ -103,6 +103,39 @@ def test_act_matches_oracle_policy(dev, algo, S, A, h1, h2):
         torch.testing.assert_close(sto, ref, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("dist", ["L", "MVN"])
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_act_policy_dists_match_oracle(dev, dist, precision):
+    """Laplace and MVN samplers (networks_sac.py:180-258) in acting: injected noise vs
+    the oracle (fp32: rows kernels' head path; bf16: the fused acting kernel, against
+    the oracle within bf16 tolerance), Philox draws finite and inside the bounds."""
+    from rlmd_amd.agent import DeviceAgent, reference_init
+
+    S, A = 6, 2
+    init = reference_init("SAC", S, A, 256, 256, seed=4)
+    ag = DeviceAgent("SAC", S, A, 256, 256, 512, 256, init=init, precision=precision, policy_dist=dist, device=dev)
+    p, t = _flat_init("SAC", S, A, 256, 256, init)
+    ora = ol.OracleLearner("SAC", S, A, 256, 256, 512, 256, "MSE", p, t, s_dist=dist)
+    rng = np.random.default_rng(7)
+    n = 4099
+    obs = torch.from_numpy(rng.standard_normal((n, S)).astype(np.float32))
+    if dist == "L":
+        noise = rng.uniform(np.finfo(np.float32).eps - 1.0, 1.0, (n, A))
+    else:
+        noise = rng.standard_normal((n, A))
+    eps = torch.from_numpy(noise.astype(np.float32))
+    with torch.no_grad():
+        ref = ora.policy(ora.nets(ora.P)["actor"], obs, eps)[0]
+        got = ag.act(obs, mode=0, eps=eps).cpu()
+        phil = ag.act(obs, mode=0).cpu()
+    err = (got - ref).abs()
+    if precision == "fp32":
+        torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    else:
+        assert (err <= 2e-3).float().mean().item() >= 0.99, err.max().item()
+    assert torch.isfinite(phil).all() and (phil.abs() <= ora.max_action).all()
+
+
 def _bf16_act_reference(p, obs, eps, algo, max_action, ls_min, ls_max, noise):
     """The fused bf16 acting numerics restated in torch: layer 1 in f32, its output and
     fc2.weight rounded to bf16 (RNE), f32 accumulation, f32 heads and sampling."""
