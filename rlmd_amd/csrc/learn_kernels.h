@@ -64,6 +64,20 @@ constexpr int kRowBlock = 16;
 
 __host__ __device__ inline int pad32(int n) { return (n + 31) & ~31; }
 
+// Compute copies of fc2.weight (wc [H2p][H1p], wt [H1p][H2p]) are stored
+// fragment-major: element (row, col) of the logical [rows][ld] matrix sits in
+// the 1-KB block of its MFMA B fragment (16 rows x KS columns; KS = 32 bf16 /
+// 16 f32), lane-ordered (lane = row % 16 + 16 * (col % KS / EPF), EPF elements
+// of 16 B per lane), blocks of one 16-row band in K order.  A wave's fragment
+// load is then one contiguous KB and a band's K sweep one contiguous run, where
+// the row-major copy spread each load over 16 half-used 128-B lines.
+__host__ __device__ inline int64_t frag_index(int row, int col, int ld, int bf16) {
+  const int KS = bf16 ? 32 : 16, EPF = KS / 4;
+  const int s = col / KS, kin = col - s * KS;
+  const int lane = (row & 15) + 16 * (kin / EPF);
+  return ((int64_t)((row >> 4) * (ld / KS) + s) * 64 + lane) * EPF + kin % EPF;
+}
+
 // A net as the row kernels see it: f32 master parameters plus compute copies of
 // fc2.weight in the MFMA operand type (bf16 or f32), zero-padded to 32:
 //   wc [H2p][H1p] (= fc2.weight, forward), wt [H1p][H2p] (transposed, backward).

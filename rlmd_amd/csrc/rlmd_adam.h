@@ -106,11 +106,12 @@ __device__ __forceinline__ void adam_apply(const AdamArgs& a, int i, float g, co
     const int j = i - net * ns - (int)a.w2_off;
     if (net < a.ncopy && j >= 0 && j < a.H1 * a.H2) {
       const int n = j / a.H1, k = j - n * a.H1;
-      store_copy(a.wc[net], (int64_t)n * a.H1p + k, p, a.bf16);
-      store_copy(a.wt[net], (int64_t)k * a.H2p + n, p, a.bf16);
+      const int64_t ic = frag_index(n, k, a.H1p, a.bf16), it = frag_index(k, n, a.H2p, a.bf16);
+      store_copy(a.wc[net], ic, p, a.bf16);
+      store_copy(a.wt[net], it, p, a.bf16);
       if (polyak && a.twc[net]) {
-        store_copy(a.twc[net], (int64_t)n * a.H1p + k, tv, a.bf16);
-        store_copy(a.twt[net], (int64_t)k * a.H2p + n, tv, a.bf16);
+        store_copy(a.twc[net], ic, tv, a.bf16);
+        store_copy(a.twt[net], it, tv, a.bf16);
       }
     }
   }

@@ -155,15 +155,16 @@ __device__ __forceinline__ void frag_load(FragArr<PREC, NBW, MULTI>& f,
   constexpr int EPF = 16 / sizeof(typename CT<PREC>::T);
   constexpr int TS = sizeof(typename CT<PREC>::T);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const uint32_t base = (uint32_t)((wave * 16 + (lane & 15)) * ldb + EPF * (lane >> 4));
-  // the copy is [nblk * 16 rows][ldb]; fragments past it read 0 (never used)
+  // fragment-major copy (frag_index): block (band nb, step s) at ((nb * nS + s) * 64 + lane) * EPF
+  const int nS = ldb / CT<PREC>::KS;
+  const uint32_t base = (uint32_t)((wave * nS * 64 + lane) * EPF);
   const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(Bg, (int64_t)nblk * 16 * ldb * TS);
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
       const bool ok = wave + NW * i < nblk && s0 + g < nsteps;
-      const uint32_t e = base + (uint32_t)(NW * 16 * i * ldb) + (uint32_t)((s0 + g) * CT<PREC>::KS);
+      const uint32_t e = base + (uint32_t)((NW * i * nS + s0 + g) * 64 * EPF);
       f[g][i] = __builtin_bit_cast(typename CT<PREC>::Frag,
                                    __builtin_amdgcn_raw_buffer_load_b128(rs, ok ? (int)(e * TS) : 0x7fffffff, 0, 0));
     }
@@ -959,8 +960,8 @@ __global__ void __launch_bounds__(256) w2_copy_kernel(CopyJobs jobs, int H1, int
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < H1 * H2; i += gridDim.x * blockDim.x) {
     const int n = i / H1, k = i - n * H1;
     const T v = CT<PREC>::cvt(j.w2[i]);
-    wc[(int64_t)n * H1p + k] = v;
-    wt[(int64_t)k * H2p + n] = v;
+    wc[frag_index(n, k, H1p, PREC == RLMD_BF16)] = v;
+    wt[frag_index(k, n, H2p, PREC == RLMD_BF16)] = v;
   }
 }
 
