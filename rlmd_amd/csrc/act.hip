@@ -35,9 +35,14 @@ __device__ __forceinline__ unsigned short f2bf_rne(float f) {
   return (unsigned short)(u >> 16);
 }
 
-__global__ void w_to_bf16_kernel(const float* __restrict__ w, unsigned short* __restrict__ out, int n) {
+// fc2.weight [H2][H1] f32 -> bf16 in the fragment-major order (frag_index) the
+// MFMA loop reads: each wave's fragment load is one contiguous KB
+__global__ void w_to_bf16_kernel(const float* __restrict__ w, unsigned short* __restrict__ out, int H1, int n) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = f2bf_rne(w[i]);
+  if (i < n) {
+    const int row = i / H1, col = i - row * H1;
+    out[frag_index(row, col, H1, 1)] = f2bf_rne(w[i]);
+  }
 }
 
 struct FusedActArgs {
@@ -66,20 +71,56 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
   const int row0 = blockIdx.x * kRows;
   const NetOff& o = a.off;
   const int S = a.S, A = a.A;
-  // -- stage W1, b1 and this block's observations
-  for (int e = tid; e < H1 * S; e += 256) w1s[e] = a.params[o.w1 + e];
-  for (int e = tid; e < H1; e += 256) w1s[H1 * S + e] = a.params[o.b1 + e];
-  for (int e = tid; e < kRows * S; e += 256) {
-    const int r = row0 + e / S;
-    obs_s[e] = r < a.n ? a.obs[(int64_t)row0 * S + e] : 0.f;
+  // -- stage W1, b1 (contiguous in torch order) and this block's observations:
+  //    8 loads per thread per operand in flight before any LDS store (one round
+  //    trip at these sizes); rows past n read 0 through the range check
+  {
+    const int nW = H1 * S + H1, nO = kRows * S;
+    const int rows = a.n - row0 < kRows ? a.n - row0 : kRows;
+    const __amdgpu_buffer_rsrc_t rw = rlmd_rsrc(a.params + o.w1, (int64_t)nW * 4);
+    const __amdgpu_buffer_rsrc_t ro = rlmd_rsrc(a.obs + (int64_t)row0 * S, (int64_t)rows * S * 4);
+    const int nmax = nW > nO ? nW : nO;
+    for (int base = 0; base < nmax; base += 8 * 256) {
+      float vw[8], vo[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = base + j * 256 + tid;
+        vw[j] = rlmd_ldf(rw, e, e < nW);
+        vo[j] = rlmd_ldf(ro, e, e < nO);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int e = base + j * 256 + tid;
+        if (e < nW) w1s[e] = vw[j];
+        if (e < nO) obs_s[e] = vo[j];
+      }
+    }
   }
   __syncthreads();
-  // -- layer 1 on the VALU (K = S is tiny), bf16 into LDS
-  for (int e = tid; e < kRows * H1; e += 256) {
-    const int r = e / H1, c = e % H1;
-    float acc = w1s[H1 * S + c];
-    for (int k = 0; k < S; ++k) acc = fmaf(obs_s[r * S + k], w1s[c * S + k], acc);
-    h1s[r * HP + c] = f2bf_rne(fmaxf(acc, 0.f));
+  // -- layer 1 on the VALU (K = S is tiny), bf16 into LDS.  For S <= 16 each
+  //    thread keeps its unit's fc1 row in registers and sweeps rows reading the
+  //    observations as LDS broadcasts.
+  if (S <= 16) {
+    constexpr int NR = 256 / H1;  // threads per hidden unit
+    const int c = tid % H1, rg = tid / H1;
+    float w[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = k < S ? w1s[c * S + k] : 0.f;
+    const float b = w1s[H1 * S + c];
+    for (int r = rg; r < kRows; r += NR) {
+      float acc = b;
+#pragma unroll
+      for (int k = 0; k < 16; ++k)
+        if (k < S) acc = fmaf(obs_s[r * S + k], w[k], acc);
+      h1s[r * HP + c] = f2bf_rne(fmaxf(acc, 0.f));
+    }
+  } else {
+    for (int e = tid; e < kRows * H1; e += 256) {
+      const int r = e / H1, c = e % H1;
+      float acc = w1s[H1 * S + c];
+      for (int k = 0; k < S; ++k) acc = fmaf(obs_s[r * S + k], w1s[c * S + k], acc);
+      h1s[r * HP + c] = f2bf_rne(fmaxf(acc, 0.f));
+    }
   }
   __syncthreads();
   // -- layer 2: 64 rows x 64 columns per wave, K = H1 in steps of 32
@@ -90,10 +131,12 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
     for (int nb = 0; nb < 4; ++nb) acc[m][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int col0 = 64 * wave;
   const int kq = 8 * (lane >> 4);
+  // fragment (band 4 wave + nb, K-step s): 64 lanes x 16 B at ((band * H1/32 + s) * 64 + lane) * 8
+  constexpr int nS = H1 / 32;
+  const bf16x8* wf = reinterpret_cast<const bf16x8*>(a.w2bf) + (int64_t)(4 * wave) * nS * 64 + lane;
   bf16x8 bnext[4];
 #pragma unroll
-  for (int nb = 0; nb < 4; ++nb)
-    bnext[nb] = *reinterpret_cast<const bf16x8*>(a.w2bf + (int64_t)(col0 + 16 * nb + (lane & 15)) * H1 + kq);
+  for (int nb = 0; nb < 4; ++nb) bnext[nb] = wf[nb * nS * 64];
 #pragma unroll 2
   for (int k0 = 0; k0 < H1; k0 += 32) {
     bf16x8 bcur[4];
@@ -101,8 +144,7 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
     for (int nb = 0; nb < 4; ++nb) bcur[nb] = bnext[nb];
     if (k0 + 32 < H1) {
 #pragma unroll
-      for (int nb = 0; nb < 4; ++nb)
-        bnext[nb] = *reinterpret_cast<const bf16x8*>(a.w2bf + (int64_t)(col0 + 16 * nb + (lane & 15)) * H1 + k0 + 32 + kq);
+      for (int nb = 0; nb < 4; ++nb) bnext[nb] = wf[(nb * nS + k0 / 32 + 1) * 64];
     }
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
@@ -195,7 +237,7 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
                      uint64_t seed, uint32_t ctr, const float* eps, hipStream_t st) {
   const int nw2 = c.h2 * c.h1;
   hipLaunchKernelGGL(w_to_bf16_kernel, dim3((nw2 + 255) / 256), dim3(256), 0, st, actor_params + off.w2,
-                     w2bf, nw2);
+                     w2bf, c.h1, nw2);
   RLMD_LAUNCH_CHECK();
   FusedActArgs a{};
   a.obs = obs;
