@@ -51,6 +51,7 @@ __device__ __forceinline__ int64_t b_off(const rlmd::GemmProblem& p, int r, int 
   return MODE == rlmd::GEMM_FWD ? (int64_t)j * p.ldb + r : (int64_t)r * p.ldb + j;
 }
 constexpr int kOutOfRange = 0x7fffffff;
+constexpr int kSC1 = 16;  // buffer cache-policy bit: sc1 (write-through store / L2-coherent load)
 
 __device__ __forceinline__ float buf_load(__amdgpu_buffer_rsrc_t r, int byte_off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
@@ -204,14 +205,14 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
   const rlmd::GemmShape s = batch.shape[pi];
   const int tile = (int)blockIdx.x - batch.tile_begin[pi];
   const int tile_x = tile % batch.tiles_n[pi], tile_y = tile / batch.tiles_n[pi];
-  // split-K (weight gradients): split `sp` reduces rows [sp*chunk, min(K, (sp+1)*chunk))
-  // of the batch.  Unfused: blockIdx.z is the split and writes its own partial
-  // slab (the optimiser sums the slabs in order).  Fused: the block runs every
-  // split in order, keeping each split's sum in its own accumulator and adding
-  // them slab by slab, as the optimiser would.
+  // split-K (weight gradients): blockIdx.z = split `sp` reduces batch rows
+  // [sp*chunk, min(K, (sp+1)*chunk)) and publishes its partial: a slab of C /
+  // bias_grad (the optimiser sums the slabs in order), or with fuse_adam a
+  // private write-through slab, the tile's last arriving split then summing the
+  // slabs in order and stepping the parameters (rlmd_adam.h).
   const bool fused = MODE == rlmd::GEMM_BWD_W && batch.fuse_adam;
   const int chunk = (s.K + batch.splits - 1) / batch.splits;
-  const int sp0 = fused ? 0 : (int)blockIdx.z, nsp = fused ? batch.splits : 1;
+  const int sp0 = (int)blockIdx.z, nsp = 1;
   if (!fused && sp0) {
     p.C += (int64_t)sp0 * batch.split_stride;
     if (p.bias_grad) p.bias_grad += (int64_t)sp0 * batch.split_stride;
@@ -358,20 +359,41 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
       close_step(q);
     }
   }
-  if constexpr (MODE == rlmd::GEMM_BWD_W) {
+  if constexpr (MODE == rlmd::GEMM_BWD_W && MB == 1) {
     if (fused) {
-      // optimiser epilogue: this block's dW elements (and db when the tile holds
-      // the ones column), then the per-step scalars once
+      // publish this split's partial write-through (sc1), drain, then one lane
+      // takes an arrival ticket on the tile's counter (MI355X_MICROARCH.md,
+      // inter-workgroup hand-off: sc1 stores + vmcnt(0) + agent atomic; the
+      // last arriver reads with sc1 loads after its add returned / a barrier)
+      const int tg = (int)blockIdx.x, ns = batch.splits;
+      // one uniform resource over the tile's slabs; the lane offset in voffset
+      const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+          batch.slabs + (int64_t)tg * ns * 256, (short)0, ns * 256 * 16, 0x00020000);
+      const int lo = (int)threadIdx.x * 16;
+      __builtin_amdgcn_raw_buffer_store_b128(
+          __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, tot[0][0]), rsl, lo + sp0 * 4096, 0, kSC1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      __shared__ int s_last;
+      if (threadIdx.x == 0) {
+        const unsigned prev =
+            __hip_atomic_fetch_add(batch.tile_ctr + tg, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = (prev % (unsigned)ns) == (unsigned)(ns - 1);
+      }
+      __syncthreads();
+      if (!s_last) return;
+      f32x4 g = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sp = 0; sp < ns; ++sp) {
+        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl, lo + sp * 4096, 0, kSC1));
+        g = sp == 0 ? v : g + v;  // slab order, as adam_kernel sums them
+      }
       const rlmd::AdamArgs& ad = batch.adam;
 #pragma unroll
-      for (int mi = 0; mi < MB; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < MB; ++ni)
-#pragma unroll
-          for (int rg = 0; rg < 4; ++rg)
-            if (pidx[mi][ni][rg] >= 0)
-              rlmd::adam_apply(ad, pidx[mi][ni][rg], tot[mi][ni][rg], ain[mi][ni][rg], polyak);
-      if (blockIdx.x == 0 && threadIdx.x == 0) rlmd::adam_scalar_step(ad);
+      for (int rg = 0; rg < 4; ++rg)
+        if (pidx[0][0][rg] >= 0) rlmd::adam_apply(ad, pidx[0][0][rg], g[rg], ain[0][0][rg], polyak);
+      if (tg == 0) {
+        if (threadIdx.x == 0) rlmd::adam_scalar_step(ad);
+      }
       return;
     }
   }
@@ -443,7 +465,9 @@ int gemm_launch(int prec, int mode, const GemmBatch& b_in, hipStream_t stream) {
   }
   b.tile_begin[b.nprob] = tiles;
   if (tiles == 0) return 0;
-  dim3 grid(tiles, 1, b.fuse_adam ? 1 : b.splits);
+  RLMD_CHECK(!b.fuse_adam || (!big && b.slabs && b.tile_ctr && tiles <= b.max_tiles),
+             "fused optimiser epilogue: 32x32 tiles and enough slab space");
+  dim3 grid(tiles, 1, b.splits);
 #define RLMD_GEMM_CASE(P, M)                                                                  \
   if (prec == P && mode == M) {                                                               \
     if (big) hipLaunchKernelGGL((gemm_kernel<P, M, 64, 64>), grid, dim3(256), 0, stream, b);  \

@@ -265,6 +265,11 @@ struct rlmd_agent_s {
   unsigned short* act_w2bf = nullptr;  // fused acting: bf16 copy of the actor's fc2.weight
   int64_t act_cap = 0;
   int64_t host_cntr = 0;
+  // fused optimiser epilogue of the weight-gradient GEMM (rlmd_gemm.h)
+  __attribute__((ext_vector_type(4))) float* slabs = nullptr;
+  unsigned* tile_ctr = nullptr;
+  int32_t max_tiles = 0;
+  bool fuse_adam = false;
 };
 
 namespace rlmd {
@@ -359,9 +364,14 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a, int64_t split_str
 
 // Weight gradients of one phase, then the optimiser step.  Two launches: the
 // split-K GEMM writes RLMD_GRAD_SPLITS slabs over 4x the workgroups, and
-// adam_kernel reduces them.  (Folding the reduction and Adam into the GEMM's
-// epilogue, GemmBatch::fuse_adam, runs each tile's splits serially in one
-// workgroup and measured slower at these sizes: 18.3 vs 8.4 + 6.4 us.)
+// adam_kernel reduces them.  GemmBatch::fuse_adam instead lets each tile's last
+// arriving split sum the slabs and step its parameters inside the GEMM
+// (write-through slabs + arrival tickets); it is exact (same slab order) but
+// measured slower at C2: 18.4 + 13.1 us against 8.0 + 6.3 and 6.5 + 5.2 us
+// separate, the publish / ticket / cross-XCD read tail costing more than the
+// launch it saves.  Kept selectable (RLMD_FUSE_ADAM=1 at agent creation) for
+// larger nets and covered by tests/test_learn_gpu.py.
+
 int launch_bwd_w_adam(rlmd_agent_s* ag, GemmBatch& b, const AdamArgs& ad_in, hipStream_t s) {
   b.splits = RLMD_GRAD_SPLITS;
   b.split_stride = ag->n_params;
@@ -369,10 +379,12 @@ int launch_bwd_w_adam(rlmd_agent_s* ag, GemmBatch& b, const AdamArgs& ad_in, hip
   adam_scalars(a.lr, a.cnt / a.interval, a.step_size, a.bc2_sqrt);
   if (a.temp && a.cnt % a.temp_interval == 0)
     adam_scalars(a.lr_temp, a.cnt / a.temp_interval, a.temp_step_size, a.temp_bc2_sqrt);
-  constexpr bool kFuse = false;
-  if (kFuse) {
+  if (ag->fuse_adam) {
     b.fuse_adam = 1;
     b.adam = a;
+    b.slabs = ag->slabs;
+    b.tile_ctr = ag->tile_ctr;
+    b.max_tiles = ag->max_tiles;
     return gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, s);
   }
   RLMD_TRY(gemm_launch(ag->cfg.precision, GEMM_BWD_W, b, s));
@@ -849,6 +861,17 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.dh1, B * H1);
   RLMD_ALLOC(s.stats, 16);
   RLMD_ALLOC(s.qbias, 4);
+  {  // weight-gradient tiles of the larger phase (critics: both nets; actor)
+    using rlmd::bwd_w_tiles;
+    const int tc = 2 * (bwd_w_tiles(1, H2) + bwd_w_tiles(H2, H1) + bwd_w_tiles(H1, X));
+    const int ta = 2 * bwd_w_tiles(A, H2) + bwd_w_tiles(H2, H1) + bwd_w_tiles(H1, S);
+    ag->max_tiles = tc > ta ? tc : ta;
+    RLMD_ALLOC(ag->slabs, (size_t)ag->max_tiles * RLMD_GRAD_SPLITS * 256);
+    RLMD_ALLOC(ag->tile_ctr, ag->max_tiles);
+    RLMD_HIP(hipMemset(ag->tile_ctr, 0, sizeof(unsigned) * ag->max_tiles));
+    const char* fz = getenv("RLMD_FUSE_ADAM");
+    ag->fuse_adam = fz && atoi(fz) != 0;
+  }
   for (int g = 0; g < 2; ++g) {
     RLMD_ALLOC(s.tpart[g], B);
     RLMD_ALLOC(s.c1[g], B * H1);

@@ -48,12 +48,17 @@ struct GemmBatch {
   int32_t tile_begin[RLMD_GEMM_MAX_PROBS + 1];  // set by gemm_launch
   int32_t splits;        // BWD_W split-K: slabs written at C + s*split_stride (and bias_grad)
   int64_t split_stride;  // floats between slabs
-  // BWD_W with fuse_adam: each workgroup reduces all `splits` slabs of its tile
-  // itself (same slab order and rounding as separate slabs summed by Adam) and
-  // steps the parameters it covers (rlmd_adam.h) instead of storing gradients.
-  // Parameter index = (C or bias_grad) - adam.g + element offset.
+  // BWD_W with fuse_adam (32x32 tiles): each split publishes its partial to a
+  // private slab (slabs: [tiles][splits][256 threads] x 16 B) and takes an
+  // arrival ticket on tile_ctr[tile] (monotonic, zero-initialised once); the
+  // tile's last arrival sums the slabs in order (the rounding of adam_kernel)
+  // and steps the parameters it covers (rlmd_adam.h).  Parameter index = (C or
+  // bias_grad) - adam.g + element offset.
   int32_t fuse_adam;
   AdamArgs adam;
+  __attribute__((ext_vector_type(4))) float* slabs;
+  unsigned* tile_ctr;
+  int32_t max_tiles;  // capacity of slabs / tile_ctr
 };
 
 // Appends one problem; returns its index.
@@ -64,5 +69,8 @@ inline int gemm_add(GemmBatch& b, const GemmShape& s, const GemmProblem& p) {
 }
 
 int gemm_launch(int prec, int mode, const GemmBatch& b, hipStream_t stream);
+
+// 32x32 output tiles of a weight-gradient problem [M = out, N = in] (+ the db column)
+inline int bwd_w_tiles(int M, int N) { return ((N + 1 + 31) / 32) * ((M + 31) / 32); }
 
 }  // namespace rlmd

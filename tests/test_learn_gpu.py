@@ -116,6 +116,14 @@ def test_remaining_losses_fp32(dev, loss):
     test_full_size_fp32_matches_oracle(dev, "SAC", 5, 1, 256, 256, 512, 256, loss)
 
 
+@pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL[:2])
+def test_fused_optimiser_epilogue(dev, monkeypatch, algo, S, A, h1, h2, B, k):
+    """RLMD_FUSE_ADAM=1: the weight-gradient GEMM's last arriving split steps the
+    parameters (write-through slabs + arrival tickets); same numerics as adam_kernel."""
+    monkeypatch.setenv("RLMD_FUSE_ADAM", "1")
+    test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, "MSE")
+
+
 @pytest.mark.parametrize("s_dist", ["L", "MVN"])
 def test_full_size_policy_dists(dev, s_dist):
     """Laplace / MVN samplers through the whole update at full size (SAC 256/256)."""
