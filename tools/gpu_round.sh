@@ -1,0 +1,6 @@
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 900 bash tools/profile_round.sh r01 && echo ALLOK
