@@ -197,7 +197,7 @@ def main():
     cnt = (C.c_int64 * 3)()
     _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
     _abi.check(_abi.lib().rlmd_profile_enable(0))
-    t_max, slab_all = reduce_ranks(elapsed, tr.ep_stats.double(), float(N * args.steps), world, dev)
+    t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(N * args.steps), world, dev)
     total_steps = float(slab_all[:, 4].sum().item())
     value = total_steps / t_max
 

@@ -217,7 +217,10 @@ int rlmd_agent_scalars(rlmd_agent_t ag, double* out_host5);
  * current state (read and advanced in place); actions_dev f32 [N, A] scratch.
  * cum_step is the per-lane step counter of the warm-up / smoothing schedule
  * (rl_multiplicative.py:192-211).  episode_stats_dev (nullable) f64 [4]
- * accumulates {finished episodes, sum of final rewards, sum of lengths, steps}. */
+ * accumulates {finished episodes, sum of final rewards, sum of lengths, -}
+ * with one step of delay: each step's episodes are folded in by the next
+ * rlmd_train_step on the same env, or by rlmd_train_flush_stats (call it before
+ * reading the accumulator). */
 typedef struct {
   int64_t cum_step;
   int32_t warmup_steps;    /* inputs["random"] */
@@ -229,6 +232,10 @@ typedef struct {
 int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlmd_train_cfg* cfg,
                     float* obs_dev, float* actions_dev, double* episode_stats_dev,
                     float* stats_dev, void* stream);
+
+/* Fold the last rlmd_train_step's pending episode statistics into the
+ * accumulator it was given (stream-ordered; no-op when nothing is pending). */
+int rlmd_train_flush_stats(rlmd_env_t env, void* stream);
 
 /* Initialise obs_dev f32 [N, S] with every lane reset (episode start). */
 int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);

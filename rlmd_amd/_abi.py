@@ -88,6 +88,7 @@ SIGNATURES = {
     "rlmd_agent_scalars": (C.c_int, [P, P]),
     "rlmd_train_step": (C.c_int, [P, P, P, C.POINTER(TrainCfg), P, P, P, P, P]),
     "rlmd_train_reset": (C.c_int, [P, P, P]),
+    "rlmd_train_flush_stats": (C.c_int, [P, P]),
     "rlmd_profile_enable": (C.c_int, [I32]),
     "rlmd_profile_read": (C.c_int, [P, P]),
     "rlmd_gemm": (C.c_int, [I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, P, I32, P, I32, P, P]),

@@ -43,7 +43,7 @@ struct FamConst {
   double max_value, min_reward, min_return, max_return, lev_factor;
 };
 
-__host__ __device__ inline FamConst fam_const(int fam) {
+__host__ __device__ constexpr FamConst fam_const(int fam) {
   switch (fam) {
     case RLMD_COIN: return {1e18, 1e-3, -0.9, 1e10, 2.0};
     case RLMD_DICE: return {1e18, 1e-3, -0.9, 1e10, 2.0};
@@ -88,20 +88,21 @@ __device__ __host__ inline double dice_value(int idx) {
 }
 
 // Fisher–Yates permutation of a block of `bs` (<= 16) rows for market shuffles.
+// The permutation lives in one 64-bit register as 16 four-bit entries (no
+// per-thread array, hence no scratch).
 __device__ inline int market_perm(uint64_t seed, uint32_t lane, uint32_t ep, uint32_t blk, int bs,
                                   int pos) {
-  int p[16];
-  for (int i = 0; i < bs; ++i) p[i] = i;
+  uint64_t p = 0xFEDCBA9876543210ull;  // entry i = i
   rlmd_u32x4 w = {0, 0, 0, 0};
   for (int i = bs - 1, k = 0; i >= 1; --i, ++k) {
     if ((k & 3) == 0) w = rlmd_philox(seed, lane, ep, RLMD_TAG_MKT_PERM, blk * 4u + (k >> 2));
     const uint32_t word = (k & 3) == 0 ? w.x : (k & 3) == 1 ? w.y : (k & 3) == 2 ? w.z : w.w;
     const int j = (int)(((uint64_t)word * (uint64_t)(i + 1)) >> 32);
-    const int t = p[i];
-    p[i] = p[j];
-    p[j] = t;
+    const uint64_t pi = (p >> (4 * i)) & 15u, pj = (p >> (4 * j)) & 15u;
+    p &= ~((15ull << (4 * i)) | (15ull << (4 * j)));
+    p |= (pj << (4 * i)) | (pi << (4 * j));
   }
-  return p[pos];
+  return (int)((p >> (4 * pos)) & 15u);
 }
 
 // source price row of extract row e (time_slice + shuffle_data)
@@ -168,12 +169,17 @@ struct StepOut {
 // quantity follows NumPy 2's promotion from it: with f32 actions, GBM/market
 // leverage (x Python int) and the half-shifted stop-loss / retention / safe-haven
 // weights stay f32; with f64 actions everything is f64.
-template <typename AT, typename ActF, typename DrawF, typename StF, typename RkF>
+//
+// FAM (the env family) is a template parameter, so each family's kernel holds
+// only its own code; NG > 0 fixes n_gambles / n_assets at compile time (the
+// n == 1 configurations), NG == 0 reads it from P.
+template <int FAM, int NG, typename AT, typename ActF, typename DrawF, typename StF, typename RkF>
 __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, double w0, int t,
                                         int start, uint32_t ep, ActF act, DrawF draw, StF st,
                                         RkF rk) {
-  const FamConst C = fam_const(P.fam);
-  const int fam = P.fam, inv = P.inv, n = P.n;
+  constexpr FamConst C = fam_const(FAM);
+  constexpr int fam = FAM;
+  const int inv = P.inv, n = NG ? NG : P.n;
   const bool use_all = (fam == RLMD_GBM || fam == RLMD_MARKET);  // lev_max: np.all (Q4)
   const bool f32lev = use_all && sizeof(AT) == 4;                // lev = f32 action * int
   const double lev_cap64 = kMaxAbsAction * C.lev_factor;
@@ -340,9 +346,10 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
 }
 
 // draws for gamble j: Philox(seed, lane, step, ENV_DRAW, j/2), two per block
+template <int FAM>
 __device__ inline double philox_draw(const EnvParams& P, uint32_t lane, uint32_t step, int j) {
   const rlmd_u32x4 v = rlmd_philox(P.seed, lane, step, RLMD_TAG_ENV_DRAW, (uint32_t)(j >> 1));
-  if (P.fam == RLMD_GBM) {
+  if (FAM == RLMD_GBM) {
     double z0, z1;
     rlmd_normal2(v, z0, z1);
     return (j & 1) ? z1 : z0;
@@ -351,18 +358,18 @@ __device__ inline double philox_draw(const EnvParams& P, uint32_t lane, uint32_t
 }
 
 // reset one lane: episode start (market: new slice), state element writer
-template <typename StF>
+template <int FAM, typename StF>
 __device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st) {
   P.wealth[lane] = kInitialValue;
   P.time[lane] = 1;
   const uint32_t ep = P.episode[lane] + 1;
   P.episode[lane] = ep;
-  const FamConst C = fam_const(P.fam);
+  constexpr FamConst C = fam_const(FAM);
   st(0, kInitialValue / C.max_value);
   st(1, 0.0);
   st(2, 1.0 / C.max_value);
   st(3, 1.0 / C.max_value);
-  if (P.fam == RLMD_MARKET) {
+  if (FAM == RLMD_MARKET) {
     const rlmd_u32x4 v = rlmd_philox(P.seed, lane, ep, RLMD_TAG_MKT_START, 0);
     const int start = (int)rlmd_below(v.x, v.y, (uint64_t)P.start_range);
     P.start[lane] = start;
@@ -374,16 +381,58 @@ __device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st)
   }
 }
 
+// Finished-episode statistics of the fused train step: each launch writes one
+// row {episodes, sum of final rewards, sum of lengths, 0} per workgroup into
+// part_out; the next launch's block 0 (or rlmd_train_flush_stats) adds the
+// rows of fold_src into the caller's f64[4] accumulator fold_dst.
+struct StatFold {
+  double* part_out;
+  const double* fold_src;
+  double* fold_dst;
+  int rows;
+};
+
+// one 256-thread block: fixed-order strided sums, then a fixed tree
+__device__ inline void fold_stat_rows(const double* src, int rows, double* dst) {
+  __shared__ double fr[3][256];
+  const int i = threadIdx.x;
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int r = i; r < rows; r += blockDim.x) {
+    a += src[(int64_t)r * 4 + 0];
+    b += src[(int64_t)r * 4 + 1];
+    c += src[(int64_t)r * 4 + 2];
+  }
+  fr[0][i] = a;
+  fr[1][i] = b;
+  fr[2][i] = c;
+  __syncthreads();
+  for (int h = blockDim.x >> 1; h > 0; h >>= 1) {
+    if (i < h) {
+      fr[0][i] += fr[0][i + h];
+      fr[1][i] += fr[1][i + h];
+      fr[2][i] += fr[2][i + h];
+    }
+    __syncthreads();
+  }
+  if (i < 3) dst[i] += fr[i][0];
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) stat_fold_kernel(const double* src, int rows, double* dst) {
+  fold_stat_rows(src, rows, dst);
+}
+
+template <int FAM>
 __global__ void __launch_bounds__(256) env_reset_kernel(EnvParams P, const uint8_t* mask, double* state) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= P.n_lanes) return;
   if (mask && !mask[lane]) return;
-  env_reset_lane(P, lane, [&](int k, double v) {
+  env_reset_lane<FAM>(P, lane, [&](int k, double v) {
     if (state) state[(int64_t)lane * P.state_dim + k] = v;
   });
 }
 
-template <typename AT>
+template <int FAM, int NG, typename AT>
 __global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t step, const AT* __restrict__ actions,
                                 const double* __restrict__ draws, double* next_state,
                                 double* reward, uint8_t* done, double* risk) {
@@ -392,12 +441,12 @@ __global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t ste
   const AT* a = actions + (int64_t)lane * P.action_dim;
   const double w0 = P.wealth[lane];
   const int t = P.time[lane];
-  const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
+  const int start = FAM == RLMD_MARKET ? P.start[lane] : 0;
   const uint32_t ep = P.episode[lane];
-  StepOut o = env_step_lane<AT>(
+  StepOut o = env_step_lane<FAM, NG, AT>(
       P, lane, w0, t, start, ep, [&](int i) { return a[i]; },
       [&](int j) {
-        return draws ? draws[(int64_t)lane * P.draw_dim + j] : philox_draw(P, lane, step, j);
+        return draws ? draws[(int64_t)lane * P.draw_dim + j] : philox_draw<FAM>(P, lane, step, j);
       },
       [&](int k, double v) { next_state[(int64_t)lane * P.state_dim + k] = v; },
       [&](int k, double v) {
@@ -410,6 +459,11 @@ __global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t ste
   done[2 * lane + 1] = o.learn_done;
 }
 
+// Upper bound of the action count when it is known at compile time (dice_sh:
+// <= 4; NG > 0: NG + 2 for InvC), else 0 (read through memory per use).
+template <int FAM, int NG>
+constexpr int kActRegs = FAM == RLMD_DICE_SH ? 4 : (NG > 0 ? NG + 2 : 0);
+
 // ---------------------------------------------------------------------------
 // fused training step: action (warm-up draw | policy) -> action_window clip ->
 // env step -> replay insert (s, a, r, s', learn_done) -> auto reset.
@@ -419,72 +473,124 @@ __global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t ste
 // the smoothing window (np.clip with np.float64 bounds, utils.py:345-373);
 // float32 for policy actions afterwards.  The replay stores the f32 cast, as the
 // reference's float64 buffer does when it batches to torch.float.
-template <typename AT>
-__global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t step, float* actions, int random_actions,
-                                 int abs_actions, double clip_lo, double clip_hi, float* obs,
-                                 rlmd::ReplayView rb, int64_t ring_base, double* ep_stats) {
+// Every load that does not depend on computed data (lane state, actions, the
+// current observation) is issued before the first store, so the lane's memory
+// traffic is one read round and one write round.
+template <int FAM, int NG, typename AT>
+__global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t step, const float* actions,
+                                                        int random_actions, int abs_actions, double clip_lo,
+                                                        double clip_hi, float* obs, rlmd::ReplayView rb,
+                                                        int64_t ring_base, StatFold sf) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  // block 0 folds the previous launch's per-block rows into the caller's
+  // accumulator first (its rows are complete: that launch has ended)
+  if (blockIdx.x == 0 && sf.fold_src) fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst);
   double st_n = 0.0, st_r = 0.0, st_t = 0.0;  // finished-episode stats of this lane
   if (lane < P.n_lanes) {
-  const int S = P.state_dim, A = P.action_dim;
-  // action i: warm-up Philox draw (|.| unless GBM/market) or the policy's, then the
-  // smoothing-window clip; recomputed per use (no per-lane array -> no scratch)
-  auto act = [&](int i) -> AT {
-    double v;
-    if (random_actions) {  // Box(-0.99, 0.99, float64).sample() = low + (high - low) * random_sample()
-      const rlmd_u32x4 w = rlmd_philox(P.seed, lane, step, RLMD_TAG_WARMUP_ACTION, (uint32_t)(i >> 1));
-      const double u = (i & 1) ? rlmd_u01(w.z, w.w) : rlmd_u01(w.x, w.y);
-      v = -kMaxAbsAction + 2.0 * kMaxAbsAction * u;
-      if (abs_actions) v = fabs(v);
-    } else {
-      v = (double)actions[(int64_t)lane * A + i];
+    const int S = P.state_dim, A = P.action_dim;
+    const double w0 = P.wealth[lane];
+    const int t = P.time[lane];
+    const int start = FAM == RLMD_MARKET ? P.start[lane] : 0;
+    const uint32_t ep = P.episode[lane];
+    // action i: warm-up Philox draw (|.| unless GBM/market) or the policy's, then the
+    // smoothing-window clip
+    auto act_of = [&](int i) -> AT {
+      double v;
+      if (random_actions) {  // Box(-0.99, 0.99, float64).sample() = low + (high - low) * random_sample()
+        const rlmd_u32x4 w = rlmd_philox(P.seed, lane, step, RLMD_TAG_WARMUP_ACTION, (uint32_t)(i >> 1));
+        const double u = (i & 1) ? rlmd_u01(w.z, w.w) : rlmd_u01(w.x, w.y);
+        v = -kMaxAbsAction + 2.0 * kMaxAbsAction * u;
+        if (abs_actions) v = fabs(v);
+      } else {
+        v = (double)actions[(int64_t)lane * A + i];
+      }
+      if (sizeof(AT) == 4) return (AT)v;  // policy action outside the window: exact f32
+      return (AT)fmin(fmax(v, clip_lo), clip_hi);
+    };
+    constexpr int AR = kActRegs<FAM, NG>;
+    AT areg[AR > 0 ? AR : 1];
+    if constexpr (AR > 0) {
+#pragma unroll
+      for (int i = 0; i < AR; ++i) areg[i] = i < A ? act_of(i) : (AT)0;
     }
-    if (sizeof(AT) == 4) return (AT)v;  // policy action outside the window: exact f32
-    return (AT)fmin(fmax(v, clip_lo), clip_hi);
-  };
-  const int64_t row = (ring_base + lane) % rb.capacity;
-  // s (current obs) goes to the ring unchanged
-  for (int k = 0; k < S; ++k) rb.state[row * S + k] = obs[(int64_t)lane * S + k];
-  for (int i = 0; i < A; ++i) rb.action[row * A + i] = (float)act(i);
+    auto act = [&](int i) -> AT {  // select chain: a runtime index into areg would spill it to scratch
+      if constexpr (AR > 0) {
+        AT v = areg[0];
+#pragma unroll
+        for (int k = 1; k < AR; ++k) v = i == k ? areg[k] : v;
+        return v;
+      } else {
+        return act_of(i);
+      }
+    };
+    const int64_t row = (ring_base + lane) % rb.capacity;
+    // s (the current obs) goes to the ring unchanged.  gfx9 counts stores in
+    // vmcnt, so a store issued before the compute would be waited on at the first
+    // use of a loaded value: the first 8 obs elements are loaded now and stored
+    // after the step; the rest (market Dx only) are copied here, before the
+    // next-state writes overwrite obs.
+    const __amdgpu_buffer_rsrc_t ro = rlmd_rsrc(obs, (int64_t)P.n_lanes * S * 4);
+    float s0[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s0[j] = rlmd_ldf(ro, (int64_t)lane * S + j, j < S);
+    for (int k0 = 8; k0 < S; k0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = rlmd_ldf(ro, (int64_t)lane * S + k0 + j, k0 + j < S);
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (k0 + j < S) rb.state[row * S + k0 + j] = v[j];
+    }
 
-  const double w0 = P.wealth[lane];
-  const int t = P.time[lane];
-  const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
-  const uint32_t ep = P.episode[lane];
-  StepOut o = env_step_lane<AT>(
-      P, lane, w0, t, start, ep, act,
-      [&](int j) { return philox_draw(P, lane, step, j); },
-      [&](int k, double v) {
-        const float f = (float)v;
-        rb.next_state[row * S + k] = f;
-        obs[(int64_t)lane * S + k] = f;
-      },
-      [&](int, double) {});
-  rb.reward[row] = (float)o.reward;  // max(reward, r_abs_zero = -inf)
-  rb.done[row] = o.learn_done;
-  if (rb.n_steps > 1) rlmd::ms_record(rb, lane, row, o.learn_done);
-  if (o.done) {
-    st_n = 1.0;
-    st_r = o.reward;
-    st_t = (double)t;
-    env_reset_lane(P, lane, [&](int k, double v) { obs[(int64_t)lane * S + k] = (float)v; });
-  } else {
-    P.wealth[lane] = o.W;
-    P.time[lane] = t + 1;
+    StepOut o = env_step_lane<FAM, NG, AT>(
+        P, lane, w0, t, start, ep, act, [&](int j) { return philox_draw<FAM>(P, lane, step, j); },
+        [&](int k, double v) {
+          const float f = (float)v;
+          rb.next_state[row * S + k] = f;
+          obs[(int64_t)lane * S + k] = f;
+        },
+        [&](int, double) {});
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < S) rb.state[row * S + j] = s0[j];
+    for (int i = 0; i < A; ++i) rb.action[row * A + i] = (float)act(i);
+    rb.reward[row] = (float)o.reward;  // max(reward, r_abs_zero = -inf)
+    rb.done[row] = o.learn_done;
+    if (rb.n_steps > 1) rlmd::ms_record(rb, lane, row, o.learn_done);
+    if (o.done) {
+      st_n = 1.0;
+      st_r = o.reward;
+      st_t = (double)t;
+      env_reset_lane<FAM>(P, lane, [&](int k, double v) { obs[(int64_t)lane * S + k] = (float)v; });
+    } else {
+      P.wealth[lane] = o.W;
+      P.time[lane] = t + 1;
+    }
   }
-  }
-  // episode statistics: one wave-reduced atomic per wave instead of one per lane
-  if (ep_stats) {
+  // episode statistics: a fixed-order block reduction into this block's row of
+  // the launch's partial buffer (plain stores; device-scope atomics on one
+  // address from every wave serialise across the XCDs and cost more than the
+  // whole env step)
+  if (sf.part_out) {
+    __shared__ double red[3][256 / 64];
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) {
       st_n += __shfl_xor(st_n, m, 64);
       st_r += __shfl_xor(st_r, m, 64);
       st_t += __shfl_xor(st_t, m, 64);
     }
-    if ((threadIdx.x & 63) == 0 && st_n > 0.0) {
-      atomicAdd(&ep_stats[0], st_n);
-      atomicAdd(&ep_stats[1], st_r);
-      atomicAdd(&ep_stats[2], st_t);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      red[0][w] = st_n;
+      red[1][w] = st_r;
+      red[2][w] = st_t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      const int q = threadIdx.x;
+      double v = 0.0;
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) v += red[q][i];
+      sf.part_out[(int64_t)blockIdx.x * 4 + q] = v;
     }
   }
 }
@@ -497,7 +603,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
 // reward, the step count and the last risk vector are kept.  Draws: injected
 // [N, max_steps, D] or Philox at (lane, step_base + k).
 // ---------------------------------------------------------------------------
-template <typename AT>
+template <int FAM, int NG, typename AT>
 __global__ void __launch_bounds__(256) eval_rollout_kernel(EnvParams P, uint32_t step_base, const float* actions,
                                                            int max_steps, double clip_lo, double clip_hi,
                                                            const double* draws, double* reward_out,
@@ -512,15 +618,15 @@ __global__ void __launch_bounds__(256) eval_rollout_kernel(EnvParams P, uint32_t
   };
   double w = P.wealth[lane];
   int t = P.time[lane];
-  const int start = P.fam == RLMD_MARKET ? P.start[lane] : 0;
+  const int start = FAM == RLMD_MARKET ? P.start[lane] : 0;
   const uint32_t ep = P.episode[lane];
   double run_reward = 0.0;
   int k = 0;
   while (k < max_steps) {
-    const StepOut o = env_step_lane<AT>(
+    const StepOut o = env_step_lane<FAM, NG, AT>(
         P, lane, w, t, start, ep, act,
         [&](int j) {
-          return draws ? draws[((int64_t)lane * max_steps + k) * D + j] : philox_draw(P, lane, step_base + k, j);
+          return draws ? draws[((int64_t)lane * max_steps + k) * D + j] : philox_draw<FAM>(P, lane, step_base + k, j);
         },
         [&](int, double) {},
         [&](int r, double v) {
@@ -538,11 +644,36 @@ __global__ void __launch_bounds__(256) eval_rollout_kernel(EnvParams P, uint32_t
   steps_out[lane] = k;
 }
 
+template <int FAM>
 __global__ void __launch_bounds__(256) env_obs_reset_kernel(EnvParams P, float* obs) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane >= P.n_lanes) return;
-  env_reset_lane(P, lane, [&](int k, double v) { obs[(int64_t)lane * P.state_dim + k] = (float)v; });
+  env_reset_lane<FAM>(P, lane, [&](int k, double v) { obs[(int64_t)lane * P.state_dim + k] = (float)v; });
 }
+
+// Host dispatch over the compile-time family (and n == 1) specialisations:
+// LAUNCH(FAM, NG) is expanded once per combination.
+#define RLMD_ENV_DISPATCH(P, LAUNCH)                        \
+  do {                                                      \
+    const bool _one = (P).n == 1;                           \
+    switch ((P).fam) {                                      \
+      case RLMD_COIN:                                       \
+        if (_one) { LAUNCH(RLMD_COIN, 1); } else { LAUNCH(RLMD_COIN, 0); } \
+        break;                                              \
+      case RLMD_DICE:                                       \
+        if (_one) { LAUNCH(RLMD_DICE, 1); } else { LAUNCH(RLMD_DICE, 0); } \
+        break;                                              \
+      case RLMD_GBM:                                        \
+        if (_one) { LAUNCH(RLMD_GBM, 1); } else { LAUNCH(RLMD_GBM, 0); } \
+        break;                                              \
+      case RLMD_DICE_SH:                                    \
+        LAUNCH(RLMD_DICE_SH, 1);                            \
+        break;                                              \
+      default:                                              \
+        if (_one) { LAUNCH(RLMD_MARKET, 1); } else { LAUNCH(RLMD_MARKET, 0); } \
+        break;                                              \
+    }                                                       \
+  } while (0)
 
 }  // namespace
 
@@ -553,6 +684,12 @@ struct rlmd_env_s {
   EnvParams P;
   uint32_t step_ctr = 0;
   double* d_prices = nullptr;
+  // episode statistics of the fused train step (StatFold): two launches' worth
+  // of per-block rows, the parity of the next launch, and the accumulator the
+  // last launch's rows still owe (nullptr when nothing is pending)
+  double* d_part = nullptr;
+  int part_rows = 0, part_parity = 0;
+  double* pending_dst = nullptr;
 };
 
 namespace rlmd {
@@ -583,18 +720,45 @@ int env_dims_for(const rlmd_env_cfg& c, int& S, int& A, int& R, int& D) {
 
 void env_train_launch_params(rlmd_env_t env, EnvParams*& P);
 
+int flush_stats(rlmd_env_t env, hipStream_t stream) {
+  if (!env->pending_dst) return 0;
+  const double* rows = env->d_part + (size_t)(env->part_parity ^ 1) * env->part_rows * 4;
+  hipLaunchKernelGGL(stat_fold_kernel, dim3(1), dim3(256), 0, stream, rows, env->part_rows, env->pending_dst);
+  RLMD_LAUNCH_CHECK();
+  env->pending_dst = nullptr;
+  return 0;
+}
+
 int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uint32_t step,
               float* actions, int random_actions, int abs_actions, int window, double clip_lo, double clip_hi,
               float* obs, double* ep_stats, hipStream_t stream) {
   const int N = env->P.n_lanes;
   const dim3 grid((N + 255) / 256), block(256);
-  if (window || random_actions)
-    hipLaunchKernelGGL(env_train_kernel<double>, grid, block, 0, stream, env->P, step, actions, random_actions,
-                       abs_actions, clip_lo, clip_hi, obs, rb, ring_base, ep_stats);
-  else
-    hipLaunchKernelGGL(env_train_kernel<float>, grid, block, 0, stream, env->P, step, actions, random_actions,
-                       abs_actions, clip_lo, clip_hi, obs, rb, ring_base, ep_stats);
+  const bool f64 = window || random_actions;
+  StatFold sf{nullptr, nullptr, nullptr, env->part_rows};
+  double* const last_rows = env->d_part + (size_t)(env->part_parity ^ 1) * env->part_rows * 4;
+  if (env->pending_dst && env->pending_dst != ep_stats) {  // different accumulator: settle it now
+    const int r = flush_stats(env, stream);
+    if (r) return r;
+  } else if (env->pending_dst) {
+    sf.fold_src = last_rows;
+    sf.fold_dst = env->pending_dst;
+  }
+  if (ep_stats) sf.part_out = env->d_part + (size_t)env->part_parity * env->part_rows * 4;
+#define TRAIN(F, NG)                                                                                       \
+  {                                                                                                        \
+    if (f64)                                                                                               \
+      hipLaunchKernelGGL((env_train_kernel<F, NG, double>), grid, block, 0, stream, env->P, step, actions, \
+                         random_actions, abs_actions, clip_lo, clip_hi, obs, rb, ring_base, sf);            \
+    else                                                                                                   \
+      hipLaunchKernelGGL((env_train_kernel<F, NG, float>), grid, block, 0, stream, env->P, step, actions,  \
+                         random_actions, abs_actions, clip_lo, clip_hi, obs, rb, ring_base, sf);            \
+  }
+  RLMD_ENV_DISPATCH(env->P, TRAIN);
+#undef TRAIN
   RLMD_LAUNCH_CHECK();
+  env->pending_dst = ep_stats;
+  if (ep_stats) env->part_parity ^= 1;
   return 0;
 }
 
@@ -656,9 +820,13 @@ int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t 
   RLMD_HIP(hipMalloc(&P.time, sizeof(int32_t) * N));
   RLMD_HIP(hipMalloc(&P.start, sizeof(int32_t) * N));
   RLMD_HIP(hipMalloc(&P.episode, sizeof(uint32_t) * N));
+  e->part_rows = (int)((N + 255) / 256);
+  RLMD_HIP(hipMalloc(&e->d_part, sizeof(double) * 8 * e->part_rows));
   RLMD_HIP(hipMemset(P.episode, 0xff, sizeof(uint32_t) * N));  // first reset -> episode 0
   RLMD_HIP(hipMemset(P.start, 0, sizeof(int32_t) * N));
-  hipLaunchKernelGGL(env_reset_kernel, dim3((N + 255) / 256), dim3(256), 0, 0, P, nullptr, nullptr);
+#define RESET(F, NG) hipLaunchKernelGGL(env_reset_kernel<F>, dim3((N + 255) / 256), dim3(256), 0, 0, P, nullptr, nullptr)
+  RLMD_ENV_DISPATCH(P, RESET);
+#undef RESET
   RLMD_LAUNCH_CHECK();
   RLMD_HIP(hipDeviceSynchronize());
   *out = e;
@@ -672,6 +840,7 @@ int rlmd_env_destroy(rlmd_env_t env) {
   (void)hipFree(env->P.start);
   (void)hipFree(env->P.episode);
   if (env->d_prices) (void)hipFree(env->d_prices);
+  (void)hipFree(env->d_part);
   delete env;
   return 0;
 }
@@ -688,8 +857,10 @@ int rlmd_env_dims(rlmd_env_t env, int32_t* S, int32_t* A, int32_t* R, int32_t* D
 int rlmd_env_reset(rlmd_env_t env, const uint8_t* mask, double* state, void* stream) {
   RLMD_CHECK(env, "null env");
   const int N = env->P.n_lanes;
-  hipLaunchKernelGGL(env_reset_kernel, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     env->P, mask, state);
+#define RESET(F, NG) \
+  hipLaunchKernelGGL(env_reset_kernel<F>, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, env->P, mask, state)
+  RLMD_ENV_DISPATCH(env->P, RESET);
+#undef RESET
   RLMD_LAUNCH_CHECK();
   return 0;
 }
@@ -698,8 +869,11 @@ int rlmd_env_step(rlmd_env_t env, const float* actions, const double* draws, dou
                   double* reward, uint8_t* done, double* risk, void* stream) {
   RLMD_CHECK(env && actions && next_state && reward && done, "null argument");
   const int N = env->P.n_lanes;
-  hipLaunchKernelGGL(env_step_kernel<float>, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     env->P, env->step_ctr, actions, draws, next_state, reward, done, risk);
+#define STEP(F, NG)                                                                                         \
+  hipLaunchKernelGGL((env_step_kernel<F, NG, float>), dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, \
+                     env->P, env->step_ctr, actions, draws, next_state, reward, done, risk)
+  RLMD_ENV_DISPATCH(env->P, STEP);
+#undef STEP
   RLMD_LAUNCH_CHECK();
   env->step_ctr++;
   return 0;
@@ -709,8 +883,11 @@ int rlmd_env_step_f64(rlmd_env_t env, const double* actions, const double* draws
                       double* reward, uint8_t* done, double* risk, void* stream) {
   RLMD_CHECK(env && actions && next_state && reward && done, "null argument");
   const int N = env->P.n_lanes;
-  hipLaunchKernelGGL(env_step_kernel<double>, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream,
-                     env->P, env->step_ctr, actions, draws, next_state, reward, done, risk);
+#define STEP(F, NG)                                                                                          \
+  hipLaunchKernelGGL((env_step_kernel<F, NG, double>), dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, \
+                     env->P, env->step_ctr, actions, draws, next_state, reward, done, risk)
+  RLMD_ENV_DISPATCH(env->P, STEP);
+#undef STEP
   RLMD_LAUNCH_CHECK();
   env->step_ctr++;
   return 0;
@@ -732,12 +909,17 @@ int rlmd_eval_rollout(rlmd_env_t env, const float* actions, int32_t max_steps, i
     hi = width * 0.99;
   }
   const dim3 grid((N + 255) / 256), block(256);
-  if (window)
-    hipLaunchKernelGGL(eval_rollout_kernel<double>, grid, block, 0, (hipStream_t)stream, env->P, env->step_ctr,
-                       actions, max_steps, lo, hi, draws, reward, steps, risk);
-  else
-    hipLaunchKernelGGL(eval_rollout_kernel<float>, grid, block, 0, (hipStream_t)stream, env->P, env->step_ctr,
-                       actions, max_steps, lo, hi, draws, reward, steps, risk);
+#define EVAL(F, NG)                                                                                           \
+  {                                                                                                           \
+    if (window)                                                                                               \
+      hipLaunchKernelGGL((eval_rollout_kernel<F, NG, double>), grid, block, 0, (hipStream_t)stream, env->P,  \
+                         env->step_ctr, actions, max_steps, lo, hi, draws, reward, steps, risk);               \
+    else                                                                                                      \
+      hipLaunchKernelGGL((eval_rollout_kernel<F, NG, float>), grid, block, 0, (hipStream_t)stream, env->P,   \
+                         env->step_ctr, actions, max_steps, lo, hi, draws, reward, steps, risk);               \
+  }
+  RLMD_ENV_DISPATCH(env->P, EVAL);
+#undef EVAL
   RLMD_LAUNCH_CHECK();
   env->step_ctr += (uint32_t)max_steps;
   return 0;
@@ -752,11 +934,18 @@ int rlmd_env_lane_state(rlmd_env_t env, double* wealth, int32_t* time) {
   return 0;
 }
 
+int rlmd_train_flush_stats(rlmd_env_t env, void* stream) {
+  RLMD_CHECK(env, "null env");
+  return rlmd::flush_stats(env, (hipStream_t)stream);
+}
+
 int rlmd_train_reset(rlmd_env_t env, float* obs, void* stream) {
   RLMD_CHECK(env && obs, "null argument");
   const int N = env->P.n_lanes;
-  hipLaunchKernelGGL(env_obs_reset_kernel, dim3((N + 255) / 256), dim3(256), 0,
-                     (hipStream_t)stream, env->P, obs);
+#define ORESET(F, NG) \
+  hipLaunchKernelGGL(env_obs_reset_kernel<F>, dim3((N + 255) / 256), dim3(256), 0, (hipStream_t)stream, env->P, obs)
+  RLMD_ENV_DISPATCH(env->P, ORESET);
+#undef ORESET
   RLMD_LAUNCH_CHECK();
   return 0;
 }

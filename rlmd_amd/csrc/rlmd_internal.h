@@ -33,18 +33,20 @@ struct ReplayView {
 // Record the multi-step tags of a transition just written to `row` by lane `l`
 // (one writer per lane per launch) and advance that lane's episode bookkeeping.
 __device__ inline void ms_record(const ReplayView& rb, int l, int64_t row, bool done) {
-  int32_t* ls = rb.lane + 4 * (int64_t)l;
-  const int32_t p = ls[0];
+  int4* lsp = reinterpret_cast<int4*>(rb.lane + 4 * (int64_t)l);  // one 16-B load, one 16-B store
+  int4 ls = *lsp;
+  const int32_t p = ls.x;
   int32_t* t = rb.tag + 3 * row;
   t[0] = p;
-  t[1] = ls[1];
-  t[2] = ls[2];
+  t[1] = ls.y;
+  t[2] = ls.z;
   if (done) {
-    if (ls[1] == 0) ls[3] = p;
-    ls[1] += 1;
-    ls[2] = p + 1;
+    if (ls.y == 0) ls.w = p;
+    ls.y += 1;
+    ls.z = p + 1;
   }
-  ls[0] = p + 1;
+  ls.x = p + 1;
+  *lsp = ls;
 }
 
 ReplayView replay_view(rlmd_replay_t rb);

@@ -105,6 +105,11 @@ class VecTrainer:
         return {"reward": reward.cpu().numpy(), "steps": steps.cpu().numpy(), "risk": risk.cpu().numpy(),
                 "stats": stats.cpu().numpy()}
 
+    def flush_stats(self):
+        """Fold the last step's pending episode statistics into ep_stats."""
+        check(_abi.lib().rlmd_train_flush_stats(self.env.h, stream_ptr()))
+        return self.ep_stats
+
     def episode_stats(self):
-        n, rsum, lsum, _ = self.ep_stats.cpu().numpy()
+        n, rsum, lsum, _ = self.flush_stats().cpu().numpy()
         return {"episodes": int(n), "mean_final_reward": rsum / max(n, 1), "mean_length": lsum / max(n, 1)}

@@ -51,6 +51,8 @@ def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
     ora = oe.OracleVecEnv(fam, oinv, N, n, seed=seed)
     obs = ora.reset()
     absw = fam != oe.GBM
+    length = np.ones(N, dtype=np.int64)  # current episode's step index (the env's t)
+    exp_n, exp_r, exp_l = 0, 0.0, 0.0
     for t in range(T):
         tr.step()
         a = warmup_actions(seed, N, ora.A, t, absw)
@@ -63,11 +65,20 @@ def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
         np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
         obs = ns.copy()
         m = d[:, 0]
+        exp_n += int(m.sum())
+        exp_r += float(r[m].sum())
+        exp_l += float(length[m].sum())
+        length += 1
+        length[m] = 1
         if m.any():
             obs[m] = ora.reset(m)[m]
+        if t in (7, 8, T - 1):  # flushed reads, also back to back (nothing pending the second time)
+            n_ep, r_sum, l_sum, _ = tr.flush_stats().cpu().numpy()
+            assert n_ep == exp_n, f"t={t}"
+            np.testing.assert_allclose([r_sum, l_sum], [exp_r, exp_l], rtol=1e-12)
     np.testing.assert_allclose(tr.obs.cpu().numpy(), obs.astype(np.float32), rtol=1e-6, atol=1e-30)
     st = tr.episode_stats()
-    assert st["episodes"] >= 0
+    assert st["episodes"] == exp_n
 
 
 def _flat_init(algo, S, A, h1, h2, init):
