@@ -61,22 +61,39 @@ struct CriticRow {
 
 // Per-row target and loss.  Every row's loads are issued unconditionally
 // (range-checked buffer loads), so the prologue is one memory round trip.
-__device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, CriticRow& o) {
+// The row's inputs, issued as one load round (callers issue it ahead of their
+// weight-fragment stream, so the loss never waits behind it: vmcnt is in order).
+struct CriticLoads {
+  float qt[2], q[2], rw, lpn;
+  int eff;
+  uint8_t dn;
+};
+__device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
+  const int b = threadIdx.x, B = a.B;
+  const bool in = b < B;
+  const int64_t nB = (int64_t)B * 4;
+  CriticLoads L;
+  for (int g = 0; g < 2; ++g) {
+    L.qt[g] = rlmd_ldf(rlmd_rsrc(a.tpart[g], nB), b, in);
+    L.q[g] = rlmd_ldf(rlmd_rsrc(a.qpart[g], nB), b, in);
+  }
+  L.rw = rlmd_ldf(rlmd_rsrc(a.r, nB), b, in);
+  L.lpn = a.logp_next ? rlmd_ldf(rlmd_rsrc(a.logp_next, nB), b, in) : 0.f;
+  L.dn = __builtin_amdgcn_raw_buffer_load_b8(rlmd_rsrc(a.done, B), in ? b : 0x7fffffff, 0, 0);
+  L.eff = a.eff ? (int)__builtin_bit_cast(
+                      int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, nB), in ? b * 4 : 0x7fffffff, 0, 0))
+                : 1;
+  return L;
+}
+
+__device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, CriticRow& o, const CriticLoads& L) {
   const int b = threadIdx.x, B = a.B;
   const bool in = b < B;
   const LearnState* st = a.st;
-  const int64_t nB = (int64_t)B * 4;
-  float qt[2], q[2];
-  for (int g = 0; g < 2; ++g) {
-    qt[g] = rlmd_ldf(rlmd_rsrc(a.tpart[g], nB), b, in);
-    q[g] = rlmd_ldf(rlmd_rsrc(a.qpart[g], nB), b, in);
-  }
-  const float rw = rlmd_ldf(rlmd_rsrc(a.r, nB), b, in);
-  const float lpn = a.logp_next ? rlmd_ldf(rlmd_rsrc(a.logp_next, nB), b, in) : 0.f;
-  const uint8_t dn = __builtin_amdgcn_raw_buffer_load_b8(rlmd_rsrc(a.done, B), in ? b : 0x7fffffff, 0, 0);
-  const int eff = a.eff ? (int)__builtin_bit_cast(
-                              int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, nB), in ? b * 4 : 0x7fffffff, 0, 0))
-                        : 1;
+  float qt[2] = {L.qt[0], L.qt[1]}, q[2] = {L.q[0], L.q[1]};
+  const float rw = L.rw, lpn = L.lpn;
+  const uint8_t dn = L.dn;
+  const int eff = L.eff;
   float y = 0.f;
   for (int g = 0; g < 2; ++g) {
     qt[g] += a.tb[g][0];
@@ -129,6 +146,10 @@ __device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, C
   o.y = y;
   for (int v = 0; v < 7; ++v) o.s1[v] = s1[v];
   o.nan = m1[0];
+}
+
+__device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, CriticRow& o) {
+  critic_row_loss(a, red, o, critic_row_load(a));
 }
 
 // top-k order: descending l1 + l2, ties by row (critic_loss.py:438-441); ~0 = absent

@@ -150,15 +150,17 @@ using FragArr = typename CT<PREC>::Frag[Pre<PREC, NBW, MULTI>::G][NBW];
 
 template <int PREC, int NBW, bool MULTI>
 __device__ __forceinline__ void frag_load(FragArr<PREC, NBW, MULTI>& f,
-                                          const typename CT<PREC>::T* Bg, int ldb, int s0, int nsteps, int nblk) {
+                                          const typename CT<PREC>::T* Bg, int ldb, int s0, int nsteps, int nblk,
+                                          int nb0 = 0) {
   constexpr int G = Pre<PREC, NBW, MULTI>::G;
   constexpr int EPF = 16 / sizeof(typename CT<PREC>::T);
   constexpr int TS = sizeof(typename CT<PREC>::T);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // fragment-major copy (frag_index): block (band nb, step s) at ((nb * nS + s) * 64 + lane) * EPF
+  // fragment-major copy (frag_index): block (band nb, step s) at ((nb * nS + s) * 64 + lane) * EPF;
+  // this workgroup's bands are nb0 .. nb0 + nblk - 1 (a column split of the output)
   const int nS = ldb / CT<PREC>::KS;
-  const uint32_t base = (uint32_t)((wave * nS * 64 + lane) * EPF);
-  const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(Bg, (int64_t)nblk * 16 * ldb * TS);
+  const uint32_t base = (uint32_t)(((nb0 + wave) * nS * 64 + lane) * EPF);
+  const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(Bg, (int64_t)(nb0 + nblk) * 16 * ldb * TS);
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -171,8 +173,9 @@ __device__ __forceinline__ void frag_load(FragArr<PREC, NBW, MULTI>& f,
 }
 
 template <int PREC, int NBW, bool MULTI>
-__device__ __forceinline__ void pre_issue(Pre<PREC, NBW, MULTI>& p, const void* Bg, int ldb, int K, int nblk) {
-  frag_load<PREC, NBW, MULTI>(p.f, static_cast<const typename CT<PREC>::T*>(Bg), ldb, 0, K / CT<PREC>::KS, nblk);
+__device__ __forceinline__ void pre_issue(Pre<PREC, NBW, MULTI>& p, const void* Bg, int ldb, int K, int nblk,
+                                          int nb0 = 0) {
+  frag_load<PREC, NBW, MULTI>(p.f, static_cast<const typename CT<PREC>::T*>(Bg), ldb, 0, K / CT<PREC>::KS, nblk, nb0);
 }
 
 template <int PREC, int NBW, bool MULTI>
@@ -199,7 +202,8 @@ __device__ __forceinline__ void frag_mfma(const FragArr<PREC, NBW, MULTI>& f,
 // pitch lda; B: compute copy, one row of K elements per output column, pitch ldb).
 template <int PREC, int NBW, bool MULTI>
 __device__ __forceinline__ void mfma_rows(Pre<PREC, NBW, MULTI>& pre, const typename CT<PREC>::T* As, int lda,
-                                          const void* Bv, int ldb, int K, int nblk, f32x4 (&acc)[NBW]) {
+                                          const void* Bv, int ldb, int K, int nblk, f32x4 (&acc)[NBW],
+                                          int nb0 = 0) {
   constexpr int G = Pre<PREC, NBW, MULTI>::G;
   const auto* Bg = static_cast<const typename CT<PREC>::T*>(Bv);
   const int nsteps = K / CT<PREC>::KS;
@@ -211,9 +215,9 @@ __device__ __forceinline__ void mfma_rows(Pre<PREC, NBW, MULTI>& pre, const type
   } else {
     FragArr<PREC, NBW, MULTI> b1;
     for (int s = 0; s < nsteps; s += 2 * G) {
-      frag_load<PREC, NBW, MULTI>(b1, Bg, ldb, s + G, nsteps, nblk);
+      frag_load<PREC, NBW, MULTI>(b1, Bg, ldb, s + G, nsteps, nblk, nb0);
       frag_mfma<PREC, NBW, MULTI>(pre.f, As, lda, s, nsteps, nblk, acc);
-      frag_load<PREC, NBW, MULTI>(pre.f, Bg, ldb, s + 2 * G, nsteps, nblk);
+      frag_load<PREC, NBW, MULTI>(pre.f, Bg, ldb, s + 2 * G, nsteps, nblk, nb0);
       frag_mfma<PREC, NBW, MULTI>(b1, As, lda, s + G, nsteps, nblk, acc);
     }
   }
@@ -238,7 +242,9 @@ __device__ __forceinline__ ElemMap elem_map(int Hp) {
 }
 
 // MFMA accumulator element (i, rg) of this lane: column and row
-__device__ __forceinline__ int acc_col(int i) { return ((threadIdx.x >> 6) + NW * i) * 16 + (threadIdx.x & 15); }
+__device__ __forceinline__ int acc_col(int i, int nb0 = 0) {
+  return (nb0 + (threadIdx.x >> 6) + NW * i) * 16 + (threadIdx.x & 15);
+}
 __device__ __forceinline__ int acc_row(int rg) { return 4 * ((threadIdx.x & 63) >> 4) + rg; }
 
 // ---------------------------------------------------------------------------
@@ -589,7 +595,7 @@ struct BwdMask {
 
 template <int NBW>
 __device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const float* h1, const float* h2, const float* w3,
-                                         const NetOff& o, int row0, int B) {
+                                         const NetOff& o, int row0, int B, int nb0 = 0) {
   const int H1 = o.h1, H2 = o.h2;
   const ElemMap m = elem_map(pad32(H2));
   const bool cin = m.c < H2;
@@ -602,7 +608,7 @@ __device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const float* h1, const
   k.w3 = w3 ? rlmd_ldf(rlmd_rsrc(w3, (int64_t)H2 * 4), m.c, cin) : 0.f;
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
-    const int col = acc_col(i);
+    const int col = acc_col(i, nb0);
 #pragma unroll
     for (int rg = 0; rg < 4; ++rg) {
       const int b = row0 + acc_row(rg);
@@ -634,10 +640,12 @@ template <int PREC, int NBW, bool MULTI>
 __device__ __forceinline__ void dh1_rows(Pre<PREC, NBW, MULTI>& pre, const RowNet& net, const NetOff& o,
                                          const BwdMask<NBW>& k, const typename CT<PREC>::T* aT, int ldaT,
                                          float* dh1_out, const float (*w1a)[NHF], int na, float* part, int row0,
-                                         int B) {
+                                         int B, int nb0 = 0, int nbp = 0) {
+  // column split: bands nb0 .. nb0 + nbp - 1 of dh1 (nbp = 0: all of them)
   const int H1 = o.h1, H1p = pad32(H1), H2p = pad32(o.h2);
+  const int nb = nbp ? nbp : H1p / 16;
   f32x4 acc[NBW];
-  mfma_rows<PREC, NBW, MULTI>(pre, aT, ldaT, net.wt, H2p, H2p, H1p / 16, acc);
+  mfma_rows<PREC, NBW, MULTI>(pre, aT, ldaT, net.wt, H2p, H2p, nb, acc, nb0);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float pd[4][NHF];
 #pragma unroll
@@ -646,8 +654,8 @@ __device__ __forceinline__ void dh1_rows(Pre<PREC, NBW, MULTI>& pre, const RowNe
     for (int j = 0; j < NHF; ++j) pd[rg][j] = 0.f;
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
-    if (wave + NW * i < H1p / 16) {
-      const int col = acc_col(i);
+    if (wave + NW * i < nb) {
+      const int col = acc_col(i, nb0);
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         const int b = row0 + acc_row(rg);
@@ -687,10 +695,18 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
   const int row0 = blockIdx.x * R, g = blockIdx.y, B = a.d.B;
   const RowNet& cn = a.crit[g];
   const int H1p = pad32(a.d.H1), H2p = pad32(a.d.H2);
-  Pre<PREC, NBW, MULTI> pw;
-  pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
+  // dh1 columns split over gridDim.z workgroups (each streams 1/z of W2^T);
+  // part 0 also writes the per-row outputs
+  const int nbp = (H1p / 16) / gridDim.z, nb0 = blockIdx.z * nbp;
+  const bool lead = blockIdx.z == 0;
+  if (g == 0 && lead) RLMD_TSR(112);
+  CriticLoads cl{};
+  if (a.loss.B > 0) cl = critic_row_load(a.loss);
   BwdMask<NBW> k;
-  bwd_mask<NBW>(k, a.c1[g], a.c2[g], cn.p + a.co.w3, a.co, row0, B);
+  bwd_mask<NBW>(k, a.c1[g], a.c2[g], cn.p + a.co.w3, a.co, row0, B, nb0);
+  Pre<PREC, NBW, MULTI> pw;
+  pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, nbp, nb0);
+  if (g == 0 && lead) RLMD_TSR(113);
   if (a.loss.B > 0) {
     // critic loss gradient of this block's rows (rlmd_loss.h): every row's loss,
     // then the rows' top-k ranks counted against all B keys
@@ -699,14 +715,16 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
     int* rank16 = reinterpret_cast<int*>(smem + L.part);
     float* dl16 = reinterpret_cast<float*>(smem + L.part) + R;
     CriticRow o;
-    critic_row_loss(a.loss, red, o);
+    critic_row_loss(a.loss, red, o, cl);
+    if (g == 0 && lead) RLMD_TSR(114);
     const int t = threadIdx.x;
-    if (a.bias_out && blockIdx.x == 0 && g == 0 && t < 4)
+    if (a.bias_out && lead && blockIdx.x == 0 && g == 0 && t < 4)
       a.bias_out[t] = t < 2 ? a.loss.qb[t][0] : a.loss.tb[t - 2][0];
     if (t < B) vkey[t] = critic_sel_key(o);
     if (t < R) rank16[t] = 0;
     if (t >= row0 && t < row0 + R) dl16[t - row0] = g == 0 ? o.dl[0] : o.dl[1];
     __syncthreads();
+    if (g == 0 && lead) RLMD_TSR(115);
     const bool topk = B > a.loss.k;
     if (topk) {
       const int r = t & (R - 1), prt = t / R;
@@ -722,15 +740,18 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
       const bool sel = b < B && (!topk || rank16[t] < kk);
       const float dq = sel ? a.loss.grad_scale * dl16[t] / (float)kk : 0.f;
       rowv[t] = dq;
-      if (b < B) a.loss.dq[g][b] = dq;
+      if (lead && b < B) a.loss.dq[g][b] = dq;
     }
   } else if ((int)threadIdx.x < R) {
     rowv[threadIdx.x] = rlmd_ldf(rlmd_rsrc(a.dq[g], (int64_t)B * 4), row0 + threadIdx.x, row0 + (int)threadIdx.x < B);
   }
   __syncthreads();
-  dh2_from_q<PREC, NBW>(k, rowv, a.co, aT, L.ldaT, a.dc2[g], row0, B);
+  if (g == 0 && lead) RLMD_TSR(116);
+  dh2_from_q<PREC, NBW>(k, rowv, a.co, aT, L.ldaT, lead ? a.dc2[g] : nullptr, row0, B);
   __syncthreads();
-  dh1_rows<PREC, NBW, MULTI>(pw, cn, a.co, k, aT, L.ldaT, a.dc1[g], nullptr, 0, nullptr, row0, B);
+  if (g == 0 && lead) RLMD_TSR(117);
+  dh1_rows<PREC, NBW, MULTI>(pw, cn, a.co, k, aT, L.ldaT, a.dc1[g], nullptr, 0, nullptr, row0, B, nb0, nbp);
+  if (g == 0 && lead) RLMD_TSR(118);
 }
 
 // Actor data-gradients (autograd of algo_sac.py:524-562 through
@@ -760,10 +781,15 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     return;
   }
   RLMD_TSR(96);
-  // ---- every independent load up front
-  Pre<PREC, NBW, MULTI> p0, p1;
-  pre_issue<PREC, NBW, MULTI>(p0, a.crit[0].wt, H2p, H2p, H1p / 16);
-  if (a.nq > 1) pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
+  // ---- every independent load up front; what the actor loss reads first and the
+  //      weight fragments last (vmcnt retires in issue order)
+  const int64_t nB = (int64_t)B * 4;
+  const __amdgpu_buffer_rsrc_t rq0 = rlmd_rsrc(a.qn[0], nB), rq1 = rlmd_rsrc(a.nq > 1 ? a.qn[1] : a.qn[0], nB),
+                               rlp = rlmd_rsrc(sac ? a.logp : a.qn[0], nB);
+  const int tq = threadIdx.x, bq = row0 + (int)threadIdx.x;
+  const float ld_q1 = rlmd_ldf(rq0, tq, tq < B), ld_q2 = rlmd_ldf(rq1, tq, tq < B && a.nq > 1);
+  const float ld_lp = rlmd_ldf(rlp, tq, tq < B && sac);
+  const float row_q1 = rlmd_ldf(rq0, bq, tq < R && bq < B), row_q2 = rlmd_ldf(rq1, bq, tq < R && bq < B && a.nq > 1);
   BwdMask<NBW> k0, k1, ka;
   bwd_mask<NBW>(k0, a.e1[0], a.e2[0], a.crit[0].p + co.w3, co, row0, B);
   if (a.nq > 1) bwd_mask<NBW>(k1, a.e1[1], a.e2[1], a.crit[1].p + co.w3, co, row0, B);
@@ -780,6 +806,9 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
         w1a[g][i][j] = rlmd_ldf(rp, co.w1 + (int64_t)col * X + S + j, g < a.nq && col < d.H1 && j < A);
     }
   }
+  Pre<PREC, NBW, MULTI> p0, p1;
+  pre_issue<PREC, NBW, MULTI>(p0, a.crit[0].wt, H2p, H2p, H1p / 16);
+  if (a.nq > 1) pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
   // ---- actor loss (algo_sac.py:546-562 / algo_td3.py:507-523): every row's
   //      objective and ranking key (SAC sorts descending, TD3 ascending, Q5)
   uint64_t* vkey = reinterpret_cast<uint64_t*>(smem + L.vkey);
@@ -788,9 +817,10 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const float alpha = sac ? expf(a.st->log_alpha) : 0.f;
   const float qb0 = a.crit[0].p[co.b3], qb1 = a.nq > 1 ? a.crit[1].p[co.b3] : 0.f;
   for (int j = threadIdx.x; j < B; j += NT) {
-    const float q1 = a.qn[0][j] + qb0;
-    const float q2 = a.nq > 1 ? a.qn[1][j] + qb1 : q1;
-    const float v = sac ? fminf(q1, q2) - alpha * a.logp[j] : q1;
+    const bool first = j == (int)threadIdx.x;  // preloaded
+    const float q1 = (first ? ld_q1 : a.qn[0][j]) + qb0;
+    const float q2 = a.nq > 1 ? (first ? ld_q2 : a.qn[1][j]) + qb1 : q1;
+    const float v = sac ? fminf(q1, q2) - alpha * (first ? ld_lp : a.logp[j]) : q1;
     vval[j] = v;
     vkey[j] = ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)j;
   }
@@ -808,7 +838,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       block_rank(t < B ? vkey[t] : ~0ull, runs, rank_of);
       sel = t < B && rank_of[t] < kk;
     }
-    float sm[2] = {sel ? vval[t] : 0.f, (t < B && sac) ? -(a.logp[t] + a.target_entropy) : 0.f};
+    float sm[2] = {sel ? vval[t] : 0.f, (t < B && sac) ? -(ld_lp + a.target_entropy) : 0.f};
     float mx[1] = {-INFINITY};
     block_allreduce<2, 0>(sm, mx, reinterpret_cast<float*>(smem + L.red));
     if (t == 0) {
@@ -841,7 +871,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       const float dv = sel ? -1.f / (float)kk : 0.f;
       if (sac) {
         // d min(q1, q2): ties split evenly (torch.minimum backward)
-        const float q1 = a.qn[0][b] + qb0, q2 = a.qn[1][b] + qb1;
+        const float q1 = row_q1 + qb0, q2 = row_q2 + qb1;
         const float g1 = q1 < q2 ? 1.f : (q1 > q2 ? 0.f : 0.5f);
         dq0 = dv * g1;
         dq1 = dv * (1.f - g1);
@@ -990,9 +1020,9 @@ void launch_kind(int kind, const void* args, dim3 grid, size_t lds, hipStream_t 
 // NBW = column blocks per wave (8 waves x 16 columns each), MULTI when the K
 // loop needs more than the 16 prefetched fragments per lane.
 template <int PREC>
-int launch_prec(const RowDims& d, int kind, const void* args, int ny, hipStream_t st, int extra_x) {
+int launch_prec(const RowDims& d, int kind, const void* args, int ny, hipStream_t st, int extra_x, int nz) {
   const int H = d.H1p > d.H2p ? d.H1p : d.H2p;
-  const dim3 grid((d.B + R - 1) / R + extra_x, ny);
+  const dim3 grid((d.B + R - 1) / R + extra_x, ny, nz);
   const size_t lds = (size_t)lds_layout(d).total;
   const int nsteps = H / CT<PREC>::KS;
   if (H <= 128) {
@@ -1008,13 +1038,13 @@ int launch_prec(const RowDims& d, int kind, const void* args, int ny, hipStream_
   return 0;
 }
 
-int launch_rows(const RowDims& d, int kind, const void* args, int ny, hipStream_t st, int extra_x = 0) {
+int launch_rows(const RowDims& d, int kind, const void* args, int ny, hipStream_t st, int extra_x = 0, int nz = 1) {
   RLMD_CHECK(d.H1 <= 512 && d.H2 <= 512, "row kernels: hidden widths up to 512");
   RLMD_CHECK(d.A <= RLMD_MAX_ACTION, "row kernels: too many actions");
   RLMD_CHECK(lds_layout(d).total <= 160 * 1024, "row kernels: LDS budget exceeded");
   if (d.B <= 0) return 0;
-  return d.prec == RLMD_BF16 ? launch_prec<RLMD_BF16>(d, kind, args, ny, st, extra_x)
-                             : launch_prec<RLMD_FP32>(d, kind, args, ny, st, extra_x);
+  return d.prec == RLMD_BF16 ? launch_prec<RLMD_BF16>(d, kind, args, ny, st, extra_x, nz)
+                             : launch_prec<RLMD_FP32>(d, kind, args, ny, st, extra_x, nz);
 }
 
 }  // namespace
@@ -1036,7 +1066,13 @@ int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st) {
   return launch_rows(a.d, 0, &a, a.with_actor ? 5 : 4, st);
 }
 int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st) { return launch_rows(a.d, 1, &a, nq, st); }
-int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st) { return launch_rows(a.d, 2, &a, 2, st); }
+// cbwd: dh1 columns in halves when each half is a whole number of column blocks
+// per wave (the per-workgroup W2^T stream is the kernel's cost)
+int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st) {
+  const int nb = a.d.H1p / 16;
+  const int nz = (nb % (2 * NW) == 0) ? 2 : 1;
+  return launch_rows(a.d, 2, &a, 2, st, 0, nz);
+}
 int abwd_rows_launch(const ABwdArgs& a, hipStream_t st) {
   const bool ext = a.dqn_ext[0] != nullptr;
   RLMD_CHECK(ext || a.d.B <= NT, "fused actor loss: mini-batch up to 512 rows");
