@@ -101,6 +101,9 @@ int rlmd_eval_stats(const double* reward_dev, const int32_t* steps_dev, const do
 
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
+/* Market lanes' episode start rows (i32 [N]) read back (eval_market's
+ * eval_start_idx = start_idx + step, rl_market.py:283-284). */
+int rlmd_env_lane_start(rlmd_env_t env, int32_t* start_host);
 
 /* ------------------------------------------------------------------ replay */
 typedef struct rlmd_replay_s* rlmd_replay_t;
@@ -190,6 +193,19 @@ int rlmd_agent_destroy(rlmd_agent_t ag);
  * counter of the acting noise; eps_dev (nullable) injects it instead. */
 int rlmd_agent_act(rlmd_agent_t ag, const float* obs_dev, int64_t n, float* actions_dev,
                    int32_t mode, uint64_t noise_ctr, const float* eps_dev, void* stream);
+
+/* Replaces eval_market (tools/eval_episodes.py:402-611) for n_eval = N lanes of
+ * a market env built with the test slice's time_length and test_shuffle_days:
+ * lane i starts at price row start_dev[i] (gap + eval_start_idx, :470-476),
+ * the extract re-shuffled per lane; each step the deterministic policy acts on
+ * the observation (eval_next_action), action_window applied when
+ * warmup_steps < cum_step <= smoothing_window (then float64 actions, :499-507),
+ * until done.  Out: last reward f64 [N], step count i32 [N], last risk f64
+ * [N, R] (nullable).  Scratch: obs_dev f32 [N, S], actions_dev f32 [N, A],
+ * live_dev u8 [N]. */
+int rlmd_eval_market(rlmd_env_t env, rlmd_agent_t ag, const int32_t* start_dev, int64_t cum_step,
+                     int32_t warmup_steps, int32_t smoothing_window, float* obs_dev, float* actions_dev,
+                     uint8_t* live_dev, double* reward_dev, int32_t* steps_dev, double* risk_dev, void* stream);
 
 /* Replaces learn() (algo_sac.py:369-595 / algo_td3.py:363-531): k_updates
  * updates, each sampling a fresh mini-batch from rb.  stats_dev (nullable) f32

@@ -153,7 +153,9 @@ class OracleVecEnv:
         return self.prices[self.rowmap[lane][rows], assets]
 
     # -- reset / step -------------------------------------------------------
-    def reset(self, mask=None):
+    def reset(self, mask=None, start_at=None):
+        """start_at (market): given first price row per lane (eval_market's gap
+        index, tools/eval_episodes.py:481-492) instead of the Philox draw."""
         mask = np.ones(self.N, bool) if mask is None else np.asarray(mask, bool)
         mv = FAM[self.f][0]
         state = np.zeros((self.N, self.S))
@@ -165,7 +167,8 @@ class OracleVecEnv:
             st[0:4] = [INITIAL_VALUE, 0, 1, 1]
             if self.f == MARKET:
                 v = px.philox(self.seed, lane, int(self.episode[lane]), px.TAG_MKT_START, 0)
-                self.start[lane] = int(px.below(v[0], v[1], self.start_range))
+                self.start[lane] = (int(px.below(v[0], v[1], self.start_range)) if start_at is None
+                                    else int(start_at[lane]))
                 self.rowmap[lane] = self._episode_rows(lane)
                 if self.obs_days > 1:
                     st[4:] = self.market_obs(lane, 0)  # Dx reset: raw prices (market_envs.py:700)

@@ -42,6 +42,50 @@ def rollout(family, investor, n, action_f32, cum, warmup, smoothing, n_eval, max
     return reward, steps, risk
 
 
+def market_rollout(algo, actor, prices, investor, obs_days, test_days, starts, cum, warmup, smoothing,
+                   shuffle_days=1, seed=0, max_action=0.99):
+    """eval_market (tools/eval_episodes.py:402-611): episode i runs a Market_Inv?_D1/Dx
+    env of time_length test_days + obs_days - 1 over the extract starting at price
+    row starts[i] (gap + eval_start_idx), shuffled in blocks of shuffle_days (the
+    Philox block permutations of oracle.envs); every step the deterministic policy
+    (tanh(mu) * max_action, algo_sac.py:220-236 / algo_td3.py:225-238) acts on the
+    f32 cast of the state (:507), action_window'd when cum <= smoothing (:509-517).
+    actor: {param name: tensor} of the actor net.  Returns (last reward, steps,
+    last risk) per episode, as eval_log[..., 1], eval_log[..., 2], eval_risk_log[..., 1:]."""
+    import torch
+
+    from .learn import mlp
+
+    n_eval = len(starts)
+    tl = test_days + obs_days - 1
+    env = oe.OracleVecEnv(oe.MARKET, investor, n_eval, prices.shape[1], seed=seed, prices=prices,
+                          obs_days=obs_days, time_length=tl, shuffle_days=shuffle_days,
+                          sample_days=tl + 1)
+    state = env.reset(start_at=np.asarray(starts))
+    head = "pi" if algo == "SAC" else "mu"
+    reward, steps = np.zeros(n_eval), np.zeros(n_eval, np.int64)
+    risk = np.zeros((n_eval, env.R))
+    live = np.ones(n_eval, bool)
+    n_steps = tl if obs_days == 1 else tl - obs_days + 1
+    with np.errstate(all="ignore"), torch.no_grad():
+        for k in range(n_steps):
+            _, mu = mlp(actor, torch.from_numpy(state.astype(np.float32)), head)
+            a = (torch.tanh(mu) * max_action).numpy()
+            a = window_action(a, cum, warmup, smoothing)
+            state, r, d, rk = env.step(a)
+            reward[live], risk[live], steps[live] = r[live], rk[live], k + 1
+            live &= ~d[:, 0]
+            if not live.any():
+                break
+    return reward, steps, risk
+
+
+def market_summary(reward, steps, risk_log):
+    """The 14 statistics of eval_market (eval_episodes.py:545-585); risk_log is
+    eval_risk_log's row [gap, risk...], so V$ is risk[0] and the 'lev' column risk[2]."""
+    return summary(reward, steps, risk_log, oe.INV_A)[1:15]
+
+
 def summary(reward, steps, risk, investor):
     """The 15 statistics of eval_episodes.py:289-330, then mean stop-loss / retention."""
     mean_reward = np.mean(reward)

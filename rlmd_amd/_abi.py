@@ -89,6 +89,8 @@ SIGNATURES = {
     "rlmd_train_step": (C.c_int, [P, P, P, C.POINTER(TrainCfg), P, P, P, P, P]),
     "rlmd_train_reset": (C.c_int, [P, P, P]),
     "rlmd_train_flush_stats": (C.c_int, [P, P]),
+    "rlmd_env_lane_start": (C.c_int, [P, P]),
+    "rlmd_eval_market": (C.c_int, [P, P, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, P, P]),
     "rlmd_profile_enable": (C.c_int, [I32]),
     "rlmd_profile_read": (C.c_int, [P, P]),
     "rlmd_gemm": (C.c_int, [I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, P, I32, P, I32, P, P]),

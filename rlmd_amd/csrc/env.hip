@@ -61,7 +61,7 @@ constexpr double kShILev = (-1.0 - 5.0) / (-0.5 - 5.0);
 
 struct EnvParams {
   int fam, inv, n_lanes, n, obs_days, time_length, action_days, shuffle_days;
-  int state_dim, action_dim, risk_dim, draw_dim, ext_len, start_range;
+  int state_dim, action_dim, risk_dim, draw_dim, ext_len, start_range, n_days;
   uint64_t seed;
   const double* prices;  // market [n_days, n]
   // lane state
@@ -358,8 +358,10 @@ __device__ inline double philox_draw(const EnvParams& P, uint32_t lane, uint32_t
 }
 
 // reset one lane: episode start (market: new slice), state element writer
+// start_at >= 0 (market): the episode's first price row is given (eval_market's
+// gap index) instead of drawn.
 template <int FAM, typename StF>
-__device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st) {
+__device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st, int start_at = -1) {
   P.wealth[lane] = kInitialValue;
   P.time[lane] = 1;
   const uint32_t ep = P.episode[lane] + 1;
@@ -371,7 +373,7 @@ __device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st)
   st(3, 1.0 / C.max_value);
   if (FAM == RLMD_MARKET) {
     const rlmd_u32x4 v = rlmd_philox(P.seed, lane, ep, RLMD_TAG_MKT_START, 0);
-    const int start = (int)rlmd_below(v.x, v.y, (uint64_t)P.start_range);
+    const int start = start_at >= 0 ? start_at : (int)rlmd_below(v.x, v.y, (uint64_t)P.start_range);
     P.start[lane] = start;
     const int m = P.obs_days * P.n;
     for (int k = 0; k < m; ++k)
@@ -644,6 +646,63 @@ __global__ void __launch_bounds__(256) eval_rollout_kernel(EnvParams P, uint32_t
   steps_out[lane] = k;
 }
 
+// ---------------------------------------------------------------------------
+// market evaluation (tools/eval_episodes.py:402-611): every lane is one eval
+// episode over the test slice starting at its gap index, re-shuffled in blocks of
+// test_shuffle_days; the policy acts on every step (the caller runs the
+// deterministic policy between steps), action_window applied when
+// warmup < cum_steps <= smoothing (float64 actions then).  A lane stops at its
+// first done; its last reward, step count and risk vector are kept.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) eval_market_reset_kernel(EnvParams P, const int32_t* start_at, float* obs,
+                                                                double* reward, int32_t* steps, uint8_t* live) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= P.n_lanes) return;
+  const int st = start_at[lane];
+  steps[lane] = 0;
+  reward[lane] = __builtin_nan("");
+  // a start whose extract would leave the price table is refused per lane (never read)
+  if (st < 0 || st + P.ext_len > P.n_days) {
+    live[lane] = 0;
+    return;
+  }
+  env_reset_lane<RLMD_MARKET>(P, lane, [&](int k, double v) { obs[(int64_t)lane * P.state_dim + k] = (float)v; },
+                              st);
+  live[lane] = 1;
+}
+
+template <int NG, typename AT>
+__global__ void __launch_bounds__(256) eval_market_step_kernel(EnvParams P, const float* actions, double clip_lo,
+                                                               double clip_hi, float* obs, double* reward_out,
+                                                               int32_t* steps_out, double* risk_out, uint8_t* live) {
+  const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= P.n_lanes || !live[lane]) return;
+  const int A = P.action_dim, S = P.state_dim, R = P.risk_dim;
+  auto act = [&](int i) -> AT {
+    const double v = (double)actions[(int64_t)lane * A + i];
+    if (sizeof(AT) == 4) return (AT)v;
+    return (AT)fmin(fmax(v, clip_lo), clip_hi);
+  };
+  const double w0 = P.wealth[lane];
+  const int t = P.time[lane];
+  const int start = P.start[lane];
+  const uint32_t ep = P.episode[lane];
+  const StepOut o = env_step_lane<RLMD_MARKET, NG, AT>(
+      P, lane, w0, t, start, ep, act, [&](int) { return 0.0; },
+      [&](int k, double v) { obs[(int64_t)lane * S + k] = (float)v; },
+      [&](int k, double v) {
+        if (risk_out) risk_out[(int64_t)lane * R + k] = v;
+      });
+  reward_out[lane] = o.reward;
+  steps_out[lane] = t;
+  if (o.done) {
+    live[lane] = 0;
+  } else {
+    P.wealth[lane] = o.W;
+    P.time[lane] = t + 1;
+  }
+}
+
 template <int FAM>
 __global__ void __launch_bounds__(256) env_obs_reset_kernel(EnvParams P, float* obs) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
@@ -762,6 +821,40 @@ int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uin
   return 0;
 }
 
+int env_market_eval_reset(rlmd_env_t env, const int32_t* start_at, float* obs, double* reward, int32_t* steps,
+                          uint8_t* live, hipStream_t stream) {
+  RLMD_CHECK(env->P.fam == RLMD_MARKET, "market evaluation needs a market env");
+  const int N = env->P.n_lanes;
+  hipLaunchKernelGGL(eval_market_reset_kernel, dim3((N + 255) / 256), dim3(256), 0, stream, env->P, start_at, obs,
+                     reward, steps, live);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int env_market_eval_step(rlmd_env_t env, const float* actions, int window, double lo, double hi, float* obs,
+                         double* reward, int32_t* steps, double* risk, uint8_t* live, hipStream_t stream) {
+  const int N = env->P.n_lanes;
+  const dim3 grid((N + 255) / 256), block(256);
+#define MSTEP(NG, AT)                                                                                        \
+  hipLaunchKernelGGL((eval_market_step_kernel<NG, AT>), grid, block, 0, stream, env->P, actions, lo, hi, obs, \
+                     reward, steps, risk, live)
+  if (env->P.n == 1) {
+    if (window) MSTEP(1, double);
+    else MSTEP(1, float);
+  } else {
+    if (window) MSTEP(0, double);
+    else MSTEP(0, float);
+  }
+#undef MSTEP
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int env_episode_steps(rlmd_env_t env) {
+  const EnvParams& P = env->P;
+  return P.obs_days == 1 ? P.time_length : P.time_length - P.obs_days + 1;
+}
+
 int env_lanes(rlmd_env_t env) { return env->P.n_lanes; }
 int env_state_dim(rlmd_env_t env) { return env->P.state_dim; }
 int env_action_dim(rlmd_env_t env) { return env->P.action_dim; }
@@ -806,6 +899,7 @@ int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t 
       RLMD_CHECK(false, "market env needs prices, time_length > 0 and shuffle_days <= 16");
     }
     P.ext_len = P.time_length * P.action_days + 1;
+    P.n_days = (int)n_days;
     P.start_range = (int)(n_days - cfg->sample_days);
     if (P.start_range < 1 || P.start_range - 1 + P.ext_len > n_days) {
       delete e;
@@ -931,6 +1025,13 @@ int rlmd_env_lane_state(rlmd_env_t env, double* wealth, int32_t* time) {
   const size_t N = env->P.n_lanes;
   if (wealth) RLMD_HIP(hipMemcpy(wealth, env->P.wealth, N * sizeof(double), hipMemcpyDeviceToHost));
   if (time) RLMD_HIP(hipMemcpy(time, env->P.time, N * sizeof(int32_t), hipMemcpyDeviceToHost));
+  return 0;
+}
+
+int rlmd_env_lane_start(rlmd_env_t env, int32_t* start_host) {
+  RLMD_CHECK(env && start_host, "null argument");
+  RLMD_HIP(hipDeviceSynchronize());
+  RLMD_HIP(hipMemcpy(start_host, env->P.start, env->P.n_lanes * sizeof(int32_t), hipMemcpyDeviceToHost));
   return 0;
 }
 

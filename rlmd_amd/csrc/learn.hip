@@ -929,6 +929,34 @@ int rlmd_agent_destroy(rlmd_agent_t ag) {
   return 0;
 }
 
+int rlmd_eval_market(rlmd_env_t env, rlmd_agent_t ag, const int32_t* start_dev, int64_t cum_step,
+                     int32_t warmup_steps, int32_t smoothing_window, float* obs_dev, float* actions_dev,
+                     uint8_t* live_dev, double* reward_dev, int32_t* steps_dev, double* risk_dev, void* stream) {
+  RLMD_CHECK(env && ag && start_dev && obs_dev && actions_dev && live_dev && reward_dev && steps_dev,
+             "null argument");
+  hipStream_t st = (hipStream_t)stream;
+  const int N = rlmd::env_lanes(env);
+  RLMD_CHECK(ag->cfg.state_dim == rlmd::env_state_dim(env) && ag->cfg.action_dim == rlmd::env_action_dim(env),
+             "agent / env dims differ");
+  // eval_episodes.py:499-507: action_window while cum_steps <= smoothing_window,
+  // which clips only past the warm-up (utils.py:366-371)
+  const bool window = cum_step <= smoothing_window && cum_step > warmup_steps;
+  double lo = -INFINITY, hi = INFINITY;
+  if (window) {
+    const double width = (sin(M_PI * ((double)cum_step / (double)smoothing_window - 0.5)) + 1.0) / 2.0;
+    lo = width * -0.99;
+    hi = width * 0.99;
+  }
+  RLMD_TRY(rlmd::env_market_eval_reset(env, start_dev, obs_dev, reward_dev, steps_dev, live_dev, st));
+  const int T = rlmd::env_episode_steps(env);
+  for (int t = 0; t < T; ++t) {
+    RLMD_TRY(rlmd::agent_act(ag, obs_dev, N, actions_dev, 1, 0, nullptr, st));  // eval_next_action
+    RLMD_TRY(rlmd::env_market_eval_step(env, actions_dev, window ? 1 : 0, lo, hi, obs_dev, reward_dev, steps_dev,
+                                        risk_dev, live_dev, st));
+  }
+  return 0;
+}
+
 int rlmd_agent_act(rlmd_agent_t ag, const float* obs, int64_t n, float* actions, int32_t mode,
                    uint64_t noise_ctr, const float* eps, void* stream) {
   RLMD_CHECK(ag && obs && actions, "null argument");

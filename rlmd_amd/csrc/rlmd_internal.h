@@ -59,6 +59,13 @@ void replay_advance(rlmd_replay_t rb, int64_t n);
 int env_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step,
               float* actions, int random_actions, int abs_actions, int window, double clip_lo, double clip_hi,
               float* obs, double* ep_stats, hipStream_t stream);
+// market evaluation (eval_episodes.py:402-611): reset every lane at its given
+// start row, then one policy-driven step of the still-running lanes
+int env_market_eval_reset(rlmd_env_t env, const int32_t* start_at, float* obs, double* reward, int32_t* steps,
+                          uint8_t* live, hipStream_t stream);
+int env_market_eval_step(rlmd_env_t env, const float* actions, int window, double lo, double hi, float* obs,
+                         double* reward, int32_t* steps, double* risk, uint8_t* live, hipStream_t stream);
+int env_episode_steps(rlmd_env_t env);  // market: steps until done_time
 int env_lanes(rlmd_env_t env);
 int env_state_dim(rlmd_env_t env);
 int env_action_dim(rlmd_env_t env);

@@ -91,6 +91,12 @@ class VecEnv:
         check(_abi.lib().rlmd_env_lane_state(self.h, w.ctypes.data_as(C.c_void_p), t.ctypes.data_as(C.c_void_p)))
         return w, t
 
+    def lane_start(self):
+        """Market lanes' episode start rows (the reference's start_idx, rl_market.py:202-205)."""
+        st = np.empty(self.n_lanes, dtype=np.int32)
+        check(_abi.lib().rlmd_env_lane_start(self.h, st.ctypes.data_as(C.c_void_p)))
+        return st
+
 
 # ----------------------------------------------------------------------------
 # Reference-named single-env classes (Gym interface of envs/*_envs.py)

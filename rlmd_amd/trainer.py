@@ -105,6 +105,24 @@ class VecTrainer:
         return {"reward": reward.cpu().numpy(), "steps": steps.cpu().numpy(), "risk": risk.cpu().numpy(),
                 "stats": stats.cpu().numpy()}
 
+    def evaluate_market(self, n_eval=100, test_days=250, gap_days=(5, 20), test_shuffle_days=3, rng=None):
+        """eval_market (tools/eval_episodes.py:402-611) for a market trainer: the
+        reference evaluates from eval_start_idx = start_idx + step of its one
+        training stream (rl_market.py:283-284); here episode i starts from lane
+        (i mod N)'s current position plus a gap drawn in [gap_min, gap_max]
+        (host draw, as the reference's np.random.randint).  The gap must keep the
+        test slice inside the price table (the reference's sample_length
+        reserves it: rl_market.py:58-60)."""
+        assert self.env.family == _abi.MARKET, "evaluate_market needs a market trainer"
+        rng = rng if rng is not None else np.random.default_rng(self.env.seed + self.cfg.cum_step)
+        _, t = self.env.lane_state()
+        eval_start = (self.env.lane_start() + t - 1)[np.arange(n_eval) % self.n_lanes]
+        starts = eval_start + rng.integers(gap_days[0], gap_days[1] + 1, size=n_eval)
+        kw = self.env.make_kw
+        return market_evaluate(self.agent, kw["prices"], self.env.investor, kw["obs_days"], test_days, starts,
+                               self.cfg.cum_step, self.cfg.warmup_steps, self.cfg.smoothing_window,
+                               shuffle_days=test_shuffle_days, seed=self.env.seed + 20011, device=self.device)
+
     def flush_stats(self):
         """Fold the last step's pending episode statistics into ep_stats."""
         check(_abi.lib().rlmd_train_flush_stats(self.env.h, stream_ptr()))
@@ -113,3 +131,43 @@ class VecTrainer:
     def episode_stats(self):
         n, rsum, lsum, _ = self.flush_stats().cpu().numpy()
         return {"episodes": int(n), "mean_final_reward": rsum / max(n, 1), "mean_length": lsum / max(n, 1)}
+
+
+def market_evaluate(agent, prices, investor, obs_days, test_days, starts, cum_step, warmup_steps,
+                    smoothing_window, shuffle_days=3, seed=0, action_days=1, device="cuda:0", env=None):
+    """eval_market (tools/eval_episodes.py:402-611) on the device, one lane per
+    episode: a Market_Inv?_D1/Dx env of time_length test_days + obs_days - 1
+    starting at price row starts[i] (gap + eval_start_idx), its extract shuffled
+    in blocks of shuffle_days; the deterministic policy acts on every state.
+    Returns per-episode last reward / steps / risk, the risk-log rows
+    [start, risk...] of eval_risk_log, and the 14 summary statistics of
+    :545-585 (rlmd_eval_stats on those rows, NumPy-exact)."""
+    dev = torch.device(device)
+    starts = np.asarray(starts, dtype=np.int32)
+    n = len(starts)
+    tl = test_days + obs_days - 1
+    if env is None:
+        env = VecEnv(_abi.MARKET, investor, n, np.asarray(prices).shape[1], seed=seed, prices=prices,
+                     obs_days=obs_days, time_length=tl, action_days=action_days, shuffle_days=shuffle_days,
+                     sample_days=tl * action_days + 1, device=dev)
+    assert env.n_lanes == n
+    assert agent.S == env.state_dim and agent.A == env.action_dim, "agent / env dims differ"
+    n_days = np.asarray(prices).shape[0]
+    if starts.min() < 0 or starts.max() + tl * action_days + 1 > n_days:
+        raise ValueError("an evaluation slice leaves the price table")
+    st = torch.from_numpy(starts).to(dev)
+    obs = torch.empty(n, env.state_dim, dtype=torch.float32, device=dev)
+    act = torch.empty(n, env.action_dim, dtype=torch.float32, device=dev)
+    live = torch.empty(n, dtype=torch.uint8, device=dev)
+    reward = torch.empty(n, dtype=torch.float64, device=dev)
+    steps = torch.empty(n, dtype=torch.int32, device=dev)
+    risk = torch.empty(n, env.risk_dim, dtype=torch.float64, device=dev)
+    lib = _abi.lib()
+    check(lib.rlmd_eval_market(env.h, agent.h, ptr(st), int(cum_step), int(warmup_steps), int(smoothing_window),
+                               ptr(obs), ptr(act), ptr(live), ptr(reward), ptr(steps), ptr(risk), stream_ptr()))
+    risk_log = torch.cat([st.double()[:, None], risk], 1).contiguous()
+    stats = torch.empty(17, dtype=torch.float64, device=dev)
+    check(lib.rlmd_eval_stats(ptr(reward), ptr(steps), ptr(risk_log), n, env.risk_dim + 1, _abi.INV_A, ptr(stats),
+                              stream_ptr()))
+    return {"reward": reward.cpu().numpy(), "steps": steps.cpu().numpy(), "risk": risk.cpu().numpy(),
+            "risk_log": risk_log.cpu().numpy(), "stats": stats[1:15].cpu().numpy()}

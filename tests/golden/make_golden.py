@@ -543,6 +543,74 @@ def eval_fixtures(seed=21, n_eval=24, max_steps=100):
     return out
 
 
+# (algo, investor, obs_days, prices file, cum_steps, warm-up, smoothing window);
+# the policy is a real reference agent whose deterministic policy acts on every
+# state (eval_next_action).  test_shuffle_days = 1 keeps the extract unshuffled
+# (the GPU's in-block shuffle is Philox and is checked against the oracle).
+EVAL_MARKET_CASES = [
+    ("SAC", "A", 1, "stooq_snp", 5000, 1000, 2000),
+    ("TD3", "B", 3, "stooq_usei", 1500, 1000, 2000),
+    ("SAC", "C", 1, "stooq_usei", 500, 1000, 2000),
+    ("TD3", "A", 4, "stooq_snp", 3000, 1000, 2000),
+]
+
+
+def eval_market_fixtures(seed=31, n_eval=12, test_days=40):
+    import algos.algo_sac as asac
+    import algos.algo_td3 as atd3
+    import envs.market_envs as me
+    import tools.eval_episodes as ev
+
+    out = {}
+    rng = np.random.default_rng(seed)
+    for ci, (algo, inv, d, pfile, cum, warm, sw) in enumerate(EVAL_MARKET_CASES):
+        prices = np.load(f"/root/reference/tools/market_data/{pfile}.npy")
+        n = prices.shape[1]
+        test_length = test_days + d - 1
+        cls = getattr(me, f"Market_Inv{inv}_{'D1' if d == 1 else 'Dx'}")
+        probe = cls(n, test_length, d)
+        S, A = probe.observation_space.shape[0], probe.action_space.shape[0]
+        T.manual_seed(seed + ci)
+        hid = (32, 24)
+        agent = (asac.Agent_sac if algo == "SAC" else atd3.Agent_td3)(_inputs(algo, S, A, hid, "MSE", 16, 8))
+        init = {}
+        for nm in _net_names(algo):
+            for pn, p in getattr(agent, nm).named_parameters():
+                init[f"{nm}.{pn}"] = p.detach().numpy().copy()
+        eval_start = int(rng.integers(0, prices.shape[0] - test_length - 40))
+        gaps = rng.integers(5, 21, size=n_eval)
+        rnd = _InjectedRandom()
+        rnd.push(gaps)
+        inputs = {"ENV_KEY": 0, "algo": algo, "s_dist": "N", "loss_fn": "MSE", "n_eval": n_eval,
+                  "env_id": f"X_Inv{inv}_D{d}_T1", "action_days": 1, "test_days": test_days,
+                  "gap_days_min": 5, "gap_days_max": 20, "test_shuffle_days": 1, "smoothing_window": sw,
+                  "max_action": np.float64(0.99), "min_action": np.float64(-0.99), "random": warm}
+        R = len(np.atleast_1d(probe.risk)) if hasattr(probe, "risk") else 0
+        eval_log = np.zeros((1, 1, n_eval, 20))
+        eval_risk = np.zeros((1, 1, n_eval, 1 + R))
+        saved = ev.np
+        ev.np = _NpProxy(rnd)
+        try:
+            ev.eval_market(prices, d, eval_start, agent, inputs, eval_log, eval_risk, 1, cum, 0, 0,
+                           [0.0] * 11, 0.0, [0.0] * 4)
+        finally:
+            ev.np = saved
+        assert not rnd.queue
+        key = f"case{ci}"
+        out[key + "/spec"] = np.array([algo, inv, pfile])
+        out[key + "/params"] = np.array([d, n, test_days, cum, warm, sw, n_eval, eval_start, hid[0], hid[1]],
+                                        dtype=np.int64)
+        out[key + "/gaps"] = gaps.astype(np.int64)
+        # the rows any episode can touch; episode i starts at row gaps[i] of this slice
+        out[key + "/prices"] = prices[eval_start: eval_start + 21 + test_length + 1]
+        out[key + "/reward"] = eval_log[0, 0, :, 1]
+        out[key + "/steps"] = eval_log[0, 0, :, 2].astype(np.int64)
+        out[key + "/risk_log"] = eval_risk[0, 0]  # [gap + eval_start_idx, risk...]
+        for kk, v in init.items():
+            out[f"{key}/init/{kk}"] = v
+    return out
+
+
 # ----------------------------------------------------------------------------
 # F5: learn() steps for SAC and TD3
 # ----------------------------------------------------------------------------
@@ -724,6 +792,7 @@ def main():
         "shadow.npz": shadow_fixtures,
         "multistep.npz": multistep_fixtures,
         "eval.npz": eval_fixtures,
+        "eval_market.npz": eval_market_fixtures,
         "learn.npz": learn_fixtures,
     }
     only = sys.argv[1:]

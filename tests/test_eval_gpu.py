@@ -77,3 +77,82 @@ def test_trainer_evaluate(dev):
     assert set(ev) >= {"reward", "steps", "risk", "stats"}
     assert ev["steps"].min() >= 1 and ev["steps"].max() <= 100
     assert np.isfinite(ev["stats"][:15]).all()
+
+
+def _market_agent(g, c, dev):
+    from rlmd_amd.agent import DeviceAgent, layer_names
+    from tests.test_oracle_golden import _eval_market_case
+
+    algo, inv, d, n, test_days, cum, warm, sw, n_eval, h1, h2 = _eval_market_case(g, c)
+    S, A = 4 + d * n, n + (1 if inv == 1 else 2 if inv == 2 else 0)
+    init = {}
+    for net in ("actor", "critic_1", "critic_2"):
+        for nm in (net, "target_" + net):
+            init[nm] = [torch.from_numpy(g[f"case{c}/init/{nm}.{pn}"]) for pn in layer_names(algo, net)]
+    return DeviceAgent(algo, S, A, h1, h2, 16, 8, precision="fp32", init=init, device=dev)
+
+
+@pytest.mark.parametrize("c", range(4))
+def test_eval_market_matches_reference(golden, dev, c):
+    """rlmd_eval_market vs the reference's eval_market (tests/golden/eval_market.npz:
+    real SAC / TD3 agents, D1 and Dx, inside / outside the action window, injected
+    gaps, unshuffled test slice).  Steps exact; last reward / risk within the
+    fp32-policy tolerance of the oracle test (rtol 1e-6: the GPU and torch-CPU
+    actor forwards differ in summation order); the 14 summary statistics within
+    rtol 1e-5 of the reference's NumPy expressions on its own arrays."""
+    from rlmd_amd.trainer import market_evaluate
+    from tests.test_oracle_golden import _eval_market_case
+
+    g = golden("eval_market.npz")
+    algo, inv, d, n, test_days, cum, warm, sw, n_eval, _, _ = _eval_market_case(g, c)
+    ag = _market_agent(g, c, dev)
+    out = market_evaluate(ag, g[f"case{c}/prices"], inv, d, test_days, g[f"case{c}/gaps"], cum, warm, sw,
+                          shuffle_days=1, device=dev)
+    np.testing.assert_array_equal(out["steps"], g[f"case{c}/steps"])
+    np.testing.assert_allclose(out["reward"], g[f"case{c}/reward"], rtol=1e-6, atol=0)
+    np.testing.assert_allclose(out["risk"], g[f"case{c}/risk_log"][:, 1:], rtol=1e-6, atol=1e-12)
+    ref = oev.market_summary(g[f"case{c}/reward"], g[f"case{c}/steps"], g[f"case{c}/risk_log"])
+    np.testing.assert_allclose(out["stats"], ref, rtol=1e-5, atol=1e-9)
+    # the device summary is NumPy-exact on the same arrays
+    got = oev.market_summary(out["reward"], out["steps"], out["risk_log"])
+    np.testing.assert_array_equal(out["stats"], got)
+
+
+@pytest.mark.parametrize("c", [0, 1])
+def test_eval_market_shuffled_matches_oracle(golden, dev, c):
+    """Test slices re-shuffled in blocks of 3 (Philox block permutations, E8) and
+    a start that would leave the price table refused per lane: GPU vs oracle."""
+    from rlmd_amd.trainer import market_evaluate
+    from tests.test_oracle_golden import _eval_market_case, _golden_actor
+
+    g = golden("eval_market.npz")
+    algo, inv, d, n, test_days, cum, warm, sw, _, _, _ = _eval_market_case(g, c)
+    prices = golden("market.npz")["prices"][:, :n]  # stooq_usei[:600]
+    rng = np.random.default_rng(40 + c)
+    starts = rng.integers(0, prices.shape[0] - test_days - d - 1, size=200)
+    ag = _market_agent(g, c, dev)
+    out = market_evaluate(ag, prices, inv, d, test_days, starts, cum, warm, sw, shuffle_days=3, seed=77, device=dev)
+    rew, steps, risk = oev.market_rollout(algo, _golden_actor(g, c), prices, inv, d, test_days, starts, cum, warm,
+                                          sw, shuffle_days=3, seed=77)
+    np.testing.assert_array_equal(out["steps"], steps)
+    np.testing.assert_allclose(out["reward"], rew, rtol=1e-6, atol=0)
+    np.testing.assert_allclose(out["risk"], risk, rtol=1e-6, atol=1e-12)
+    with pytest.raises(ValueError):
+        market_evaluate(ag, prices, inv, d, test_days, [0, prices.shape[0] - test_days], cum, warm, sw, device=dev)
+
+
+def test_trainer_evaluate_market(golden, dev):
+    """C4's loop shape on a small table: policy steps on market lanes, then
+    eval_market from the lanes' positions (gap 5..20 ahead)."""
+    from rlmd_amd.trainer import VecTrainer
+
+    prices = golden("market.npz")["prices"]  # stooq_usei[:600]
+    tr = VecTrainer("market", "A", 256, n_gambles=3, algo="SAC", k_updates=1, warmup_steps=2, smoothing_window=4,
+                    replay_capacity=256 * 16, precision="fp32", prices=prices, obs_days=1, time_length=12,
+                    shuffle_days=5, sample_days=12 + 1 + 20 + 16 + 2, device=dev)
+    for _ in range(6):
+        tr.step()
+    ev = tr.evaluate_market(n_eval=100, test_days=15)
+    assert ev["steps"].min() >= 1 and ev["steps"].max() <= 15
+    assert np.isfinite(ev["reward"]).all() and np.isfinite(ev["stats"]).all()
+    assert ev["stats"].shape == (14,)

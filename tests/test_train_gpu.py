@@ -39,18 +39,35 @@ def warmup_actions(seed, N, A, t, absw):
     return np.abs(a) if absw else a
 
 
+def _market_kw(golden, obs_days):
+    # stooq_usei[:600]; 12-day episodes so lanes finish and restart inside the test
+    return dict(prices=golden("market.npz")["prices"], obs_days=obs_days, time_length=12 + obs_days - 1,
+                shuffle_days=5, sample_days=12 + obs_days + 40)
+
+
 @pytest.mark.parametrize("env,inv,fam,oinv,n", [("gbm", "A", oe.GBM, oe.INV_A, 1), ("coin", "B", oe.COIN, oe.INV_B, 2),
-                                                ("dice_sh", "C", oe.DICE_SH, oe.INV_C, 1)])
-def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
+                                                ("dice_sh", "C", oe.DICE_SH, oe.INV_C, 1),
+                                                ("market", "B", oe.MARKET, oe.INV_B, 3),
+                                                ("market", "C", oe.MARKET, oe.INV_C, -3)])
+def test_warmup_steps_fill_ring_like_oracle(golden, dev, env, inv, fam, oinv, n):
+    """Warm-up steps (rl_multiplicative.py:192-201, rl_market.py:217-226): Philox
+    action samples (|.| unless GBM / market) through the fused step into the
+    ring, auto-reset of finished lanes (market: new Philox slice + shuffle;
+    n < 0 marks a Dx market env with obs_days 3), episode statistics."""
     from rlmd_amd.trainer import VecTrainer
 
     N, T, seed = 512, 25, 17
+    kw = {}
+    if fam == oe.MARKET:
+        kw = _market_kw(golden, 1 if n > 0 else 3)
+        n = abs(n)
     tr = VecTrainer(env=env, investor=inv, n_lanes=N, n_gambles=n, algo="SAC", k_updates=0, seed=seed,
                     warmup_steps=10_000, smoothing_window=20_000, replay_capacity=N * T, precision="fp32",
-                    device=dev)
-    ora = oe.OracleVecEnv(fam, oinv, N, n, seed=seed)
+                    device=dev, **kw)
+    ora = oe.OracleVecEnv(fam, oinv, N, n, seed=seed, **kw)
     obs = ora.reset()
-    absw = fam != oe.GBM
+    absw = fam not in (oe.GBM, oe.MARKET)
+    at = 1e-45 if fam == oe.MARKET else 1e-30  # market states are O(1e-30) (MAX_VALUE 1e34)
     length = np.ones(N, dtype=np.int64)  # current episode's step index (the env's t)
     exp_n, exp_r, exp_l = 0, 0.0, 0.0
     for t in range(T):
@@ -59,8 +76,8 @@ def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
         ns, r, d, _ = ora.step(a)  # float64 actions, as action_space.sample() gives
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
         np.testing.assert_array_equal(a_r, a.astype(np.float32), err_msg=f"t={t} actions")
-        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s")
-        np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s2")
+        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s")
+        np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s2")
         np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6)
         np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
         obs = ns.copy()
@@ -76,7 +93,7 @@ def test_warmup_steps_fill_ring_like_oracle(dev, env, inv, fam, oinv, n):
             n_ep, r_sum, l_sum, _ = tr.flush_stats().cpu().numpy()
             assert n_ep == exp_n, f"t={t}"
             np.testing.assert_allclose([r_sum, l_sum], [exp_r, exp_l], rtol=1e-12)
-    np.testing.assert_allclose(tr.obs.cpu().numpy(), obs.astype(np.float32), rtol=1e-6, atol=1e-30)
+    np.testing.assert_allclose(tr.obs.cpu().numpy(), obs.astype(np.float32), rtol=1e-6, atol=at)
     st = tr.episode_stats()
     assert st["episodes"] == exp_n
 
