@@ -34,11 +34,12 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
-def env_bytes_per_step(S, A):
+def env_bytes_per_step(S, A, n_assets=0):
     """Algorithmic HBM bytes of one lane-step of the fused env kernel:
     action read 4A + obs read 4S + wealth/time read+write 24 + obs write 4S
-    + replay row (s 4S, a 4A, r 4, s' 4S, done 1)  = 8A + 16S + 29."""
-    return 8 * A + 16 * S + 29
+    + replay row (s 4S, a 4A, r 4, s' 4S, done 1)  = 8A + 16S + 29;
+    market adds the two f64 price gathers per asset (P_t, P_0): 16 n_assets."""
+    return 8 * A + 16 * S + 29 + 16 * n_assets
 
 
 def sac_update_flops(S, A, H1, H2, B):
@@ -55,6 +56,46 @@ def sac_update_flops(S, A, H1, H2, B):
     bwd_a = 2 * (H2 + H1 * H2 + H1 * A)        # critics to the action input
     bwd_a += actor_mac + (H1 * H2 + 2 * A * H2)  # actor dW + dX
     return 2.0 * B * (fwd + bwd_c + bwd_a)
+
+
+def td3_update_flops(S, A, H1, H2, B, actor_every=2):
+    """Dense MLP FLOPs of one TD3 update (algo_td3.py:363-531): target actor fwd
+    + 2 target-critic fwd; both critics fwd + bwd (dW all layers, dX layers 2..3);
+    every `actor_every` updates: actor fwd, critic_1 fwd + bwd to the action,
+    actor bwd (dW + dX)."""
+    X = S + A
+    actor_mac = S * H1 + H1 * H2 + A * H2
+    critic_mac = X * H1 + H1 * H2 + H2
+    per = actor_mac + 2 * critic_mac + 2 * critic_mac + 2 * (critic_mac + H1 * H2 + H2)
+    act = actor_mac + critic_mac + (H2 + H1 * H2 + H1 * A) + actor_mac + H1 * H2 + A * H2
+    return 2.0 * B * (per + act / actor_every)
+
+
+def synthetic_prices(days=9167, n_assets=1, seed=7):
+    """Stand-in for tools/market_data/stooq_snp.npy (9167 x 1 daily closes; the
+    reference's data is not on the GPU box): a geometric random walk with an
+    equity-like daily drift 3e-4 and volatility 1.2 %."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    r = rng.normal(3e-4, 0.012, (days - 1, n_assets))
+    return 100.0 * np.exp(np.vstack([np.zeros((1, n_assets)), np.cumsum(r, 0)]))
+
+
+# BASELINE.json configs (SURVEY §8 C2-C5) as single-GPU workloads.  C2 is the
+# headline; the others run with --config.  Market (C4): train 1000 / test 250
+# days, obs_days 1, shuffle 5 (train) / 3 (eval), gap 5..20 (rl_market.py:54-62).
+CONFIGS = {
+    "c2": dict(env="gbm", investor="A", n=1, algo="SAC", lanes=65536, replay=1 << 20, multi_steps=1,
+               workload="C2: GBM_InvA n_gambles=1 (S=5,A=1), SAC 256/256, replay 1M/GPU"),
+    "c3": dict(env="dice_sh", investor="A", n=1, algo="TD3", lanes=65536, replay=1 << 20, multi_steps=1,
+               workload="C3: Dice_SH_InvA (key 18, S=6,A=2), TD3 400/300, B=200/k=100, replay 1M/GPU"),
+    "c4": dict(env="market", investor="A", n=1, algo="SAC", lanes=8192, replay=1 << 20, multi_steps=1,
+               workload="C4: Market_InvA_D1 on a synthetic 9167-day price table (stooq_snp shape), "
+                        "train 1000 d, shuffle 5, SAC 256/256, 8192 lanes/GPU (one seed shard per GPU)"),
+    "c5": dict(env="gbm", investor="A", n=1, algo="TD3", lanes=65536, replay=1 << 24, multi_steps=5,
+               workload="C5: GBM_InvA, TD3 400/300, multi-step n=5 (A), replay 16,777,216 transitions/GPU"),
+}
 
 
 def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
@@ -149,10 +190,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--lanes", type=int, default=65536)
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--lanes", type=int, default=None)
     ap.add_argument("--k-updates", type=int, default=8)
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
-    ap.add_argument("--replay", type=int, default=1 << 20)
+    ap.add_argument("--replay", type=int, default=None)
+    ap.add_argument("--loss", default="MSE", help="critic loss (C3 sweeps MSE/HUB/MAE/HSC)")
+    ap.add_argument("--multi-steps", type=int, default=None)
+    ap.add_argument("--eval-every", type=int, default=1000,
+                    help="vector steps between evaluations (eval_freq 1e3, main.py); amortised into value")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -173,10 +219,20 @@ def main():
     from rlmd_amd.trainer import VecTrainer
     import ctypes as C
 
-    N, K = args.lanes, args.k_updates
-    tr = VecTrainer(env="gbm", investor="A", n_lanes=N, algo="SAC", k_updates=K, replay_capacity=args.replay,
-                    seed=420 + rank, warmup_steps=0, smoothing_window=0, precision=args.precision, device=dev,
-                    init_seed=420 + rank)
+    cfg = CONFIGS[args.config]
+    N, K = args.lanes or cfg["lanes"], args.k_updates
+    replay = args.replay or cfg["replay"]
+    ms_n = args.multi_steps or cfg["multi_steps"]
+    kw = {}
+    if cfg["env"] == "market":
+        kw = dict(prices=synthetic_prices(), obs_days=1, time_length=1000, shuffle_days=5,
+                  sample_days=1000 + 250 + 1 + 20 - 1)
+    if ms_n > 1:
+        replay = (replay // N) * N  # per-lane rings: capacity a multiple of the lanes
+    tr = VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"],
+                    loss=args.loss, k_updates=K, replay_capacity=replay, seed=420 + rank, warmup_steps=0,
+                    smoothing_window=0, precision=args.precision, device=dev, init_seed=420 + rank,
+                    multi_steps=ms_n, dynamics="A", **kw)
     for _ in range(args.warmup):
         tr.step()
     torch.cuda.synchronize()
@@ -197,6 +253,18 @@ def main():
     cnt = (C.c_int64 * 3)()
     _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
     _abi.check(_abi.lib().rlmd_profile_enable(0))
+    # evaluation (eval_multiplicative / eval_market, 100 episodes) every eval_every
+    # vector steps, timed on its own and amortised into the timed region
+    ev = (lambda: tr.evaluate_market(n_eval=100, test_days=250)) if cfg["env"] == "market" else \
+        (lambda: tr.evaluate(n_eval=100, max_steps=100))
+    ev()
+    torch.cuda.synchronize()
+    te = time.perf_counter()
+    ev()
+    torch.cuda.synchronize()
+    eval_s = time.perf_counter() - te
+    if args.eval_every > 0:
+        elapsed += eval_s * args.steps / args.eval_every
     t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(N * args.steps), world, dev)
     total_steps = float(slab_all[:, 4].sum().item())
     value = total_steps / t_max
@@ -205,13 +273,15 @@ def main():
     env_ms = ms[1] / max(cnt[1], 1)
     learn_ms = ms[2] / max(cnt[2], 1)
     act_ms = ms[0] / max(cnt[0], 1)
-    env_bytes = env_bytes_per_step(S, A) * N
+    env_bytes = env_bytes_per_step(S, A, cfg["n"] if cfg["env"] == "market" else 0) * N
     achieved = env_bytes / (env_ms * 1e-3) / 1e9
     pmc = load_traffic()
     traffic = None
-    if pmc and pmc.get("lanes") == N:
+    if pmc and pmc.get("lanes") == N and pmc.get("config", "c2") == args.config:
         traffic = pmc.get("hbm_bytes_per_launch")
-    flops = K * sac_update_flops(S, A, 256, 256, tr.batch)
+    H1, H2 = tr.agent.h1, tr.agent.h2
+    upd = sac_update_flops if cfg["algo"] == "SAC" else td3_update_flops
+    flops = K * upd(S, A, H1, H2, tr.batch)
     mfma_tf = flops / (learn_ms * 1e-3) / 1e12 if learn_ms > 0 else None
 
     if rank == 0:
@@ -220,7 +290,9 @@ def main():
             "value": value, "unit": "env steps/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
-            "config": {"workload": "C2: GBM_InvA n_gambles=1 (S=5,A=1), SAC 256/256, replay 1M/GPU",
+            "config": {"workload": cfg["workload"], "config": args.config, "critic_loss": args.loss,
+                       "replay_per_gpu": replay, "multi_steps": ms_n,
+                       "eval_ms_per_event": 1e3 * eval_s, "eval_every_vector_steps": args.eval_every,
                        "lanes_per_gpu": N, "global_lanes": N * world, "k_updates_per_vector_step": K,
                        "mini_batch": tr.batch, "topk": tr.topk, "utd_updates_per_env_step": K / N,
                        "parallelism": f"independent seeds x{world} (no data-path collective)",
@@ -229,12 +301,12 @@ def main():
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms},
-            "roofline_mfma": {"kernel": "learn phase (K SAC updates, all kernels)", "bound": "mfma",
+            "roofline_mfma": {"kernel": f"learn phase (K {cfg['algo']} updates, all kernels)", "bound": "mfma",
                               "achieved": mfma_tf, "peak": BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3,
                               "unit": "TFLOP/s", "frac": (mfma_tf or 0) / (BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3),
                               "algorithmic_flops_per_step": flops, "avg_phase_ms": learn_ms},
         }
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_seconds)
         else:
             out["cpu_baseline"] = None

@@ -99,6 +99,16 @@ int rlmd_eval_rollout(rlmd_env_t env, const float* actions_dev, int32_t max_step
 int rlmd_eval_stats(const double* reward_dev, const int32_t* steps_dev, const double* risk_dev, int32_t n,
                     int32_t risk_dim, int32_t investor, double* stats_dev, void* stream);
 
+/* Replaces agent_shadow_mean / shadow_means (tools/utils.py:374-400, :441-471):
+ * for each of `rows` learn() statistic rows (stats_dev f32, leading dimension ld,
+ * loss[11] first: mean 0-1, min 2-3, max 4-5, tail index 8-9) the power-law
+ * shadow mean of critic 1 and 2 in float32, as the reference computes it on its
+ * float32 loss entries (the empirical mean when the tail index is >= 1); written
+ * to shadow_dev [rows, 2] with leading dimension ldo (stats_dev + 6 with ldo = ld
+ * fills loss[6:8] in place, as the reference's loss[6:8] = ... does). */
+int rlmd_shadow_means(const float* stats_dev, int32_t rows, int32_t ld, float low_mul, float high_mul,
+                      float* shadow_dev, int32_t ldo, void* stream);
+
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
 /* Market lanes' episode start rows (i32 [N]) read back (eval_market's

@@ -73,9 +73,18 @@ class VecTrainer:
         for _ in range(n_steps):
             self.step()
 
-    def last_stats(self):
-        """loss[11] | logtemp | loss_params[4] of the last update (numpy f64)."""
-        return self.stats[max(self.cfg.k_updates, 1) - 1].double().cpu().numpy()
+    def last_stats(self, shadow=False, low_mul=1.0, high_mul=10.0):
+        """loss[11] | logtemp | loss_params[4] of the last update (numpy f64).
+        shadow: first fill loss[6:8] with the critics' power-law shadow means on
+        the device, as the reference's loss[6:8] = agent_shadow_mean(inputs, loss)
+        does at every evaluation and episode end (tools/utils.py:441-471;
+        shadow_low_mul 1e0 / shadow_high_mul 1e1, main.py:216-217)."""
+        k = max(self.cfg.k_updates, 1) - 1
+        if shadow:
+            row = self.stats[k]
+            check(_abi.lib().rlmd_shadow_means(ptr(row), 1, 16, float(low_mul), float(high_mul),
+                                               row.data_ptr() + 6 * row.element_size(), 16, stream_ptr()))
+        return self.stats[k].double().cpu().numpy()
 
     def evaluate(self, n_eval=100, max_steps=100):
         """eval_multiplicative (tools/eval_episodes.py:176-399) on the device: n_eval

@@ -408,8 +408,32 @@ def shadow_fixtures():
     acts = np.linspace(-0.99, 0.99, 11)
     steps = np.array([0, 500, 1000, 1001, 1200, 1500, 1999, 2000])
     win = np.stack([ut.action_window(acts.copy(), 0.99, -0.99, s, 2000, 1000) for s in steps])
+    # agent_shadow_mean on float32 loss rows, as learn() returns them (0-d float32
+    # arrays): tail indices below / above 1, negative, tiny and huge maxima
+    rng = np.random.default_rng(17)
+    rows = []
+    for i in range(64):
+        l = np.full(11, np.nan, dtype=np.float32)
+        l[0:2] = rng.uniform(0.1, 5.0, 2)
+        l[2:4] = rng.uniform(1e-4, 0.1, 2)
+        l[4:6] = 10 ** rng.uniform(-3, 3, 2)
+        l[8:10] = rng.uniform(-2.0, 1.5, 2)
+        rows.append(l)
+    rows[0][8:10] = [0.999, 1.0]
+    rows[1][4:6] = [1e-5, 1e-7]  # alpha / high large: exp overflows (the reference's inf / nan)
+    rows[2][8:10] = [np.nan, 0.5]
+    rows = np.stack(rows)
+    loss32 = [[np.float32(v) for v in r] for r in rows]
+    agent = []
+    with np.errstate(all="ignore"):
+        for r in loss32:
+            sh1, sh2 = ut.agent_shadow_mean({"shadow_low_mul": 1e0, "shadow_high_mul": 1e1}, r)
+            agent.append([sh1, sh2])
+    agent = np.array(agent)
+    assert agent.dtype == np.float32
     return {"alpha": alphas, "min": mins, "max": maxs, "shadow": sh,
-            "aw_actions": acts, "aw_steps": steps, "aw_out": win}
+            "aw_actions": acts, "aw_steps": steps, "aw_out": win,
+            "loss_rows": rows, "agent_shadow": agent}
 
 
 # ----------------------------------------------------------------------------

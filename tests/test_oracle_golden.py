@@ -227,3 +227,18 @@ def test_eval_market_matches_reference(golden, c):
     st = oev.market_summary(rew, steps, np.concatenate([g[f"case{c}/risk_log"][:, :1], risk], 1))
     ref = oev.market_summary(g[f"case{c}/reward"], g[f"case{c}/steps"], g[f"case{c}/risk_log"])
     np.testing.assert_allclose(st, ref, rtol=1e-5, atol=1e-9)
+
+
+# ---------------------------------------------------------------- A9 shadow means
+def test_shadow_means_match_reference(golden):
+    """oracle.shadow vs the reference's shadow_means (float64 grid) and
+    agent_shadow_mean on float32 loss rows (its float32 dtype flow): exact up to
+    NumPy's own float32 exp / pow, i.e. bit-equal here."""
+    from oracle import shadow as osh
+
+    g = golden("shadow.npz")
+    got = np.array([osh.shadow_means(a, lo, hi, 1.0, 10.0, dtype=np.float64)
+                    for a, lo, hi in zip(g["alpha"], g["min"], g["max"])])
+    np.testing.assert_allclose(got, g["shadow"], rtol=1e-14)
+    rows = np.stack([osh.agent_shadow_mean(r) for r in g["loss_rows"]])
+    np.testing.assert_array_equal(rows, g["agent_shadow"])
