@@ -262,7 +262,6 @@ struct rlmd_agent_s {
   int32_t* kb_eff = nullptr;
   size_t wcopy_bytes = 0;  // per copy
   float *act_h1 = nullptr, *act_h2 = nullptr;
-  unsigned short* act_w2bf = nullptr;  // fused acting: bf16 copy of the actor's fc2.weight
   int64_t act_cap = 0;
   int64_t host_cntr = 0;
   // fused optimiser epilogue of the weight-gradient GEMM (rlmd_gemm.h)
@@ -715,7 +714,8 @@ float* stats_slot(rlmd_agent_s* ag, float* stats, int i) {
   return stats ? stats + 16 * (int64_t)i : ag->sc.stats;
 }
 
-int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipStream_t st) {
+int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipStream_t st,
+                  bool copies_current = false) {
   const rlmd_agent_cfg& c = ag->cfg;
   const ReplayView v = replay_view(rb);
   const int64_t mem = replay_mem_idx(rb);
@@ -738,7 +738,7 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
     RLMD_HIP(hipMalloc(&ag->kb_eff, sizeof(int32_t) * KB));
     ag->kcap = k;
   }
-  RLMD_TRY(refresh_copies(ag, st));
+  if (!copies_current) RLMD_TRY(refresh_copies(ag, st));
   // all K mini-batches at once: the ring does not change during the K updates;
   // batch i draws with counter learn_step_cntr + i (as K single draws would)
   const bool ms = v.n_steps > 1;
@@ -754,15 +754,23 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
   return 0;
 }
 
+// copies_current: the compute copies already match the f32 masters (the fused
+// training step refreshes them once at its start); otherwise the actor's copy is
+// re-derived first, as the host may have written parameters since the last update.
 int agent_act(rlmd_agent_s* ag, const float* obs, int64_t n, float* actions, int mode,
-              uint64_t noise_ctr, const float* eps, hipStream_t st) {
+              uint64_t noise_ctr, const float* eps, hipStream_t st, bool copies_current = false) {
   const rlmd_agent_cfg& c = ag->cfg;
   if (n <= 0) return 0;
   RLMD_CHECK(n <= INT32_MAX, "too many rows");
   static const bool fused_ok = getenv("RLMD_NO_FUSED_ACT") == nullptr;
   if (fused_ok && fused_act_supported(c)) {
-    if (!ag->act_w2bf) RLMD_HIP(hipMalloc(&ag->act_w2bf, sizeof(unsigned short) * c.h1 * c.h2));
-    return fused_act_launch(c, obs, n, actions, ag->params + ag->off_actor, ag->actor, ag->act_w2bf, mode,
+    if (!copies_current) {
+      const RowNet an = row_net(ag, SLOT_ACTOR);
+      const CopyJob job{an.p + ag->actor.w2, copy_wc(ag, SLOT_ACTOR), copy_wt(ag, SLOT_ACTOR)};
+      RLMD_TRY(w2_copies_launch(&job, 1, row_dims(ag), st));
+    }
+    return fused_act_launch(c, obs, n, actions, ag->params + ag->off_actor, ag->actor,
+                            static_cast<const unsigned short*>(copy_wc(ag, SLOT_ACTOR)), mode,
                             c.seed ^ 0xac7ac7ac7ull, (uint32_t)noise_ctr, eps, st);
   }
   if (n > ag->act_cap) {
@@ -921,7 +929,6 @@ int rlmd_agent_destroy(rlmd_agent_t ag) {
   for (void* p : ag->allocs) (void)hipFree(p);
   if (ag->act_h1) (void)hipFree(ag->act_h1);
   if (ag->act_h2) (void)hipFree(ag->act_h2);
-  if (ag->act_w2bf) (void)hipFree(ag->act_w2bf);
   for (void* p : {(void*)ag->kb_s, (void*)ag->kb_a, (void*)ag->kb_r, (void*)ag->kb_s2, (void*)ag->kb_xsa,
                   (void*)ag->kb_done, (void*)ag->kb_idx, (void*)ag->kb_eff})
     if (p) (void)hipFree(p);
@@ -949,8 +956,9 @@ int rlmd_eval_market(rlmd_env_t env, rlmd_agent_t ag, const int32_t* start_dev, 
   }
   RLMD_TRY(rlmd::env_market_eval_reset(env, start_dev, obs_dev, reward_dev, steps_dev, live_dev, st));
   const int T = rlmd::env_episode_steps(env);
+  RLMD_TRY(rlmd::refresh_copies(ag, st));
   for (int t = 0; t < T; ++t) {
-    RLMD_TRY(rlmd::agent_act(ag, obs_dev, N, actions_dev, 1, 0, nullptr, st));  // eval_next_action
+    RLMD_TRY(rlmd::agent_act(ag, obs_dev, N, actions_dev, 1, 0, nullptr, st, true));  // eval_next_action
     RLMD_TRY(rlmd::env_market_eval_step(env, actions_dev, window ? 1 : 0, lo, hi, obs_dev, reward_dev, steps_dev,
                                         risk_dev, live_dev, st));
   }
@@ -1072,7 +1080,9 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   if (!random) {
     RLMD_CHECK(ag, "policy acting needs an agent");
     RLMD_TRY(g_prof.record(0, 0, st));
-    RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st));
+    // one refresh of every compute copy serves the acting and the K updates below
+    RLMD_TRY(rlmd::refresh_copies(ag, st));
+    RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st, true));
     RLMD_TRY(g_prof.record(0, 1, st));
   }
   // action_window (tools/utils.py:345-373): only warmup < cum_step <= smoothing_window
@@ -1092,7 +1102,7 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   rlmd::replay_advance(rb, N);
   if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch) {
     RLMD_TRY(g_prof.record(2, 0, st));
-    RLMD_TRY(rlmd::agent_learn_k(ag, rb, cfg->k_updates, stats, st));
+    RLMD_TRY(rlmd::agent_learn_k(ag, rb, cfg->k_updates, stats, st, !random));
     RLMD_TRY(g_prof.record(2, 1, st));
   }
   return 0;

@@ -228,10 +228,11 @@ struct CopyJob {
 };
 int w2_copies_launch(const CopyJob* jobs, int n, const RowDims& d, hipStream_t st);
 
-// act.hip: fused bf16 acting (obs -> actions in one launch) for the headline nets.
+// act.hip: fused bf16 acting (obs -> actions in one launch) for the headline nets;
+// w2bf = the actor's bf16 compute copy wc (fragment-major [H2p][H1p]).
 bool fused_act_supported(const rlmd_agent_cfg& c);
 int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float* actions,
-                     const float* actor_params, const NetOff& off, unsigned short* w2bf, int mode,
+                     const float* actor_params, const NetOff& off, const unsigned short* w2bf, int mode,
                      uint64_t seed, uint32_t ctr, const float* eps, hipStream_t st);
 
 }  // namespace rlmd

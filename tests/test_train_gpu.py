@@ -180,19 +180,21 @@ def _bf16_act_reference(p, obs, eps, algo, max_action, ls_min, ls_max, noise):
     return torch.tanh(mu) * max_action, torch.tanh(mu + eps * ls.exp()) * max_action
 
 
-@pytest.mark.parametrize("algo,S,A", [("SAC", 5, 1), ("SAC", 6, 2), ("TD3", 5, 1)])
-def test_fused_bf16_act_matches_emulated_reference(dev, algo, S, A):
+@pytest.mark.parametrize("algo,S,A,h1,h2", [("SAC", 5, 1, 256, 256), ("SAC", 6, 2, 256, 256), ("TD3", 5, 1, 256, 256),
+                                            ("SAC", 5, 1, 128, 256), ("TD3", 6, 2, 400, 300), ("TD3", 5, 1, 400, 300)])
+def test_fused_bf16_act_matches_emulated_reference(dev, algo, S, A, h1, h2):
     """act.hip (one launch: VALU layer 1, bf16 MFMA layer 2, fused heads + sampling)
     against the same numerics restated in torch (bf16 rounding emulated exactly).  The
     f32 accumulation order of layer 1 differs, which now and then flips one h1 element
     to the neighbouring bf16 value: >= 99.9% of actions within 1e-4, all within 1e-3.
-    The ragged last block (4099 rows) exercises the row guard."""
+    The ragged last block (4099 rows) exercises the row guard; TD3 400/300 the
+    zero-padded K (416) and column (320) tails of the compute copy."""
     from rlmd_amd.agent import DeviceAgent, reference_init
 
-    init = reference_init(algo, S, A, 256, 256, seed=3)
-    ag = DeviceAgent(algo, S, A, 256, 256, 512, 256, init=init, precision="bf16", device=dev)
-    p, t = _flat_init(algo, S, A, 256, 256, init)
-    ora = ol.OracleLearner(algo, S, A, 256, 256, 512, 256, "MSE", p, t)
+    init = reference_init(algo, S, A, h1, h2, seed=3)
+    ag = DeviceAgent(algo, S, A, h1, h2, 512, 256, init=init, precision="bf16", device=dev)
+    p, t = _flat_init(algo, S, A, h1, h2, init)
+    ora = ol.OracleLearner(algo, S, A, h1, h2, 512, 256, "MSE", p, t)
     rng = np.random.default_rng(1)
     n = 4099
     obs = torch.from_numpy(rng.standard_normal((n, S)).astype(np.float32))
