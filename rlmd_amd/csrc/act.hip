@@ -29,11 +29,36 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int kRows = 64;
 constexpr int kMaxA = 2;
 
+#ifdef RLMD_TIMING
+// experiment builds only (tools/ts_probe.py act): per-workgroup checkpoints of
+// thread 0 — [0] s_memrealtime at entry, [1..5] s_memtime after each phase,
+// [6] s_memrealtime at exit; up to 4096 workgroups
+__device__ unsigned long long g_ts_act[4096][8];
+#define RLMD_TSA(i, v)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_ts_act[blockIdx.x][i] = (v);       \
+  } while (0)
+#else
+#define RLMD_TSA(i, v) \
+  do {                 \
+  } while (0)
+#endif
+
+// RNE f32 -> bf16, NaN kept quiet; branch-free (a select, not a divergent branch)
 __device__ __forceinline__ unsigned short f2bf_rne(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+  const unsigned u = __float_as_uint(f);
+  const unsigned r = (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+  return (unsigned short)((u & 0x7fffffffu) > 0x7f800000u ? ((u >> 16) | 0x40u) : r);
+}
+
+// sum over the 16 lanes of a DPP row (every lane gets it): quad butterflies, then
+// half-row and row mirrors — VALU-rate lane moves instead of ds_bpermute shuffles
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
+  return v;
 }
 
 struct FusedActArgs {
@@ -50,40 +75,80 @@ struct FusedActArgs {
   int32_t dist;  // SAC sampler (rlmd_policy.h)
 };
 
-template <int H1P, int NB>
+// Layer-1 LDS operands, zero padded so every MFMA operand read is unconditional:
+//   w1g [SP][16][NTP]: W1[16 t + j][k] at (k * 16 + j) * NTP + t — a lane's 8
+//                      tiles of one K row are 2 contiguous 16-B reads, and the
+//                      pitch NTP (= 4 mod 8 dwords... 20 / 36) keeps the 16
+//                      lanes of a K row on distinct bank quads;
+//   b1  [H1P];
+//   obs [64][SP].
+template <int H1P>
+struct L1Tiles {
+  static constexpr int NT = H1P / 16;
+  static constexpr int NTP = (NT + 7) / 8 * 8 + 4;
+};
+
+template <int H1P, int NB, int SP>
 __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
   constexpr int HP = H1P + 8;  // bf16 row pitch: 16-B aligned fragment reads
+  constexpr int NT = L1Tiles<H1P>::NT, NTP = L1Tiles<H1P>::NTP;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned short* h1s = reinterpret_cast<unsigned short*>(smem);                 // [64][HP]
   float* part = reinterpret_cast<float*>(smem + kRows * HP * 2);                 // [4][64][2A]
-  float* w1s = part + 4 * kRows * 2 * kMaxA;                                      // [H1][S] + b1[H1]
   const int H1 = a.H1, H2 = a.H2;
-  float* obs_s = w1s + H1 * a.S + H1;                                             // [64][S]
+  float* w1s = part + 4 * kRows * 2 * kMaxA;                                      // w1g [SP][16][NTP]
+  float* b1s = w1s + SP * 16 * NTP;                                               // [H1P]
+  float* obs_s = b1s + H1P;                                                       // [64][SP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * kRows;
   const NetOff& o = a.off;
   const int S = a.S, A = a.A;
-  // -- stage W1, b1 (contiguous in torch order) and this block's observations:
-  //    8 loads per thread per operand in flight before any LDS store (one round
-  //    trip at these sizes); rows past n read 0 through the range check
+  RLMD_TSA(0, __builtin_amdgcn_s_memrealtime());
+  RLMD_TSA(1, __builtin_amdgcn_s_memtime());
+  // epilogue operands (fc2 bias, head weights of this wave's columns; columns
+  // past H2 read 0): issued first, so their latency hides under layers 1-2
+  const int nh = a.algo == RLMD_SAC ? 2 * A : A;  // heads: pi (+ log_scale)
+  const int col0 = 16 * NB * wave;
+  float hw[NB][2 * kMaxA];
+  float b2v[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int c = col0 + 16 * nb + (lane & 15);
+    const bool live = c < H2;
+    b2v[nb] = live ? a.params[o.b2 + c] : 0.f;
+#pragma unroll
+    for (int h = 0; h < 2 * kMaxA; ++h) {
+      const int64_t base = h < A ? o.w3 + (int64_t)h * H2 : o.w4 + (int64_t)(h - A) * H2;
+      hw[nb][h] = live && h < nh ? a.params[base + c] : 0.f;
+    }
+  }
+  // -- stage W1, b1 and this block's observations into the zero-padded LDS
+  //    tiles (destination-indexed gathers, compile-time index math; padding
+  //    reads 0 through the predicate), 8 loads per thread in flight per pass
   {
-    const int nW = H1 * S + H1, nO = kRows * S;
+    constexpr int nW = SP * 16 * NTP + H1P, nO = kRows * SP;
+    constexpr int nmax = nW > nO ? nW : nO;
     const int rows = a.n - row0 < kRows ? a.n - row0 : kRows;
-    const __amdgpu_buffer_rsrc_t rw = rlmd_rsrc(a.params + o.w1, (int64_t)nW * 4);
+    const __amdgpu_buffer_rsrc_t rw = rlmd_rsrc(a.params + o.w1, (int64_t)(H1 * S + H1) * 4);
     const __amdgpu_buffer_rsrc_t ro = rlmd_rsrc(a.obs + (int64_t)row0 * S, (int64_t)rows * S * 4);
-    const int nmax = nW > nO ? nW : nO;
     for (int base = 0; base < nmax; base += 8 * 256) {
       float vw[8], vo[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int e = base + j * 256 + tid;
-        vw[j] = rlmd_ldf(rw, e, e < nW);
-        vo[j] = rlmd_ldf(ro, e, e < nO);
+        const bool isb = e >= SP * 16 * NTP;  // the b1 tail
+        const int k = e / (16 * NTP), jt = e - k * (16 * NTP);
+        const int jj = jt / NTP, t = jt - jj * NTP;
+        const int c = isb ? e - SP * 16 * NTP : 16 * t + jj;
+        const bool wl = e < nW && c < H1 && (isb || (t < NT && k < S));
+        vw[j] = rlmd_ldf(rw, isb ? H1 * S + c : c * S + k, wl);
+        const int r = e / SP, ko = e - r * SP;
+        vo[j] = rlmd_ldf(ro, r * S + ko, e < nO && ko < S && r < rows);
       }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int e = base + j * 256 + tid;
-        if (e < nW) w1s[e] = vw[j];
+        if (e < nW) w1s[e] = vw[j];  // b1 follows w1g contiguously
         if (e < nO) obs_s[e] = vo[j];
       }
     }
@@ -96,49 +161,58 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) bnext[nb] = wf[nb * nS * 64];
   __syncthreads();
-  // -- layer 1 on the VALU (K = S is tiny), bf16 into LDS; padded units are 0.
-  //    For S <= 16 each thread keeps its unit's fc1 row in registers and sweeps
-  //    rows reading the observations as LDS broadcasts.
-  if (S <= 16) {
-    constexpr int NR = H1P >= 256 ? 1 : 256 / H1P;  // threads per hidden unit
-    constexpr int UPT = H1P >= 256 ? (H1P + 255) / 256 : 1;  // hidden units per thread
+  RLMD_TSA(2, __builtin_amdgcn_s_memtime());
+  // -- layer 1 on the f32 MFMA (v_mfma_f32_16x16x4f32, K = SP in steps of 4),
+  //    computed transposed (h1^T = W1 obs^T) so a lane ends with 4 consecutive
+  //    units of one row: one 8-B LDS store per tile.  Wave w owns rows
+  //    [16w, 16w + 16) and all H1P units in 16-wide tiles, in groups of 8 tiles
+  //    whose operands arrive as 16-B LDS reads and whose MFMAs issue back to back.
+  {
+    typedef float f32x8 __attribute__((ext_vector_type(8)));
+    const int j = lane & 15, kl = lane >> 4;
+    const int ra = 16 * wave + j;
 #pragma unroll
-    for (int u = 0; u < UPT; ++u) {
-      const int c = H1P >= 256 ? tid + 256 * u : tid % H1P, rg = H1P >= 256 ? 0 : tid / H1P;
-      if (c < H1P) {
-        const bool live = c < H1;
-        float w[16];
+    for (int t0 = 0; t0 < NT; t0 += 8) {
+      f32x4 h[8];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) w[k] = live && k < S ? w1s[c * S + k] : 0.f;
-        const float b = live ? w1s[H1 * S + c] : 0.f;
-        for (int r = rg; r < kRows; r += NR) {
-          float acc = b;
+      for (int u = 0; u < 8; ++u) h[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float av[SP / 4];
+      f32x8 bv[SP / 4];
 #pragma unroll
-          for (int k = 0; k < 16; ++k)
-            if (k < S) acc = fmaf(obs_s[r * S + k], w[k], acc);
-          h1s[r * HP + c] = f2bf_rne(fmaxf(acc, 0.f));
+      for (int ks = 0; ks < SP / 4; ++ks) {
+        av[ks] = obs_s[ra * SP + 4 * ks + kl];
+        bv[ks] = *reinterpret_cast<const f32x8*>(&w1s[((4 * ks + kl) * 16 + j) * NTP + t0]);
+      }
+      f32x4 bias[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (t0 + u < NT) bias[u] = *reinterpret_cast<const f32x4*>(&b1s[16 * (t0 + u) + 4 * kl]);
+#pragma unroll
+      for (int ks = 0; ks < SP / 4; ++ks)
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (t0 + u < NT) h[u] = __builtin_amdgcn_mfma_f32_16x16x4f32(bv[ks][u], av[ks], h[u], 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (t0 + u < NT) {
+          uint2 pk;
+          pk.x = (uint32_t)f2bf_rne(fmaxf(h[u][0] + bias[u][0], 0.f)) |
+                 ((uint32_t)f2bf_rne(fmaxf(h[u][1] + bias[u][1], 0.f)) << 16);
+          pk.y = (uint32_t)f2bf_rne(fmaxf(h[u][2] + bias[u][2], 0.f)) |
+                 ((uint32_t)f2bf_rne(fmaxf(h[u][3] + bias[u][3], 0.f)) << 16);
+          *reinterpret_cast<uint2*>(&h1s[ra * HP + 16 * (t0 + u) + 4 * kl]) = pk;
         }
       }
     }
-  } else {
-    for (int e = tid; e < kRows * H1P; e += 256) {
-      const int r = e / H1P, c = e % H1P;
-      float acc = 0.f;
-      if (c < H1) {
-        acc = w1s[H1 * S + c];
-        for (int k = 0; k < S; ++k) acc = fmaf(obs_s[r * S + k], w1s[c * S + k], acc);
-      }
-      h1s[r * HP + c] = f2bf_rne(fmaxf(acc, 0.f));
-    }
   }
   __syncthreads();
+  RLMD_TSA(3, __builtin_amdgcn_s_memtime());
   // -- layer 2: 64 rows x 16 NB columns per wave, K = H1P in steps of 32
   f32x4 acc[4][NB];
 #pragma unroll
   for (int m = 0; m < 4; ++m)
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) acc[m][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int col0 = 16 * NB * wave;
   const int kq = 8 * (lane >> 4);
 #pragma unroll 2
   for (int k0 = 0; k0 < H1P; k0 += 32) {
@@ -157,22 +231,9 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
         acc[m][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bcur[nb], acc[m][nb], 0, 0, 0);
     }
   }
+  RLMD_TSA(4, __builtin_amdgcn_s_memtime());
   // -- epilogue: relu(h2 + b2) . heads, partial per row over this wave's columns
   //    (columns past H2 have zero weights and biases)
-  const int nh = a.algo == RLMD_SAC ? 2 * A : A;  // heads: pi (+ log_scale)
-  float hw[NB][2 * kMaxA];
-  float b2v[NB];
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    const int c = col0 + 16 * nb + (lane & 15);
-    const bool live = c < H2;
-    b2v[nb] = live ? a.params[o.b2 + c] : 0.f;
-#pragma unroll
-    for (int h = 0; h < 2 * kMaxA; ++h) {
-      const int64_t base = h < A ? o.w3 + (int64_t)h * H2 : o.w4 + (int64_t)(h - A) * H2;
-      hw[nb][h] = live && h < nh ? a.params[base + c] : 0.f;
-    }
-  }
 #pragma unroll
   for (int m = 0; m < 4; ++m) {
 #pragma unroll
@@ -187,22 +248,18 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
         for (int h = 0; h < 2 * kMaxA; ++h) ph[h] = fmaf(v, hw[nb][h], ph[h]);
       }
 #pragma unroll
-      for (int h = 0; h < 2 * kMaxA; ++h) {
-        float c = ph[h];
-        c += __shfl_xor(c, 1, 64);
-        c += __shfl_xor(c, 2, 64);
-        c += __shfl_xor(c, 4, 64);
-        c += __shfl_xor(c, 8, 64);
-        ph[h] = c;
-      }
+      for (int h = 0; h < 2 * kMaxA; ++h)
+        if (h < nh) ph[h] = row16_sum(ph[h]);
       if ((lane & 15) == 0) {
         const int r = 16 * m + 4 * (lane >> 4) + rg;
 #pragma unroll
-        for (int h = 0; h < 2 * kMaxA; ++h) part[(wave * kRows + r) * 2 * kMaxA + h] = ph[h];
+        for (int h = 0; h < 2 * kMaxA; ++h)
+          if (h < nh) part[(wave * kRows + r) * 2 * kMaxA + h] = ph[h];
       }
     }
   }
   __syncthreads();
+  RLMD_TSA(5, __builtin_amdgcn_s_memtime());
   // -- per row: sum the 4 wave partials, sample, write the action
   if (tid < kRows && row0 + tid < a.n) {
     const int r = tid, b = row0 + tid;
@@ -228,6 +285,7 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
       a.actions[(int64_t)b * A + j] = act;
     }
   }
+  RLMD_TSA(6, __builtin_amdgcn_s_memrealtime());
 }
 
 }  // namespace
@@ -242,7 +300,7 @@ static bool fused_shape(const rlmd_agent_cfg& c, int& h1p, int& nb) {
 bool fused_act_supported(const rlmd_agent_cfg& c) {
   int h1p, nb;
   return c.precision == RLMD_BF16 && fused_shape(c, h1p, nb) && (c.h2 + 31) / 32 * 32 <= 16 * 4 * nb &&
-         c.action_dim <= kMaxA && c.state_dim <= 64;
+         c.action_dim <= kMaxA && c.state_dim <= 16;
 }
 
 int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float* actions,
@@ -273,16 +331,36 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
   a.noise_std = c.policy_noise;
   a.dist = c.policy_dist;
   const dim3 grid((unsigned)((n + kRows - 1) / kRows));
-  const size_t lds_bytes = (size_t)kRows * (h1p + 8) * 2 + 4 * kRows * 2 * kMaxA * 4 +
-                           ((size_t)c.h1 * c.state_dim + c.h1 + kRows * c.state_dim) * 4;
+  const int sp = c.state_dim <= 8 ? 8 : 16;
+  auto lds = [&](int ntp) {
+    return (size_t)kRows * (h1p + 8) * 2 + 4 * kRows * 2 * kMaxA * 4 + ((size_t)sp * 16 * ntp + h1p + kRows * sp) * 4;
+  };
+#define ACT_LAUNCH(H1P_, NB_, SP_)                                                                  \
+  hipLaunchKernelGGL((fused_act_kernel<H1P_, NB_, SP_>), grid, dim3(256), lds(L1Tiles<H1P_>::NTP), st, a)
   if (h1p == 256)
-    hipLaunchKernelGGL((fused_act_kernel<256, 4>), grid, dim3(256), lds_bytes, st, a);
+  {
+    if (sp == 8) ACT_LAUNCH(256, 4, 8);
+    else ACT_LAUNCH(256, 4, 16);
+  }
   else if (h1p == 128)
-    hipLaunchKernelGGL((fused_act_kernel<128, 4>), grid, dim3(256), lds_bytes, st, a);
+  {
+    if (sp == 8) ACT_LAUNCH(128, 4, 8);
+    else ACT_LAUNCH(128, 4, 16);
+  }
   else
-    hipLaunchKernelGGL((fused_act_kernel<416, 5>), grid, dim3(256), lds_bytes, st, a);
+  {
+    if (sp == 8) ACT_LAUNCH(416, 5, 8);
+    else ACT_LAUNCH(416, 5, 16);
+  }
+#undef ACT_LAUNCH
   RLMD_LAUNCH_CHECK();
   return 0;
 }
 
 }  // namespace rlmd
+
+#ifdef RLMD_TIMING
+extern "C" int rlmd_debug_ts_act(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(rlmd::g_ts_act), sizeof(unsigned long long) * 8 * n) != hipSuccess;
+}
+#endif

@@ -21,7 +21,7 @@ def build():
 
     b.build()
     os.makedirs(OUT, exist_ok=True)
-    timed = ("learn.hip", "rows.hip")
+    timed = ("learn.hip", "rows.hip", "act.hip")
     tobjs = []
     for src in timed:
         obj = os.path.join(OUT, src.replace(".hip", "_ts.o"))
@@ -80,5 +80,43 @@ def run():
     seq("cbwd_rows (0, 0, 0)", [112, 113, 114, 115, 116, 117, 118])
 
 
+def run_act():
+    """Per-workgroup timeline of fused_act_kernel over 65,536 rows (C2 SAC, and
+    TD3 400/300 with --td3): block start spread, block spans, phase cycles."""
+    import numpy as np
+    import torch
+
+    from rlmd_amd import _abi
+
+    _abi._LIB = _abi.load(LIB)
+    lib = _abi._LIB
+    lib.rlmd_debug_ts_act.restype = C.c_int
+    lib.rlmd_debug_ts_act.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    from rlmd_amd.agent import DeviceAgent
+
+    td3 = "--td3" in sys.argv
+    algo, S, A, h1, h2 = ("TD3", 6, 2, 400, 300) if td3 else ("SAC", 5, 1, 256, 256)
+    ag = DeviceAgent(algo, S, A, h1, h2, 512, 256, precision="bf16", device="cuda:0")
+    n = 65536
+    obs = torch.randn(n, S, device="cuda:0") * 1e-3
+    out = torch.empty(n, A, device="cuda:0")
+    nb = n // 64
+    buf = (C.c_ulonglong * (8 * nb))()
+    for it in range(5):
+        ag.act(obs, mode=0, noise_ctr=it, out=out)
+        torch.cuda.synchronize()
+    t = np.array(buf[:], dtype=np.int64)
+    lib.rlmd_debug_ts_act(buf, nb)
+    t = np.array(buf[:], dtype=np.int64).reshape(nb, 8)
+    st, en = t[:, 0] - t[:, 0].min(), t[:, 6] - t[:, 0].min()
+    print(f"{algo} {h1}/{h2}: {nb} workgroups; realtime ticks (100 MHz = 10 ns)")
+    print("  start  pct 0/25/50/75/100:", np.percentile(st, [0, 25, 50, 75, 100]))
+    print("  end    pct 0/25/50/75/100:", np.percentile(en, [0, 25, 50, 75, 100]))
+    print("  span   pct 0/25/50/75/100:", np.percentile(en - st, [0, 25, 50, 75, 100]))
+    ph = np.diff(t[:, 1:6], axis=1)
+    for i, name in enumerate(["stage", "layer1", "layer2", "epilogue"]):
+        print(f"  {name:9s} cycles median {np.median(ph[:, i]):8.0f}  p90 {np.percentile(ph[:, i], 90):8.0f}")
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run}[sys.argv[1]]()
+    {"build": build, "run": run, "act": run_act}[sys.argv[1]]()
