@@ -756,8 +756,11 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
 
 // Actor data-gradients (autograd of algo_sac.py:524-562 through
 // networks_sac.py:163-178; algo_td3.py:507-523 through networks_td3.py:91).
-template <int PREC, int NBW, bool MULTI>
+// NQ: critics the actor loss reads (SAC min(q1, q2): 2; TD3 q1: 1) — a compile-time
+// count, so TD3's instantiations hold no second critic's fragments or masks.
+template <int PREC, int NBW, bool MULTI, int NQ>
 __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
+  const int nq = NQ == 1 ? 1 : a.nq;  // NQ = 2 keeps the runtime count (its register allocation measured best)
   using T = typename CT<PREC>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowDims& d = a.d;
@@ -784,42 +787,42 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   // ---- every independent load up front; what the actor loss reads first and the
   //      weight fragments last (vmcnt retires in issue order)
   const int64_t nB = (int64_t)B * 4;
-  const __amdgpu_buffer_rsrc_t rq0 = rlmd_rsrc(a.qn[0], nB), rq1 = rlmd_rsrc(a.nq > 1 ? a.qn[1] : a.qn[0], nB),
+  const __amdgpu_buffer_rsrc_t rq0 = rlmd_rsrc(a.qn[0], nB), rq1 = rlmd_rsrc(nq > 1 ? a.qn[1] : a.qn[0], nB),
                                rlp = rlmd_rsrc(sac ? a.logp : a.qn[0], nB);
   const int tq = threadIdx.x, bq = row0 + (int)threadIdx.x;
-  const float ld_q1 = rlmd_ldf(rq0, tq, tq < B), ld_q2 = rlmd_ldf(rq1, tq, tq < B && a.nq > 1);
+  const float ld_q1 = rlmd_ldf(rq0, tq, tq < B), ld_q2 = rlmd_ldf(rq1, tq, tq < B && nq > 1);
   const float ld_lp = rlmd_ldf(rlp, tq, tq < B && sac);
-  const float row_q1 = rlmd_ldf(rq0, bq, tq < R && bq < B), row_q2 = rlmd_ldf(rq1, bq, tq < R && bq < B && a.nq > 1);
+  const float row_q1 = rlmd_ldf(rq0, bq, tq < R && bq < B), row_q2 = rlmd_ldf(rq1, bq, tq < R && bq < B && nq > 1);
   BwdMask<NBW> k0, k1, ka;
   bwd_mask<NBW>(k0, a.e1[0], a.e2[0], a.crit[0].p + co.w3, co, row0, B);
-  if (a.nq > 1) bwd_mask<NBW>(k1, a.e1[1], a.e2[1], a.crit[1].p + co.w3, co, row0, B);
+  if (nq > 1) bwd_mask<NBW>(k1, a.e1[1], a.e2[1], a.crit[1].p + co.w3, co, row0, B);
   bwd_mask<NBW>(ka, a.h1a, a.h2a, nullptr, ao, row0, B);
-  float w1a[2][NBW][NHF];  // W1_g[c][S + j] for this lane's dh1 columns
+  float w1a[NQ][NBW][NHF];  // W1_g[c][S + j] for this lane's dh1 columns
 #pragma unroll
-  for (int g = 0; g < 2; ++g) {
-    const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(a.crit[g < a.nq ? g : 0].p, co.size * 4);
+  for (int g = 0; g < NQ; ++g) {
+    const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(a.crit[g < nq ? g : 0].p, co.size * 4);
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
       const int col = acc_col(i);
 #pragma unroll
       for (int j = 0; j < NHF; ++j)
-        w1a[g][i][j] = rlmd_ldf(rp, co.w1 + (int64_t)col * X + S + j, g < a.nq && col < d.H1 && j < A);
+        w1a[g][i][j] = rlmd_ldf(rp, co.w1 + (int64_t)col * X + S + j, g < nq && col < d.H1 && j < A);
     }
   }
   Pre<PREC, NBW, MULTI> p0, p1;
   pre_issue<PREC, NBW, MULTI>(p0, a.crit[0].wt, H2p, H2p, H1p / 16);
-  if (a.nq > 1) pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
+  if (nq > 1) pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
   // ---- actor loss (algo_sac.py:546-562 / algo_td3.py:507-523): every row's
   //      objective and ranking key (SAC sorts descending, TD3 ascending, Q5)
   uint64_t* vkey = reinterpret_cast<uint64_t*>(smem + L.vkey);
   float* vval = reinterpret_cast<float*>(smem + L.vval);
   int* rank16 = reinterpret_cast<int*>(part);  // [R] (part is free until the first dh1)
   const float alpha = sac ? expf(a.st->log_alpha) : 0.f;
-  const float qb0 = a.crit[0].p[co.b3], qb1 = a.nq > 1 ? a.crit[1].p[co.b3] : 0.f;
+  const float qb0 = a.crit[0].p[co.b3], qb1 = nq > 1 ? a.crit[1].p[co.b3] : 0.f;
   for (int j = threadIdx.x; j < B; j += NT) {
     const bool first = j == (int)threadIdx.x;  // preloaded
     const float q1 = (first ? ld_q1 : a.qn[0][j]) + qb0;
-    const float q2 = a.nq > 1 ? (first ? ld_q2 : a.qn[1][j]) + qb1 : q1;
+    const float q2 = nq > 1 ? (first ? ld_q2 : a.qn[1][j]) + qb1 : q1;
     const float v = sac ? fminf(q1, q2) - alpha * (first ? ld_lp : a.logp[j]) : q1;
     vval[j] = v;
     vkey[j] = ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)j;
@@ -864,7 +867,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     float dq0 = 0.f, dq1 = 0.f, dlp = 0.f;
     if (ext && b < B) {
       dq0 = a.dqn_ext[0][b];
-      dq1 = a.nq > 1 ? a.dqn_ext[1][b] : 0.f;
+      dq1 = nq > 1 ? a.dqn_ext[1][b] : 0.f;
       dlp = sac ? a.dlogp_ext[b] : 0.f;
     } else if (b < B) {
       const bool sel = !a.topk || rank16[r] < kk;
@@ -886,13 +889,14 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   }
   __syncthreads();
   // ---- dL/da through each critic: dh2 -> dh1 (MFMA) -> . W1[:, S:S+A]
-  for (int g = 0; g < a.nq; ++g) {
+  for (int g = 0; g < nq; ++g) {
     const BwdMask<NBW>& k = g == 0 ? k0 : k1;
     dh2_from_q<PREC, NBW>(k, rowv + g * R, co, aT, L.ldaT, nullptr, row0, B);
     __syncthreads();
     RLMD_TSR(99 + 4 * g);
     if (fused_da) {
-      dh1_rows<PREC, NBW, MULTI>(g == 0 ? p0 : p1, a.crit[g], co, k, aT, L.ldaT, nullptr, w1a[g], A, part, row0, B);
+      dh1_rows<PREC, NBW, MULTI>(g == 0 ? p0 : p1, a.crit[g], co, k, aT, L.ldaT, nullptr, w1a[NQ > 1 ? g : 0], A,
+                                 part, row0, B);
       RLMD_TSR(100 + 4 * g);
       __syncthreads();
       RLMD_TSR(101 + 4 * g);
@@ -1011,8 +1015,12 @@ void launch_kind(int kind, const void* args, dim3 grid, size_t lds, hipStream_t 
                          *static_cast<const CBwdArgs*>(args));
       break;
     default:
-      hipLaunchKernelGGL((abwd_rows_kernel<PREC, NBW, MULTI>), grid, dim3(NT), lds, st,
-                         *static_cast<const ABwdArgs*>(args));
+      if (static_cast<const ABwdArgs*>(args)->nq > 1)
+        hipLaunchKernelGGL((abwd_rows_kernel<PREC, NBW, MULTI, 2>), grid, dim3(NT), lds, st,
+                           *static_cast<const ABwdArgs*>(args));
+      else
+        hipLaunchKernelGGL((abwd_rows_kernel<PREC, NBW, MULTI, 1>), grid, dim3(NT), lds, st,
+                           *static_cast<const ABwdArgs*>(args));
       break;
   }
 }
