@@ -300,7 +300,9 @@ def main():
             "roofline": {"kernel": "env_train_kernel (fused env step + replay insert + reset)",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms},
+                         "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms,
+                         "timing": "HIP events attached to every env_train_kernel dispatch of the timed region "
+                                   "(hipExtLaunchKernelGGL start/stop: the dispatch's own begin/end)"},
             "roofline_mfma": {"kernel": f"learn phase (K {cfg['algo']} updates, all kernels)", "bound": "mfma",
                               "achieved": mfma_tf, "peak": BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3,
                               "unit": "TFLOP/s", "frac": (mfma_tf or 0) / (BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3),

@@ -24,6 +24,7 @@
 #pragma clang fp contract(off)
 #include <math.h>
 #include <string.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <vector>
@@ -790,7 +791,7 @@ int flush_stats(rlmd_env_t env, hipStream_t stream) {
 
 int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uint32_t step,
               float* actions, int random_actions, int abs_actions, int window, double clip_lo, double clip_hi,
-              float* obs, double* ep_stats, hipStream_t stream) {
+              float* obs, double* ep_stats, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
   const int N = env->P.n_lanes;
   const dim3 grid((N + 255) / 256), block(256);
   const bool f64 = window || random_actions;
@@ -804,14 +805,17 @@ int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uin
     sf.fold_dst = env->pending_dst;
   }
   if (ep_stats) sf.part_out = env->d_part + (size_t)env->part_parity * env->part_rows * 4;
-#define TRAIN(F, NG)                                                                                       \
-  {                                                                                                        \
-    if (f64)                                                                                               \
-      hipLaunchKernelGGL((env_train_kernel<F, NG, double>), grid, block, 0, stream, env->P, step, actions, \
-                         random_actions, abs_actions, clip_lo, clip_hi, obs, rb, ring_base, sf);            \
-    else                                                                                                   \
-      hipLaunchKernelGGL((env_train_kernel<F, NG, float>), grid, block, 0, stream, env->P, step, actions,  \
-                         random_actions, abs_actions, clip_lo, clip_hi, obs, rb, ring_base, sf);            \
+  // hipExtLaunchKernelGGL: the optional events are stamped at this dispatch's begin / end
+#define TRAIN(F, NG)                                                                                          \
+  {                                                                                                           \
+    if (f64)                                                                                                  \
+      hipExtLaunchKernelGGL((env_train_kernel<F, NG, double>), grid, block, 0, stream, ev_start, ev_stop, 0,  \
+                            env->P, step, (const float*)actions, random_actions, abs_actions, clip_lo, clip_hi, \
+                            obs, rb, ring_base, sf);                                                          \
+    else                                                                                                      \
+      hipExtLaunchKernelGGL((env_train_kernel<F, NG, float>), grid, block, 0, stream, ev_start, ev_stop, 0,   \
+                            env->P, step, (const float*)actions, random_actions, abs_actions, clip_lo, clip_hi, \
+                            obs, rb, ring_base, sf);                                                          \
   }
   RLMD_ENV_DISPATCH(env->P, TRAIN);
 #undef TRAIN

@@ -1038,6 +1038,24 @@ struct PhaseProfiler {
     if (which == 0) used[phase]++;
     return 0;
   }
+  // a {start, stop} pair for one kernel launch (hipExtLaunchKernelGGL stamps
+  // them at the dispatch's own begin / end, like rocprofv3's kernel trace);
+  // {null, null} when disabled
+  int pair(int phase, hipEvent_t* start, hipEvent_t* stop) {
+    *start = *stop = nullptr;
+    if (!enabled) return 0;
+    const size_t i = used[phase];
+    for (int w = 0; w < 2; ++w)
+      if (i >= ev[phase][w].size()) {
+        hipEvent_t e;
+        RLMD_HIP(hipEventCreate(&e));
+        ev[phase][w].push_back(e);
+      }
+    *start = ev[phase][0][i];
+    *stop = ev[phase][1][i];
+    used[phase]++;
+    return 0;
+  }
 };
 PhaseProfiler g_prof;
 }  // namespace
@@ -1095,10 +1113,10 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
     hi = width * 0.99;
   }
   const int64_t base = rlmd::replay_mem_idx(rb);
-  RLMD_TRY(g_prof.record(1, 0, st));
+  hipEvent_t e0, e1;
+  RLMD_TRY(g_prof.pair(1, &e0, &e1));
   RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, window ? 1 : 0,
-                           lo, hi, obs, ep_stats, st));
-  RLMD_TRY(g_prof.record(1, 1, st));
+                           lo, hi, obs, ep_stats, st, e0, e1));
   rlmd::replay_advance(rb, N);
   if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch) {
     RLMD_TRY(g_prof.record(2, 0, st));

@@ -58,7 +58,8 @@ void replay_advance(rlmd_replay_t rb, int64_t n);
 // reference's float64 action space and np.clip with np.float64 bounds do.
 int env_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step,
               float* actions, int random_actions, int abs_actions, int window, double clip_lo, double clip_hi,
-              float* obs, double* ep_stats, hipStream_t stream);
+              float* obs, double* ep_stats, hipStream_t stream, hipEvent_t ev_start = nullptr,
+              hipEvent_t ev_stop = nullptr);
 // market evaluation (eval_episodes.py:402-611): reset every lane at its given
 // start row, then one policy-driven step of the still-running lanes
 int env_market_eval_reset(rlmd_env_t env, const int32_t* start_at, float* obs, double* reward, int32_t* steps,
