@@ -51,16 +51,6 @@ __device__ __forceinline__ unsigned short f2bf_rne(float f) {
   return (unsigned short)((u & 0x7fffffffu) > 0x7f800000u ? ((u >> 16) | 0x40u) : r);
 }
 
-// sum over the 16 lanes of a DPP row (every lane gets it): quad butterflies, then
-// half-row and row mirrors — VALU-rate lane moves instead of ds_bpermute shuffles
-__device__ __forceinline__ float row16_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));   // quad [1,0,3,2]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));   // quad [2,3,0,1]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
-  return v;
-}
-
 struct FusedActArgs {
   const float* obs;             // [n, S]
   const float* params;          // actor params (f32 masters)
@@ -249,7 +239,7 @@ __global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
       }
 #pragma unroll
       for (int h = 0; h < 2 * kMaxA; ++h)
-        if (h < nh) ph[h] = row16_sum(ph[h]);
+        if (h < nh) ph[h] = rlmd_row16_sum(ph[h]);
       if ((lane & 15) == 0) {
         const int r = 16 * m + 4 * (lane >> 4) + rg;
 #pragma unroll

@@ -427,11 +427,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
                                j < s.N ? j * 4 : kOutOfRange);
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
-        float c = out[0][0][rg] * w;
-        c += __shfl_xor(c, 1, 64);
-        c += __shfl_xor(c, 2, 64);
-        c += __shfl_xor(c, 4, 64);
-        c += __shfl_xor(c, 8, 64);
+        const float c = rlmd_row16_sum(out[0][0][rg] * w);
         if ((lane & 15) == 0) hp[wc][row0 + 4 * (lane >> 4) + rg] = c;
       }
       __syncthreads();

@@ -10,9 +10,17 @@
 namespace rlmd {
 namespace {
 
+// 64-lane sum: DPP within each 16-lane row, then two cross-row shuffles
 __device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  v = rlmd_row16_sum(v);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+  v = rlmd_row16_max(v);
+  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
 
@@ -35,9 +43,7 @@ __device__ __forceinline__ void block_allreduce(float* sm, float* mx, float* red
 #pragma unroll
   for (int v = 0; v < NS; ++v) sm[v] = wave_sum(sm[v]);
 #pragma unroll
-  for (int v = 0; v < NM; ++v)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) mx[v] = fmaxf(mx[v], __shfl_xor(mx[v], o, 64));
+  for (int v = 0; v < NM; ++v) mx[v] = wave_max(mx[v]);
   if (lane == 0) {
 #pragma unroll
     for (int v = 0; v < NS; ++v) red[v * 16 + w] = sm[v];
@@ -48,13 +54,9 @@ __device__ __forceinline__ void block_allreduce(float* sm, float* mx, float* red
   if ((int)threadIdx.x < 16 * NV) {
     const int v = threadIdx.x >> 4, q = threadIdx.x & 15;
     const bool is_sum = v < NS;
-    float t = q < nw ? red[threadIdx.x] : (is_sum ? 0.f : -INFINITY);
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-      const float u = __shfl_xor(t, o, 64);
-      t = is_sum ? t + u : fmaxf(t, u);
-    }
-    if (q == 0) res[v] = t;
+    const float t = q < nw ? red[threadIdx.x] : (is_sum ? 0.f : -INFINITY);
+    const float r = is_sum ? rlmd_row16_sum(t) : rlmd_row16_max(t);  // one 16-lane row per value
+    if (q == 0) res[v] = r;
   }
   __syncthreads();
 #pragma unroll

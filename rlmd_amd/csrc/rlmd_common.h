@@ -86,6 +86,29 @@ __host__ __device__ __forceinline__ uint64_t rlmd_below(uint32_t a, uint32_t b, 
 // it; threads >= n sort their own n-aligned segments, each ascending, so several
 // independent sorts of n keys can share one call.
 // ---------------------------------------------------------------------------
+// DPP lane moves (VALU rate, no LDS crossbar): a 16-lane row reduction with
+// quad butterflies then the half-row and row mirrors; every lane of the row
+// ends with the row's result (quad [1,0,3,2] = 0xB1, [2,3,0,1] = 0x4E,
+// row_half_mirror = 0x141, row_mirror = 0x140).
+template <int CTRL>
+__device__ __forceinline__ float rlmd_dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float rlmd_row16_sum(float v) {
+  v += rlmd_dpp<0xB1>(v);
+  v += rlmd_dpp<0x4E>(v);
+  v += rlmd_dpp<0x141>(v);
+  v += rlmd_dpp<0x140>(v);
+  return v;
+}
+__device__ __forceinline__ float rlmd_row16_max(float v) {
+  v = fmaxf(v, rlmd_dpp<0xB1>(v));
+  v = fmaxf(v, rlmd_dpp<0x4E>(v));
+  v = fmaxf(v, rlmd_dpp<0x141>(v));
+  v = fmaxf(v, rlmd_dpp<0x140>(v));
+  return v;
+}
+
 __device__ __forceinline__ uint64_t rlmd_shfl_xor_u64(uint64_t v, int m) {
   const uint32_t lo = __shfl_xor((uint32_t)v, m, 64), hi = __shfl_xor((uint32_t)(v >> 32), m, 64);
   return ((uint64_t)hi << 32) | lo;

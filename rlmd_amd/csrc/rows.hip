@@ -339,11 +339,7 @@ __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdC
 #pragma unroll
       for (int h = 0; h < NHF; ++h) {
         if (h < nh) {
-          float c = ph[rg][h];
-          c += __shfl_xor(c, 1, 64);
-          c += __shfl_xor(c, 2, 64);
-          c += __shfl_xor(c, 4, 64);
-          c += __shfl_xor(c, 8, 64);
+          const float c = rlmd_row16_sum(ph[rg][h]);
           if ((lane & 15) == 0) part[(wave * R + acc_row(rg)) * NHF + h] = c;
         }
       }
@@ -674,11 +670,7 @@ __device__ __forceinline__ void dh1_rows(Pre<PREC, NBW, MULTI>& pre, const RowNe
 #pragma unroll
       for (int j = 0; j < NHF; ++j) {
         if (j < na) {
-          float c = pd[rg][j];
-          c += __shfl_xor(c, 1, 64);
-          c += __shfl_xor(c, 2, 64);
-          c += __shfl_xor(c, 4, 64);
-          c += __shfl_xor(c, 8, 64);
+          const float c = rlmd_row16_sum(pd[rg][j]);
           if ((lane & 15) == 0) part[(wave * R + acc_row(rg)) * NHF + j] = c;
         }
       }

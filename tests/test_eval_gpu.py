@@ -136,7 +136,9 @@ def test_eval_market_shuffled_matches_oracle(golden, dev, c):
                                           sw, shuffle_days=3, seed=77)
     np.testing.assert_array_equal(out["steps"], steps)
     np.testing.assert_allclose(out["reward"], rew, rtol=1e-6, atol=0)
-    np.testing.assert_allclose(out["risk"], risk, rtol=1e-6, atol=1e-12)
+    # risk holds float32 leverages 3 * a: the fp32 policy's summation order (GPU
+    # GEMM vs torch-CPU) moves a by a few float32 ulps on 200 x 40 steps
+    np.testing.assert_allclose(out["risk"], risk, rtol=1e-5, atol=1e-12)
     with pytest.raises(ValueError):
         market_evaluate(ag, prices, inv, d, test_days, [0, prices.shape[0] - test_days], cum, warm, sw, device=dev)
 
