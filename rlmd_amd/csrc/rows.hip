@@ -264,8 +264,10 @@ __device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, cons
   const ElemMap m = elem_map(pad32(o.h1));
   const bool own = m.c < o.h1 && m.r0 < R;
   const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(p, o.size * 4);
+  // j < in and h < nh are uniform: skipped loads are not issued (a wave holds at
+  // most 63 loads in flight, and the first load round is at that limit)
 #pragma unroll
-  for (int j = 0; j < W1P; ++j) k.w1[j] = rlmd_ldf(rp, o.w1 + (int64_t)m.c * in + j, own && j < in);
+  for (int j = 0; j < W1P; ++j) k.w1[j] = j < in ? rlmd_ldf(rp, o.w1 + (int64_t)m.c * in + j, own) : 0.f;
   k.b1 = rlmd_ldf(rp, o.b1 + m.c, own);
   const int64_t oa = wa - p, ob = (wb ? wb : wa) - p;  // head rows relative to p
 #pragma unroll
@@ -276,7 +278,7 @@ __device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, cons
 #pragma unroll
     for (int h = 0; h < NHF; ++h) {
       const int64_t row = h < na ? oa + (int64_t)h * o.h2 : ob + (int64_t)(h - na) * o.h2;
-      k.hw[i][h] = rlmd_ldf(rp, row + col, cin && h < nh);
+      k.hw[i][h] = h < nh ? rlmd_ldf(rp, row + col, cin) : 0.f;
     }
   }
 }
@@ -784,6 +786,8 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const int tq = threadIdx.x, bq = row0 + (int)threadIdx.x;
   const float ld_q1 = rlmd_ldf(rq0, tq, tq < B), ld_q2 = rlmd_ldf(rq1, tq, tq < B && nq > 1);
   const float ld_lp = rlmd_ldf(rlp, tq, tq < B && sac);
+  const float log_alpha = sac ? a.st->log_alpha : 0.f;  // scalar loads, issued with the first round
+  const float qb0 = a.crit[0].p[co.b3], qb1 = nq > 1 ? a.crit[1].p[co.b3] : 0.f;
   const float row_q1 = rlmd_ldf(rq0, bq, tq < R && bq < B), row_q2 = rlmd_ldf(rq1, bq, tq < R && bq < B && nq > 1);
   BwdMask<NBW> k0, k1, ka;
   bwd_mask<NBW>(k0, a.e1[0], a.e2[0], a.crit[0].p + co.w3, co, row0, B);
@@ -798,19 +802,19 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       const int col = acc_col(i);
 #pragma unroll
       for (int j = 0; j < NHF; ++j)
-        w1a[g][i][j] = rlmd_ldf(rp, co.w1 + (int64_t)col * X + S + j, g < nq && col < d.H1 && j < A);
+        w1a[g][i][j] = g < nq && j < A ? rlmd_ldf(rp, co.w1 + (int64_t)col * X + S + j, col < d.H1) : 0.f;
     }
   }
   Pre<PREC, NBW, MULTI> p0, p1;
   pre_issue<PREC, NBW, MULTI>(p0, a.crit[0].wt, H2p, H2p, H1p / 16);
   if (nq > 1) pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
+  RLMD_TSR(95);
   // ---- actor loss (algo_sac.py:546-562 / algo_td3.py:507-523): every row's
   //      objective and ranking key (SAC sorts descending, TD3 ascending, Q5)
   uint64_t* vkey = reinterpret_cast<uint64_t*>(smem + L.vkey);
   float* vval = reinterpret_cast<float*>(smem + L.vval);
   int* rank16 = reinterpret_cast<int*>(part);  // [R] (part is free until the first dh1)
-  const float alpha = sac ? expf(a.st->log_alpha) : 0.f;
-  const float qb0 = a.crit[0].p[co.b3], qb1 = nq > 1 ? a.crit[1].p[co.b3] : 0.f;
+  const float alpha = sac ? expf(log_alpha) : 0.f;
   for (int j = threadIdx.x; j < B; j += NT) {
     const bool first = j == (int)threadIdx.x;  // preloaded
     const float q1 = (first ? ld_q1 : a.qn[0][j]) + qb0;
@@ -823,6 +827,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const int kk = a.topk ? (B < a.k ? B : a.k) : B;
   const bool ext = a.dqn_ext[0] != nullptr;  // loss from actor_loss_kernel (B > 512)
   __syncthreads();
+  RLMD_TSR(97);
   if (!ext && blockIdx.x == gridDim.x - 1 - (a.cstats.B > 0 ? 1 : 0)) {
     // the loss workgroup: selection over all rows -> loss value, temperature gradient
     uint64_t* runs = reinterpret_cast<uint64_t*>(smem + L.runs);
@@ -853,6 +858,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     atomicAdd(&rank16[r], c);
   }
   __syncthreads();
+  RLMD_TSR(98);
   float* dlogp_r = rowv + 2 * R;  // [R]
   if ((int)threadIdx.x < R) {
     const int r = threadIdx.x, b = row0 + r;
