@@ -1,0 +1,80 @@
+"""Vectorised counterpart of the reference drivers' trial loop with their logs.
+
+scripts/rl_multiplicative.py:154-450 (and rl_market.py:167-480) run n_trials
+independent agents, evaluate every eval_freq steps (100 episodes) with the
+critics' shadow means filled in first (loss[6:8] = agent_shadow_mean, :255,
+:275), and save the trial / eval logs as .npy under utils.save_directory
+(:447-450).  Here one trial is one VecTrainer (its own seed); a "step" is one
+vector step over all lanes; trial rows aggregate `log_every` vector steps (see
+rlmd_amd/logs.py); evaluation rows are per episode as in the reference.
+"""
+import os
+import time
+
+import numpy as np
+import torch
+
+from . import logs
+from .trainer import VecTrainer
+
+ENV_NAMES = {"coin": "Coin", "dice": "Dice", "gbm": "GBM", "dice_sh": "Dice_SH"}
+
+
+def env_id(env, investor, n_gambles=1, market_name="SNP", obs_days=1, action_days=1):
+    """The reference's inputs["env_id"]: main.py gym_envs name + "_n" + n_gambles
+    (rl_multiplicative.py:49-51; Dice_SH_* too), market name + "_D" + obs_days +
+    "_T" + action_days (rl_market.py:62-65)."""
+    if env == "market":
+        return f"{market_name}_Inv{investor}_D{obs_days}_T{action_days}"
+    if env == "dice_sh":
+        return f"Dice_SH_{investor if investor == 'INSURED' else 'Inv' + investor}_n{n_gambles}"
+    return f"{ENV_NAMES[env]}_Inv{investor}_n{n_gambles}"
+
+
+def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE", n_lanes=4096, n_cumsteps=2000,
+                   eval_freq=1000, n_eval=100, max_eval_steps=100, n_trials=1, k_updates=1, log_every=1,
+                   warmup_steps=1000, smoothing_window=2000, buffer=1_000_000, multi_steps=1, precision="bf16",
+                   seed=0, results_root=".", test_agent=True, device="cuda:0", test_days=250, **trainer_kw):
+    """Train n_trials independent vectorised agents and save the reference's four
+    log arrays; returns (file stem, ExperimentLog)."""
+    market = env == "market"
+    dyn = "MKT" if market else "M"
+    eid = env_id(env, investor, n_gambles, obs_days=trainer_kw.get("obs_days", 1))
+    inputs = {"env_id": eid, "dynamics": dyn, "algo": algo, "s_dist": trainer_kw.get("s_dist", "N"),
+              "loss_fn": loss, "critic_mean_type": "E", "buffer": buffer, "multi_steps": multi_steps,
+              "n_cumsteps": n_cumsteps, "n_trials": n_trials, "test_agent": test_agent}
+    n_rows = (n_cumsteps + log_every - 1) // log_every
+    n_evals = n_cumsteps // eval_freq
+    rdim = (logs.market_log_dim(eid, n_gambles) if market else logs.multi_log_dim(eid, n_gambles))
+    lg = logs.ExperimentLog(n_trials, n_rows, n_evals, n_eval, rdim, market=market)
+    for trial in range(n_trials):
+        tr = VecTrainer(env, investor, n_lanes, n_gambles, algo=algo, loss=loss, k_updates=k_updates,
+                        replay_capacity=(buffer // n_lanes) * n_lanes if multi_steps > 1 else buffer,
+                        seed=seed + trial, warmup_steps=warmup_steps, smoothing_window=smoothing_window,
+                        precision=precision, device=device, multi_steps=multi_steps, **trainer_kw)
+        prev = np.zeros(3)
+        t_row = time.perf_counter()
+        eval_run = 0
+        for step in range(1, n_cumsteps + 1):
+            tr.step()
+            if step % log_every == 0 or step == n_cumsteps:
+                n, rs, ls, _ = tr.flush_stats().cpu().numpy()
+                dn, dr, dl = n - prev[0], rs - prev[1], ls - prev[2]
+                prev = np.array([n, rs, ls])
+                now = time.perf_counter()
+                lg.log_row(trial, now - t_row, dr / dn if dn else np.nan, dl / dn if dn else np.nan,
+                           tr.last_stats(shadow=True))
+                t_row = now
+            if step % eval_freq == 0 and eval_run < n_evals:
+                st = tr.last_stats(shadow=True)  # loss[6:8] = agent_shadow_mean(...) first
+                t0 = time.perf_counter()
+                ev = (tr.evaluate_market(n_eval=n_eval, test_days=test_days) if market
+                      else tr.evaluate(n_eval=n_eval, max_steps=max_eval_steps))
+                torch.cuda.synchronize()
+                lg.log_eval(trial, eval_run, ev, time.perf_counter() - t0, st, step)
+                eval_run += 1
+        del tr
+    stem = logs.save_directory(inputs, results=True)
+    path = os.path.join(results_root, stem[2:] if stem.startswith("./") else stem)
+    lg.save(path)
+    return path, lg

@@ -636,6 +636,33 @@ def eval_market_fixtures(seed=31, n_eval=12, test_days=40):
 
 
 # ----------------------------------------------------------------------------
+# §8f-2: experiment file naming and risk-log widths (tools/utils.py:170-307)
+# ----------------------------------------------------------------------------
+LOG_CASES = [  # (env_id, dynamics, algo, s_dist, loss, buffer, multi_steps, n_cumsteps, n_trials, test, n)
+    ("Coin_InvA_n1", "M", "SAC", "N", "MSE", 1e6, 1, 5e4, 10, False, 1),
+    ("GBM_InvC_n5", "M", "TD3", "N", "HUB", 1e6, 3, 4e5, 5, True, 5),
+    ("Dice_SH_InvB", "M", "SAC", "L", "HSC", 2e5, 5, 1e5, 1, False, 1),
+    ("SNP_InvB_D1_T1", "MKT", "TD3", "N", "MAE", 1e6, 1, 3e5, 8, False, 1),
+    ("USEI_InvC_D5_T1", "MKT", "SAC", "MVN", "CAU", 1e7, 7, 1e6, 3, True, 3),
+]
+
+
+def log_fixtures():
+    import tools.utils as ut
+
+    names, models, dims = [], [], []
+    for env_id, dyn, algo, sd, lf, buf, ms, ncs, nt, test, n in LOG_CASES:
+        inputs = {"env_id": env_id, "dynamics": dyn, "algo": algo, "s_dist": sd, "loss_fn": lf,
+                  "critic_mean_type": "E", "buffer": buf, "multi_steps": ms, "n_cumsteps": ncs, "n_trials": nt,
+                  "test_agent": test, "trial": 2}
+        names.append(ut.save_directory(inputs, results=True))
+        models.append(ut.save_directory(inputs, results=False))
+        dims.append(ut.market_log_dim(inputs, n) if dyn == "MKT" else ut.multi_log_dim(inputs, n))
+    cases = np.array([[str(x) for x in c] for c in LOG_CASES])
+    return {"cases": cases, "results": np.array(names), "models": np.array(models), "risk_dim": np.array(dims)}
+
+
+# ----------------------------------------------------------------------------
 # F5: learn() steps for SAC and TD3
 # ----------------------------------------------------------------------------
 def _inputs(algo, S, A, hidden, loss_fn="MSE", B=None, k=None, s_dist="N"):
@@ -817,6 +844,7 @@ def main():
         "multistep.npz": multistep_fixtures,
         "eval.npz": eval_fixtures,
         "eval_market.npz": eval_market_fixtures,
+        "logs.npz": log_fixtures,
         "learn.npz": learn_fixtures,
     }
     only = sys.argv[1:]

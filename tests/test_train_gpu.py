@@ -273,3 +273,21 @@ def test_window_steps_feed_the_env_float64_actions(dev, env, inv, fam, oinv):
         m = d[:, 0]
         if m.any():
             obs[m] = ora.reset(m)[m]
+
+
+def test_run_experiment_writes_reference_logs(dev, tmp_path):
+    """Two short trials with evaluations: the four .npy arrays in the reference
+    layout under utils.save_directory's stem (rlmd_amd/logs.py)."""
+    from rlmd_amd.experiment import run_experiment
+
+    path, lg = run_experiment("coin", "B", 1, algo="SAC", n_lanes=512, n_cumsteps=12, eval_freq=5, n_eval=20,
+                              max_eval_steps=30, n_trials=2, k_updates=1, warmup_steps=3, smoothing_window=6,
+                              buffer=512 * 16, precision="fp32", results_root=str(tmp_path), device=dev)
+    assert path.endswith("Coin_InvB_n1--M_SAC-N_MSE-E_B81e2_M1_S12e0_N2")
+    tr = np.load(path + "_trial.npy")
+    ev = np.load(path + "_eval.npy")
+    assert tr.shape == (2, 12, 19) and ev.shape == (2, 2, 20, 20)
+    assert np.load(path + "_eval_risk.npy").shape == (2, 2, 20, 5)
+    assert (ev[:, :, :, 19] == np.array([5, 10])[None, :, None]).all()
+    assert (ev[..., 2] >= 1).all() and (ev[..., 2] <= 30).all()
+    assert np.isfinite(tr[:, 4:, 3]).all()  # learning from step 4 (mem_idx > batch)
