@@ -109,6 +109,13 @@ int rlmd_eval_stats(const double* reward_dev, const int32_t* steps_dev, const do
 int rlmd_shadow_means(const float* stats_dev, int32_t rows, int32_t ld, float low_mul, float high_mul,
                       float* shadow_dev, int32_t ldo, void* stream);
 
+/* Replaces shadow_equiv (tools/utils.py:406-438) as tools/aggregate_data.py:
+ * 441-447 applies it over arrays: out[i] = the max multiplier at which the
+ * float64 shadow mean of (alpha[i], min[i], max[i], min_mul) equals mean[i],
+ * solved from 1 (1 itself when alpha[i] >= 1).  All arrays f64 [n], device. */
+int rlmd_shadow_equiv(const double* mean_dev, const double* alpha_dev, const double* min_dev, const double* max_dev,
+                      double min_mul, int64_t n, double* out_dev, void* stream);
+
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
 /* Market lanes' episode start rows (i32 [N]) read back (eval_market's

@@ -32,3 +32,15 @@ def agent_shadow_mean(loss, low_mul=1.0, high_mul=10.0):
         a = F32(loss[8 + c])
         out.append(shadow_means(a, loss[2 + c], loss[4 + c], low_mul, high_mul) if a < 1 else F32(loss[c]))
     return np.array(out, dtype=np.float32)
+
+
+def shadow_equiv(mean, alpha, mn, mx, min_mul=1):
+    """tools/utils.py:406-438 on float64 scalars: SciPy's MINPACK hybrd root of
+    shadow_means(alpha, min, max, min_mul, m) - mean from m = 1 (the published
+    algorithm the reference calls); 1 when alpha >= 1."""
+    import scipy.optimize as op
+
+    if alpha < 1:
+        f = lambda m: shadow_means(alpha, mn, mx, min_mul, m, dtype=np.float64) - mean  # noqa: E731
+        return float(np.atleast_1d(op.root(f, 1, method="hybr").x)[0])
+    return 1.0

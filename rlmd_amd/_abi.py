@@ -91,6 +91,7 @@ SIGNATURES = {
     "rlmd_train_flush_stats": (C.c_int, [P, P]),
     "rlmd_env_lane_start": (C.c_int, [P, P]),
     "rlmd_shadow_means": (C.c_int, [P, I32, I32, C.c_float, C.c_float, P, I32, P]),
+    "rlmd_shadow_equiv": (C.c_int, [P, P, P, P, C.c_double, I64, P, P]),
     "rlmd_eval_market": (C.c_int, [P, P, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, P, P]),
     "rlmd_profile_enable": (C.c_int, [I32]),
     "rlmd_profile_read": (C.c_int, [P, P]),

@@ -386,6 +386,7 @@ __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>
   float* hout = reinterpret_cast<float*>(smem + L.hout);
   float* h2s = reinterpret_cast<float*>(smem + L.h2s);
   layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, row0, B);
+  if (blockIdx.y == 2) RLMD_TSR(63);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(64);
   f32x4 acc[NBW];

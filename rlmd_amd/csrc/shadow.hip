@@ -125,6 +125,55 @@ __device__ float shadow_mean(float alpha, float mn, float mx, float low_mul, flo
   return low + (high - low) * expf(x) * powf(x, alpha) * up;
 }
 
+// shadow_means on float64 inputs (the aggregation path: tools/aggregate_data.py
+// passes float64 arrays, so every operation is double)
+__device__ double shadow_mean_f64(double alpha, double mn, double mx, double low_mul, double high_mul) {
+  const double low = mn * low_mul, high = mx * high_mul;
+  const double x = alpha / high;
+  const double up = sp_gamma(1.0 - alpha) * gammaincc(1.0 - alpha, x);
+  return low + (high - low) * exp(x) * pow(x, alpha) * up;
+}
+
+// shadow_equiv (tools/utils.py:406-438): the max multiplier m with
+// shadow_means(alpha, min, max, min_mul, m) == mean, from x0 = 1 (x0 itself when
+// alpha >= 1 or NaN).  The reference solves it with MINPACK hybrd; in one
+// dimension that is a Newton iteration on a forward-difference derivative
+// (step sqrt(eps)|x|) inside a trust region of 100 |x0| scaled by |f'|, which
+// is restated here with step halving while |f| does not decrease, stopping at
+// hybrd's xtol (1.49012e-8 relative) or f == 0.
+__global__ void __launch_bounds__(64) shadow_equiv_kernel(const double* mean, const double* alpha, const double* mn,
+                                                          const double* mx, double min_mul, int64_t n, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double a = alpha[i], mu = mean[i], lo = mn[i], hi = mx[i];
+  if (!(a < 1.0)) {
+    out[i] = 1.0;
+    return;
+  }
+  auto F = [&](double m) { return shadow_mean_f64(a, lo, hi, min_mul, m) - mu; };
+  constexpr double kXtol = 1.49012e-8, kEps = 1.4901161193847656e-8;  // sqrt(DBL_EPSILON)
+  double x = 1.0, f = F(x);
+  const double delta_scale = 100.0;  // hybrd's factor: trust radius 100 |x0| in scaled units
+  for (int it = 0; it < 200 && f != 0.0 && isfinite(f); ++it) {
+    const double h = kEps * (x != 0.0 ? fabs(x) : 1.0);
+    const double J = (F(x + h) - f) / h;
+    if (!(J != 0.0) || !isfinite(J)) break;
+    double p = -f / J;
+    const double cap = delta_scale * fabs(x);
+    if (fabs(p) > cap) p = p > 0 ? cap : -cap;
+    double fn = F(x + p);
+    for (int k = 0; k < 60 && !(isfinite(fn) && fabs(fn) < fabs(f)); ++k) {
+      p *= 0.5;
+      fn = F(x + p);
+    }
+    if (!(isfinite(fn) && fabs(fn) <= fabs(f))) break;
+    x += p;
+    f = fn;
+    if (fabs(p) <= kXtol * fabs(x)) break;
+  }
+  out[i] = x;
+}
+
 // one thread per (row, critic): stats rows [loss[11] | ...] with leading dimension ld
 __global__ void __launch_bounds__(64) shadow_kernel(const float* stats, int rows, int ld, float low_mul,
                                                     float high_mul, float* out, int ldo) {
@@ -147,6 +196,17 @@ int rlmd_shadow_means(const float* stats_dev, int32_t rows, int32_t ld, float lo
   if (rows == 0) return 0;
   hipLaunchKernelGGL(shadow_kernel, dim3((2 * rows + 63) / 64), dim3(64), 0, (hipStream_t)stream, stats_dev, rows,
                      ld, low_mul, high_mul, shadow_dev, ldo);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+int rlmd_shadow_equiv(const double* mean_dev, const double* alpha_dev, const double* min_dev, const double* max_dev,
+                      double min_mul, int64_t n, double* out_dev, void* stream) {
+  RLMD_CHECK(mean_dev && alpha_dev && min_dev && max_dev && out_dev, "null argument");
+  RLMD_CHECK(n >= 0, "bad length");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(shadow_equiv_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream,
+                     mean_dev, alpha_dev, min_dev, max_dev, min_mul, n, out_dev);
   RLMD_LAUNCH_CHECK();
   return 0;
 }

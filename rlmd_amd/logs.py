@@ -112,3 +112,21 @@ class ExperimentLog:
         np.save(directory + "_trial_risk.npy", self.trial_risk[:, :m, :])
         np.save(directory + "_eval_risk.npy", self.eval_risk)
         return m
+
+
+def shadow_equiv(mean, alpha, cmin, cmax, min_mul=1.0, device="cuda:0"):
+    """tools/aggregate_data.py:441-447's keqv over whole arrays on the device
+    (rlmd_shadow_equiv): the max multiplier equating the shadow and empirical
+    means, 1 where the tail index is >= 1.  Inputs broadcast to one shape."""
+    import torch
+
+    from . import _abi
+
+    arrs = np.broadcast_arrays(*(np.asarray(x, dtype=np.float64) for x in (mean, alpha, cmin, cmax)))
+    shape = arrs[0].shape
+    t = [torch.from_numpy(np.ascontiguousarray(a).reshape(-1)).to(device) for a in arrs]
+    out = torch.empty_like(t[0])
+    P = _abi.ptr
+    _abi.check(_abi.lib().rlmd_shadow_equiv(P(t[0]), P(t[1]), P(t[2]), P(t[3]), float(min_mul), t[0].numel(), P(out),
+                                            _abi.stream_ptr()))
+    return out.cpu().numpy().reshape(shape)

@@ -431,9 +431,19 @@ def shadow_fixtures():
             agent.append([sh1, sh2])
     agent = np.array(agent)
     assert agent.dtype == np.float32
+    # shadow_equiv as tools/aggregate_data.py:441-447 calls it: (mean, tail, cmin,
+    # mean, 1) on float64 aggregates; tail indices on both sides of 1
+    rng = np.random.default_rng(23)
+    eq_mean = 10 ** rng.uniform(-3, 2, 64)
+    eq_alpha = rng.uniform(0.05, 1.3, 64)
+    eq_min = eq_mean * 10 ** rng.uniform(-4, -0.1, 64)
+    with np.errstate(all="ignore"):
+        eq = np.array([float(np.atleast_1d(ut.shadow_equiv(m, a, lo, m, 1))[0])
+                       for m, a, lo in zip(eq_mean, eq_alpha, eq_min)])
     return {"alpha": alphas, "min": mins, "max": maxs, "shadow": sh,
             "aw_actions": acts, "aw_steps": steps, "aw_out": win,
-            "loss_rows": rows, "agent_shadow": agent}
+            "loss_rows": rows, "agent_shadow": agent,
+            "eq_mean": eq_mean, "eq_alpha": eq_alpha, "eq_min": eq_min, "eq_out": eq}
 
 
 # ----------------------------------------------------------------------------

@@ -242,3 +242,15 @@ def test_shadow_means_match_reference(golden):
     np.testing.assert_allclose(got, g["shadow"], rtol=1e-14)
     rows = np.stack([osh.agent_shadow_mean(r) for r in g["loss_rows"]])
     np.testing.assert_array_equal(rows, g["agent_shadow"])
+
+
+def test_shadow_equiv_matches_reference(golden):
+    """oracle.shadow.shadow_equiv (SciPy hybrd, the reference's own solver) vs the
+    reference's utils.shadow_equiv as aggregate_data.py calls it."""
+    from oracle import shadow as osh
+
+    g = golden("shadow.npz")
+    with np.errstate(all="ignore"):
+        got = np.array([osh.shadow_equiv(m, a, lo, m, 1) for m, a, lo in zip(g["eq_mean"], g["eq_alpha"], g["eq_min"])])
+    np.testing.assert_allclose(got, g["eq_out"], rtol=1e-12)
+    assert (g["eq_out"][g["eq_alpha"] >= 1] == 1).all()

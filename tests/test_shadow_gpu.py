@@ -69,3 +69,18 @@ def test_trainer_last_stats_shadow(dev):
     ref = osh.agent_shadow_mean(raw[:11].astype(np.float32))
     _check(st[6:8].astype(np.float32), ref)
     np.testing.assert_array_equal(st[:6], raw[:6])
+
+
+def test_shadow_equiv_matches_reference(golden, dev):
+    """rlmd_shadow_equiv (1-D Newton restatement of hybrd) vs the reference's
+    MINPACK root: the same root within rtol 1e-6 (hybrd's xtol is 1.5e-8
+    relative; the two iterations stop at different points inside it)."""
+    from rlmd_amd import _abi
+
+    g = golden("shadow.npz")
+    t = [torch.from_numpy(np.ascontiguousarray(g[k])).to(dev) for k in ("eq_mean", "eq_alpha", "eq_min")]
+    out = torch.empty_like(t[0])
+    P = _abi.ptr
+    _abi.check(_abi.lib().rlmd_shadow_equiv(P(t[0]), P(t[1]), P(t[2]), P(t[0]), 1.0, t[0].numel(), P(out),
+                                            _abi.stream_ptr()))
+    np.testing.assert_allclose(out.cpu().numpy(), g["eq_out"], rtol=1e-6)
