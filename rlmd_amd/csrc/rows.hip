@@ -100,9 +100,9 @@ __host__ __device__ inline Lds lds_layout(const RowDims& d) {
   Lds l{};
   auto up = [](int v) { return (v + 15) & ~15; };
   int o = 0;
-  l.ldx = d.X;
+  l.ldx = d.X > W1P ? d.X : W1P;  // >= W1P: layer 1 reads W1P columns unconditionally (zero padded)
   l.xs = o;
-  o = up(o + R * d.X * 4);
+  o = up(o + R * l.ldx * 4);
   l.lda1 = hmax + pad;  // A operand of the forward (h1) and backward (dh2) MFMAs
   l.a1 = o;
   o = up(o + R * l.lda1 * ts);
@@ -295,9 +295,10 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
     float v = 0.f;
     if (m.c < H1) {
       float acc = 0.f;
+      // xs rows are zero padded to ldx >= W1P and k.w1[j] = 0 for j >= in: no branch
+      // between the LDS reads, so a row's W1P reads issue together
 #pragma unroll
-      for (int j = 0; j < W1P; ++j)
-        if (j < in) acc = fmaf(xs[r * ldx + j], k.w1[j], acc);
+      for (int j = 0; j < W1P; ++j) acc = fmaf(xs[r * ldx + j], k.w1[j], acc);
       for (int j = W1P; j < in; ++j) acc = fmaf(xs[r * ldx + j], w[j], acc);
       v = fmaxf(acc + k.b1, 0.f);
       if (h1_out && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + m.c] = v;
@@ -464,12 +465,39 @@ __device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, 
   if (logp_out && valid) logp_out[b] = policy_logp(smp.dist, A, lp_sum, m2_sum, hld_sum, jac_sum);
 }
 
-// Stage rows [row0, row0 + 16) of a [B, in] matrix into xs (pitch ldx), zeros past B.
+// Stage rows [row0, row0 + 16) of a [B, in] matrix into xs (pitch ldx), zeros
+// past B and in columns [in, ldx) (layer 1 reads the first W1P columns of every
+// row without a bound check).
 __device__ __forceinline__ void stage_rows(const float* src, int in, float* xs, int ldx, int row0, int B) {
   const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(src, (int64_t)B * in * 4);
-  for (int e = threadIdx.x; e < R * in; e += NT) {
-    const int r = e / in, k = e % in;
-    xs[r * ldx + k] = rlmd_ldf(rs, (int64_t)(row0 + r) * in + k, row0 + r < B);
+  for (int e = threadIdx.x; e < R * ldx; e += NT) {
+    const int r = e / ldx, k = e % ldx;
+    xs[r * ldx + k] = rlmd_ldf(rs, (int64_t)(row0 + r) * in + k, k < in && row0 + r < B);
+  }
+}
+
+// stage_rows in two halves around the parameter prefetch: the row load is issued
+// first, its LDS store after the prefetch is issued, so the store waits on the
+// row load only (vmcnt retires in order) and layer 1 overlaps the fragment flight.
+struct StageReg {
+  float v;
+  int e;
+};
+__device__ __forceinline__ StageReg stage_issue(const float* src, int in, int ldx, int row0, int B) {
+  StageReg sr{0.f, (int)threadIdx.x};
+  if (R * ldx <= NT) {
+    const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(src, (int64_t)B * in * 4);
+    const int r = sr.e / ldx, k = sr.e - r * ldx;
+    sr.v = rlmd_ldf(rs, (int64_t)(row0 + r) * in + k, sr.e < R * ldx && k < in && row0 + r < B);
+  }
+  return sr;
+}
+__device__ __forceinline__ void stage_commit(const StageReg& sr, const float* src, int in, float* xs, int ldx, int row0,
+                                             int B) {
+  if (R * ldx <= NT) {
+    if (sr.e < R * ldx) xs[sr.e] = sr.v;  // element e = r * ldx + k
+  } else {
+    stage_rows(src, in, xs, ldx, row0, B);
   }
 }
 
@@ -501,14 +529,15 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     RLMD_TSR(16 * job + 0);
     const RowNet& an = a.tactor;
     const RowNet& cn = a.tcrit[job];
-    Pre<PREC, NBW, MULTI> pa, pc;
-    pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
-    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    const StageReg sr = stage_issue(a.s2, d.S, L.ldx, row0, B);
     FwdConst<NBW> ka, kc;
     actor_const<NBW>(ka, an, a.ao, d);
+    Pre<PREC, NBW, MULTI> pa, pc;
+    pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
     critic_const<NBW>(kc, cn, a.co, d);
+    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
     RLMD_TSR(16 * job + 1);
-    stage_rows(a.s2, d.S, xs, L.ldx, row0, B);
+    stage_commit(sr, a.s2, d.S, xs, L.ldx, row0, B);
     __syncthreads();
     RLMD_TSR(16 * job + 2);
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
@@ -526,11 +555,12 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     if (job == 2) RLMD_TSR(60);
     const int g = job - 2;
     const RowNet& cn = a.crit[g];
-    Pre<PREC, NBW, MULTI> pc;
-    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    const StageReg sr = stage_issue(a.xsa, d.X, L.ldx, row0, B);
     FwdConst<NBW> kc;
     critic_const<NBW>(kc, cn, a.co, d);
-    stage_rows(a.xsa, d.X, xs, L.ldx, row0, B);
+    Pre<PREC, NBW, MULTI> pc;
+    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    stage_commit(sr, a.xsa, d.X, xs, L.ldx, row0, B);
     __syncthreads();
     if (job == 2) RLMD_TSR(61);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.c1[g],
@@ -539,11 +569,12 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)
     const RowNet& an = a.actor;
-    Pre<PREC, NBW, MULTI> pa;
-    pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
+    const StageReg sr = stage_issue(a.s, d.S, L.ldx, row0, B);
     FwdConst<NBW> ka;
     actor_const<NBW>(ka, an, a.ao, d);
-    stage_rows(a.s, d.S, xs, L.ldx, row0, B);
+    Pre<PREC, NBW, MULTI> pa;
+    pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
+    stage_commit(sr, a.s, d.S, xs, L.ldx, row0, B);
     __syncthreads();
     for (int e = threadIdx.x; e < R * d.S; e += NT) {
       const int r = e / d.S, k = e % d.S;
