@@ -952,6 +952,21 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   }
   RLMD_TSR(108);
   // ---- through the sampling and the heads
+  // this thread's head-weight column for the dh2 pass below (A <= 2: registers),
+  // issued ahead of the actor's fragments so its first use does not wait on
+  // them (vmcnt retires in issue order); loaded once instead of per row (the
+  // dh2 stores may alias the parameters for the compiler)
+  float wp[2], wl[2];
+  {
+    const ElemMap m = elem_map(H2p);
+    const bool cin = m.c < ao.h2, few = A <= 2;
+    const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(a.actor.p, ao.size * 4);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      wp[j] = few && j < A ? rlmd_ldf(rp, ao.w3 + (int64_t)j * ao.h2 + m.c, cin) : 0.f;
+      wl[j] = few && sac && j < A ? rlmd_ldf(rp, ao.w4 + (int64_t)j * ao.h2 + m.c, cin) : 0.f;
+    }
+  }
   Pre<PREC, NBW, MULTI>& pa = p0;  // reuse the first critic's fragment registers
   pre_issue<PREC, NBW, MULTI>(pa, a.actor.wt, H2p, H2p, H1p / 16);
   const int r = threadIdx.x;
@@ -979,6 +994,8 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     } else {
       for (int j = 0; j < 2 * A; ++j) ghs[r * kHeadsMax + j] = 0.f;
     }
+    // the dh2 pass reads columns 0..3 of every row unconditionally (A <= 2)
+    for (int q = sac ? 2 * A : A; q < 4; ++q) ghs[r * kHeadsMax + q] = 0.f;
   }
   __syncthreads();
   RLMD_TSR(109);
@@ -987,12 +1004,24 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     const int H2 = ao.h2;
     const ElemMap m = elem_map(H2p);
     const float* P = a.actor.p;
+    const bool cin = m.c < H2, few = A <= 2;
+    RLMD_TSR(106);
 #pragma unroll
     for (int rr = 0; rr < kMR<NBW>; ++rr) {
       const int rw = m.r0 + rr;
       if (rw < m.r1) {
         float acc = 0.f;
-        if (m.c < H2) {
+        if (few) {
+          // unconditional reads (zero-filled columns, zero weights past A): no
+          // branch between them; the log-scale gradients sit at columns A + j
+          const float* gr = ghs + rw * kHeadsMax;
+          const float g0 = gr[0], g1 = gr[1], g2 = gr[2], g3 = gr[3];
+          const float l0 = A == 1 ? g1 : g2, l1 = A == 1 ? g2 : g3;
+          acc = fmaf(g0, wp[0], acc);
+          acc = fmaf(l0, wl[0], acc);
+          acc = fmaf(g1, wp[1], acc);
+          acc = fmaf(l1, wl[1], acc);
+        } else if (cin) {
           for (int j = 0; j < A; ++j) {
             acc = fmaf(ghs[rw * kHeadsMax + j], P[ao.w3 + (int64_t)j * H2 + m.c], acc);
             if (sac) acc = fmaf(ghs[rw * kHeadsMax + A + j], P[ao.w4 + (int64_t)j * H2 + m.c], acc);
@@ -1004,6 +1033,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       }
     }
   }
+  RLMD_TSR(107);
   __syncthreads();
   RLMD_TSR(110);
   dh1_rows<PREC, NBW, MULTI>(pa, a.actor, ao, ka, aT, L.ldaT, a.dh1, nullptr, 0, nullptr, row0, B);

@@ -76,7 +76,7 @@ def run():
         print("  total", np.median(r[:, idx[-1]] - r[:, idx[0]]))
     seq("fwd_rows target job 0", [0, 1, 2, 3, 4, 5])
     seq("fwd_rows critic job 2", [60, 61, 63, 64, 65, 66, 67, 62])
-    seq("abwd_rows", [96, 95, 97, 98, 99, 100, 101, 103, 104, 105, 108, 109, 110, 111])
+    seq("abwd_rows", [96, 95, 97, 98, 99, 100, 101, 103, 104, 105, 108, 109, 106, 107, 110, 111])
     seq("cbwd_rows (0, 0, 0)", [112, 113, 114, 115, 116, 117, 118])
 
 
