@@ -821,10 +821,11 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const float log_alpha = sac ? a.st->log_alpha : 0.f;  // scalar loads, issued with the first round
   const float qb0 = a.crit[0].p[co.b3], qb1 = nq > 1 ? a.crit[1].p[co.b3] : 0.f;
   const float row_q1 = rlmd_ldf(rq0, bq, tq < R && bq < B), row_q2 = rlmd_ldf(rq1, bq, tq < R && bq < B && nq > 1);
+  // first round: what the loss and critic 1 need (under the 63-load vmcnt cap);
+  // critic 2's masks / fragments follow after the key pass, the actor's before
+  // the sampling pass
   BwdMask<NBW> k0, k1, ka;
   bwd_mask<NBW>(k0, a.e1[0], a.e2[0], a.crit[0].p + co.w3, co, row0, B);
-  if (nq > 1) bwd_mask<NBW>(k1, a.e1[1], a.e2[1], a.crit[1].p + co.w3, co, row0, B);
-  bwd_mask<NBW>(ka, a.h1a, a.h2a, nullptr, ao, row0, B);
   float w1a[NQ][NBW][NHF];  // W1_g[c][S + j] for this lane's dh1 columns
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
@@ -839,7 +840,6 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   }
   Pre<PREC, NBW, MULTI> p0, p1;
   pre_issue<PREC, NBW, MULTI>(p0, a.crit[0].wt, H2p, H2p, H1p / 16);
-  if (nq > 1) pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
   RLMD_TSR(95);
   // ---- actor loss (algo_sac.py:546-562 / algo_td3.py:507-523): every row's
   //      objective and ranking key (SAC sorts descending, TD3 ascending, Q5)
@@ -860,6 +860,10 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const bool ext = a.dqn_ext[0] != nullptr;  // loss from actor_loss_kernel (B > 512)
   __syncthreads();
   RLMD_TSR(97);
+  if (nq > 1) {
+    bwd_mask<NBW>(k1, a.e1[1], a.e2[1], a.crit[1].p + co.w3, co, row0, B);
+    pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
+  }
   if (!ext && blockIdx.x == gridDim.x - 1 - (a.cstats.B > 0 ? 1 : 0)) {
     // the loss workgroup: selection over all rows -> loss value, temperature gradient
     uint64_t* runs = reinterpret_cast<uint64_t*>(smem + L.runs);
@@ -967,6 +971,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       wl[j] = few && sac && j < A ? rlmd_ldf(rp, ao.w4 + (int64_t)j * ao.h2 + m.c, cin) : 0.f;
     }
   }
+  bwd_mask<NBW>(ka, a.h1a, a.h2a, nullptr, ao, row0, B);
   Pre<PREC, NBW, MULTI>& pa = p0;  // reuse the first critic's fragment registers
   pre_issue<PREC, NBW, MULTI>(pa, a.actor.wt, H2p, H2p, H1p / 16);
   const int r = threadIdx.x;
