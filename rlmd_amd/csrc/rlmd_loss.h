@@ -67,6 +67,8 @@ struct CriticLoads {
   float qt[2], q[2], rw, lpn;
   int eff;
   uint8_t dn;
+  // uniform scalars issued with the row loads: head biases, log alpha, Cauchy scales
+  float tb[2], qb[2], log_alpha, cauchy[2];
 };
 __device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
   const int b = threadIdx.x, B = a.B;
@@ -83,6 +85,12 @@ __device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
   L.eff = a.eff ? (int)__builtin_bit_cast(
                       int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, nB), in ? b * 4 : 0x7fffffff, 0, 0))
                 : 1;
+  for (int g = 0; g < 2; ++g) {
+    L.tb[g] = a.tb[g][0];
+    L.qb[g] = a.qb[g][0];
+    L.cauchy[g] = a.st->cauchy[g];
+  }
+  L.log_alpha = a.st->log_alpha;
   return L;
 }
 
@@ -96,19 +104,19 @@ __device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, C
   const int eff = L.eff;
   float y = 0.f;
   for (int g = 0; g < 2; ++g) {
-    qt[g] += a.tb[g][0];
-    q[g] += a.qb[g][0];
+    qt[g] += L.tb[g];
+    q[g] += L.qb[g];
   }
   if (in) {
     if (dn) qt[0] = qt[1] = 0.f;
     const float m = fminf(qt[0], qt[1]);
     const float ge = powf(a.gamma, (float)eff);
-    if (a.algo == RLMD_SAC) y = (a.reward_scale * rw + ge * m) - expf(st->log_alpha) * lpn;
+    if (a.algo == RLMD_SAC) y = (a.reward_scale * rw + ge * m) - expf(L.log_alpha) * lpn;
     else y = rw + ge * m;
   } else {
     q[0] = q[1] = 0.f;
   }
-  const float scale[2] = {st->cauchy[0], st->cauchy[1]};
+  const float scale[2] = {L.cauchy[0], L.cauchy[1]};
   // R1: means of (t - q)^2 (CIM kernel), of y, q (TCAU), Nagy terms; NaN flag
   const float e0 = (y - q[0]) * (y - q[0]), e1 = (y - q[1]) * (y - q[1]);
   const float z0 = (y - q[0]) / scale[0], z1 = (y - q[1]) / scale[1];
