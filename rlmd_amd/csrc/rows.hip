@@ -653,11 +653,15 @@ __device__ __forceinline__ void dh2_from_q(const BwdMask<NBW>& k, const float* d
                                            typename CT<PREC>::T* aT, int ldaT, float* dh2_out, int row0, int B) {
   const int H2 = o.h2;
   const ElemMap m = elem_map(pad32(H2));
+  // every row's dq read first (clamped row, no branch between the LDS reads)
+  float dq[kMR<NBW>];
+#pragma unroll
+  for (int rr = 0; rr < kMR<NBW>; ++rr) dq[rr] = dqr[m.r0 + rr < R ? m.r0 + rr : R - 1];
 #pragma unroll
   for (int rr = 0; rr < kMR<NBW>; ++rr) {
     const int r = m.r0 + rr;
     if (r < m.r1) {
-      const float v = k.m2[rr] > 0.f ? dqr[r] * k.w3 : 0.f;
+      const float v = k.m2[rr] > 0.f ? dq[rr] * k.w3 : 0.f;
       aT[r * ldaT + m.c] = CT<PREC>::cvt(v);
       if (dh2_out && m.c < H2 && row0 + r < B) dh2_out[(int64_t)(row0 + r) * H2 + m.c] = v;
     }
