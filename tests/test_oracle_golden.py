@@ -244,6 +244,7 @@ def test_shadow_means_match_reference(golden):
     np.testing.assert_array_equal(rows, g["agent_shadow"])
 
 
+@pytest.mark.filterwarnings("ignore::RuntimeWarning")  # SciPy's hybrd probes overflow exp on the way
 def test_shadow_equiv_matches_reference(golden):
     """oracle.shadow.shadow_equiv (SciPy hybrd, the reference's own solver) vs the
     reference's utils.shadow_equiv as aggregate_data.py calls it."""
