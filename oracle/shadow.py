@@ -41,6 +41,7 @@ def shadow_equiv(mean, alpha, mn, mx, min_mul=1):
     import scipy.optimize as op
 
     if alpha < 1:
-        f = lambda m: shadow_means(alpha, mn, mx, min_mul, m, dtype=np.float64) - mean  # noqa: E731
+        f = lambda m: np.atleast_1d(  # noqa: E731  (hybrd hands over m as a 1-element array)
+            shadow_means(alpha, mn, mx, min_mul, float(np.ravel(m)[0]), dtype=np.float64) - mean)
         return float(np.atleast_1d(op.root(f, 1, method="hybr").x)[0])
     return 1.0
