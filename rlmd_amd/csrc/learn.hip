@@ -235,6 +235,8 @@ struct Scratch {
   float *h1, *h2, *logp, *xsan, *save;
   float *e1[2], *e2[2], *qnpart[2], *dqn[2], *dlogp;
   float *gh, *dh2, *dh1;
+  // ReLU masks (bytes, rows.hip m1_index / m2_index layouts) of c1/c2, e1/e2, h1/h2
+  uint8_t *cm1[2], *cm2[2], *em1[2], *em2[2], *am1, *am2;
   float* stats;  // [16] when the caller passes none
 };
 
@@ -511,6 +513,8 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       f.crit[g] = crit[g];
       f.c1[g] = S_.c1[g];
       f.c2[g] = S_.c2[g];
+      f.cm1[g] = S_.cm1[g];
+      f.cm2[g] = S_.cm2[g];
       f.q[g] = S_.qpart[g];
     }
     f.xsa = mb.xsa;
@@ -522,6 +526,8 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     f.eps_cur = eps_b;
     f.h1a = S_.h1;
     f.h2a = S_.h2;
+    f.am1 = S_.am1;
+    f.am2 = S_.am2;
     f.xsan = S_.xsan;
     f.logp = S_.logp;
     f.save = S_.save;
@@ -581,8 +587,8 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     for (int g = 0; g < 2; ++g) {
       cb.crit[g] = crit[g];
       cb.dq[g] = S_.dq[g];
-      cb.c1[g] = S_.c1[g];
-      cb.c2[g] = S_.c2[g];
+      cb.cm1[g] = S_.cm1[g];
+      cb.cm2[g] = S_.cm2[g];
       cb.dc2[g] = S_.dc2[g];
       cb.dc1[g] = S_.dc1[g];
     }
@@ -624,8 +630,10 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     qe.x = S_.xsan;
     for (int g = 0; g < 2; ++g) {
       qe.crit[g] = crit[g];
-      qe.e1[g] = S_.e1[g];
-      qe.e2[g] = S_.e2[g];
+      qe.e1[g] = nullptr;  // only the masks are consumed (abwd)
+      qe.e2[g] = nullptr;
+      qe.em1[g] = S_.em1[g];
+      qe.em2[g] = S_.em2[g];
       qe.qn[g] = S_.qnpart[g];
     }
     RLMD_TRY(qeval_rows_launch(qe, nq, st));
@@ -661,16 +669,16 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     for (int g = 0; g < 2; ++g) {
       ab.crit[g] = crit[g];
       ab.qn[g] = S_.qnpart[g];
-      ab.e1[g] = S_.e1[g];
-      ab.e2[g] = S_.e2[g];
+      ab.em1[g] = S_.em1[g];
+      ab.em2[g] = S_.em2[g];
       ab.dqn_ext[g] = fused_loss ? nullptr : S_.dqn[g];
     }
     ab.dlogp_ext = fused_loss ? nullptr : S_.dlogp;
     ab.actor = row_net(ag, SLOT_ACTOR);
     ab.logp = S_.logp;
     ab.save = S_.save;
-    ab.h1a = S_.h1;
-    ab.h2a = S_.h2;
+    ab.am1 = S_.am1;
+    ab.am2 = S_.am2;
     ab.st = ag->st;
     ab.stats = stats;
     ab.k = c.topk;
@@ -860,6 +868,17 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.y, B);
   RLMD_ALLOC(s.h1, B * H1);
   RLMD_ALLOC(s.h2, B * H2);
+  {
+    const size_t nrb = (size_t)(B + 15) / 16, m1b = nrb * rlmd::pad32(H1) * 16, m2b = nrb * rlmd::pad32(H2) * 16;
+    RLMD_ALLOC(s.am1, m1b);
+    RLMD_ALLOC(s.am2, m2b);
+    for (int g = 0; g < 2; ++g) {
+      RLMD_ALLOC(s.cm1[g], m1b);
+      RLMD_ALLOC(s.cm2[g], m2b);
+      RLMD_ALLOC(s.em1[g], m1b);
+      RLMD_ALLOC(s.em2[g], m2b);
+    }
+  }
   RLMD_ALLOC(s.logp, B);
   RLMD_ALLOC(s.xsan, B * X);
   RLMD_ALLOC(s.save, B * 5 * A);

@@ -116,6 +116,8 @@ struct FwdRowsArgs {
   const float* xsa;
   float* c1[2];
   float* c2[2];
+  uint8_t* cm1[2];  // ReLU masks of c1 / c2 in the backward layouts (rows.hip m1_index / m2_index)
+  uint8_t* cm2[2];
   float* q[2];
   int32_t with_actor, a_mode, a_tag;
   RowNet actor;
@@ -123,6 +125,8 @@ struct FwdRowsArgs {
   const float* eps_cur;
   float* h1a;
   float* h2a;
+  uint8_t* am1;
+  uint8_t* am2;
   float* xsan;
   float* logp;
   float* save;  // [B, 5A]
@@ -134,8 +138,10 @@ struct QEvalArgs {
   NetOff co;
   RowNet crit[2];
   const float* x;
-  float* e1[2];
+  float* e1[2];  // nullable: the activations are needed only as masks
   float* e2[2];
+  uint8_t* em1[2];
+  uint8_t* em2[2];
   float* qn[2];
 };
 
@@ -170,8 +176,8 @@ struct CBwdArgs {
   NetOff co;
   RowNet crit[2];
   const float* dq[2];
-  const float* c1[2];
-  const float* c2[2];
+  const uint8_t* cm1[2];
+  const uint8_t* cm2[2];
   float* dc2[2];
   float* dc1[2];
   // B <= 512: the row workgroups form dq from the loss inputs themselves
@@ -195,11 +201,11 @@ struct ABwdArgs {
   RowNet actor;
   const float* qn[2];  // updated critics on (s, a_new), no head bias [B]
   const float* logp;   // SAC
-  const float* e1[2];
-  const float* e2[2];
+  const uint8_t* em1[2];
+  const uint8_t* em2[2];
   const float* save;
-  const float* h1a;
-  const float* h2a;
+  const uint8_t* am1;
+  const uint8_t* am2;
   LearnState* st;
   float* stats;
   int32_t k, topk;

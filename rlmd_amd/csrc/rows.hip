@@ -283,11 +283,23 @@ __device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, cons
   }
 }
 
+// ReLU masks as bytes in the layouts their consumers read (one wide load each):
+//   m1 [row block][band][lane][4]: the MFMA accumulator layout over H1p (dh1) —
+//      a lane's 4 rows of one column are one 4-byte word;
+//   m2 [row block][column][16 rows]: the elementwise map over H2p (dh2) — a
+//      thread's kMR consecutive rows are kMR contiguous bytes.
+__device__ __forceinline__ int64_t m1_index(int rb, int H1p, int row, int col) {
+  return ((((int64_t)rb * (H1p >> 4) + (col >> 4)) * 64 + (col & 15) + 16 * ((row & 15) >> 2)) << 2) + (row & 3);
+}
+__device__ __forceinline__ int64_t m2_index(int rb, int H2p, int row, int col) {
+  return (((int64_t)rb * H2p + col) << 4) + (row & 15);
+}
+
 // h1 = relu(x W1^T + b1): A operand (T, zero-padded to H1p) + f32 to HBM (nullable)
 template <int PREC, int NBW>
 __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, const NetOff& o, const float* xs,
-                                       int ldx, int in, typename CT<PREC>::T* a1, int lda1, float* h1_out, int row0,
-                                       int B) {
+                                       int ldx, int in, typename CT<PREC>::T* a1, int lda1, float* h1_out,
+                                       uint8_t* m1_out, int row0, int B) {
   const int H1 = o.h1;
   const ElemMap m = elem_map(pad32(H1));
   const float* w = p + o.w1 + (int64_t)m.c * in;
@@ -303,6 +315,7 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
       v = fmaxf(acc + k.b1, 0.f);
       if (h1_out && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + m.c] = v;
     }
+    if (m1_out) m1_out[m1_index(row0 / R, pad32(H1), r, m.c)] = v > 0.f ? 1 : 0;
     a1[r * lda1 + m.c] = CT<PREC>::cvt(v);
   }
 }
@@ -311,8 +324,8 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
 // partials part[wave][row][h] (nh <= NHF).
 template <int NBW>
 __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdConst<NBW>& k, const NetOff& o,
-                                             int nh, float* h2_out, float* h2s, int ldh2, float* part, int row0,
-                                             int B) {
+                                             int nh, float* h2_out, uint8_t* m2_out, float* h2s, int ldh2,
+                                             float* part, int row0, int B) {
   const int H2 = o.h2, nblk = pad32(H2) / 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float ph[4][NHF];
@@ -325,15 +338,18 @@ __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdC
     if (wave + NW * i < nblk) {
       const int col = acc_col(i);
       const bool cin = col < H2;
+      uint32_t mw = 0;
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         const int r = acc_row(rg);
         const float v = cin ? fmaxf(acc[i][rg] + k.b2[i], 0.f) : 0.f;
         if (h2_out && cin && row0 + r < B) h2_out[(int64_t)(row0 + r) * H2 + col] = v;
         if (h2s) h2s[r * ldh2 + col] = v;
+        mw |= (v > 0.f ? 1u : 0u) << (8 * rg);
 #pragma unroll
         for (int h = 0; h < NHF; ++h) ph[rg][h] = fmaf(v, k.hw[i][h], ph[rg][h]);
       }
+      if (m2_out) *reinterpret_cast<uint32_t*>(m2_out + m2_index(row0 / R, pad32(H2), acc_row(0), col)) = mw;
     }
   }
   if (nh <= NHF) {
@@ -380,13 +396,14 @@ __device__ void row_dots(const float* src, int lds, int ncols, int nh, const flo
 template <int PREC, int NBW, bool MULTI>
 __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>& k, Pre<PREC, NBW, MULTI>& pre,
                          const float* xs, int ldx, int in, int nh, const float* wa, const float* wb, int na,
-                         unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B) {
+                         unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B,
+                         uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr) {
   using T = typename CT<PREC>::T;
   T* a1 = reinterpret_cast<T*>(smem + L.a1);
   float* part = reinterpret_cast<float*>(smem + L.part);
   float* hout = reinterpret_cast<float*>(smem + L.hout);
   float* h2s = reinterpret_cast<float*>(smem + L.h2s);
-  layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, row0, B);
+  layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, m1_out, row0, B);
   if (blockIdx.y == 2) RLMD_TSR(63);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(64);
@@ -395,7 +412,7 @@ __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>
   mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, pad32(o.h2) / 16, acc);
   if (blockIdx.y == 2) RLMD_TSR(65);
   const bool fused = nh <= NHF;
-  fwd_epilogue<NBW>(acc, k, o, nh, h2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B);
+  fwd_epilogue<NBW>(acc, k, o, nh, h2_out, m2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B);
   if (blockIdx.y == 2) RLMD_TSR(66);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(67);
@@ -564,7 +581,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     __syncthreads();
     if (job == 2) RLMD_TSR(61);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.c1[g],
-                               a.c2[g], row0, B);
+                               a.c2[g], row0, B, a.cm1[g], a.cm2[g]);
     if (job == 2) RLMD_TSR(62);
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)
@@ -581,7 +598,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
       if (row0 + r < B) a.xsan[(int64_t)(row0 + r) * d.X + k] = xs[r * L.ldx + k];
     }
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
-                               d.A, smem, L, a.h1a, a.h2a, row0, B);
+                               d.A, smem, L, a.h1a, a.h2a, row0, B, a.am1, a.am2);
     sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, a.a_mode, a.a_tag, a.eps_cur, 0.f, 0.f, 0, a.logp, a.save,
                 a.xsan, row0, B);
   }
@@ -603,7 +620,7 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   stage_rows(a.x, d.X, xs, L.ldx, row0, B);
   __syncthreads();
   mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.e1[g], a.e2[g],
-                             row0, B);
+                             row0, B, a.em1[g], a.em2[g]);
   if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qn[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
 }
 
@@ -624,26 +641,41 @@ struct BwdMask {
 };
 
 template <int NBW>
-__device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const float* h1, const float* h2, const float* w3,
+__device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const uint8_t* m1, const uint8_t* m2, const float* w3,
                                          const NetOff& o, int row0, int B, int nb0 = 0) {
-  const int H1 = o.h1, H2 = o.h2;
-  const ElemMap m = elem_map(pad32(H2));
+  const int H2 = o.h2, H1p = pad32(o.h1), H2p = pad32(o.h2), rb = row0 / R;
+  const ElemMap m = elem_map(H2p);
   const bool cin = m.c < H2;
-  const __amdgpu_buffer_rsrc_t r1 = rlmd_rsrc(h1, (int64_t)B * H1 * 4), r2 = rlmd_rsrc(h2, (int64_t)B * H2 * 4);
+  const int nrb = (B + R - 1) / R;
+  const __amdgpu_buffer_rsrc_t r1 = rlmd_rsrc(m1, (int64_t)nrb * H1p * 16),
+                               r2 = rlmd_rsrc(m2, (int64_t)nrb * H2p * 16);
+  // m2: this thread's kMR consecutive rows of column m.c from kMR / 4 aligned
+  // words (+ one when its first row is not word aligned: fewer than 4 rows per
+  // thread, H2p < 128)
+  constexpr int NWD = kMR<NBW> / 4;
+  const int sh = m.r0 & 3, rbase = m.r0 & ~3;
+  uint32_t wd[NWD + 1];
+#pragma unroll
+  for (int w = 0; w <= NWD; ++w) {
+    const int64_t e = m2_index(rb, H2p, rbase + 4 * w, m.c);
+    const bool need = m.r0 < R && (w < NWD || sh != 0);
+    wd[w] = __builtin_amdgcn_raw_buffer_load_b32(r2, need ? (int)e : 0x7fffffff, 0, 0);
+  }
 #pragma unroll
   for (int rr = 0; rr < kMR<NBW>; ++rr) {
-    const int r = m.r0 + rr;
-    k.m2[rr] = rlmd_ldf(r2, (int64_t)(row0 + r) * H2 + m.c, r < m.r1 && cin && row0 + r < B);
+    const int bb = (rr & 3) + sh;
+    const uint32_t w = bb < 4 ? wd[rr >> 2] >> (8 * bb) : wd[(rr >> 2) + 1] >> (8 * (bb - 4));
+    k.m2[rr] = (w & 0xffu) ? 1.f : 0.f;
   }
   k.w3 = w3 ? rlmd_ldf(rlmd_rsrc(w3, (int64_t)H2 * 4), m.c, cin) : 0.f;
+  // m1: one word (this lane's 4 rows) per accumulator band
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
     const int col = acc_col(i, nb0);
+    const int64_t e = m1_index(rb, H1p, acc_row(0), col);
+    const uint32_t word = __builtin_amdgcn_raw_buffer_load_b32(r1, col < H1p ? (int)e : 0x7fffffff, 0, 0);
 #pragma unroll
-    for (int rg = 0; rg < 4; ++rg) {
-      const int b = row0 + acc_row(rg);
-      k.m1[i][rg] = rlmd_ldf(r1, (int64_t)b * H1 + col, col < H1 && b < B);
-    }
+    for (int rg = 0; rg < 4; ++rg) k.m1[i][rg] = (word >> (8 * rg)) & 0xffu ? 1.f : 0.f;
   }
 }
 
@@ -733,7 +765,7 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
   CriticLoads cl{};
   if (a.loss.B > 0) cl = critic_row_load(a.loss);
   BwdMask<NBW> k;
-  bwd_mask<NBW>(k, a.c1[g], a.c2[g], cn.p + a.co.w3, a.co, row0, B, nb0);
+  bwd_mask<NBW>(k, a.cm1[g], a.cm2[g], cn.p + a.co.w3, a.co, row0, B, nb0);
   Pre<PREC, NBW, MULTI> pw;
   pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, nbp, nb0);
   if (g == 0 && lead) RLMD_TSR(113);
@@ -829,7 +861,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   // critic 2's masks / fragments follow after the key pass, the actor's before
   // the sampling pass
   BwdMask<NBW> k0, k1, ka;
-  bwd_mask<NBW>(k0, a.e1[0], a.e2[0], a.crit[0].p + co.w3, co, row0, B);
+  bwd_mask<NBW>(k0, a.em1[0], a.em2[0], a.crit[0].p + co.w3, co, row0, B);
   float w1a[NQ][NBW][NHF];  // W1_g[c][S + j] for this lane's dh1 columns
 #pragma unroll
   for (int g = 0; g < NQ; ++g) {
@@ -865,7 +897,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   __syncthreads();
   RLMD_TSR(97);
   if (nq > 1) {
-    bwd_mask<NBW>(k1, a.e1[1], a.e2[1], a.crit[1].p + co.w3, co, row0, B);
+    bwd_mask<NBW>(k1, a.em1[1], a.em2[1], a.crit[1].p + co.w3, co, row0, B);
     pre_issue<PREC, NBW, MULTI>(p1, a.crit[1].wt, H2p, H2p, H1p / 16);
   }
   if (!ext && blockIdx.x == gridDim.x - 1 - (a.cstats.B > 0 ? 1 : 0)) {
@@ -975,7 +1007,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       wl[j] = few && sac && j < A ? rlmd_ldf(rp, ao.w4 + (int64_t)j * ao.h2 + m.c, cin) : 0.f;
     }
   }
-  bwd_mask<NBW>(ka, a.h1a, a.h2a, nullptr, ao, row0, B);
+  bwd_mask<NBW>(ka, a.am1, a.am2, nullptr, ao, row0, B);
   Pre<PREC, NBW, MULTI>& pa = p0;  // reuse the first critic's fragment registers
   pre_issue<PREC, NBW, MULTI>(pa, a.actor.wt, H2p, H2p, H1p / 16);
   const int r = threadIdx.x;
