@@ -366,6 +366,14 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
       // inter-workgroup hand-off: sc1 stores + vmcnt(0) + agent atomic; the
       // last arriver reads with sc1 loads after its add returned / a barrier)
       const int tg = (int)blockIdx.x, ns = batch.splits;
+      const rlmd::AdamArgs& ad = batch.adam;
+      if (ns == 1) {  // one split owns the whole reduction: step straight from the registers
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg)
+          if (pidx[0][0][rg] >= 0) rlmd::adam_apply(ad, pidx[0][0][rg], tot[0][0][rg], ain[0][0][rg], polyak);
+        if (tg == 0 && threadIdx.x == 0) rlmd::adam_scalar_step(ad);
+        return;
+      }
       // one uniform resource over the tile's slabs; the lane offset in voffset
       const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
           batch.slabs + (int64_t)tg * ns * 256, (short)0, ns * 256 * 16, 0x00020000);
@@ -387,7 +395,6 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
         const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsl, lo + sp * 4096, 0, kSC1));
         g = sp == 0 ? v : g + v;  // slab order, as adam_kernel sums them
       }
-      const rlmd::AdamArgs& ad = batch.adam;
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg)
         if (pidx[0][0][rg] >= 0) rlmd::adam_apply(ad, pidx[0][0][rg], g[rg], ain[0][0][rg], polyak);

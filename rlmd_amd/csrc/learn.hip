@@ -271,6 +271,7 @@ struct rlmd_agent_s {
   unsigned* tile_ctr = nullptr;
   int32_t max_tiles = 0;
   bool fuse_adam = false;
+  int fuse_splits = RLMD_GRAD_SPLITS;
 };
 
 namespace rlmd {
@@ -371,10 +372,13 @@ __global__ void __launch_bounds__(256) adam_kernel(AdamArgs a, int64_t split_str
 // measured slower at C2: 18.4 + 13.1 us against 8.0 + 6.3 and 6.5 + 5.2 us
 // separate, the publish / ticket / cross-XCD read tail costing more than the
 // launch it saves.  Kept selectable (RLMD_FUSE_ADAM=1 at agent creation) for
-// larger nets and covered by tests/test_learn_gpu.py.
+// larger nets and covered by tests/test_learn_gpu.py; RLMD_FUSE_SPLITS=1 / 2
+// (one tile owns the whole K-sum and steps from its accumulators) is slower
+// still at C2 (bench 77.2M / 82.5M against 84.1M fused split-4 and 90.7M
+// separate): the critic phase has ~150 tiles, too few to fill 256 CUs.
 
 int launch_bwd_w_adam(rlmd_agent_s* ag, GemmBatch& b, const AdamArgs& ad_in, hipStream_t s) {
-  b.splits = RLMD_GRAD_SPLITS;
+  b.splits = ag->fuse_adam ? ag->fuse_splits : RLMD_GRAD_SPLITS;
   b.split_stride = ag->n_params;
   AdamArgs a = ad_in;
   adam_scalars(a.lr, a.cnt / a.interval, a.step_size, a.bc2_sqrt);
@@ -898,6 +902,8 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
     RLMD_HIP(hipMemset(ag->tile_ctr, 0, sizeof(unsigned) * ag->max_tiles));
     const char* fz = getenv("RLMD_FUSE_ADAM");
     ag->fuse_adam = fz && atoi(fz) != 0;
+    const char* fs = getenv("RLMD_FUSE_SPLITS");  // splits of the fused GEMM (1..RLMD_GRAD_SPLITS)
+    ag->fuse_splits = fs ? std::max(1, std::min(RLMD_GRAD_SPLITS, atoi(fs))) : RLMD_GRAD_SPLITS;
   }
   for (int g = 0; g < 2; ++g) {
     RLMD_ALLOC(s.tpart[g], B);

@@ -116,11 +116,14 @@ def test_remaining_losses_fp32(dev, loss):
     test_full_size_fp32_matches_oracle(dev, "SAC", 5, 1, 256, 256, 512, 256, loss)
 
 
+@pytest.mark.parametrize("splits", ["4", "1"])
 @pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL[:2])
-def test_fused_optimiser_epilogue(dev, monkeypatch, algo, S, A, h1, h2, B, k):
+def test_fused_optimiser_epilogue(dev, monkeypatch, algo, S, A, h1, h2, B, k, splits):
     """RLMD_FUSE_ADAM=1: the weight-gradient GEMM's last arriving split steps the
-    parameters (write-through slabs + arrival tickets); same numerics as adam_kernel."""
+    parameters (write-through slabs + arrival tickets; with one split straight from
+    the accumulators); same numerics as adam_kernel up to the K-sum order."""
     monkeypatch.setenv("RLMD_FUSE_ADAM", "1")
+    monkeypatch.setenv("RLMD_FUSE_SPLITS", splits)
     test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, "MSE")
 
 
