@@ -116,6 +116,22 @@ int rlmd_shadow_means(const float* stats_dev, int32_t rows, int32_t ld, float lo
 int rlmd_shadow_equiv(const double* mean_dev, const double* alpha_dev, const double* min_dev, const double* max_dev,
                       double min_mul, int64_t n, double* out_dev, void* stream);
 
+/* --------------------------------------------------- leverage sweeps (§8f-4) */
+/* Workspace for rlmd_lev_coin_sweep: u16 up-count prefixes per 64-step chunk
+ * and the up-count histogram u32 [horizon][horizon + 1]; -1 on bad sizes. */
+int64_t rlmd_lev_workspace_bytes(int64_t investors, int32_t horizon);
+/* Replaces coin_smart_lev (lev/lev_exp.py:128-237; lev/coin_flip.py:178-191):
+ * outcomes_dev u8 [investors][ld] (1 = up; ld % 16 == 0, ld >= horizon rounded
+ * up to 64; 16-byte aligned), levs_host the param_range leverages (negated
+ * inside when -down_r > up_r, as the reference).  Writes data_dev f32
+ * [n_lev][13][horizon - 1] (mean, mean_top, mean_adj, mad x3, std x3,
+ * median x3, lev after each step t + 2) and, when non-null, data_T_dev f32
+ * [n_lev][investors] (final values, the reference's sequential f32 products).
+ * n_lev <= 32, horizon <= 5459. */
+int rlmd_lev_coin_sweep(const uint8_t* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld, int64_t top,
+                        float value_0, float up_r, float down_r, const float* levs_host, int32_t n_lev,
+                        void* workspace_dev, float* data_dev, float* data_T_dev, void* stream);
+
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
 /* Market lanes' episode start rows (i32 [N]) read back (eval_market's

@@ -1,0 +1,59 @@
+"""CPU restatement of the fixed-leverage Monte-Carlo sweep.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker of
+rlmd_lev_coin_sweep; never called by the product path.
+
+Follows lev/lev_exp.py:29-53 (param_range) and :128-237 (coin_smart_lev):
+for each leverage l (negated when -down_r > up_r), every investor's value
+is multiplied step by step by 1 + l*up_r (outcome 1) or 1 + l*down_r (0) in
+float32; after each step t >= 1 the values are sorted descending, the first
+`top` form the top group and the rest the adjusted group, and the table row
+[mean, mean_top, mean_adj, mad, mad_top, mad_adj, std, std_top, std_adj,
+ med, med_top, med_adj, lev] is stored (std unbiased=False, median = the
+lower middle element, as torch.median).  data_T holds the values after all
+`horizon` steps.  Pinned to the reference run on torch CPU
+(tests/golden/lev.npz, make_golden.py:lev_fixtures).
+"""
+import numpy as np
+
+
+def param_range(low, high, increment):
+    """lev/lev_exp.py:29-53."""
+    lo = int(low / increment)
+    hi = int(high / increment + 1)
+    mod = low / increment - lo
+    params = [(x + mod) * increment for x in range(lo, hi, 1)]
+    if 0 in params and len(params) > 1:
+        params.remove(0)
+    return params
+
+
+def _group(v):
+    """mean, mad, std, lower median of one group (float32 values, f64 sums)."""
+    if v.size == 0:
+        return np.nan, np.nan, np.nan, np.nan
+    v = v.astype(np.float64)
+    m = v.mean()
+    return m, np.abs(v - m).mean(), np.sqrt(((v - m) ** 2).mean()), np.sort(v)[(v.size - 1) // 2]
+
+
+def coin_smart_lev(outcomes, top, value_0, up_r, down_r, lev_low, lev_high, lev_incr):
+    """lev/lev_exp.py:128-237 on a [investors, horizon] 0/1 matrix."""
+    levs = np.array(param_range(lev_low, lev_high, lev_incr), dtype=np.float32)
+    levs = -levs if -down_r > up_r else levs
+    inv, hor = outcomes.shape
+    data = np.zeros((len(levs), 13, hor - 1), dtype=np.float32)
+    data_T = np.zeros((len(levs), inv), dtype=np.float32)
+    up = outcomes == 1
+    for i, lev in enumerate(levs):
+        gu = np.float32(1) + lev * np.float32(up_r)
+        gd = np.float32(1) + lev * np.float32(down_r)
+        g = np.where(up, gu, gd).astype(np.float32)
+        val = np.float32(value_0) * g[:, 0]
+        for t in range(hor - 1):
+            val = (val * g[:, t + 1]).astype(np.float32)
+            s = np.sort(val)[::-1]
+            a, tp, ad = _group(val), _group(s[:top]), _group(s[top:])
+            data[i, :, t] = [a[0], tp[0], ad[0], a[1], tp[1], ad[1], a[2], tp[2], ad[2], a[3], tp[3], ad[3], lev]
+        data_T[i] = val
+    return data, data_T

@@ -92,6 +92,8 @@ SIGNATURES = {
     "rlmd_env_lane_start": (C.c_int, [P, P]),
     "rlmd_shadow_means": (C.c_int, [P, I32, I32, C.c_float, C.c_float, P, I32, P]),
     "rlmd_shadow_equiv": (C.c_int, [P, P, P, P, C.c_double, I64, P, P]),
+    "rlmd_lev_workspace_bytes": (I64, [I64, I32]),
+    "rlmd_lev_coin_sweep": (C.c_int, [P, I64, I32, I64, I64, C.c_float, C.c_float, C.c_float, P, I32, P, P, P, P]),
     "rlmd_eval_market": (C.c_int, [P, P, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, P, P]),
     "rlmd_profile_enable": (C.c_int, [I32]),
     "rlmd_profile_read": (C.c_int, [P, P]),
@@ -105,7 +107,7 @@ def header_symbols():
 
     hdr = os.path.join(HERE, "..", "include", "rlmd_abi.h")
     txt = open(hdr).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(rlmd_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|int64_t|const char\*)\s+(rlmd_\w+)\(", txt, re.M)))
 
 
 def load(path=LIB_PATH):

@@ -841,6 +841,32 @@ def learn_fixtures(seed=5):
     return out
 
 
+def lev_fixtures(seed=41):
+    """lev/lev_exp.py:128-237 coin_smart_lev on small Bernoulli outcome matrices
+    (torch CPU, float32, as lev/coin_flip.py:160-176 calls it): the per-step
+    summary table [n_lev, 13, T-1] and the final values [n_lev, I]."""
+    import contextlib
+    import io
+
+    from lev import lev_exp
+
+    out = {}
+    cases = [("pos", 1500, 40, 15, 100.0, 0.5, -0.4, 0.1, 1.0, 0.1),
+             ("neg", 1001, 25, 7, 100.0, 0.3, -0.6, 0.25, 1.0, 0.25),
+             ("odd", 777, 33, 1, 50.0, 0.5, -0.5, 0.2, 0.6, 0.2)]
+    for name, inv, hor, top, v0, up, dn, lo, hi, inc in cases:
+        g = T.Generator().manual_seed(seed)
+        outc = T.bernoulli(T.full((inv, hor), 0.5), generator=g)
+        with contextlib.redirect_stdout(io.StringIO()):
+            data, data_T = lev_exp.coin_smart_lev(T.device("cpu"), outc, inv, hor, top, v0, up, dn, lo, hi, inc)
+        out[name + "_outcomes"] = outc.numpy().astype(np.uint8)
+        out[name + "_args"] = np.array([inv, hor, top, v0, up, dn, lo, hi, inc], dtype=np.float64)
+        out[name + "_levs"] = np.array(lev_exp.param_range(lo, hi, inc), dtype=np.float64)
+        out[name + "_data"] = data.numpy()
+        out[name + "_data_T"] = data_T.numpy()
+    return out
+
+
 def main():
     work = tempfile.mkdtemp(prefix="rlmd_golden_")
     os.chdir(work)  # the reference creates ./results/... relative to cwd
@@ -856,6 +882,7 @@ def main():
         "eval_market.npz": eval_market_fixtures,
         "logs.npz": log_fixtures,
         "learn.npz": learn_fixtures,
+        "lev.npz": lev_fixtures,
     }
     only = sys.argv[1:]
     for fn, job in jobs.items():

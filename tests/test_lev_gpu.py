@@ -1,0 +1,63 @@
+"""rlmd_lev_coin_sweep (lev.hip) against the reference's coin_smart_lev
+fixtures and the oracle (lev/lev_exp.py:128-237).  Final values are the
+reference's sequential float32 products, bit-exact; the summary table is
+computed from up-count histograms with each bin's value rounded once, so it
+agrees with the reference's step-by-step products to a few f32 ulps
+(rtol 1e-5; mad / std rows also within 1e-5 of their group mean)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import lev as olev
+from tests.test_lev_cpu import CASES, Z, close_table
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_sweep_matches_reference(case):
+    from rlmd_amd import lev
+
+    a = Z[case + "_args"]
+    inv, hor, top = int(a[0]), int(a[1]), int(a[2])
+    d, dT = lev.coin_smart_lev("cuda:0", torch.from_numpy(Z[case + "_outcomes"]), inv, hor, top, *a[3:])
+    d, dT = d.cpu().numpy(), dT.cpu().numpy()
+    np.testing.assert_array_equal(dT, Z[case + "_data_T"])
+    ok = close_table(d, Z[case + "_data"], 1e-5)
+    assert ok.all(), np.argwhere(~ok)[:5]
+
+
+@pytest.mark.parametrize("inv,hor,top,up,dn,extremes", [(20000, 300, 40, 0.5, -0.4, False),
+                                                         (3000, 520, 10, 0.5, -0.4, True),
+                                                         (4097, 130, 4097, 0.2, -0.2, False),
+                                                         (5000, 64, 0, 0.5, -0.6, False)])
+def test_sweep_matches_oracle(inv, hor, top, up, dn, extremes):
+    """Larger random matrices; `extremes` adds all-up / all-down investors so a
+    hist workgroup's up-count window exceeds its LDS (global-atomic path);
+    top = investors leaves the adjusted group empty (NaN rows), top = 0 the top group."""
+    from rlmd_amd import lev
+
+    rng = np.random.default_rng(inv + hor)
+    o = (rng.random((inv, hor)) < 0.5).astype(np.uint8)
+    if extremes:
+        o[0], o[1] = 1, 0
+    d, dT = lev.coin_smart_lev("cuda:0", o, inv, hor, top, 100.0, up, dn, 0.25, 1.0, 0.25)
+    od, odT = olev.coin_smart_lev(o, top, 100.0, up, dn, 0.25, 1.0, 0.25)
+    d, dT = d.cpu().numpy(), dT.cpu().numpy()
+    np.testing.assert_array_equal(dT, odT)
+    fin = np.isfinite(od)
+    bad = np.isfinite(d) != fin
+    assert not bad.any(), (np.argwhere(bad)[:6], d[bad][:6], od[bad][:6])
+    ok = close_table(np.where(fin, d, 0), np.where(fin, od, 0), 1e-5)
+    assert ok.all(), np.argwhere(~ok)[:5]
+
+
+def test_bad_arguments_fail_loudly():
+    from rlmd_amd import _abi, lev
+
+    o = np.ones((8, 10), dtype=np.uint8)
+    with pytest.raises(_abi.RlmdError):  # gd = 1 + 3 * -0.4 < 0: values not monotone in the up-count
+        lev.coin_smart_lev("cuda:0", o, 8, 10, 1, 1.0, 0.5, -0.4, 3.0, 3.0, 1.0)
+    with pytest.raises(ValueError):
+        lev.coin_smart_lev("cuda:0", o, 9, 10, 1, 1.0, 0.5, -0.4, 0.5, 0.5, 0.5)
+    assert _abi.lib().rlmd_lev_workspace_bytes(10, 0) == -1

@@ -1,0 +1,65 @@
+"""Full-size leverage sweep: lev/coin_flip.py's investor-1 run,
+coin_smart_lev over 1e6 investors x 3e3 steps x 10 leverages (0.1..1.0), on one
+MI355X.  Prints one JSON line: investor-steps-leverages per second over the
+whole sweep (outcomes resident in HBM), each kernel's HIP-event time, and the
+oracle (the reference's sort-per-step algorithm restated in NumPy) timed on a
+bounded sample on the host cores."""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from rlmd_amd import lev  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--investors", type=int, default=1_000_000)
+    ap.add_argument("--horizon", type=int, default=3000)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    inv, hor = a.investors, a.horizon
+    g = torch.Generator(device=dev).manual_seed(420)
+    ld = (hor + 63) // 64 * 64
+    buf = torch.zeros((inv, ld), dtype=torch.uint8, device=dev)
+    step = 1 << 17
+    for i in range(0, inv, step):  # Bernoulli(0.5) outcomes, generated in slabs
+        n = min(step, inv - i)
+        buf[i:i + n, :hor] = (torch.rand((n, hor), generator=g, device=dev) < 0.5).to(torch.uint8)
+    top = int(inv * 1e-4)
+    args = (inv, hor, top, 100.0, 0.5, -0.4, 0.1, 1.0, 0.1)
+    lev.coin_smart_lev(dev, (buf, hor), *args)  # warm-up
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.reps):
+        data, data_T = lev.coin_smart_lev(dev, (buf, hor), *args)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    n_lev = data.shape[0]
+    units = inv * hor * n_lev
+    out = {"metric": "coin_smart_lev investor-steps-leverages/s", "value": units / (ms / 1e3), "unit": "1/s",
+           "ms_per_sweep": ms, "config": {"investors": inv, "horizon": hor, "n_lev": n_lev, "top": top},
+           "outcome_bytes": inv * ld, "finite_rows": int(torch.isfinite(data).all(dim=(1, 2)).sum())}
+    if not a.no_cpu_baseline:
+        from oracle import lev as olev
+
+        o = buf[:20000, :200].cpu().numpy()
+        t0 = time.perf_counter()
+        olev.coin_smart_lev(o, 2, 100.0, 0.5, -0.4, 0.1, 1.0, 0.1)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": 20000 * 200 * 10 / dt, "unit": "1/s", "cores": 1, "kind": "port",
+                               "sample": "20000 investors x 200 steps x 10 leverages, sort per step (NumPy)"}
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
