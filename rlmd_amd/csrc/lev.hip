@@ -32,7 +32,8 @@
 namespace {
 
 constexpr int kChunk = 64;        // steps per histogram chunk
-constexpr int kInvPerThread = 16;  // investors per thread in lev_hist_kernel
+constexpr int kHistThreads = 1024;  // lev_hist_kernel workgroup: 16 waves share one LDS histogram
+constexpr int kInvPerThread = 4;    // investors per thread in lev_hist_kernel
 constexpr int kHistLds = 24576;    // u32 LDS bins per hist workgroup (96 KB)
 constexpr int kMaxLev = 32;
 
@@ -48,40 +49,56 @@ struct LevArgs {
   float* data_T;   // [n_lev][investors] (nullable)
 };
 
-__device__ __forceinline__ void load64(const uint8_t* row, int t0, int horizon, uint8_t (&o)[kChunk]) {
+// the 64 outcomes of one row chunk as four 16-byte words (rows padded to 64
+// steps); walked with compile-time indices so nothing spills to scratch
+struct Chunk64 {
+  uint32_t w[16];
+  __device__ __forceinline__ void load(const uint8_t* row, int t0) {
 #pragma unroll
-  for (int q = 0; q < kChunk / 16; ++q) {
-    const uint4 v = *reinterpret_cast<const uint4*>(row + t0 + 16 * q);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int b = 0; b < 16; ++b) {
-      const int t = t0 + 16 * q + b;
-      o[16 * q + b] = t < horizon && ((w[b >> 2] >> (8 * (b & 3))) & 0xff) == 1;
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(row + t0 + 16 * q);
+      w[4 * q] = v.x;
+      w[4 * q + 1] = v.y;
+      w[4 * q + 2] = v.z;
+      w[4 * q + 3] = v.w;
     }
   }
-}
+  __device__ __forceinline__ int up(int b) const { return ((w[b >> 2] >> (8 * (b & 3))) & 0xff) == 1; }
+};
 
 template <int NL>
 __global__ void __launch_bounds__(256) lev_prefix_kernel(LevArgs a) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.investors) return;
   const uint8_t* row = a.outcomes + (int64_t)i * a.ld;
-  float val[NL > 0 ? NL : 1];
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  f32x2 val[NL > 0 ? NL / 2 : 1], gu[NL > 0 ? NL / 2 : 1], gd[NL > 0 ? NL / 2 : 1];
+#pragma unroll
+  for (int l = 0; l < (NL > 0 ? NL / 2 : 1); ++l) {
+    val[l] = f32x2{a.value_0, a.value_0};
+    gu[l] = f32x2{a.gu[2 * l], a.gu[2 * l + 1]};
+    gd[l] = f32x2{a.gd[2 * l], a.gd[2 * l + 1]};
+  }
   int k = 0;
   const int chunks = (a.horizon + kChunk - 1) / kChunk;
+  Chunk64 nx;
+  nx.load(row, 0);
   for (int c = 0; c < chunks; ++c) {
     a.pre[(int64_t)c * a.investors + i] = (uint16_t)k;
-    uint8_t o[kChunk];
-    load64(row, c * kChunk, a.horizon, o);
+    const Chunk64 ch = nx;
+    if (c + 1 < chunks) nx.load(row, (c + 1) * kChunk);  // next chunk in flight while this one is walked
     const int tn = min(kChunk, a.horizon - c * kChunk);
-    for (int tt = 0; tt < tn; ++tt) {
-      k += o[tt];
-      if constexpr (NL > 0) {
 #pragma unroll
-        for (int l = 0; l < NL; ++l) {
-          const float g = o[tt] ? a.gu[l] : a.gd[l];
-          // initial = value_0 * g[:, 0]; value_t = initial * g[:, t + 1] (lev_exp.py:170-176)
-          val[l] = (c == 0 && tt == 0) ? a.value_0 * g : val[l] * g;
+    for (int tt = 0; tt < kChunk; ++tt) {
+      if (tt < tn) {
+        const int o = ch.up(tt);
+        k += o;
+        if constexpr (NL > 0) {
+          // initial = value_0 * g[:, 0]; value_t = initial * g[:, t + 1]
+          // (lev_exp.py:170-176): one f32 product per step, two leverages per
+          // packed multiply (v_pk_mul_f32)
+#pragma unroll
+          for (int l = 0; l < NL / 2; ++l) val[l] *= o ? gu[l] : gd[l];
         }
       }
     }
@@ -89,20 +106,20 @@ __global__ void __launch_bounds__(256) lev_prefix_kernel(LevArgs a) {
   if constexpr (NL > 0) {
 #pragma unroll
     for (int l = 0; l < NL; ++l)
-      if (l < a.n_lev) a.data_T[(int64_t)l * a.investors + i] = val[l];
+      if (l < a.n_lev) a.data_T[(int64_t)l * a.investors + i] = val[l >> 1][l & 1];
   }
 }
 
-__global__ void __launch_bounds__(256) lev_hist_kernel(LevArgs a) {
+__global__ void __launch_bounds__(kHistThreads) lev_hist_kernel(LevArgs a) {
   __shared__ uint32_t h[kHistLds];
   __shared__ int s_lo, s_hi;
   const int c = blockIdx.y, t0 = c * kChunk, tn = min(kChunk, a.horizon - t0);
-  const int base = blockIdx.x * 256 * kInvPerThread;
+  const int base = blockIdx.x * kHistThreads * kInvPerThread;
   const int H1 = a.horizon + 1;
   int st[kInvPerThread], lo = 1 << 30, hi = -1;
 #pragma unroll
   for (int j = 0; j < kInvPerThread; ++j) {
-    const int i = base + j * 256 + threadIdx.x;
+    const int i = base + j * kHistThreads + threadIdx.x;
     st[j] = i < a.investors ? a.pre[(int64_t)c * a.investors + i] : -1;
     if (st[j] >= 0) {
       lo = min(lo, st[j]);
@@ -121,25 +138,28 @@ __global__ void __launch_bounds__(256) lev_hist_kernel(LevArgs a) {
   if (s_hi < 0) return;  // uniform: no investors in this block
   const bool in_lds = (int64_t)W * tn <= kHistLds;
   if (in_lds) {
-    for (int e = threadIdx.x; e < W * tn; e += 256) h[e] = 0;
+    for (int e = threadIdx.x; e < W * tn; e += kHistThreads) h[e] = 0;
     __syncthreads();
   }
 #pragma unroll 1
   for (int j = 0; j < kInvPerThread; ++j) {
     if (st[j] < 0) continue;
-    const int i = base + j * 256 + threadIdx.x;
-    uint8_t o[kChunk];
-    load64(a.outcomes + (int64_t)i * a.ld, t0, a.horizon, o);
+    const int i = base + j * kHistThreads + threadIdx.x;
+    Chunk64 ch;
+    ch.load(a.outcomes + (int64_t)i * a.ld, t0);
     int k = st[j];
-    for (int tt = 0; tt < tn; ++tt) {
-      k += o[tt];
-      if (in_lds) atomicAdd(&h[tt * W + (k - klo)], 1u);
-      else atomicAdd(&a.hist[(int64_t)(t0 + tt) * H1 + k], 1u);
+#pragma unroll
+    for (int tt = 0; tt < kChunk; ++tt) {
+      if (tt < tn) {
+        k += ch.up(tt);
+        if (in_lds) atomicAdd(&h[tt * W + (k - klo)], 1u);
+        else atomicAdd(&a.hist[(int64_t)(t0 + tt) * H1 + k], 1u);
+      }
     }
   }
   if (!in_lds) return;
   __syncthreads();
-  for (int e = threadIdx.x; e < W * tn; e += 256) {
+  for (int e = threadIdx.x; e < W * tn; e += kHistThreads) {
     const uint32_t v = h[e];
     if (v) {
       const int tt = e / W, k = klo + e - tt * W;
@@ -326,8 +346,8 @@ int rlmd_lev_coin_sweep(const uint8_t* outcomes_dev, int64_t investors, int32_t 
   else RLMD_LEV_PRE(32);
 #undef RLMD_LEV_PRE
   RLMD_LAUNCH_CHECK();
-  const unsigned ib = (unsigned)((investors + 256 * kInvPerThread - 1) / (256 * kInvPerThread));
-  hipLaunchKernelGGL(lev_hist_kernel, dim3(ib, (unsigned)chunks_of(horizon)), dim3(256), 0, s, a);
+  const unsigned ib = (unsigned)((investors + kHistThreads * kInvPerThread - 1) / (kHistThreads * kInvPerThread));
+  hipLaunchKernelGGL(lev_hist_kernel, dim3(ib, (unsigned)chunks_of(horizon)), dim3(kHistThreads), 0, s, a);
   RLMD_LAUNCH_CHECK();
   hipLaunchKernelGGL(lev_stats_kernel, dim3((unsigned)(horizon - 1), (unsigned)n_lev), dim3(256),
                      (size_t)stats_lds, s, a);
