@@ -98,10 +98,12 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
+def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H=256, B=512, topk=256):
     """The same loop on the host: CPU oracle (oracle/envs.py + oracle/learn.py,
     the restatement pinned to the reference) — NumPy env over all lanes,
-    torch-CPU policy forward, K torch-CPU SAC updates per vector step."""
+    torch-CPU policy forward, a replay ring of `replay` transitions (the C2
+    1,048,576) filled lane-major each vector step, and K torch-CPU SAC updates
+    per vector step on B distinct uniform ring rows (replay.py:356-364)."""
     import numpy as np
     import torch
 
@@ -109,7 +111,6 @@ def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
     from oracle import learn as ol
     from rlmd_amd.agent import reference_init
 
-    threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     env = oe.OracleVecEnv(oe.GBM, oe.INV_A, lanes, 1, seed=420)
     init = reference_init("SAC", S, A, H, H, seed=420)
@@ -120,7 +121,10 @@ def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
     learner = ol.OracleLearner("SAC", S, A, H, H, B, topk, "MSE", p, t)
     rng = np.random.default_rng(0)
     obs = env.reset()
-    ring_s, ring_a, ring_r, ring_s2, ring_d = [], [], [], [], []
+    cap = max(replay, lanes)
+    ring_s, ring_s2 = np.zeros((cap, S), np.float32), np.zeros((cap, S), np.float32)
+    ring_a, ring_r, ring_d = np.zeros((cap, A), np.float32), np.zeros(cap, np.float32), np.zeros(cap, bool)
+    mem = 0
     steps, t0 = 0, time.perf_counter()
     while True:
         with torch.no_grad():
@@ -128,19 +132,17 @@ def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
             eps = torch.from_numpy(rng.standard_normal((lanes, A)).astype(np.float32))
             act = learner.policy(Pn["actor"], torch.from_numpy(obs.astype(np.float32)), eps)[0].numpy()
         ns, r, d, _ = env.step(act)
-        ring_s.append(obs.astype(np.float32))
-        ring_a.append(act)
-        ring_r.append(r.astype(np.float32))
-        ring_s2.append(ns.astype(np.float32))
-        ring_d.append(d[:, 1])
+        rows = (mem + np.arange(lanes)) % cap
+        ring_s[rows], ring_a[rows], ring_r[rows] = obs, act, r
+        ring_s2[rows], ring_d[rows] = ns, d[:, 1]
+        mem += lanes
         obs = ns.copy()
         if d[:, 0].any():
             obs[d[:, 0]] = env.reset(d[:, 0])[d[:, 0]]
-        S_, A_ = np.concatenate(ring_s[-16:]), np.concatenate(ring_a[-16:])
-        R_, S2_, D_ = np.concatenate(ring_r[-16:]), np.concatenate(ring_s2[-16:]), np.concatenate(ring_d[-16:])
+        filled = min(mem, cap)
         for _ in range(k_updates):
-            idx = rng.choice(S_.shape[0], B, replace=False)
-            learner.learn(S_[idx], A_[idx], R_[idx], S2_[idx], D_[idx],
+            idx = rng.choice(filled, B, replace=False)
+            learner.learn(ring_s[idx], ring_a[idx], ring_r[idx], ring_s2[idx], ring_d[idx],
                           rng.standard_normal((B, A)).astype(np.float32), rng.standard_normal((B, A)).astype(np.float32))
         steps += 1
         el = time.perf_counter() - t0
@@ -148,7 +150,8 @@ def cpu_baseline(lanes, k_updates, seconds, S=5, A=1, H=256, B=512, topk=256):
             break
     return {"value": lanes * steps / el, "unit": "env steps/sec", "cores": threads, "kind": "port",
             "sample": f"{steps} vector steps x {lanes} GBM lanes, SAC 256/256 fp32, K={k_updates} updates "
-                      f"of B={B} per vector step (oracle/envs.py + oracle/learn.py on torch-CPU), {el:.1f} s"}
+                      f"of B={B} per vector step from a {cap}-row ring (oracle/envs.py + oracle/learn.py on "
+                      f"torch-CPU, {threads} thread(s)), {el:.1f} s"}
 
 
 def load_traffic():
@@ -164,17 +167,18 @@ def load_traffic():
         return None
 
 
-def reduce_ranks(elapsed, ep_stats, steps, world, device):
+def reduce_ranks(elapsed, ep_stats, steps, world, device, extra=()):
     """Logging-time exchange across ranks (the only collective of the run): the
     max-over-ranks wall time, and one all_gather of every rank's log slab
-    [episodes, sum final reward, sum length, steps seen, env steps timed].
+    [episodes, sum final reward, sum length, steps seen, env steps timed,
+    *extra] (extra: e.g. the rank's multi-step n).
     RCCL ("nccl") on the GPU box; tests/test_multirank_cpu.py runs it on gloo."""
     import torch
     import torch.distributed as dist
 
     el_t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     slab = torch.cat([ep_stats.to(device=device, dtype=torch.float64),
-                      torch.tensor([steps], dtype=torch.float64, device=device)])
+                      torch.tensor([steps, *extra], dtype=torch.float64, device=device)])
     if world > 1:
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
         gathered = [torch.empty_like(slab) for _ in range(world)]
@@ -183,6 +187,49 @@ def reduce_ranks(elapsed, ep_stats, steps, world, device):
     else:
         slab_all = slab[None]
     return float(el_t.item()), slab_all
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` started without a launcher: start N rank processes
+    (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* in their env) as
+    children of this process, which has not touched the GPU, and exit with the
+    worst return code.  Rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=abs)
+
+
+def parse_multi_steps(spec, rank, default):
+    """--multi-steps "5" or a per-rank list "3,5,7" (C5: one n per GPU, rank r
+    takes entry r mod len)."""
+    if spec is None:
+        return default
+    vals = [int(v) for v in str(spec).split(",") if v.strip()]
+    return vals[rank % len(vals)]
+
+
+def timed_steps(tr, steps, k=None):
+    """Mean wall ms per vector step over `steps` steps at K = k (rank-local)."""
+    import torch
+
+    for _ in range(3):
+        tr.step(k)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step(k)
+    torch.cuda.synchronize()
+    return 1e3 * (time.perf_counter() - t0) / steps
 
 
 def main():
@@ -196,17 +243,25 @@ def main():
     ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--replay", type=int, default=None)
     ap.add_argument("--loss", default="MSE", help="critic loss (C3 sweeps MSE/HUB/MAE/HSC)")
-    ap.add_argument("--multi-steps", type=int, default=None)
+    ap.add_argument("--multi-steps", default=None, help="n-step returns; a comma list gives one n per rank (C5)")
+    ap.add_argument("--k-sweep", default="1,8,32,64",
+                    help="K values timed after the headline region (env steps/s and updates/s each); '' = off")
+    ap.add_argument("--no-companion", action="store_true", help="skip the fp32 companion measurement")
     ap.add_argument("--eval-every", type=int, default=1000,
                     help="vector steps between evaluations (eval_freq 1e3, main.py); amortised into value")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -222,7 +277,7 @@ def main():
     cfg = CONFIGS[args.config]
     N, K = args.lanes or cfg["lanes"], args.k_updates
     replay = args.replay or cfg["replay"]
-    ms_n = args.multi_steps or cfg["multi_steps"]
+    ms_n = parse_multi_steps(args.multi_steps, rank, cfg["multi_steps"])
     kw = {}
     if cfg["env"] == "market":
         kw = dict(prices=synthetic_prices(), obs_days=1, time_length=1000, shuffle_days=5,
@@ -265,9 +320,33 @@ def main():
     eval_s = time.perf_counter() - te
     if args.eval_every > 0:
         elapsed += eval_s * args.steps / args.eval_every
-    t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(N * args.steps), world, dev)
+    t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(N * args.steps), world, dev,
+                                   extra=(float(ms_n),))
     total_steps = float(slab_all[:, 4].sum().item())
     value = total_steps / t_max
+    ms_per_rank = [int(v) for v in slab_all[:, 5].tolist()]
+
+    # after the headline region (rank-local, no collective): K sweep at the same
+    # lanes, and the fp32 companion (the reference's arithmetic) at the headline K
+    sweep = {}
+    for kk in [int(v) for v in args.k_sweep.split(",") if v.strip()]:
+        ms_k = timed_steps(tr, max(5, min(args.steps, 20)), kk)
+        sweep[str(kk)] = {"ms_per_step": ms_k, "env_steps_per_s": N * 1e3 / ms_k,
+                          "updates_per_s": kk * 1e3 / ms_k, "utd_updates_per_env_step": kk / N}
+    tr.step(K)
+    companion = None
+    if not args.no_companion and world == 1 and args.precision == "bf16":
+        tr32 = VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"],
+                          algo=cfg["algo"], loss=args.loss, k_updates=K, replay_capacity=replay, seed=421,
+                          warmup_steps=0, smoothing_window=0, precision="fp32", device=dev, init_seed=421,
+                          multi_steps=ms_n, dynamics="A", **kw)
+        for _ in range(args.warmup):
+            tr32.step()
+        ms32 = timed_steps(tr32, args.steps)
+        companion = {"dtype": "fp32", "value": N * 1e3 / ms32, "unit": "env steps/sec", "ms_per_step": ms32,
+                     "k_updates_per_vector_step": K, "note": "same workload, fp32 GEMM operands (exact-f32 MFMA); "
+                                                            "eval not amortised"}
+        del tr32
 
     S, A = tr.env.state_dim, tr.env.action_dim
     env_ms = ms[1] / max(cnt[1], 1)
@@ -291,12 +370,15 @@ def main():
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
             "config": {"workload": cfg["workload"], "config": args.config, "critic_loss": args.loss,
-                       "replay_per_gpu": replay, "multi_steps": ms_n,
+                       "replay_per_gpu": replay, "multi_steps": ms_n, "multi_steps_per_rank": ms_per_rank,
                        "eval_ms_per_event": 1e3 * eval_s, "eval_every_vector_steps": args.eval_every,
                        "lanes_per_gpu": N, "global_lanes": N * world, "k_updates_per_vector_step": K,
                        "mini_batch": tr.batch, "topk": tr.topk, "utd_updates_per_env_step": K / N,
                        "parallelism": f"independent seeds x{world} (no data-path collective)",
                        "phase_ms_per_step": {"act": act_ms, "env_kernel": env_ms, "learn_k": learn_ms}},
+            "updates_per_s": K * args.steps * world / t_max,
+            "k_sweep": sweep,
+            "fp32_companion": companion,
             "roofline": {"kernel": "env_train_kernel (fused env step + replay insert + reset)",
                          "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -309,7 +391,10 @@ def main():
                               "algorithmic_flops_per_step": flops, "avg_phase_ms": learn_ms},
         }
         if not args.no_cpu_baseline and world == 1 and args.config == "c2":
-            out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_seconds)
+            # all host cores of this GPU's share (16 on the box), and one core
+            allc = min(16, os.cpu_count() or 1)
+            out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_seconds, allc, replay=replay)
+            out["cpu_baseline_1core"] = cpu_baseline(N, K, args.cpu_seconds, 1, replay=replay)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

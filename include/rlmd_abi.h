@@ -127,10 +127,17 @@ int64_t rlmd_lev_workspace_bytes(int64_t investors, int32_t horizon);
  * [n_lev][13][horizon - 1] (mean, mean_top, mean_adj, mad x3, std x3,
  * median x3, lev after each step t + 2) and, when non-null, data_T_dev f32
  * [n_lev][investors] (final values, the reference's sequential f32 products).
- * n_lev <= 32, horizon <= 5459. */
+ * n_lev <= 32, horizon <= 5459.  workspace_bytes must be at least
+ * rlmd_lev_workspace_bytes(investors, horizon) (checked).
+ * Supported leverage domain: 1 + lev * up_r >= 0 and 1 + lev * down_r >= 0 for
+ * every (sign-adjusted) leverage, i.e. both gamble factors non-negative, so a
+ * value is monotone in the up-count (e.g. lev <= 2.5 at down_r = -0.4).  The
+ * reference also runs leverages past that bound by sorting signed values; here
+ * they are rejected (RLMD error), not approximated. */
 int rlmd_lev_coin_sweep(const uint8_t* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld, int64_t top,
                         float value_0, float up_r, float down_r, const float* levs_host, int32_t n_lev,
-                        void* workspace_dev, float* data_dev, float* data_T_dev, void* stream);
+                        void* workspace_dev, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
+                        void* stream);
 
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
@@ -254,6 +261,18 @@ int rlmd_agent_learn_batch(rlmd_agent_t ag, const float* s_dev, const float* a_d
                            const float* r_dev, const float* s2_dev, const uint8_t* done_dev,
                            const int32_t* eff_dev, const float* eps_a_dev, const float* eps_b_dev,
                            float* stats_dev, void* stream);
+
+/* Learner status word (sticky bits; the reference's NaN guards of
+ * tests/test_live_learning.py become flags, never a process exit):
+ *   RLMD_STATUS_NAN_BATCH  NaN in a mini-batch's q1 / q2 / critic target
+ *                          (sac_critic_stability / td3_critic_stability :29-116)
+ *   RLMD_STATUS_NAN_STATS  NaN in the critic statistics loss[0:6] + loss[8:10]
+ *                          (critic_learning :119-255, the condition that exit()s)
+ * Replaces the guard calls at scripts/rl_multiplicative.py:229-244.  Reads two
+ * words on `stream` and synchronises it; nan_update_host (nullable) gets the
+ * learn counter at which a flag was first set, -1 when none is. */
+enum { RLMD_STATUS_NAN_BATCH = 1, RLMD_STATUS_NAN_STATS = 2 };
+int rlmd_status_poll(rlmd_agent_t ag, int32_t* flags_host, int32_t* nan_update_host, void* stream);
 
 /* Device scalars: [cauchy_1, cauchy_2, log_alpha, learn_step_cntr, nan_flag]. */
 int rlmd_agent_scalars(rlmd_agent_t ag, double* out_host5);

@@ -15,6 +15,7 @@ LIB_PATH = os.path.join(HERE, "librlmd_amd.so")
 COIN, DICE, GBM, DICE_SH, MARKET = range(5)
 INV_A, INV_B, INV_C, INV_INSURED = range(4)
 SAC, TD3 = 0, 1
+STATUS_NAN_BATCH, STATUS_NAN_STATS = 1, 2
 FP32, BF16 = 0, 1
 DIST_N, DIST_L, DIST_MVN = 0, 1, 2
 LOSSES = ["MSE", "HUB", "MAE", "HSC", "CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"]
@@ -86,6 +87,7 @@ SIGNATURES = {
     "rlmd_agent_learn": (C.c_int, [P, P, I32, P, P]),
     "rlmd_agent_learn_batch": (C.c_int, [P, P, P, P, P, P, P, P, P, P, P]),
     "rlmd_agent_scalars": (C.c_int, [P, P]),
+    "rlmd_status_poll": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), P]),
     "rlmd_train_step": (C.c_int, [P, P, P, C.POINTER(TrainCfg), P, P, P, P, P]),
     "rlmd_train_reset": (C.c_int, [P, P, P]),
     "rlmd_train_flush_stats": (C.c_int, [P, P]),
@@ -93,7 +95,8 @@ SIGNATURES = {
     "rlmd_shadow_means": (C.c_int, [P, I32, I32, C.c_float, C.c_float, P, I32, P]),
     "rlmd_shadow_equiv": (C.c_int, [P, P, P, P, C.c_double, I64, P, P]),
     "rlmd_lev_workspace_bytes": (I64, [I64, I32]),
-    "rlmd_lev_coin_sweep": (C.c_int, [P, I64, I32, I64, I64, C.c_float, C.c_float, C.c_float, P, I32, P, P, P, P]),
+    "rlmd_lev_coin_sweep": (C.c_int, [P, I64, I32, I64, I64, C.c_float, C.c_float, C.c_float, P, I32, P, I64, P, P,
+                                       P]),
     "rlmd_eval_market": (C.c_int, [P, P, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, P, P]),
     "rlmd_profile_enable": (C.c_int, [I32]),
     "rlmd_profile_read": (C.c_int, [P, P]),

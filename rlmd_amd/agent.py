@@ -173,6 +173,14 @@ class DeviceAgent:
         check(_abi.lib().rlmd_agent_learn_batch(self.h, *[ptr(x) for x in args], ptr(self.stats), stream_ptr()))
         return self.stats[0]
 
+    def status(self, stream=None):
+        """(flags, nan_update) from rlmd_status_poll: bit 0 NaN in a mini-batch's
+        q / target, bit 1 NaN in the critic statistics (the reference's
+        test_live_learning guards); nan_update = learn counter at first set."""
+        f, u = C.c_int32(), C.c_int32()
+        check(_abi.lib().rlmd_status_poll(self.h, C.byref(f), C.byref(u), stream_ptr(stream)))
+        return f.value, u.value
+
     def scalars(self):
         out = (C.c_double * 5)()
         check(_abi.lib().rlmd_agent_scalars(self.h, out))

@@ -12,6 +12,7 @@
 // All per-update scalars (Cauchy scales, log alpha, learn counter) stay on the
 // device in LearnState; nothing synchronises with the host inside learn().
 #include <math.h>
+#include <stddef.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1041,6 +1042,20 @@ int rlmd_agent_scalars(rlmd_agent_t ag, double* out) {
   out[2] = st.log_alpha;
   out[3] = st.learn_cntr;
   out[4] = st.nan_flag;
+  return 0;
+}
+
+int rlmd_status_poll(rlmd_agent_t ag, int32_t* flags_host, int32_t* nan_update_host, void* stream) {
+  RLMD_CHECK(ag && flags_host, "null argument");
+  hipStream_t s = (hipStream_t)stream;
+  int32_t v[2];
+  static_assert(offsetof(rlmd::LearnState, nan_update) == offsetof(rlmd::LearnState, nan_flag) + 8,
+                "LearnState layout");
+  RLMD_HIP(hipMemcpyAsync(&v[0], &ag->st->nan_flag, 4, hipMemcpyDeviceToHost, s));
+  RLMD_HIP(hipMemcpyAsync(&v[1], &ag->st->nan_update, 4, hipMemcpyDeviceToHost, s));
+  RLMD_HIP(hipStreamSynchronize(s));
+  *flags_host = v[0];
+  if (nan_update_host) *nan_update_host = v[0] ? v[1] : -1;
   return 0;
 }
 

@@ -20,6 +20,7 @@ struct LearnState {
   int32_t learn_cntr;  // learn_step_cntr (algo_sac.py:475)
   int32_t nan_flag;    // tests/test_live_learning.py guards -> flag, no exit()
   float pad_temp_grad;  // temperature gradient handed from actor_loss to adam
+  int32_t nan_update;   // learn_cntr when nan_flag was first set
 };
 
 // Per-net parameter offsets (floats) inside a flat buffer, torch nn.Linear

@@ -180,6 +180,19 @@ __device__ double block_sum(double v, double* red) {
   return s;
 }
 
+// f32 value of a bin: v0 * gu^k * gd^m, rounded once.  Formed in log space so
+// the two powers cannot overflow / underflow independently (inf * 0 = NaN for a
+// populated bin whose true value is finite); a zero factor with a positive
+// exponent gives 0, as the reference's sequential products do; a value past
+// the f32 range rounds to inf, as they do too.
+__device__ __forceinline__ float bin_value(float v0, float gu, float gd, int k, int m) {
+  if (v0 == 0.f || (k > 0 && gu == 0.f) || (m > 0 && gd == 0.f)) return 0.f;
+  double lg = log((double)v0);
+  if (k > 0) lg += (double)k * log((double)gu);
+  if (m > 0) lg += (double)m * log((double)gd);
+  return (float)exp(lg);
+}
+
 // one workgroup per (step t, leverage): the table column data[lev][:, t]
 __global__ void __launch_bounds__(256) lev_stats_kernel(LevArgs a) {
   extern __shared__ unsigned char smem[];
@@ -197,8 +210,7 @@ __global__ void __launch_bounds__(256) lev_stats_kernel(LevArgs a) {
   for (int r = threadIdx.x; r < nb; r += 256) {
     const int k = up_first ? n - r : r;
     cnt[r] = hrow[k];
-    // f32 value of the bin: v0 * gu^k * gd^(n-k), rounded once
-    val[r] = (float)((double)a.value_0 * pow((double)gu, (double)k) * pow((double)gd, (double)(n - k)));
+    val[r] = bin_value(a.value_0, gu, gd, k, n - k);
   }
   __syncthreads();
   const int per = (nb + 255) / 256, r0 = threadIdx.x * per, r1 = min(nb, r0 + per);
@@ -304,9 +316,12 @@ int64_t rlmd_lev_workspace_bytes(int64_t investors, int32_t horizon) {
 
 int rlmd_lev_coin_sweep(const uint8_t* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld, int64_t top,
                         float value_0, float up_r, float down_r, const float* levs_host, int32_t n_lev,
-                        void* workspace_dev, float* data_dev, float* data_T_dev, void* stream) {
+                        void* workspace_dev, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
+                        void* stream) {
   RLMD_CHECK(outcomes_dev && levs_host && workspace_dev && data_dev, "null argument");
   RLMD_CHECK(investors >= 1 && investors < (1ll << 31) && horizon >= 2 && horizon <= 65535, "bad shape");
+  RLMD_CHECK(workspace_bytes >= rlmd_lev_workspace_bytes(investors, horizon),
+             "workspace smaller than rlmd_lev_workspace_bytes(investors, horizon)");
   RLMD_CHECK(ld >= horizon && ld % 16 == 0 && ((uintptr_t)outcomes_dev & 15) == 0,
              "outcome rows: 16-byte aligned, leading dimension a multiple of 16 and >= horizon");
   RLMD_CHECK(ld >= chunks_of(horizon) * kChunk, "outcome rows padded to a multiple of 64 steps");
@@ -328,7 +343,9 @@ int rlmd_lev_coin_sweep(const uint8_t* outcomes_dev, int64_t investors, int32_t 
     a.lev[l] = lev;
     a.gu[l] = 1.0f + lev * up_r;
     a.gd[l] = 1.0f + lev * down_r;
-    RLMD_CHECK(a.gu[l] >= 0.f && a.gd[l] >= 0.f, "a leverage makes a gamble factor negative (values not monotone)");
+    RLMD_CHECK(a.gu[l] >= 0.f && a.gd[l] >= 0.f,
+               "leverage outside the supported domain: 1 + lev*up_r and 1 + lev*down_r must be >= 0 "
+               "(a negative factor flips the value order; see rlmd_abi.h)");
   }
   const int64_t pre_bytes = (chunks_of(horizon) * investors * 2 + 255) / 256 * 256;
   a.pre = static_cast<uint16_t*>(workspace_dev);

@@ -222,7 +222,19 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
     st->cauchy[1] = newc[1];
     st->kernel[0] = o.kern[0];
     st->kernel[1] = o.kern[1];
-    if (o.nan > 0.f) st->nan_flag = 1;
+    // NaN guards (tests/test_live_learning.py): bit 0 = NaN in the mini-batch's
+    // q1 / q2 / target (sac_ / td3_critic_stability :29-116), bit 1 = NaN in the
+    // critic statistics loss[0:6] + loss[8:10] (critic_learning :119-255, whose
+    // exit() becomes this sticky flag); nan_update = learn counter at first set
+    int32_t fl = st->nan_flag;
+    if (o.nan > 0.f) fl |= RLMD_STATUS_NAN_BATCH;
+    bool sn = false;
+#pragma unroll
+    for (int v = 0; v < 10; ++v)
+      if (v < 6 || v >= 8) sn |= isnan(a.stats[v]);
+    if (sn) fl |= RLMD_STATUS_NAN_STATS;
+    if (fl && !st->nan_flag) st->nan_update = st->learn_cntr;
+    st->nan_flag = fl;
     if (!a.keep_actor_slot) a.stats[10] = NAN;
     a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
     a.stats[12] = newc[0];

@@ -51,6 +51,6 @@ def coin_smart_lev(device, outcomes, investors, horizon, top, value_0, up_r, dow
     data_T = torch.empty((n_lev, inv), dtype=torch.float32, device=dev) if final_values else None
     P = _abi.ptr
     _abi.check(lib.rlmd_lev_coin_sweep(P(buf), inv, hor, buf.stride(0), int(top), float(value_0), float(up_r),
-                                       float(down_r), levs.ctypes.data, n_lev, P(ws), P(data),
+                                       float(down_r), levs.ctypes.data, n_lev, P(ws), ws.numel(), P(data),
                                        P(data_T) if data_T is not None else None, _abi.stream_ptr()))
     return data, data_T

@@ -86,7 +86,7 @@ class VecTrainer:
                                                row.data_ptr() + 6 * row.element_size(), 16, stream_ptr()))
         return self.stats[k].double().cpu().numpy()
 
-    def evaluate(self, n_eval=100, max_steps=100):
+    def evaluate(self, n_eval=100, max_steps=100, with_stats=True):
         """eval_multiplicative (tools/eval_episodes.py:176-399) on the device: n_eval
         episodes of a separate env (its own seed), each from the reset state with
         the deterministic policy action held constant, the action window applied
@@ -109,10 +109,11 @@ class VecTrainer:
         check(lib.rlmd_eval_rollout(env.h, ptr(actions), int(max_steps), int(self.cfg.cum_step),
                                     int(self.cfg.warmup_steps), int(self.cfg.smoothing_window), None, ptr(reward),
                                     ptr(steps), ptr(risk), stream_ptr()))
-        check(lib.rlmd_eval_stats(ptr(reward), ptr(steps), ptr(risk), n_eval, env.risk_dim, env.investor,
-                                  ptr(stats), stream_ptr()))
+        if with_stats:  # the NumPy-exact summary (rlmd_eval_stats) covers 1..1024 episodes
+            check(lib.rlmd_eval_stats(ptr(reward), ptr(steps), ptr(risk), n_eval, env.risk_dim, env.investor,
+                                      ptr(stats), stream_ptr()))
         return {"reward": reward.cpu().numpy(), "steps": steps.cpu().numpy(), "risk": risk.cpu().numpy(),
-                "stats": stats.cpu().numpy()}
+                "stats": stats.cpu().numpy() if with_stats else None}
 
     def evaluate_market(self, n_eval=100, test_days=250, gap_days=(5, 20), test_shuffle_days=3, rng=None):
         """eval_market (tools/eval_episodes.py:402-611) for a market trainer: the

@@ -1,0 +1,73 @@
+"""Run the reference's own multiplicative training loop (config C1 shape) on CPU
+and keep its evaluation curve as a fixture: the calibration of what the
+reference *converges to* on Coin / Dice / Dice_SH_INSURED, against which
+tests/test_converge_gpu.py holds the vectorised MI355X loop.
+
+Build container only (imports /root/reference through the §8c shims of
+_refshim.py; the reference never travels).  Calls
+scripts/rl_multiplicative.multiplicative_env (rl_multiplicative.py:41-457)
+with main.py's gym_envs table and inputs dict (main.py:41-259) widened by
+utils.input_initialisation (tools/utils.py:80-106), one trial, SAC, MSE,
+seeded np.random + torch.  From the saved logs it keeps, per evaluation
+(every eval_freq = 1e3 steps, 100 episodes of <= 100 steps at one constant
+deterministic action): the mean leverage (eval_risk_log[..., 3],
+eval_episodes.py:296-297) and the final rewards (eval_log[..., 1]).
+
+    python tests/golden/run_reference_loop.py --key 8 --steps 50000 --seed 0
+writes tests/golden/converge_ref_<key>_s<seed>.npz
+"""
+import argparse
+import glob
+import os
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import _refshim  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--key", type=int, default=8, help="main.py gym_envs key (8 Coin_InvA, 11 Dice_InvA, "
+                                                     "17 Dice_SH_INSURED)")
+    ap.add_argument("--steps", type=int, default=50000)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--threads", type=int, default=1)
+    a = ap.parse_args()
+    _refshim.install()
+    import torch
+
+    torch.set_num_threads(a.threads)
+    import main as ref_main  # noqa: E402  (module level only defines the tables)
+    from tools import utils
+
+    inputs = dict(ref_main.inputs)
+    inputs.update({"n_trials_mul": 1, "n_cumsteps_mul": float(a.steps), "gpu": "cpu", "buffer_gpu": False})
+    inputs = utils.input_initialisation(inputs, [a.key], ["SAC"], ["MSE"], [1])
+    inputs["test_agent"] = True
+    inputs["ENV_KEY"] = a.key
+    out = os.path.join(HERE, f"converge_ref_{a.key}_s{a.seed}.npz")
+    np.random.seed(a.seed)
+    torch.manual_seed(a.seed)
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)
+        try:
+            from scripts.rl_multiplicative import multiplicative_env
+
+            multiplicative_env(ref_main.gym_envs, inputs, n_gambles=1)
+            ev = np.load(glob.glob("results/**/*_eval.npy", recursive=True)[0])
+            er = np.load(glob.glob("results/**/*_eval_risk.npy", recursive=True)[0])
+        finally:
+            os.chdir(cwd)
+    np.savez_compressed(out, key=a.key, seed=a.seed, steps=a.steps, env=ref_main.gym_envs[str(a.key)][0],
+                        cum_steps=ev[0, :, 0, 19], reward=ev[0, :, :, 1], eval_steps=ev[0, :, :, 2],
+                        lev=er[0, :, :, 3])
+    print("wrote", out, "final mean lev", er[0, -5:, :, 3].mean(), "final mean reward", ev[0, -5:, :, 1].mean())
+
+
+if __name__ == "__main__":
+    main()

@@ -165,3 +165,41 @@ def test_bf16_tracks_oracle(dev, algo, S, A, h1, h2, B, k):
         np.testing.assert_allclose(st[:6], lo[:6], rtol=3e-2, err_msg=f"step {step}")
         diff = np.abs(ag.params.cpu().numpy() - ora.P.numpy())
         assert np.mean(diff <= lr * 1.01 * (step + 1)) >= 0.99, np.quantile(diff, [0.5, 0.99, 1.0])
+
+
+@pytest.mark.parametrize("algo", ["SAC", "TD3"])
+def test_nan_guard_sets_status(dev, algo):
+    """The reference's NaN guards (tests/test_live_learning.py:29-255) as the
+    sticky status word of rlmd_status_poll: a NaN reward in one mini-batch
+    makes the critic target NaN (bit 0, *_critic_stability) and the critic
+    statistics NaN (bit 1, critic_learning's exit() condition).  Finite batches
+    before it leave the word 0; later batches do not clear it."""
+    from rlmd_amd import _abi
+    from rlmd_amd.agent import reference_init
+
+    S, A, h1, h2, B, k = 5, 1, 64, 48, 64, 32
+    ag = device_agent(algo, S, A, h1, h2, B, k, "MSE", reference_init(algo, S, A, h1, h2, seed=3))
+    rng = np.random.default_rng(0)
+
+    def batch(nan_row=None):
+        s = torch.from_numpy(rng.normal(size=(B, S)).astype(np.float32))
+        a = torch.from_numpy(rng.uniform(-0.9, 0.9, (B, A)).astype(np.float32))
+        r = torch.from_numpy(rng.normal(1.0, 0.1, B).astype(np.float32))
+        if nan_row is not None:
+            r[nan_row] = float("nan")
+        s2 = torch.from_numpy(rng.normal(size=(B, S)).astype(np.float32))
+        d = torch.zeros(B, dtype=torch.uint8)
+        e = torch.from_numpy(rng.normal(size=(B, A)).astype(np.float32))
+        return s, a, r, s2, d, e, (e.clone() if algo == "SAC" else None)
+
+    for _ in range(3):
+        ag.learn_batch(*batch())
+    assert ag.status() == (0, -1)
+    st = ag.learn_batch(*batch(nan_row=7)).cpu().numpy()
+    assert np.isnan(st[0])
+    flags, upd = ag.status()
+    assert flags & _abi.STATUS_NAN_BATCH and flags & _abi.STATUS_NAN_STATS, flags
+    assert upd >= 0
+    ag.learn_batch(*batch())
+    assert ag.status()[0] == flags  # sticky
+    assert ag.scalars()["nan_flag"] == flags

@@ -52,6 +52,42 @@ def test_sweep_matches_oracle(inv, hor, top, up, dn, extremes):
     assert ok.all(), np.argwhere(~ok)[:5]
 
 
+@pytest.mark.parametrize("inv,hor,lo,hi", [(2000, 3500, 1.0, 1.0), (1500, 2400, 2.0, 2.0)])
+def test_sweep_long_horizon_matches_oracle(inv, hor, lo, hi):
+    """Horizons / leverages where gu^k and gd^(n-k) leave the double range on
+    their own (lev 1: n = 3300, k = 1751 gives inf * 0; lev 2: gu = 2, gd = 0.2
+    at n ~ 2050): the bin value is formed in log space, so populated bins stay
+    finite.  Tolerance 1e-4: the reference's 3500 sequential f32 roundings
+    drift up to ~n ulp from the once-rounded bin value."""
+    from rlmd_amd import lev
+
+    rng = np.random.default_rng(inv + hor)
+    o = (rng.random((inv, hor)) < 0.5).astype(np.uint8)
+    d, dT = lev.coin_smart_lev("cuda:0", o, inv, hor, 10, 100.0, 0.5, -0.4, lo, hi, 1.0)
+    od, odT = olev.coin_smart_lev(o, 10, 100.0, 0.5, -0.4, lo, hi, 1.0)
+    d, dT = d.cpu().numpy(), dT.cpu().numpy()
+    np.testing.assert_array_equal(dT, odT)
+    assert np.isfinite(od).all()
+    assert np.isfinite(d).all(), np.argwhere(~np.isfinite(d))[:6]
+    ok = close_table(d, od, 1e-4)
+    assert ok.all(), np.argwhere(~ok)[:5]
+
+
+def test_workspace_size_is_checked():
+    from rlmd_amd import _abi, lev
+
+    lib = _abi.lib()
+    o, hor = lev.pack_outcomes(np.ones((64, 100), dtype=np.uint8))
+    need = int(lib.rlmd_lev_workspace_bytes(64, hor))
+    ws = torch.empty(need, dtype=torch.uint8, device="cuda:0")
+    levs = np.array([0.5], dtype=np.float32)
+    data = torch.empty((1, 13, hor - 1), dtype=torch.float32, device="cuda:0")
+    P = _abi.ptr
+    rc = lib.rlmd_lev_coin_sweep(P(o), 64, hor, o.stride(0), 1, 1.0, 0.5, -0.4, levs.ctypes.data, 1, P(ws),
+                                 need - 1, P(data), None, _abi.stream_ptr())
+    assert rc != 0 and b"workspace" in lib.rlmd_last_error()
+
+
 def test_bad_arguments_fail_loudly():
     from rlmd_amd import _abi, lev
 

@@ -1,0 +1,134 @@
+"""Convergence of the vectorised loop to the analytic Kelly optima.
+
+north_star's second parity bar: the headline loop (VecTrainer, SAC, bf16,
+K updates per vector step) must learn the growth-optimal leverage of the
+multiplicative gambles.  The reference's own yardstick is the Kelly fraction
+(lev/lev_exp.py:495-496: kelly = pu/rd - (1-pu)/ru); the growth rate of a
+constant leverage l is g(l) = sum_i p_i log(1 + l r_i) for the envs'
+outcome tables (envs/coin_flip_envs.py:40-93, dice_roll_envs.py:39-96,
+dice_roll_sh_envs.py:39-118).
+
+The observation of these envs is divided by MAX_VALUE = 1e18, so the policy is
+effectively state-independent and its deterministic action IS the learned
+constant leverage (lev = action * LEV_FACTOR).  Every `--eval-every` vector
+steps this tool records
+  * the deterministic action at the reset state and its leverage,
+  * eval_multiplicative on the device (rlmd_eval_rollout, n_eval episodes of
+    100 steps at that constant action) -> mean time-average growth per step,
+  * the analytic growth g(lev) of that leverage,
+and writes one JSON line per record (progress for the GPU box).
+
+    python tools/converge.py --env coin --lanes 65536 --k 8 --steps 20000
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# outcome tables (p_i, r_i) and the action -> leverage map of each env
+GAMBLES = {
+    # coin_flip_envs.py:40-93: +50 % / -40 %, p = 1/2, LEV_FACTOR = 2
+    "coin": dict(p=[0.5, 0.5], r=[0.5, -0.4], lev_factor=2.0, investor="A"),
+    # dice_roll_envs.py:39-96: +50 % (1/6), -50 % (1/6), +5 % (2/3), LEV_FACTOR = 2
+    "dice": dict(p=[1 / 6, 1 / 6, 2 / 3], r=[0.5, -0.5, 0.05], lev_factor=2.0, investor="A"),
+}
+# dice_roll_sh_envs.py:39-118: die + safe haven; INSURED: lev = a * I_LF, lev_sh = 1 - lev;
+# R = lev * r + lev_sh * r_sh, with r_sh = -0.99 on UP / MID and +5 on DOWN
+SH_I_LF = (-1 - 5) / (-0.5 - 5)
+SH = dict(p=[1 / 6, 1 / 6, 2 / 3], r=[0.5, -0.5, 0.05], r_sh=[-0.99, 5.0, -0.99], lev_factor=SH_I_LF,
+          investor="INSURED")
+
+
+def growth(env, lev):
+    """Expected log growth per step of a constant leverage (natural log)."""
+    if env == "dice_sh":
+        p, r, rs = np.array(SH["p"]), np.array(SH["r"]), np.array(SH["r_sh"])
+        R = lev * r + (1.0 - lev) * rs
+    else:
+        g = GAMBLES[env]
+        p, R = np.array(g["p"]), lev * np.array(g["r"])
+    R = np.maximum(R, -0.99 if env == "dice_sh" else -0.9)  # env MIN_RETURN clips
+    return float(np.sum(p * np.log1p(R)))
+
+
+def kelly(env):
+    """Growth-optimal leverage (golden-section search of g) and its growth %/step."""
+    lf = SH["lev_factor"] if env == "dice_sh" else GAMBLES[env]["lev_factor"]
+    lo, hi = 0.0, 0.99 * lf
+    for _ in range(200):
+        m1, m2 = lo + (hi - lo) * 0.382, lo + (hi - lo) * 0.618
+        if growth(env, m1) < growth(env, m2):
+            lo = m1
+        else:
+            hi = m2
+    l = 0.5 * (lo + hi)
+    return l, 100.0 * math.expm1(growth(env, l))
+
+
+def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eval_every=500, n_eval=4096,
+        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0"):
+    import torch
+
+    from rlmd_amd.trainer import VecTrainer
+
+    fam = "dice_sh" if env == "dice_sh" else env
+    inv = SH["investor"] if env == "dice_sh" else GAMBLES[env]["investor"]
+    lf = SH["lev_factor"] if env == "dice_sh" else GAMBLES[env]["lev_factor"]
+    tr = VecTrainer(env=fam, investor=inv, n_lanes=lanes, n_gambles=1, algo=algo, k_updates=k,
+                    replay_capacity=replay, seed=seed, warmup_steps=warmup, smoothing_window=smoothing,
+                    precision=precision, device=device, init_seed=seed)
+    l_star, g_star = kelly(env)
+    reset_obs = tr.env.reset()[:1].float().clone()  # the reset state (identical for every lane)
+    tr2 = None
+    recs = []
+    t0 = time.perf_counter()
+    for step in range(1, steps + 1):
+        tr.step()
+        if step % eval_every == 0 or step == steps:
+            a = float(tr.agent.act(reset_obs, mode=1)[0, 0].item())
+            ev = tr.evaluate(n_eval=n_eval, max_steps=100, with_stats=False)
+            grow = 100.0 * float(np.mean(ev["reward"] - 1.0))
+            lev = a * lf
+            rec = {"env": env, "precision": precision, "lanes": lanes, "k": k, "step": step,
+                   "updates": step * k, "env_steps": step * lanes, "action": a, "lev": lev,
+                   "eval_growth_pct": grow, "analytic_growth_pct": 100.0 * math.expm1(growth(env, lev)),
+                   "kelly_lev": l_star, "kelly_growth_pct": g_star, "wall_s": time.perf_counter() - t0,
+                   "nan_flag": tr.agent.scalars()["nan_flag"]}
+            recs.append(rec)
+            log(json.dumps(rec))
+            if out is not None:
+                out.write(json.dumps(rec) + "\n")
+                out.flush()
+    return recs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--env", default="coin", choices=["coin", "dice", "dice_sh"])
+    ap.add_argument("--lanes", type=int, default=65536)
+    ap.add_argument("--k", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20000)
+    ap.add_argument("--precision", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--warmup", type=int, default=1000)
+    ap.add_argument("--smoothing", type=int, default=2000)
+    ap.add_argument("--eval-every", type=int, default=500)
+    ap.add_argument("--n-eval", type=int, default=4096)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--replay", type=int, default=1 << 20)
+    ap.add_argument("--algo", default="SAC", choices=["SAC", "TD3"])
+    ap.add_argument("--out", default=None, help="append JSON lines here")
+    a = ap.parse_args()
+    out = open(a.out, "a") if a.out else None
+    run(a.env, a.lanes, a.k, a.steps, a.precision, a.warmup, a.smoothing, a.eval_every, a.n_eval, a.seed,
+        a.replay, a.algo, out)
+
+
+if __name__ == "__main__":
+    main()
