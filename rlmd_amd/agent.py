@@ -288,7 +288,15 @@ class _Agent:
         self.memory = ReplayMemory(buf, S, A, device=device, multi_steps=int(inputs.get("multi_steps", 1)),
                                    dynamics=inputs.get("dynamics", "A"), gamma=float(inputs["discount"]))
         self._act_ctr = 0
+        self._batch_ctr = 0
         self.file_prefix = None
+        if all(k in inputs for k in ("env_id", "dynamics", "s_dist", "loss_fn", "critic_mean_type", "n_cumsteps",
+                                     "n_trials", "trial", "multi_steps")):
+            # algo_sac.py:121-141: ./results/<dyna>models/<env_id>/ + save_directory(results=False)
+            from . import logs
+
+            self.file_prefix = logs.save_directory(inputs, results=False)
+            os.makedirs(os.path.dirname(self.file_prefix), exist_ok=True)
 
     # -- reference methods --------------------------------------------------
     def store_transistion(self, state, action, reward, next_state, done):
@@ -313,6 +321,33 @@ class _Agent:
         logtemp = np.float32(st[11]) if self.algo == "SAC" else np.nan
         return loss, logtemp, [float(x) for x in st[12:16]]
 
+    def _mini_batch(self):
+        """algo_sac.py:238-262: one mini-batch of B distinct uniform ring rows,
+        sampled and gathered on the device (rlmd_replay_sample): (states,
+        actions, rewards, next_states, dones, effective n-step counts)."""
+        dev, B, S, A = self.dev.device, self.batch_size, self.dev.S, self.dev.A
+        m = self.memory
+        idx = torch.empty(B, dtype=torch.int64, device=dev)
+        s, s2 = torch.empty(B, S, device=dev), torch.empty(B, S, device=dev)
+        a, r = torch.empty(B, A, device=dev), torch.empty(B, device=dev)
+        d, eff = torch.empty(B, dtype=torch.uint8, device=dev), torch.empty(B, dtype=torch.int32, device=dev)
+        self._batch_ctr += 1
+        check(_abi.lib().rlmd_replay_sample(m.h, B, int(self.dev.cfg.seed) ^ 0xBA7C4, self._batch_ctr, ptr(idx),
+                                            ptr(s), ptr(a), ptr(r), ptr(s2), ptr(d), ptr(eff), stream_ptr()))
+        return s, a, r, s2, d.bool(), eff
+
+    def _multi_step_target(self, *args, **kw):
+        """algo_sac.py:300-367: the target is formed inside the fused learn()
+        kernels on the device (fwd_rows target jobs + the critic-loss epilogue),
+        never materialised for the host; kept for the reference's hasattr contract
+        (tests/test_input_agent.py:587-734)."""
+        raise NotImplementedError("the target is fused into learn() (rlmd_agent_learn)")
+
+    def _update_critic_parameters(self, *args, **kw):
+        """algo_sac.py:597-615: the Polyak update runs inside the device Adam step of
+        every learn(); kept for the reference's hasattr contract."""
+        raise NotImplementedError("Polyak averaging is fused into learn() (rlmd_agent_learn)")
+
     def _ckpt(self, net):
         prefix = self.file_prefix or os.path.join(".", "rlmd_amd_model")
         return f"{prefix}_{net}.pt"
@@ -321,9 +356,12 @@ class _Agent:
         for net in ("actor", "critic_1", "critic_2"):
             torch.save({k: v.detach().cpu() for k, v in self.dev.state_dict(net).items()}, self._ckpt(net))
 
-    def load_models(self):
+    def load_models(self, prefix=None):
+        """algo_sac.py:625-632; prefix: another file stem (the driver's `continue`
+        loads the previous trial's checkpoints)."""
         for net in ("actor", "critic_1", "critic_2"):
-            sd = torch.load(self._ckpt(net), weights_only=True)
+            path = self._ckpt(net) if prefix is None else f"{prefix}_{net}.pt"
+            sd = torch.load(path, weights_only=True)
             for k, v in self.dev.state_dict(net).items():
                 v.copy_(sd[k])
 

@@ -1,0 +1,81 @@
+"""Evaluation episodes of the single-agent drivers, on the device.
+
+``eval_multiplicative`` keeps tools/eval_episodes.py:176-399's signature and
+log layout: n_eval episodes of <= max_eval_steps on a fresh env, each with ONE
+constant action (the deterministic policy at the episode's reset state, the
+action window applied as at cum_steps, :231-243), logging per episode
+[time, reward, steps, loss[11], logtemp, loss_params[4], cum_steps] and the
+last risk row (:263-273).  All episodes run as lanes of one rlmd_eval_rollout
+launch; the event's wall time is split evenly over them.  The reference's
+printed summary statistics come from rlmd_eval_stats (NumPy-exact).
+
+``agent_shadow_mean`` is tools/utils.py:441-471 on the device
+(rlmd_shadow_means on the 16-entry statistics row).
+"""
+import time
+
+import numpy as np
+import torch
+
+from . import _abi
+from ._abi import check, ptr, stream_ptr
+from .envs import ENV_CLASSES, VecEnv
+
+_EVAL_ENVS = {}
+
+
+def env_class_name(env_id):
+    """main.py gym_envs name of an inputs["env_id"] (name + "_n" + n_gambles)."""
+    name = str(env_id)
+    return name.rsplit("_n", 1)[0] if name.rsplit("_n", 1)[-1].isdigit() else name
+
+
+def _eval_env(inputs, n_gambles, n_eval, device):
+    cls = ENV_CLASSES[env_class_name(inputs["env_id"])]
+    key = (cls.family, cls.investor, n_gambles, n_eval, str(device))
+    env = _EVAL_ENVS.get(key)
+    if env is None:
+        seed = int(inputs.get("eval_seed", np.random.randint(0, 2**31 - 1)))
+        env = VecEnv(cls.family, cls.investor, n_eval, n_gambles, seed=seed, device=device)
+        _EVAL_ENVS[key] = env
+    return env
+
+
+def agent_shadow_mean(inputs, loss, device=None):
+    """[shadow1, shadow2] of tools/utils.py:441-471 (loss[0:2] where the tail index
+    is >= 1), computed by rlmd_shadow_means."""
+    dev = torch.device(device or "cuda:0")
+    row = torch.tensor(np.asarray(list(loss[:11]) + [0.0] * 5, dtype=np.float32), device=dev)
+    out = torch.empty(2, dtype=torch.float32, device=dev)
+    check(_abi.lib().rlmd_shadow_means(ptr(row), 1, 16, float(inputs["shadow_low_mul"]),
+                                       float(inputs["shadow_high_mul"]), ptr(out), 2, stream_ptr()))
+    s = out.cpu().numpy().astype(np.float64)
+    return [float(s[0]), float(s[1])]
+
+
+def eval_multiplicative(n_gambles, agent, inputs, eval_log, eval_risk_log, multi_step, cum_steps, round, eval_run,
+                        loss, logtemp, loss_params, device=None):
+    dev = torch.device(device or agent.dev.device)
+    n_eval = int(inputs["n_eval"])
+    env = _eval_env(inputs, n_gambles, n_eval, dev)
+    t0 = time.perf_counter()
+    obs = env.reset().float()
+    actions = agent.dev.act(obs, mode=1)
+    reward = torch.empty(n_eval, dtype=torch.float64, device=dev)
+    steps = torch.empty(n_eval, dtype=torch.int32, device=dev)
+    risk = torch.empty(n_eval, env.risk_dim, dtype=torch.float64, device=dev)
+    check(_abi.lib().rlmd_eval_rollout(env.h, ptr(actions), int(inputs["max_eval_steps"]), int(cum_steps),
+                                       int(inputs["random"]), int(inputs["smoothing_window"]), None, ptr(reward),
+                                       ptr(steps), ptr(risk), stream_ptr()))
+    r, st, rk = reward.cpu().numpy(), steps.cpu().numpy(), risk.cpu().numpy()
+    dt = time.perf_counter() - t0
+    e = eval_log[round, eval_run]
+    e[:, 0] = dt / n_eval
+    e[:, 1] = r
+    e[:, 2] = st
+    e[:, 3:14] = np.asarray(loss, dtype=np.float64)
+    e[:, 14] = logtemp
+    e[:, 15:19] = np.asarray(loss_params, dtype=np.float64)
+    e[:, 19] = cum_steps
+    eval_risk_log[round, eval_run] = rk
+    return {"reward": r, "steps": st, "risk": rk}

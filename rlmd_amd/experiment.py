@@ -7,6 +7,13 @@ critics' shadow means filled in first (loss[6:8] = agent_shadow_mean, :255,
 (:447-450).  Here one trial is one VecTrainer (its own seed); a "step" is one
 vector step over all lanes; trial rows aggregate `log_every` vector steps (see
 rlmd_amd/logs.py); evaluation rows are per episode as in the reference.
+
+Trials are independent (the reference runs them one after another and shares
+nothing but the output arrays), so under torch.distributed they shard over
+ranks: trial t runs on rank t % world, each rank on its own GPU, and the only
+collective is one all_gather of the four log arrays after the last trial (RCCL
+over xGMI on the GPU box, gloo in tests/test_multirank_cpu.py); rank 0 writes
+the .npy files.
 """
 import os
 import time
@@ -15,7 +22,6 @@ import numpy as np
 import torch
 
 from . import logs
-from .trainer import VecTrainer
 
 ENV_NAMES = {"coin": "Coin", "dice": "Dice", "gbm": "GBM", "dice_sh": "Dice_SH"}
 
@@ -31,12 +37,44 @@ def env_id(env, investor, n_gambles=1, market_name="SNP", obs_days=1, action_day
     return f"{ENV_NAMES[env]}_Inv{investor}_n{n_gambles}"
 
 
+def _world():
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_world_size(), dist.get_rank()
+    return 1, 0
+
+
+def gather_logs(lg, owner, world, device):
+    """One all_gather of every rank's four log arrays (flattened f64, lossless for
+    the f32 logs) plus per-trial row counts; trial t is taken from rank owner[t]."""
+    import torch.distributed as dist
+
+    parts = [lg.trial, lg.eval, lg.trial_risk, lg.eval_risk, lg.rows.astype(np.float64)]
+    flat = torch.from_numpy(np.concatenate([np.asarray(p, np.float64).ravel() for p in parts])).to(device)
+    out = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(out, flat)
+    got = [o.cpu().numpy() for o in out]
+    sizes = [p.size for p in parts]
+    offs = np.concatenate([[0], np.cumsum(sizes)])
+    for t, r in enumerate(owner):
+        src = [got[r][offs[i]:offs[i + 1]].reshape(parts[i].shape) for i in range(len(parts))]
+        lg.trial[t], lg.eval[t], lg.trial_risk[t], lg.eval_risk[t] = src[0][t], src[1][t], src[2][t], src[3][t]
+        lg.rows[t] = int(src[4][t])
+    return lg
+
+
 def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE", n_lanes=4096, n_cumsteps=2000,
                    eval_freq=1000, n_eval=100, max_eval_steps=100, n_trials=1, k_updates=1, log_every=1,
                    warmup_steps=1000, smoothing_window=2000, buffer=1_000_000, multi_steps=1, precision="bf16",
-                   seed=0, results_root=".", test_agent=True, device="cuda:0", test_days=250, **trainer_kw):
-    """Train n_trials independent vectorised agents and save the reference's four
-    log arrays; returns (file stem, ExperimentLog)."""
+                   seed=0, results_root=".", test_agent=True, device="cuda:0", test_days=250,
+                   trainer_factory=None, gather_device=None, **trainer_kw):
+    """Train n_trials independent vectorised agents (sharded over the ranks of an
+    initialised process group, trial t on rank t % world) and save the
+    reference's four log arrays on rank 0; returns (file stem, ExperimentLog),
+    the log complete on every rank.  trainer_factory(seed) replaces the
+    VecTrainer construction (tests)."""
+    world, rank = _world()
     market = env == "market"
     dyn = "MKT" if market else "M"
     eid = env_id(env, investor, n_gambles, obs_days=trainer_kw.get("obs_days", 1))
@@ -47,11 +85,19 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
     n_evals = n_cumsteps // eval_freq
     rdim = (logs.market_log_dim(eid, n_gambles) if market else logs.multi_log_dim(eid, n_gambles))
     lg = logs.ExperimentLog(n_trials, n_rows, n_evals, n_eval, rdim, market=market)
+    if trainer_factory is None:
+        from .trainer import VecTrainer
+
+        def trainer_factory(sd):
+            return VecTrainer(env, investor, n_lanes, n_gambles, algo=algo, loss=loss, k_updates=k_updates,
+                              replay_capacity=(buffer // n_lanes) * n_lanes if multi_steps > 1 else buffer,
+                              seed=sd, warmup_steps=warmup_steps, smoothing_window=smoothing_window,
+                              precision=precision, device=device, multi_steps=multi_steps, **trainer_kw)
+    owner = [t % world for t in range(n_trials)]
     for trial in range(n_trials):
-        tr = VecTrainer(env, investor, n_lanes, n_gambles, algo=algo, loss=loss, k_updates=k_updates,
-                        replay_capacity=(buffer // n_lanes) * n_lanes if multi_steps > 1 else buffer,
-                        seed=seed + trial, warmup_steps=warmup_steps, smoothing_window=smoothing_window,
-                        precision=precision, device=device, multi_steps=multi_steps, **trainer_kw)
+        if owner[trial] != rank:
+            continue
+        tr = trainer_factory(seed + trial)
         prev = np.zeros(3)
         t_row = time.perf_counter()
         eval_run = 0
@@ -70,11 +116,19 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
                 t0 = time.perf_counter()
                 ev = (tr.evaluate_market(n_eval=n_eval, test_days=test_days) if market
                       else tr.evaluate(n_eval=n_eval, max_steps=max_eval_steps))
-                torch.cuda.synchronize()
+                if torch.cuda.is_available():
+                    torch.cuda.synchronize()
                 lg.log_eval(trial, eval_run, ev, time.perf_counter() - t0, st, step)
                 eval_run += 1
         del tr
+    if world > 1:
+        import torch.distributed as dist
+
+        dev = gather_device or (torch.device("cuda", torch.cuda.current_device())
+                                if dist.get_backend() == "nccl" else torch.device("cpu"))
+        gather_logs(lg, owner, world, dev)
     stem = logs.save_directory(inputs, results=True)
     path = os.path.join(results_root, stem[2:] if stem.startswith("./") else stem)
-    lg.save(path)
+    if rank == 0:
+        lg.save(path)
     return path, lg

@@ -867,6 +867,136 @@ def lev_fixtures(seed=41):
     return out
 
 
+# ----------------------------------------------------------------------------
+# F6: the reference's own C1 loop (scripts/rl_multiplicative.py), recorded
+# ----------------------------------------------------------------------------
+class _RecordingRandom:
+    """``np.random`` of coin_flip_envs that draws from the real, seeded global
+    generator and records each coin draw u: legacy ``choice(a, p)`` is
+    a[searchsorted(cumsum(p)/cumsum(p)[-1], random_sample(), 'right')]
+    (pinned by rng_choice_kat), so the stream is consumed exactly as before."""
+
+    def __init__(self, sink):
+        self.sink = sink
+
+    def __getattr__(self, name):
+        return getattr(np.random, name)
+
+    def choice(self, a, size=None, replace=True, p=None):
+        u = np.random.random_sample(size)
+        self.sink(np.atleast_1d(u).astype(np.float64))
+        cdf = np.asarray(p, dtype=np.float64).cumsum()
+        cdf /= cdf[-1]
+        return np.asarray(a)[cdf.searchsorted(u, side="right")]
+
+
+def c1_trace(n_steps=2500, seed=0):
+    """Config C1 as the reference runs it: main.py's tables (Coin_InvA, key 8),
+    SAC, MSE, one trial of n_steps with eval_freq 1e3, seeded np.random + torch,
+    through scripts/rl_multiplicative.multiplicative_env.  n_steps = 2500 covers
+    the warm-up (|sample|, <= 1e3), the smoothing window (f64 clip, <= 2e3) and
+    the policy phase.  Recorded for the TRAINING env instance: every step's
+    action as the env received it, the coin draw u, state / next_state / reward /
+    done / risk; every select_next_action output (pre-window) and learn() return;
+    the cum_steps of every save_models(); and the saved trial / trial_risk logs."""
+    import importlib
+
+    import main as ref_main
+    import envs.coin_flip_envs as cf
+    from algos import algo_sac
+    from tools import utils
+
+    rec = {k: [] for k in ("action", "u", "state", "next_state", "reward", "done", "risk", "policy",
+                           "learn_loss", "learn_logtemp", "learn_params", "learn_step", "save_step")}
+    env_ids = []
+    ctr = {"steps": 0}
+    cur_u = []
+    cf_np = _NpProxy(_RecordingRandom(cur_u.append))
+    saved_np = cf.np
+    cls = cf.Coin_InvA
+    orig_init, orig_step, orig_reset = cls.__init__, cls.step, cls.reset
+    orig_sel, orig_learn, orig_save = algo_sac.Agent_sac.select_next_action, algo_sac.Agent_sac.learn, \
+        algo_sac.Agent_sac.save_models
+
+    def init(self, *a, **kw):
+        orig_init(self, *a, **kw)
+        env_ids.append(id(self))
+
+    def step(self, action):
+        train = id(self) == env_ids[0]
+        if train:
+            rec["state"].append(self._c1_last.copy())
+            rec["action"].append(np.asarray(action).astype(np.float64).copy())
+            rec.setdefault("action_dtype", []).append(np.asarray(action).dtype == np.float64)
+        cur_u.clear()
+        s2, r, d, risk = orig_step(self, action)
+        if train:
+            rec["u"].append(np.array(cur_u[0], dtype=np.float64).copy())
+            rec["next_state"].append(np.asarray(s2, np.float64).copy())
+            rec["reward"].append(float(r))
+            rec["done"].append(list(d))
+            rec["risk"].append(np.asarray(risk, np.float64).ravel().copy())
+            self._c1_last = np.asarray(s2, np.float64).copy()
+            ctr["steps"] += 1
+        return s2, r, d, risk
+
+    def reset(self):
+        s = orig_reset(self)
+        self._c1_last = np.asarray(s, np.float64).copy()
+        return s
+
+    def sel(self, state):
+        a = orig_sel(self, state)
+        rec["policy"].append(np.asarray(a).astype(np.float64).copy())
+        return a
+
+    def learn(self):
+        loss, logtemp, params = orig_learn(self)
+        rec["learn_loss"].append(np.asarray([float(x) for x in loss], np.float64))
+        rec["learn_logtemp"].append(float(logtemp))
+        rec["learn_params"].append(np.asarray([float(x) for x in params], np.float64))
+        rec["learn_step"].append(ctr["steps"] - 1)
+        return loss, logtemp, params
+
+    def save(self):
+        rec["save_step"].append(ctr["steps"])
+        orig_save(self)
+
+    cf.np = cf_np
+    cls.__init__, cls.step, cls.reset = init, step, reset
+    algo_sac.Agent_sac.select_next_action, algo_sac.Agent_sac.learn = sel, learn
+    algo_sac.Agent_sac.save_models = save
+    rl = importlib.import_module("scripts.rl_multiplicative")
+    rl.Agent_sac = algo_sac.Agent_sac
+    import contextlib
+    import glob
+    import io
+
+    try:
+        inputs = dict(ref_main.inputs)
+        inputs.update({"n_trials_mul": 1, "n_cumsteps_mul": float(n_steps), "gpu": "cpu", "buffer_gpu": False})
+        inputs = utils.input_initialisation(inputs, [8], ["SAC"], ["MSE"], [1])
+        inputs["test_agent"] = True
+        inputs["ENV_KEY"] = 8
+        np.random.seed(seed)
+        T.manual_seed(seed)
+        with contextlib.redirect_stdout(io.StringIO()):
+            rl.multiplicative_env(ref_main.gym_envs, inputs, n_gambles=1)
+        trial = np.load(glob.glob("results/test_multiplicative/**/*_trial.npy", recursive=True)[0])
+        trial_risk = np.load(glob.glob("results/test_multiplicative/**/*_trial_risk.npy", recursive=True)[0])
+    finally:
+        cf.np = saved_np
+        cls.__init__, cls.step, cls.reset = orig_init, orig_step, orig_reset
+        algo_sac.Agent_sac.select_next_action, algo_sac.Agent_sac.learn = orig_sel, orig_learn
+        algo_sac.Agent_sac.save_models = orig_save
+    out = {k: np.asarray(v) for k, v in rec.items()}
+    out["trial"] = trial
+    out["trial_risk"] = trial_risk
+    out["n_steps"] = np.array(n_steps)
+    out["seed"] = np.array(seed)
+    return out
+
+
 def main():
     work = tempfile.mkdtemp(prefix="rlmd_golden_")
     os.chdir(work)  # the reference creates ./results/... relative to cwd
@@ -883,6 +1013,7 @@ def main():
         "logs.npz": log_fixtures,
         "learn.npz": learn_fixtures,
         "lev.npz": lev_fixtures,
+        "c1_trace.npz": c1_trace,
     }
     only = sys.argv[1:]
     for fn, job in jobs.items():

@@ -49,6 +49,22 @@ def main():
     inputs = utils.input_initialisation(inputs, [a.key], ["SAC"], ["MSE"], [1])
     inputs["test_agent"] = True
     inputs["ENV_KEY"] = a.key
+    import envs.dice_roll_sh_envs as sh_mod
+
+    class _ArrayFix:
+        """dice_roll_sh_envs' np with NumPy 1.22's array() of a list holding a
+        size-1 ndarray (Dice_SH_INSURED risk list); np.random stays
+        the real (seeded) generator."""
+
+        def __getattr__(self, name):
+            return getattr(np, name)
+
+        def array(self, obj, *args, **kw):
+            if isinstance(obj, list):
+                obj = [o.reshape(()) if isinstance(o, np.ndarray) and o.size == 1 else o for o in obj]
+            return np.array(obj, *args, **kw)
+
+    sh_mod.np = _ArrayFix()
     out = os.path.join(HERE, f"converge_ref_{a.key}_s{a.seed}.npz")
     np.random.seed(a.seed)
     torch.manual_seed(a.seed)
