@@ -305,6 +305,20 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
  * accumulator it was given (stream-ordered; no-op when nothing is pending). */
 int rlmd_train_flush_stats(rlmd_env_t env, void* stream);
 
+/* Per-episode log of rlmd_train_step (the reference's per-episode trial rows,
+ * rl_multiplicative.py:275-283, :400-414): with cap_per_wave > 0 every lane that
+ * finishes an episode appends one f32 row [env step counter, lane, final reward,
+ * episode length, risk[R]] (4 + R floats; R from rlmd_env_dims) to its wave's
+ * region of cap_per_wave rows; rows past the cap are counted, not kept.
+ * cap_per_wave = 0 disables it (the default).  Synchronises the device. */
+int rlmd_train_episode_log(rlmd_env_t env, int32_t cap_per_wave);
+/* Move the logged rows into out_dev f32 [out_cap, 4 + R] (packed, wave order;
+ * within a wave in append order, lanes ascending per step), reset the log, and
+ * return the rows written (*n_out_host) and the rows appended since the last
+ * drain including dropped ones (*appended_host, nullable).  Synchronises stream. */
+int rlmd_train_episode_drain(rlmd_env_t env, float* out_dev, int64_t out_cap, int64_t* n_out_host,
+                             int64_t* appended_host, void* stream);
+
 /* Initialise obs_dev f32 [N, S] with every lane reset (episode start). */
 int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
 

@@ -91,6 +91,8 @@ SIGNATURES = {
     "rlmd_train_step": (C.c_int, [P, P, P, C.POINTER(TrainCfg), P, P, P, P, P]),
     "rlmd_train_reset": (C.c_int, [P, P, P]),
     "rlmd_train_flush_stats": (C.c_int, [P, P]),
+    "rlmd_train_episode_log": (C.c_int, [P, C.c_int32]),
+    "rlmd_train_episode_drain": (C.c_int, [P, P, C.c_int64, P, P, P]),
     "rlmd_env_lane_start": (C.c_int, [P, P]),
     "rlmd_shadow_means": (C.c_int, [P, I32, I32, C.c_float, C.c_float, P, I32, P]),
     "rlmd_shadow_equiv": (C.c_int, [P, P, P, P, C.c_double, I64, P, P]),

@@ -181,6 +181,18 @@ class DeviceAgent:
         check(_abi.lib().rlmd_status_poll(self.h, C.byref(f), C.byref(u), stream_ptr(stream)))
         return f.value, u.value
 
+    def save(self, prefix):
+        """The reference's checkpoint files: <prefix>_{actor,critic_1,critic_2}.pt
+        (networks_sac.py:87-88, :287-292), state dicts with its layer names."""
+        for net in ("actor", "critic_1", "critic_2"):
+            torch.save({k: v.detach().cpu() for k, v in self.state_dict(net).items()}, f"{prefix}_{net}.pt")
+
+    def load(self, prefix):
+        for net in ("actor", "critic_1", "critic_2"):
+            sd = torch.load(f"{prefix}_{net}.pt", weights_only=True)
+            for k, v in self.state_dict(net).items():
+                v.copy_(sd[k])
+
     def scalars(self):
         out = (C.c_double * 5)()
         check(_abi.lib().rlmd_agent_scalars(self.h, out))
@@ -348,22 +360,19 @@ class _Agent:
         every learn(); kept for the reference's hasattr contract."""
         raise NotImplementedError("Polyak averaging is fused into learn() (rlmd_agent_learn)")
 
+    def _prefix(self):
+        return self.file_prefix or os.path.join(".", "rlmd_amd_model")
+
     def _ckpt(self, net):
-        prefix = self.file_prefix or os.path.join(".", "rlmd_amd_model")
-        return f"{prefix}_{net}.pt"
+        return f"{self._prefix()}_{net}.pt"
 
     def save_models(self):
-        for net in ("actor", "critic_1", "critic_2"):
-            torch.save({k: v.detach().cpu() for k, v in self.dev.state_dict(net).items()}, self._ckpt(net))
+        self.dev.save(self._prefix())
 
     def load_models(self, prefix=None):
         """algo_sac.py:625-632; prefix: another file stem (the driver's `continue`
         loads the previous trial's checkpoints)."""
-        for net in ("actor", "critic_1", "critic_2"):
-            path = self._ckpt(net) if prefix is None else f"{prefix}_{net}.pt"
-            sd = torch.load(path, weights_only=True)
-            for k, v in self.dev.state_dict(net).items():
-                v.copy_(sd[k])
+        self.dev.load(self._prefix() if prefix is None else prefix)
 
 
 class Agent_sac(_Agent):

@@ -70,6 +70,12 @@ struct EnvParams {
   int32_t* time;
   int32_t* start;
   uint32_t* episode;
+  // per-episode log of the fused train step (nullable): one region of ep_cap
+  // rows [step, lane, final reward, length, risk...] (ep_w floats) per wave,
+  // ep_cnt[wave] = rows appended since the last drain (counts past ep_cap too)
+  float* ep_rows;
+  uint32_t* ep_cnt;
+  int ep_cap, ep_w;
 };
 
 // --- categorical outcome from a uniform: NumPy legacy choice(a, p) =
@@ -161,6 +167,10 @@ struct StepOut {
   bool done, learn_done;
 };
 
+struct NoDoneHook {
+  __device__ void operator()(const StepOut&) const {}
+};
+
 // One env step for one lane.  `act(i)` yields action i as AT, `draw(j)` the
 // j-th uniform/normal.  Writes state element k through st(k, v) and risk
 // element k through rk(k, v).
@@ -174,10 +184,11 @@ struct StepOut {
 // FAM (the env family) is a template parameter, so each family's kernel holds
 // only its own code; NG > 0 fixes n_gambles / n_assets at compile time (the
 // n == 1 configurations), NG == 0 reads it from P.
-template <int FAM, int NG, typename AT, typename ActF, typename DrawF, typename StF, typename RkF>
+template <int FAM, int NG, typename AT, typename ActF, typename DrawF, typename StF, typename RkF,
+          typename DoneF = NoDoneHook>
 __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, double w0, int t,
                                         int start, uint32_t ep, ActF act, DrawF draw, StF st,
-                                        RkF rk) {
+                                        RkF rk, DoneF on_done = DoneF{}) {
   constexpr FamConst C = fam_const(FAM);
   constexpr int fam = FAM;
   const int inv = P.inv, n = NG ? NG : P.n;
@@ -321,6 +332,7 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
   o.reward = reward;
   o.done = done;
   o.learn_done = done && !done_state && !done_time;
+  on_done(o);  // the done flags are known before the risk vector is emitted
 
   // risk vector
   rk(0, reward);
@@ -495,6 +507,9 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
     const int t = P.time[lane];
     const int start = FAM == RLMD_MARKET ? P.start[lane] : 0;
     const uint32_t ep = P.episode[lane];
+    // per-episode log: this wave's row count, loaded with the lane state
+    const uint32_t ep_base = P.ep_rows ? P.ep_cnt[lane >> 6] : 0u;
+    int64_t ep_slot = -1;
     // action i: warm-up Philox draw (|.| unless GBM/market) or the policy's, then the
     // smoothing-window clip
     auto act_of = [&](int i) -> AT {
@@ -552,7 +567,29 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
           rb.next_state[row * S + k] = f;
           obs[(int64_t)lane * S + k] = f;
         },
-        [&](int, double) {});
+        [&](int k, double v) {
+          if (ep_slot >= 0 && k < P.ep_w - 4) P.ep_rows[ep_slot * P.ep_w + 4 + k] = (float)v;
+        },
+        [&](const StepOut& so) {
+          // finished lanes of this wave take consecutive rows of its region in lane
+          // order (ballot prefix); the lowest finishing lane publishes the count
+          if (!P.ep_rows) return;
+          const uint64_t m = __ballot(so.done);
+          if (m == 0) return;
+          const int lid = threadIdx.x & 63;
+          if (so.done) {
+            const uint32_t at = ep_base + (uint32_t)__popcll(m & ((1ull << lid) - 1ull));
+            if (at < (uint32_t)P.ep_cap) ep_slot = (int64_t)(lane >> 6) * P.ep_cap + at;
+          }
+          if (lid == __ffsll((unsigned long long)m) - 1) P.ep_cnt[lane >> 6] = ep_base + (uint32_t)__popcll(m);
+        });
+    if (ep_slot >= 0) {
+      float* er = P.ep_rows + ep_slot * P.ep_w;
+      er[0] = (float)step;
+      er[1] = (float)lane;
+      er[2] = (float)o.reward;
+      er[3] = (float)t;
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j)
       if (j < S) rb.state[row * S + j] = s0[j];
@@ -712,6 +749,59 @@ __global__ void __launch_bounds__(256) env_obs_reset_kernel(EnvParams P, float* 
 }
 
 // Host dispatch over the compile-time family (and n == 1) specialisations:
+// ---------------------------------------------------------------------------
+// per-episode log drain: exclusive scan of the waves' kept row counts (one
+// workgroup), then one 64-lane workgroup per wave copies its rows into the
+// packed output in wave order.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(1024) ep_scan_kernel(const uint32_t* cnt, int n_waves, int cap, int64_t* offs,
+                                                       int64_t* totals) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (n_waves + 1023) / 1024;
+  int64_t kept = 0, seen = 0;
+  for (int i = t * per; i < (t + 1) * per && i < n_waves; ++i) {
+    const uint32_t c = cnt[i];
+    kept += c < (uint32_t)cap ? c : (uint32_t)cap;
+    seen += c;
+  }
+  part[t] = kept;
+  __syncthreads();
+  for (int h = 1; h < 1024; h <<= 1) {  // Hillis-Steele inclusive scan
+    const int64_t v = t >= h ? part[t - h] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t o = part[t] - kept;
+  for (int i = t * per; i < (t + 1) * per && i < n_waves; ++i) {
+    offs[i] = o;
+    const uint32_t c = cnt[i];
+    o += c < (uint32_t)cap ? c : (uint32_t)cap;
+  }
+  // totals: [kept rows, rows appended]
+  __shared__ unsigned long long seen_all;
+  if (t == 0) seen_all = 0;
+  __syncthreads();
+  atomicAdd(&seen_all, (unsigned long long)seen);
+  __syncthreads();
+  if (t == 0) {
+    totals[0] = part[1023];
+    totals[1] = (int64_t)seen_all;
+  }
+}
+
+__global__ void __launch_bounds__(64) ep_copy_kernel(const float* rows, const uint32_t* cnt, const int64_t* offs,
+                                                     int cap, int w, float* out, int64_t out_cap) {
+  const int wave = blockIdx.x;
+  const uint32_t c = cnt[wave];
+  const int64_t n = (int64_t)(c < (uint32_t)cap ? c : (uint32_t)cap) * w;
+  const int64_t o = offs[wave] * w, lim = out_cap * w;
+  const float* src = rows + (int64_t)wave * cap * w;
+  for (int64_t i = threadIdx.x; i < n; i += 64)
+    if (o + i < lim) out[o + i] = src[i];
+}
+
 // LAUNCH(FAM, NG) is expanded once per combination.
 #define RLMD_ENV_DISPATCH(P, LAUNCH)                        \
   do {                                                      \
@@ -750,6 +840,9 @@ struct rlmd_env_s {
   double* d_part = nullptr;
   int part_rows = 0, part_parity = 0;
   double* pending_dst = nullptr;
+  // per-episode log (EnvParams::ep_rows / ep_cnt) and the drain's scratch
+  int64_t* ep_offs = nullptr;
+  int64_t* ep_tot = nullptr;
 };
 
 namespace rlmd {
@@ -939,6 +1032,10 @@ int rlmd_env_destroy(rlmd_env_t env) {
   (void)hipFree(env->P.episode);
   if (env->d_prices) (void)hipFree(env->d_prices);
   (void)hipFree(env->d_part);
+  if (env->P.ep_rows) (void)hipFree(env->P.ep_rows);
+  if (env->P.ep_cnt) (void)hipFree(env->P.ep_cnt);
+  if (env->ep_offs) (void)hipFree(env->ep_offs);
+  if (env->ep_tot) (void)hipFree(env->ep_tot);
   delete env;
   return 0;
 }
@@ -1042,6 +1139,56 @@ int rlmd_env_lane_start(rlmd_env_t env, int32_t* start_host) {
 int rlmd_train_flush_stats(rlmd_env_t env, void* stream) {
   RLMD_CHECK(env, "null env");
   return rlmd::flush_stats(env, (hipStream_t)stream);
+}
+
+int rlmd_train_episode_log(rlmd_env_t env, int32_t cap_per_wave) {
+  RLMD_CHECK(env, "null env");
+  RLMD_CHECK(cap_per_wave >= 0, "cap_per_wave must be >= 0");
+  EnvParams& P = env->P;
+  RLMD_HIP(hipDeviceSynchronize());
+  if (P.ep_rows) (void)hipFree(P.ep_rows);
+  if (P.ep_cnt) (void)hipFree(P.ep_cnt);
+  if (env->ep_offs) (void)hipFree(env->ep_offs);
+  if (env->ep_tot) (void)hipFree(env->ep_tot);
+  P.ep_rows = nullptr;
+  P.ep_cnt = nullptr;
+  env->ep_offs = env->ep_tot = nullptr;
+  P.ep_cap = cap_per_wave;
+  P.ep_w = 4 + P.risk_dim;
+  if (cap_per_wave == 0) return 0;
+  const int64_t waves = ((int64_t)P.n_lanes + 63) / 64;
+  RLMD_HIP(hipMalloc(&P.ep_rows, sizeof(float) * waves * cap_per_wave * P.ep_w));
+  RLMD_HIP(hipMalloc(&P.ep_cnt, sizeof(uint32_t) * waves));
+  RLMD_HIP(hipMalloc(&env->ep_offs, sizeof(int64_t) * waves));
+  RLMD_HIP(hipMalloc(&env->ep_tot, sizeof(int64_t) * 2));
+  RLMD_HIP(hipMemset(P.ep_cnt, 0, sizeof(uint32_t) * waves));
+  RLMD_HIP(hipDeviceSynchronize());
+  return 0;
+}
+
+int rlmd_train_episode_drain(rlmd_env_t env, float* out_dev, int64_t out_cap, int64_t* n_out_host,
+                             int64_t* appended_host, void* stream) {
+  RLMD_CHECK(env && n_out_host, "null argument");
+  EnvParams& P = env->P;
+  RLMD_CHECK(P.ep_rows, "episode log not enabled (rlmd_train_episode_log)");
+  RLMD_CHECK(out_dev || out_cap == 0, "null output");
+  const int waves = (P.n_lanes + 63) / 64;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ep_scan_kernel, dim3(1), dim3(1024), 0, st, P.ep_cnt, waves, P.ep_cap, env->ep_offs,
+                     env->ep_tot);
+  RLMD_LAUNCH_CHECK();
+  if (out_cap > 0) {
+    hipLaunchKernelGGL(ep_copy_kernel, dim3(waves), dim3(64), 0, st, P.ep_rows, P.ep_cnt, env->ep_offs, P.ep_cap,
+                       P.ep_w, out_dev, out_cap);
+    RLMD_LAUNCH_CHECK();
+  }
+  RLMD_HIP(hipMemsetAsync(P.ep_cnt, 0, sizeof(uint32_t) * waves, st));
+  int64_t tot[2];
+  RLMD_HIP(hipMemcpyAsync(tot, env->ep_tot, sizeof(tot), hipMemcpyDeviceToHost, st));
+  RLMD_HIP(hipStreamSynchronize(st));
+  *n_out_host = tot[0] < out_cap ? tot[0] : out_cap;
+  if (appended_host) *appended_host = tot[1];
+  return 0;
 }
 
 int rlmd_train_reset(rlmd_env_t env, float* obs, void* stream) {

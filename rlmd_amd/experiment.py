@@ -5,8 +5,10 @@ independent agents, evaluate every eval_freq steps (100 episodes) with the
 critics' shadow means filled in first (loss[6:8] = agent_shadow_mean, :255,
 :275), and save the trial / eval logs as .npy under utils.save_directory
 (:447-450).  Here one trial is one VecTrainer (its own seed); a "step" is one
-vector step over all lanes; trial rows aggregate `log_every` vector steps (see
-rlmd_amd/logs.py); evaluation rows are per episode as in the reference.
+vector step over all lanes; trial rows are per finished episode from the
+device episode log (rlmd_amd/logs.py), with the trailing-score checkpoints of
+:285-293 and the `continue` chain of :172-183; evaluation rows are per episode
+as in the reference.
 
 Trials are independent (the reference runs them one after another and shares
 nothing but the output arrays), so under torch.distributed they shard over
@@ -47,9 +49,14 @@ def _world():
 
 def gather_logs(lg, owner, world, device):
     """One all_gather of every rank's four log arrays (flattened f64, lossless for
-    the f32 logs) plus per-trial row counts; trial t is taken from rank owner[t]."""
+    the f32 logs) plus per-trial row counts; trial t is taken from rank owner[t].
+    The trial arrays are first widened to the largest row count of any rank (one
+    all_reduce of that count)."""
     import torch.distributed as dist
 
+    width = torch.tensor([lg.trial.shape[1]], dtype=torch.int64, device=device)
+    dist.all_reduce(width, op=dist.ReduceOp.MAX)
+    lg.grow(int(width.item()))
     parts = [lg.trial, lg.eval, lg.trial_risk, lg.eval_risk, lg.rows.astype(np.float64)]
     flat = torch.from_numpy(np.concatenate([np.asarray(p, np.float64).ravel() for p in parts])).to(device)
     out = [torch.empty_like(flat) for _ in range(world)]
@@ -64,15 +71,53 @@ def gather_logs(lg, owner, world, device):
     return lg
 
 
+class _Checkpoint:
+    """rl_multiplicative.py:285-293: save the actor / critics at every new high of
+    the trailing mean of the last `trail` episode scores (checked after every
+    episode, in episode order; one save per logging interval at most, as all its
+    episodes end with the same parameters)."""
+
+    def __init__(self, trail, prefix, floor):
+        self.trail, self.prefix, self.best = int(trail), prefix, floor
+        self.scores = np.zeros(0)
+        self.saves = 0
+
+    def update(self, trainer, scores):
+        if len(scores) == 0 or self.prefix is None:
+            return False
+        allv = np.concatenate([self.scores[-(self.trail - 1):] if self.trail > 1 else self.scores[:0], scores])
+        c = np.concatenate([[0.0], np.cumsum(allv)])
+        k = len(allv) - len(scores)
+        ends = np.arange(k + 1, len(allv) + 1)
+        lo = np.maximum(ends - self.trail, 0)
+        trail = (c[ends] - c[lo]) / (ends - lo)
+        self.scores = allv[-self.trail:]
+        if trail.max() > self.best:
+            self.best = float(trail.max())
+            os.makedirs(os.path.dirname(self.prefix) or ".", exist_ok=True)
+            trainer.agent.save(self.prefix)
+            self.saves += 1
+            return True
+        return False
+
+
 def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE", n_lanes=4096, n_cumsteps=2000,
                    eval_freq=1000, n_eval=100, max_eval_steps=100, n_trials=1, k_updates=1, log_every=1,
                    warmup_steps=1000, smoothing_window=2000, buffer=1_000_000, multi_steps=1, precision="bf16",
                    seed=0, results_root=".", test_agent=True, device="cuda:0", test_days=250,
-                   trainer_factory=None, gather_device=None, **trainer_kw):
+                   trainer_factory=None, gather_device=None, episode_rows=True, episode_cap=256, trail=50,
+                   checkpoint=True, continue_trials=False, **trainer_kw):
     """Train n_trials independent vectorised agents (sharded over the ranks of an
     initialised process group, trial t on rank t % world) and save the
     reference's four log arrays on rank 0; returns (file stem, ExperimentLog),
-    the log complete on every rank.  trainer_factory(seed) replaces the
+    the log complete on every rank.
+
+    episode_rows: one trial row per finished episode from the device episode log
+    (drained every `log_every` vector steps); False: one aggregate row per
+    interval.  checkpoint: trailing-`trail` checkpoints under the reference's
+    models/ path.  continue_trials: inputs["continue"] — trial t starts from
+    trial t-1's last checkpoint and final log temperature (run on one rank, as
+    the chain is sequential).  trainer_factory(seed, init_logtemp) replaces the
     VecTrainer construction (tests)."""
     world, rank = _world()
     market = env == "market"
@@ -88,29 +133,50 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
     if trainer_factory is None:
         from .trainer import VecTrainer
 
-        def trainer_factory(sd):
+        def trainer_factory(sd, init_logtemp=0.0):
             return VecTrainer(env, investor, n_lanes, n_gambles, algo=algo, loss=loss, k_updates=k_updates,
                               replay_capacity=(buffer // n_lanes) * n_lanes if multi_steps > 1 else buffer,
                               seed=sd, warmup_steps=warmup_steps, smoothing_window=smoothing_window,
-                              precision=precision, device=device, multi_steps=multi_steps, **trainer_kw)
-    owner = [t % world for t in range(n_trials)]
+                              precision=precision, device=device, multi_steps=multi_steps,
+                              initial_logtemp=init_logtemp, **trainer_kw)
+    # a `continue` chain is sequential: rank 0 runs every trial
+    owner = [0 if continue_trials else t % world for t in range(n_trials)]
+    prev_prefix, prev_logtemp = None, 0.0
+    floor = 1e-6 if env == "dice_sh" else 1e-3  # env.reward_range[0] (MIN_REWARD)
     for trial in range(n_trials):
         if owner[trial] != rank:
             continue
-        tr = trainer_factory(seed + trial)
+        cont = continue_trials and trial > 0 and prev_prefix is not None
+        tr = trainer_factory(seed + trial, prev_logtemp if cont else 0.0)
+        if cont and os.path.exists(prev_prefix + "_actor.pt"):
+            tr.agent.load(prev_prefix)
+        prefix = None
+        if checkpoint:
+            st = logs.save_directory(dict(inputs, trial=trial + 1), results=False)
+            prefix = os.path.join(results_root, st[2:] if st.startswith("./") else st)
+        ck = _Checkpoint(trail, prefix, floor)
+        if episode_rows:
+            tr.episode_log(episode_cap)
         prev = np.zeros(3)
-        t_row = time.perf_counter()
+        t_row, steps_in_row = time.perf_counter(), 0
         eval_run = 0
         for step in range(1, n_cumsteps + 1):
             tr.step()
+            steps_in_row += 1
             if step % log_every == 0 or step == n_cumsteps:
-                n, rs, ls, _ = tr.flush_stats().cpu().numpy()
-                dn, dr, dl = n - prev[0], rs - prev[1], ls - prev[2]
-                prev = np.array([n, rs, ls])
                 now = time.perf_counter()
-                lg.log_row(trial, now - t_row, dr / dn if dn else np.nan, dl / dn if dn else np.nan,
-                           tr.last_stats(shadow=True))
-                t_row = now
+                stats = tr.last_stats(shadow=True)
+                if episode_rows:
+                    rows, _ = tr.drain_episodes()
+                    per_step = (now - t_row) / steps_in_row
+                    lg.log_episodes(trial, rows[:, 3] * per_step, rows[:, 2], rows[:, 3], stats, rows[:, 4:])
+                    ck.update(tr, rows[:, 2])
+                else:
+                    n, rs, ls, _ = tr.flush_stats().cpu().numpy()
+                    dn, dr, dl = n - prev[0], rs - prev[1], ls - prev[2]
+                    prev = np.array([n, rs, ls])
+                    lg.log_row(trial, now - t_row, dr / dn if dn else np.nan, dl / dn if dn else np.nan, stats)
+                t_row, steps_in_row = now, 0
             if step % eval_freq == 0 and eval_run < n_evals:
                 st = tr.last_stats(shadow=True)  # loss[6:8] = agent_shadow_mean(...) first
                 t0 = time.perf_counter()
@@ -120,6 +186,8 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
                     torch.cuda.synchronize()
                 lg.log_eval(trial, eval_run, ev, time.perf_counter() - t0, st, step)
                 eval_run += 1
+        prev_logtemp = float(tr.last_stats()[11]) if algo == "SAC" else 0.0
+        prev_prefix = prefix if ck.saves else None
         del tr
     if world > 1:
         import torch.distributed as dist

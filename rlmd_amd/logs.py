@@ -12,10 +12,13 @@ risk width), named by tools/utils.py:170-220 (save_directory):
   <dir>_eval_risk.npy   [n_trials, n_evals, n_eval, risk_dim]  (market: [gap, risk...])
 
 so tools/aggregate_data.py and the plotting scripts read this build's output
-unchanged.  The vectorised loop has no single episode stream: one trial row is
-one vector step (score = mean final reward of the episodes that ended in it,
-steps = their mean length, risk = NaN), stated in the row layout here and in
-DESIGN.md.  Evaluation rows are per episode, exactly as the reference's.
+unchanged.  Trial rows are per finished episode as in the reference (the
+device episode log of the fused train step: final reward, length, last risk
+vector; the learner statistics of the vector step the episode ended in; time =
+length x that interval's wall time per vector step).  ``log_row`` keeps the
+older aggregate mode (one row per logging interval: mean final reward and
+length of the episodes that ended in it, risk = NaN).  Evaluation rows are per
+episode, exactly as the reference's.
 """
 import os
 
@@ -68,6 +71,36 @@ class ExperimentLog:
         self.eval_risk = np.zeros((n_trials, n_evals, n_eval, risk_dim + (1 if market else 0)), dtype=np.float32)
         self.market = market
         self.rows = np.zeros(n_trials, dtype=np.int64)
+
+    def grow(self, n_rows):
+        """Widen the trial arrays to at least n_rows rows per trial (zero rows)."""
+        cur = self.trial.shape[1]
+        if n_rows <= cur:
+            return
+        t = np.zeros((self.trial.shape[0], n_rows, 19), dtype=np.float32)
+        r = np.zeros((self.trial.shape[0], n_rows, self.trial_risk.shape[2]), dtype=np.float32)
+        t[:, :cur], r[:, :cur] = self.trial, self.trial_risk
+        self.trial, self.trial_risk = t, r
+
+    def log_episodes(self, trial, seconds, score, steps, stats16, risk):
+        """One row per finished episode (rl_multiplicative.py:275-283, :400-414):
+        [time, score, steps, loss[11], logtemp, loss_params[4]] with the learner
+        statistics of the vector step the episodes ended in, and each episode's
+        own last risk vector."""
+        n = len(score)
+        if n == 0:
+            return
+        i = int(self.rows[trial])
+        if i + n > self.trial.shape[1]:
+            self.grow(max(2 * self.trial.shape[1], i + n))
+        st = np.asarray(stats16, dtype=np.float64)
+        t = self.trial[trial, i:i + n]
+        t[:, 0], t[:, 1], t[:, 2] = seconds, score, steps
+        t[:, 3:14] = st[:11]
+        t[:, 14] = st[11]
+        t[:, 15:19] = st[12:16]
+        self.trial_risk[trial, i:i + n] = np.asarray(risk, dtype=np.float64)[:, :self.trial_risk.shape[2]]
+        self.rows[trial] += n
 
     def log_row(self, trial, seconds, score, steps, stats16, risk=None):
         """One trial row: [time, score, steps, loss[11], logtemp, loss_params[4]] (rl_multiplicative.py:402-413)."""

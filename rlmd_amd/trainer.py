@@ -31,7 +31,8 @@ class VecTrainer:
                  k_updates=1, replay_capacity=1 << 20, seed=0, warmup_steps=1000,
                  smoothing_window=2000, precision="bf16", hidden=None, batch=None, topk=None,
                  prices=None, obs_days=1, time_length=0, shuffle_days=5, sample_days=0,
-                 device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99, s_dist="N"):
+                 device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99, s_dist="N",
+                 initial_logtemp=0.0):
         self.device = torch.device(device)
         self.env = VecEnv(env, investor, n_lanes, n_gambles, seed=seed, prices=prices, obs_days=obs_days,
                           time_length=time_length, shuffle_days=shuffle_days, sample_days=sample_days,
@@ -42,7 +43,8 @@ class VecTrainer:
         self.topk = topk or d["topk"]
         S, A = self.env.state_dim, self.env.action_dim
         self.agent = DeviceAgent(algo, S, A, h1, h2, self.batch, self.topk, loss=loss, precision=precision,
-                                 seed=seed, init_seed=init_seed, policy_dist=s_dist, device=device)
+                                 seed=seed, init_seed=init_seed, policy_dist=s_dist, device=device,
+                                 initial_logtemp=initial_logtemp)
         self.replay = ReplayMemory(replay_capacity, S, A, device=device, multi_steps=multi_steps, lanes=n_lanes,
                                    dynamics=dynamics, gamma=gamma)
         self.n_lanes, self.k_updates = n_lanes, k_updates
@@ -132,6 +134,30 @@ class VecTrainer:
         return market_evaluate(self.agent, kw["prices"], self.env.investor, kw["obs_days"], test_days, starts,
                                self.cfg.cum_step, self.cfg.warmup_steps, self.cfg.smoothing_window,
                                shuffle_days=test_shuffle_days, seed=self.env.seed + 20011, device=self.device)
+
+    def episode_log(self, cap_per_wave=256):
+        """Log every finished episode on the device (rlmd_train_episode_log): rows
+        [env step, lane, final reward, length, risk...]; 0 disables."""
+        check(_abi.lib().rlmd_train_episode_log(self.env.h, int(cap_per_wave)))
+        self._ep_cap = int(cap_per_wave)
+        self._ep_out = None
+
+    def drain_episodes(self):
+        """The episodes logged since the last drain as f64 rows [env step, lane,
+        final reward, length, risk...] ordered by (step, lane), and the number of
+        rows the per-wave caps dropped."""
+        w = 4 + self.env.risk_dim
+        cap = ((self.n_lanes + 63) // 64) * self._ep_cap
+        if self._ep_out is None:
+            self._ep_out = torch.empty(cap, w, dtype=torch.float32, device=self.device)
+        import ctypes as C
+
+        n, seen = C.c_int64(), C.c_int64()
+        check(_abi.lib().rlmd_train_episode_drain(self.env.h, ptr(self._ep_out), cap, C.byref(n), C.byref(seen),
+                                                  stream_ptr()))
+        rows = self._ep_out[:n.value].double().cpu().numpy()
+        rows = rows[np.lexsort((rows[:, 1], rows[:, 0]))]
+        return rows, int(seen.value) - int(n.value)
 
     def flush_stats(self):
         """Fold the last step's pending episode statistics into ep_stats."""

@@ -997,6 +997,36 @@ def c1_trace(n_steps=2500, seed=0):
     return out
 
 
+# ----------------------------------------------------------------------------
+# F9: the reference's readers (tools/aggregate_data.py) on the build's log files
+# ----------------------------------------------------------------------------
+def _logs_mod():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("make_golden_logs", os.path.join(HERE, "make_golden_logs.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def aggregate_fixtures():
+    """mul_inv_aggregate (aggregate_data.py:289-353) and mul_inv_n_summary
+    (:356-447) of the reference, run on log files the build wrote: the arrays the
+    reference's figure scripts (scripts/gen_figures.py:344-359) would plot."""
+    import main as ref_main
+    from tools import aggregate_data as ag
+
+    ml = _logs_mod()
+    ml.write_build_logs(".")
+    agg = ag.mul_inv_aggregate([8, 9, 10], 1, ref_main.gym_envs, dict(ml.AGG_INPUTS))
+    summ = ag.mul_inv_n_summary(dict(ml.AGG_INPUTS), agg)
+    names = ["reward", "lev", "stop", "reten", "loss", "tail", "shadow", "cmax", "keqv", "lev_sh"]
+    out = {"aggregate": agg}
+    for n, v in zip(names, summ):
+        out["summary_" + n] = np.asarray(v, dtype=np.float64)
+    return out
+
+
 def main():
     work = tempfile.mkdtemp(prefix="rlmd_golden_")
     os.chdir(work)  # the reference creates ./results/... relative to cwd
@@ -1014,6 +1044,7 @@ def main():
         "learn.npz": learn_fixtures,
         "lev.npz": lev_fixtures,
         "c1_trace.npz": c1_trace,
+        "aggregate.npz": aggregate_fixtures,
     }
     only = sys.argv[1:]
     for fn, job in jobs.items():

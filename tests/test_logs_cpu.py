@@ -3,6 +3,8 @@
 save_directory / multi_log_dim / market_log_dim vs the reference's own
 tools/utils.py outputs (tests/golden/logs.npz); ExperimentLog array shapes,
 row layout and the reference's trial truncation (rl_multiplicative.py:437-450)."""
+import os
+
 import numpy as np
 
 from rlmd_amd import logs
@@ -57,3 +59,37 @@ def test_env_ids_follow_reference_naming():
     assert env_id("dice_sh", "INSURED") == "Dice_SH_INSURED_n1"
     assert env_id("dice_sh", "B") == "Dice_SH_InvB_n1"
     assert env_id("market", "B", obs_days=5) == "SNP_InvB_D5_T1"
+
+
+def test_reference_readers_accept_build_logs(golden, tmp_path, monkeypatch):
+    """tests/golden/aggregate.npz holds what the reference's own readers
+    (tools/aggregate_data.py:289-447: mul_inv_aggregate + mul_inv_n_summary, the
+    inputs of scripts/gen_figures.py:344-359) returned on log files written by
+    this build's run_experiment (make_golden.write_build_logs: Coin_InvA/B/C,
+    deterministic stub trainer).  Rewriting those files now must give the same
+    arrays the readers consumed: eval || eval_risk per investor, and the summary's
+    reward / leverage / loss / tail / shadow columns at the readers' offsets."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("mg", os.path.join(os.path.dirname(__file__), "golden",
+                                                                     "make_golden_logs.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    monkeypatch.chdir(tmp_path)
+    paths = mg.write_build_logs(".")
+    g = golden("aggregate.npz")
+    agg = g["aggregate"]
+    n_eval, n_tr = mg.AGG_INPUTS["n_eval"], mg.AGG_INPUTS["n_trials"]
+    for i, p in enumerate(paths):
+        ev, rk = np.load(p + "_eval.npy"), np.load(p + "_eval_risk.npy")
+        both = np.concatenate([ev, rk], axis=3)
+        np.testing.assert_array_equal(agg[i, :, :, :, 1:both.shape[3]], both[..., 1:])  # col 0: wall time
+        for t in range(ev.shape[1]):
+            for n in range(n_tr):
+                sl = slice(n * n_eval, (n + 1) * n_eval)
+                np.testing.assert_array_equal(g["summary_reward"][i, t, sl], ev[n, t, :, 1])
+                np.testing.assert_array_equal(g["summary_lev"][i, t, sl], rk[n, t, :, 3])
+                np.testing.assert_array_equal(g["summary_loss"][i, t, 2 * n:2 * n + 2], ev[n, t, 0, 3:5])
+                np.testing.assert_array_equal(g["summary_tail"][i, t, 2 * n:2 * n + 2], ev[n, t, 0, 11:13])
+                np.testing.assert_array_equal(g["summary_shadow"][i, t, 2 * n:2 * n + 2], ev[n, t, 0, 9:11])
+    assert np.all(np.isfinite(g["summary_keqv"]))  # the reference's equivalence solver ran on them

@@ -51,29 +51,7 @@ def test_single_rank_no_collective():
     assert t_max == 2.0 and slab.shape == (1, 5) and slab[0, 4] == 10.0
 
 
-class _StubTrainer:
-    """CPU stand-in for VecTrainer with seed-determined outputs (the sharding and
-    the gather are what is under test)."""
-
-    def __init__(self, seed):
-        self.seed, self.t = seed, 0
-
-    def step(self):
-        self.t += 1
-
-    def flush_stats(self):
-        return torch.tensor([float(self.t), 1.5 * self.t + self.seed, 10.0 * self.t, 0.0])
-
-    def last_stats(self, shadow=False):
-        import numpy as np
-
-        return np.full(16, self.seed + 0.001 * self.t)
-
-    def evaluate(self, n_eval=100, max_steps=100):
-        import numpy as np
-
-        r = np.arange(n_eval, dtype=np.float64) + 100 * self.seed
-        return {"reward": r, "steps": np.full(n_eval, 7), "risk": np.tile(r[:, None], (1, 4))}
+from tests.stub_trainer import StubTrainer as _StubTrainer  # noqa: E402
 
 
 def _exp_worker(rank, world, port, root, out):
@@ -82,7 +60,8 @@ def _exp_worker(rank, world, port, root, out):
     from rlmd_amd.experiment import run_experiment
 
     path, lg = run_experiment(env="coin", investor="A", n_trials=5, n_cumsteps=40, eval_freq=20, n_eval=6,
-                              log_every=10, seed=3, results_root=root, trainer_factory=_StubTrainer)
+                              log_every=10, seed=3, results_root=root, trainer_factory=_StubTrainer,
+                              checkpoint=False)
     out[rank] = (path, lg.trial.tolist(), lg.eval.tolist(), lg.rows.tolist())
     dist.barrier()
     dist.destroy_process_group()
@@ -102,14 +81,16 @@ def test_run_experiment_trial_shards_world2_gloo(tmp_path):
         mp.spawn(_exp_worker, args=(world, port, str(tmp_path / "mr"), out), nprocs=world, join=True)
         res = dict(out)
     _, ref = run_experiment(env="coin", investor="A", n_trials=5, n_cumsteps=40, eval_freq=20, n_eval=6,
-                            log_every=10, seed=3, results_root=str(tmp_path / "one"), trainer_factory=_StubTrainer)
+                            log_every=10, seed=3, results_root=str(tmp_path / "one"), trainer_factory=_StubTrainer,
+                            checkpoint=False)
     for rank in range(world):
         path, trial, ev, rows = res[rank]
         np.testing.assert_array_equal(np.array(trial, np.float32)[..., 1:], ref.trial[..., 1:])
         np.testing.assert_array_equal(np.array(ev, np.float32)[..., 1:], ref.eval[..., 1:])
-        assert rows == ref.rows.tolist() == [4] * 5
-    assert np.array(res[0][2])[4, 1, 0, 1] == 100 * (3 + 4)  # trial 4 (rank 0) eval rewards
-    assert np.array(res[1][2])[3, 0, 0, 1] == 100 * (3 + 3)  # trial 3 came from rank 1
+        assert rows == ref.rows.tolist() == [8] * 5  # 4 drains x 2 episodes
+    # eval reward of episode 0 at step 20 / 40 is 1 + 0.001 (100 seed + step), seed = 3 + trial
+    assert np.array(res[0][2])[4, 1, 0, 1] == np.float32(1 + 0.001 * (100 * 7 + 40))  # trial 4 (rank 0)
+    assert np.array(res[1][2])[3, 0, 0, 1] == np.float32(1 + 0.001 * (100 * 6 + 20))  # trial 3 came from rank 1
     assert os.path.exists(res[0][0] + "_trial.npy")
     saved = np.load(res[0][0] + "_eval.npy")
     np.testing.assert_array_equal(saved[..., 1:], ref.eval[..., 1:])

@@ -66,6 +66,7 @@ def test_warmup_steps_fill_ring_like_oracle(golden, dev, env, inv, fam, oinv, n)
                     device=dev, **kw)
     ora = oe.OracleVecEnv(fam, oinv, N, n, seed=seed, **kw)
     obs = ora.reset()
+    tr.episode_log(64)  # per-episode rows, drained every step (at most 64 per wave per step)
     absw = fam not in (oe.GBM, oe.MARKET)
     at = 1e-45 if fam == oe.MARKET else 1e-30  # market states are O(1e-30) (MAX_VALUE 1e34)
     length = np.ones(N, dtype=np.int64)  # current episode's step index (the env's t)
@@ -73,7 +74,7 @@ def test_warmup_steps_fill_ring_like_oracle(golden, dev, env, inv, fam, oinv, n)
     for t in range(T):
         tr.step()
         a = warmup_actions(seed, N, ora.A, t, absw)
-        ns, r, d, _ = ora.step(a)  # float64 actions, as action_space.sample() gives
+        ns, r, d, risk = ora.step(a)  # float64 actions, as action_space.sample() gives
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
         np.testing.assert_array_equal(a_r, a.astype(np.float32), err_msg=f"t={t} actions")
         np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s")
@@ -82,6 +83,14 @@ def test_warmup_steps_fill_ring_like_oracle(golden, dev, env, inv, fam, oinv, n)
         np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
         obs = ns.copy()
         m = d[:, 0]
+        rows, dropped = tr.drain_episodes()
+        assert dropped == 0
+        lanes = np.nonzero(m)[0]
+        np.testing.assert_array_equal(rows[:, 1], lanes, err_msg=f"t={t} finished lanes")
+        assert np.all(rows[:, 0] == rows[0, 0]) if len(rows) else True
+        np.testing.assert_array_equal(rows[:, 2], r[m].astype(np.float32), err_msg=f"t={t} final rewards")
+        np.testing.assert_array_equal(rows[:, 3], length[m], err_msg=f"t={t} lengths")
+        np.testing.assert_allclose(rows[:, 4:], risk[m].astype(np.float32), rtol=1e-6, atol=0, err_msg=f"t={t} risk")
         exp_n += int(m.sum())
         exp_r += float(r[m].sum())
         exp_l += float(length[m].sum())
@@ -286,8 +295,19 @@ def test_run_experiment_writes_reference_logs(dev, tmp_path):
     assert path.endswith("Coin_InvB_n1--M_SAC-N_MSE-E_B81e2_M1_S12e0_N2")
     tr = np.load(path + "_trial.npy")
     ev = np.load(path + "_eval.npy")
-    assert tr.shape == (2, 12, 19) and ev.shape == (2, 2, 20, 20)
+    trk = np.load(path + "_trial_risk.npy")
+    # one trial row per finished episode (rl_multiplicative.py:400-414), truncated to
+    # the longer trial
+    assert tr.shape[0] == 2 and tr.shape[2] == 19 and trk.shape[:2] == tr.shape[:2] and trk.shape[2] == 5
+    assert tr.shape[1] == lg.rows.max() and lg.rows.min() > 0
+    for t in range(2):
+        k = int(lg.rows[t])
+        assert np.all((tr[t, :k, 2] >= 1) & (tr[t, :k, 2] <= 12)) and np.all(tr[t, :k, 0] > 0)
+        assert np.all(tr[t, k:] == 0)
+        assert np.all(np.isfinite(trk[t, :k]))  # each episode's own last risk vector
+        assert np.all(trk[t, :k, 0] == tr[t, :k, 1])  # risk[0] is the final reward (the score)
+        assert np.isfinite(tr[t, k - 1, 3])  # learning from step 4 (mem_idx > batch)
+    assert ev.shape == (2, 2, 20, 20)
     assert np.load(path + "_eval_risk.npy").shape == (2, 2, 20, 5)
     assert (ev[:, :, :, 19] == np.array([5, 10])[None, :, None]).all()
     assert (ev[..., 2] >= 1).all() and (ev[..., 2] <= 30).all()
-    assert np.isfinite(tr[:, 4:, 3]).all()  # learning from step 4 (mem_idx > batch)

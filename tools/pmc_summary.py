@@ -10,6 +10,7 @@ separate FETCH_SIZE and WRITE_SIZE passes.  Units and gfx950 corrections
 half the bytes of wide coalesced reads on gfx950, so it is doubled.
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -27,6 +28,31 @@ def counter(path, name, kernel="env_train_kernel"):
                 vals.append(float(row["Counter_Value"]))
                 grids.add(int(row["Grid_Size"]))
     return vals, grids
+
+
+def mfma_summary(path, stat_rows, dst):
+    """MFMA utilisation per learn / acting kernel from one --pmc pass:
+    SQ_VALU_MFMA_BUSY_CYCLES (cycles a SIMD's MFMA pipe is busy, summed over the
+    chip) / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs): the fraction of the chip's
+    MFMA pipe-cycles used while the kernel ran."""
+    per = {}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            m = re.search(r"(\w+_kernel)", row["Kernel_Name"])
+            k = m.group(1) if m else row["Kernel_Name"][:60]
+            d = per.setdefault(k, {}).setdefault(row["Dispatch_Id"], {})
+            d[row["Counter_Name"]] = d.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+    out = {}
+    for k, ds in per.items():
+        busy = statistics.median(d.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for d in ds.values())
+        gui = statistics.median(d.get("GRBM_GUI_ACTIVE", 0.0) for d in ds.values())
+        sq = statistics.median(d.get("SQ_BUSY_CYCLES", 0.0) for d in ds.values())
+        out[k] = {"dispatches": len(ds), "mfma_busy_cycles": busy, "grbm_gui_active": gui, "sq_busy_cycles": sq,
+                  "mfma_util": busy / (gui / 8.0 * 1024.0) if gui else None}
+    out["_method"] = ("medians over dispatches; mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 "
+                      "SIMDs); GRBM_GUI_ACTIVE is summed over the 8 XCDs by rocprofv3 (MI355X_MICROARCH.md)")
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps(out, indent=1))
 
 
 def main(tag):
@@ -54,6 +80,9 @@ def main(tag):
            "method": "median over launches of separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes; KiB x 1024; "
                      "FETCH_SIZE doubled (gfx950 half-count of wide coalesced reads)"}
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc_env.json"), "w"), indent=1)
+    mf = os.path.join(src, "mfma", "mfma_counter_collection.csv")
+    if os.path.exists(mf):
+        mfma_summary(mf, rows, os.path.join(dst, f"{tag}_pmc_mfma.json"))
     print(json.dumps(out, indent=1))
     print("\n".join(lines[:14]))
 
