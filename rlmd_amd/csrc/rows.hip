@@ -427,27 +427,70 @@ __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>
   __syncthreads();
 }
 
+// Head biases of the policy for A <= 2, loaded by the sampling threads with the
+// kernel's first load round: read at sampling time they would wait behind the
+// whole fragment stream (vmcnt retires in issue order).
+struct HeadBias {
+  float mu[2], ls[2];
+};
+__device__ __forceinline__ HeadBias head_bias(const float* p, const NetOff& ao, const RowDims& d) {
+  HeadBias hb{{0.f, 0.f}, {0.f, 0.f}};
+  if ((int)threadIdx.x < R) {
+    const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(p, ao.size * 4);
+    const bool sac = d.algo == RLMD_SAC;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      hb.mu[j] = rlmd_ldf(rp, ao.b3 + j, j < d.A);
+      hb.ls[j] = rlmd_ldf(rp, ao.b4 + j, sac && j < d.A);
+    }
+  }
+  return hb;
+}
+
+// The policy noise of a row's first two components (Philox -> f64 Box-Muller /
+// Laplace uniform), drawn at kernel start: it depends on nothing computed, and
+// its f64 log / sincospi chain then overlaps the fragment loads instead of
+// sitting between the two MLPs of the target path.
+struct Noise2 {
+  float v[2];
+};
+__device__ __forceinline__ Noise2 noise_pre(const SampleCfg& smp, const RowDims& d, int tag, int row0) {
+  Noise2 n{{0.f, 0.f}};
+  const int r = threadIdx.x;
+  if (r < R && row0 + r < d.B) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      if (j < d.A) n.v[j] = policy_draw(smp.dist, smp.seed, (uint32_t)(row0 + r), smp.ctr, (uint32_t)tag, j);
+  }
+  return n;
+}
+
 // Policy sample per row from hout (mu | log_scale without biases): writes the
 // action into xs[:, S:S+A] and xa_out (nullable).  Same arithmetic as
-// learn.hip's actor_head_kernel.  mode 0 stochastic, 1 deterministic.
+// learn.hip's actor_head_kernel.  mode 0 stochastic, 1 deterministic.  hb: the
+// head biases preloaded (A <= 2) when has_hb, else read here.
 __device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, const SampleCfg& smp, float* xs,
                             int ldx, const float* hout, int mode, int tag, const float* eps_in, float noise_std,
                             float noise_clip, int clamp_noise, float* logp_out, float* save, float* xa_out, int row0,
-                            int B) {
+                            int B, HeadBias hbv = HeadBias{{0.f, 0.f}, {0.f, 0.f}}, bool has_hb = false,
+                            Noise2 nz2 = Noise2{{0.f, 0.f}}, bool has_nz = false) {
   const int r = threadIdx.x;
   if (r >= R) return;
   const int S = d.S, A = d.A, b = row0 + r;
   const bool valid = b < B, sac = d.algo == RLMD_SAC;
   const uint32_t c1 = smp.ctr;
   float lp_sum = 0.f, m2_sum = 0.f, hld_sum = 0.f, jac_sum = 0.f;
+  const bool pre = has_hb && A <= 2;
   for (int j = 0; j < A; ++j) {
-    const float mu = hout[r * kHeadsMax + j] + p[ao.b3 + j];
+    const float mu = hout[r * kHeadsMax + j] + (pre ? (j == 0 ? hbv.mu[0] : hbv.mu[1]) : p[ao.b3 + j]);
     float noise = 0.f;
     if (mode == 0 && valid)
-      noise = eps_in ? eps_in[(int64_t)b * A + j] : policy_draw(smp.dist, smp.seed, (uint32_t)b, c1, (uint32_t)tag, j);
+      noise = eps_in ? eps_in[(int64_t)b * A + j]
+                     : (has_nz && A <= 2 ? (j == 0 ? nz2.v[0] : nz2.v[1])
+                                         : policy_draw(smp.dist, smp.seed, (uint32_t)b, c1, (uint32_t)tag, j));
     float act;
     if (sac) {
-      const float ls_raw = hout[r * kHeadsMax + A + j] + p[ao.b4 + j];
+      const float ls_raw = hout[r * kHeadsMax + A + j] + (pre ? (j == 0 ? hbv.ls[0] : hbv.ls[1]) : p[ao.b4 + j]);
       const PolicyComp pc = policy_comp(smp.dist, mu, ls_raw, noise, smp.ls_min, smp.ls_max);
       if (mode == 1) {
         act = tanhf(pc.mu) * smp.max_action;
@@ -547,12 +590,15 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     const RowNet& an = a.tactor;
     const RowNet& cn = a.tcrit[job];
     const StageReg sr = stage_issue(a.s2, d.S, L.ldx, row0, B);
+    const HeadBias hb = head_bias(an.p, a.ao, d);
+    const bool pre_nz = a.eps_next == nullptr;
     FwdConst<NBW> ka, kc;
     actor_const<NBW>(ka, an, a.ao, d);
     Pre<PREC, NBW, MULTI> pa, pc;
     pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
     critic_const<NBW>(kc, cn, a.co, d);
     pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    const Noise2 nz = pre_nz ? noise_pre(a.smp, d, a.t_tag, row0) : Noise2{{0.f, 0.f}};
     RLMD_TSR(16 * job + 1);
     stage_commit(sr, a.s2, d.S, xs, L.ldx, row0, B);
     __syncthreads();
@@ -561,7 +607,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
                                d.A, smem, L, nullptr, nullptr, row0, B);
     RLMD_TSR(16 * job + 3);
     sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, 0, a.t_tag, a.eps_next, a.t_noise_std, a.t_noise_clip,
-                a.t_clamp, job == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B);
+                a.t_clamp, job == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz, pre_nz);
     __syncthreads();
     RLMD_TSR(16 * job + 4);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
@@ -587,10 +633,13 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)
     const RowNet& an = a.actor;
     const StageReg sr = stage_issue(a.s, d.S, L.ldx, row0, B);
+    const HeadBias hb = head_bias(an.p, a.ao, d);
     FwdConst<NBW> ka;
     actor_const<NBW>(ka, an, a.ao, d);
     Pre<PREC, NBW, MULTI> pa;
     pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
+    const bool pre_nz = a.eps_cur == nullptr && a.a_mode == 0;
+    const Noise2 nz = pre_nz ? noise_pre(a.smp, d, a.a_tag, row0) : Noise2{{0.f, 0.f}};
     stage_commit(sr, a.s, d.S, xs, L.ldx, row0, B);
     __syncthreads();
     for (int e = threadIdx.x; e < R * d.S; e += NT) {
@@ -600,7 +649,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
                                d.A, smem, L, a.h1a, a.h2a, row0, B, a.am1, a.am2);
     sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, a.a_mode, a.a_tag, a.eps_cur, 0.f, 0.f, 0, a.logp, a.save,
-                a.xsan, row0, B);
+                a.xsan, row0, B, hb, true, nz, pre_nz);
   }
 }
 
@@ -1007,30 +1056,49 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
       wl[j] = few && sac && j < A ? rlmd_ldf(rp, ao.w4 + (int64_t)j * ao.h2 + m.c, cin) : 0.f;
     }
   }
+  // the sampling save rows (A <= 2: registers) before the masks and fragments, so
+  // the sampling backward waits on them alone (vmcnt retires in issue order)
+  const int r = threadIdx.x;
+  float svr[5][2];  // [mu, sigma, c, u, log_scale] x action j
+  {
+    const bool few = A <= 2, own = r < R && row0 + r < B;
+    const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc(a.save, (int64_t)B * 5 * A * 4);
+#pragma unroll
+    for (int q = 0; q < 5; ++q)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        svr[q][j] = rlmd_ldf(rs, (int64_t)(row0 + r) * 5 * A + q * A + j, few && own && j < A);
+  }
   bwd_mask<NBW>(ka, a.am1, a.am2, nullptr, ao, row0, B);
   Pre<PREC, NBW, MULTI>& pa = p0;  // reuse the first critic's fragment registers
   pre_issue<PREC, NBW, MULTI>(pa, a.actor.wt, H2p, H2p, H1p / 16);
-  const int r = threadIdx.x;
   if (r < R) {
     const int b = row0 + r;
     if (b < B) {
       const float* sv = a.save + (int64_t)b * 5 * A;
-      for (int j = 0; j < A; ++j) {
+      auto one = [&](int j, float mu, float sg, float c, float u, float ls) {
         const float da = hout[r * kHeadsMax + j];
         if (sac) {
           float dmu, dls;
-          policy_comp_bwd(a.smp.dist, sv[j], sv[A + j], sv[2 * A + j], sv[3 * A + j], sv[4 * A + j], da,
-                          dlogp_r[r], a.smp.max_action, a.smp.reparam_noise, a.smp.ls_min, a.smp.ls_max, dmu, dls);
+          policy_comp_bwd(a.smp.dist, mu, sg, c, u, ls, da, dlogp_r[r], a.smp.max_action, a.smp.reparam_noise,
+                          a.smp.ls_min, a.smp.ls_max, dmu, dls);
           ghs[r * kHeadsMax + j] = dmu;
           ghs[r * kHeadsMax + A + j] = dls;
           a.gh[(int64_t)b * 2 * A + j] = dmu;
           a.gh[(int64_t)b * 2 * A + A + j] = dls;
         } else {
-          const float t = tanhf(sv[j]);
+          const float t = tanhf(mu);
           const float dpre = da * a.smp.max_action * (1.f - t * t);
           ghs[r * kHeadsMax + j] = dpre;
           a.gh[(int64_t)b * 2 * A + j] = dpre;
         }
+      };
+      if (A <= 2) {  // the preloaded registers, constant indices
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          if (j < A) one(j, svr[0][j], svr[1][j], svr[2][j], svr[3][j], svr[4][j]);
+      } else {
+        for (int j = 0; j < A; ++j) one(j, sv[j], sv[A + j], sv[2 * A + j], sv[3 * A + j], sv[4 * A + j]);
       }
     } else {
       for (int j = 0; j < 2 * A; ++j) ghs[r * kHeadsMax + j] = 0.f;

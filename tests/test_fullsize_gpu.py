@@ -1,0 +1,89 @@
+"""The BASELINE configs at their full sizes (GPU).
+
+C2 exactly as bench.py runs it: 65,536 GBM_InvA lanes, SAC 256/256 in bf16,
+a 1,048,576-transition ring (16 vector steps: it wraps during the test), K = 8
+updates of B = 512 per vector step.  Every step's 65,536 new ring rows (the
+actions the env received, its rewards, next states and learn_done flags) are
+replayed through the oracle env with the same Philox draws: f32-exact.  After
+the run: learn counter = steps x K, status word clear, finite statistics.
+
+C5's ring: 16,777,216 transitions (256 per lane over 65,536 lanes), n = 5
+step returns (dynamics A), TD3 400/300 acting; 250 vector steps fill 16.4M
+rows without overwriting (the reference requires buffer >= cumulative steps,
+tools/replay.py:163).  For 256 lanes spread over the whole ring, every row's
+n-step gather (eff, initial state / action, discounted return) is compared with
+oracle/replay.MultiStepRing fed those lanes' raw rows: bit-exact / f32.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import envs as oe
+from oracle.replay import MultiStepRing
+from tests.test_train_gpu import read_ring
+
+pytestmark = pytest.mark.gpu
+
+
+def test_c2_full_size_ring_and_learner(dev):
+    from rlmd_amd.trainer import VecTrainer
+
+    N, T, K, seed = 65536, 20, 8, 420
+    tr = VecTrainer("gbm", "A", N, algo="SAC", k_updates=K, replay_capacity=1 << 20, seed=seed, warmup_steps=0,
+                    smoothing_window=0, precision="bf16", device=dev, init_seed=seed)
+    ora = oe.OracleVecEnv(oe.GBM, oe.INV_A, N, 1, seed=seed)
+    obs = ora.reset()
+    cap = 1 << 20
+    for t in range(T):
+        tr.step()
+        s_r, a_r, r_r, s2_r, d_r = read_ring(tr, (t * N) % cap, N)
+        ns, r, d, _ = ora.step(a_r.astype(np.float32))  # policy actions: f32 (NumPy-2 dtype flow)
+        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s")
+        np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6, err_msg=f"t={t} r")
+        np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s2")
+        np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
+        obs = ns.copy()
+        m = d[:, 0]
+        if m.any():
+            obs[m] = ora.reset(m)[m]
+    assert np.abs(a_r).max() <= 0.99 and np.unique(a_r).size > N // 2  # stochastic policy actions
+    sc = tr.agent.scalars()
+    assert sc["learn_step_cntr"] == T * K and sc["nan_flag"] == 0
+    assert tr.agent.status()[0] == 0  # no NaN flag (nan_update -1: never set)
+    st = tr.last_stats()
+    assert np.all(np.isfinite(st[[0, 1, 2, 3, 4, 5, 10, 11]])), st
+    assert tr.replay.mem_idx == T * N
+
+
+def test_c5_full_ring_multistep_gathers(dev):
+    from rlmd_amd.trainer import VecTrainer
+
+    N, T, n, cap = 65536, 250, 5, 1 << 24
+    tr = VecTrainer("gbm", "A", N, algo="TD3", k_updates=0, replay_capacity=cap, seed=7, warmup_steps=0,
+                    smoothing_window=0, precision="bf16", device=dev, multi_steps=n, dynamics="A")
+    lanes = np.linspace(0, N - 1, 256).astype(np.int64)
+    S, A = tr.env.state_dim, tr.env.action_dim
+    ora = MultiStepRing(256 * (cap // N), S, A, 256, n, "A", 0.99)
+    done_seen = 0
+    for t in range(T):
+        tr.step()
+        s, a, r, s2, d = read_ring(tr, t * N, N)
+        ora.insert(s[lanes], a[lanes], r[lanes], s2[lanes], d[lanes].astype(bool))
+        done_seen += int(d[lanes].sum())
+    assert tr.replay.mem_idx == T * N
+    assert done_seen > 0  # episode boundaries inside the histories
+    pos = np.arange(T)
+    rows = (pos[:, None] * N + lanes[None, :]).ravel()  # GPU row of (position p, lane)
+    orows = (pos[:, None] * 256 + np.arange(256)[None, :]).ravel()
+    S0, A0, R, S2, D, eff = (x.cpu().numpy() for x in tr.replay.gather(rows))
+    oR, oS, oA, _, _, oE = ora.gather(orows)
+    np.testing.assert_array_equal(eff, oE)
+    assert eff.min() >= 1 and eff.max() == n
+    np.testing.assert_array_equal(S0, oS.astype(np.float32))
+    np.testing.assert_array_equal(A0, oA.astype(np.float32))
+    np.testing.assert_allclose(R, oR.astype(np.float32), rtol=1e-7, atol=0)
+    # and one learner mini-batch from the full ring (TD3, B = 200, gamma^eff)
+    st = tr.agent.learn(tr.replay, 2)
+    assert np.all(np.isfinite(st.cpu().numpy()[:, [0, 1, 2, 3, 4, 5]]))
+    f, _ = tr.agent.status()
+    assert f == 0
