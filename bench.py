@@ -34,12 +34,19 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E (MI355X_MICROARCH.md)
 BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
-def env_bytes_per_step(S, A, n_assets=0):
-    """Algorithmic HBM bytes of one lane-step of the fused env kernel:
+def env_bytes_per_step(S, A, n_assets=0, fused=False):
+    """Algorithmic HBM bytes of one lane-step of the env step + replay insert:
     action read 4A + obs read 4S + wealth/time read+write 24 + obs write 4S
     + replay row (s 4S, a 4A, r 4, s' 4S, done 1)  = 8A + 16S + 29;
-    market adds the two f64 price gathers per asset (P_t, P_0): 16 n_assets."""
-    return 8 * A + 16 * S + 29 + 16 * n_assets
+    market adds the two f64 price gathers per asset (P_t, P_0): 16 n_assets.
+    Fused into the acting kernel the action never leaves registers (no 4A read):
+    16S + 4A + 29."""
+    return (4 if fused else 8) * A + 16 * S + 29 + 16 * n_assets
+
+
+def act_flops_per_row(S, A, H1, H2, algo):
+    """Policy forward MACs x 2 per acting row (heads: mu + log-scale for SAC)."""
+    return 2.0 * (S * H1 + H1 * H2 + (2 if algo == "SAC" else 1) * A * H2)
 
 
 def sac_update_flops(S, A, H1, H2, B):
@@ -308,6 +315,7 @@ def main():
     cnt = (C.c_int64 * 3)()
     _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
     _abi.check(_abi.lib().rlmd_profile_enable(0))
+    fused = bool(_abi.lib().rlmd_train_last_fused())
     # evaluation (eval_multiplicative / eval_market, 100 episodes) every eval_every
     # vector steps, timed on its own and amortised into the timed region
     ev = (lambda: tr.evaluate_market(n_eval=100, test_days=250)) if cfg["env"] == "market" else \
@@ -352,13 +360,64 @@ def main():
     env_ms = ms[1] / max(cnt[1], 1)
     learn_ms = ms[2] / max(cnt[2], 1)
     act_ms = ms[0] / max(cnt[0], 1)
-    env_bytes = env_bytes_per_step(S, A, cfg["n"] if cfg["env"] == "market" else 0) * N
-    achieved = env_bytes / (env_ms * 1e-3) / 1e9
+    n_assets = cfg["n"] if cfg["env"] == "market" else 0
     pmc = load_traffic()
     traffic = None
     if pmc and pmc.get("lanes") == N and pmc.get("config", "c2") == args.config:
         traffic = pmc.get("hbm_bytes_per_launch")
     H1, H2 = tr.agent.h1, tr.agent.h2
+    lib = _abi.lib()
+    if fused:
+        # the env step lives in the acting kernel's epilogue: its cost is the fused
+        # kernel minus the standalone acting kernel on the same rows (both timed by
+        # events attached to the kernels' own dispatches), and, for comparison, the
+        # separate env kernel of unfused steps
+        fused_ms = env_ms
+        _abi.check(lib.rlmd_profile_enable(1))
+        for i in range(20):
+            tr.agent.act(tr.obs, mode=0, noise_ctr=1_000_000 + i, out=tr.actions)
+        _abi.check(lib.rlmd_profile_read(ms, cnt))
+        act_only_ms = ms[0] / max(cnt[0], 1)
+        _abi.check(lib.rlmd_train_set_fused(0))
+        _abi.check(lib.rlmd_profile_enable(1))
+        for _ in range(10):
+            tr.step()
+        _abi.check(lib.rlmd_profile_read(ms, cnt))
+        _abi.check(lib.rlmd_profile_enable(0))
+        _abi.check(lib.rlmd_train_set_fused(1))
+        sep_env_ms = ms[1] / max(cnt[1], 1)
+        env_bytes = env_bytes_per_step(S, A, n_assets, fused=True) * N
+        marginal_ms = max(fused_ms - act_only_ms, 1e-6)
+        achieved = env_bytes / (marginal_ms * 1e-3) / 1e9
+        sep_bytes = env_bytes_per_step(S, A, n_assets) * N
+        act_fl = act_flops_per_row(S, A, H1, H2, cfg["algo"]) * N
+        roofline = {"kernel": "act_env_kernel: env step + replay insert + auto-reset in the acting kernel's epilogue",
+                    "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes_per_launch": env_bytes,
+                    "avg_launch_ms": marginal_ms,
+                    "timing": "marginal: act_env_kernel (kernel-attached HIP events, every timed step) minus the "
+                              "standalone fused acting kernel on the same rows (kernel-attached events, 20 launches)",
+                    "fused_kernel_ms": fused_ms, "act_only_kernel_ms": act_only_ms,
+                    "separate_env_kernel": {"avg_launch_ms": sep_env_ms, "algorithmic_bytes_per_launch": sep_bytes,
+                                            "achieved": sep_bytes / (sep_env_ms * 1e-3) / 1e9,
+                                            "frac": sep_bytes / (sep_env_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                            "note": "env_train_kernel of unfused steps (RLMD_NO_FUSED_ENV path), 10 "
+                                                    "steps after the timed region"}}
+        roofline_fused = {"kernel": "act_env_kernel (whole kernel)", "bound": "mfma",
+                          "achieved": act_fl / (fused_ms * 1e-3) / 1e12, "peak": BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                          "frac": act_fl / (fused_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, "avg_launch_ms": fused_ms,
+                          "algorithmic_flops_per_launch": act_fl,
+                          "hbm_GBs": (env_bytes + 0.0) / (fused_ms * 1e-3) / 1e9}
+    else:
+        env_bytes = env_bytes_per_step(S, A, n_assets) * N
+        achieved = env_bytes / (env_ms * 1e-3) / 1e9
+        roofline = {"kernel": "env_train_kernel (fused env step + replay insert + reset)",
+                    "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms,
+                    "timing": "HIP events attached to every env_train_kernel dispatch of the timed region "
+                              "(hipExtLaunchKernelGGL start/stop: the dispatch's own begin/end)"}
+        roofline_fused = None
     upd = sac_update_flops if cfg["algo"] == "SAC" else td3_update_flops
     flops = K * upd(S, A, H1, H2, tr.batch)
     mfma_tf = flops / (learn_ms * 1e-3) / 1e12 if learn_ms > 0 else None
@@ -375,16 +434,13 @@ def main():
                        "lanes_per_gpu": N, "global_lanes": N * world, "k_updates_per_vector_step": K,
                        "mini_batch": tr.batch, "topk": tr.topk, "utd_updates_per_env_step": K / N,
                        "parallelism": f"independent seeds x{world} (no data-path collective)",
+                       "fused_act_env": fused,
                        "phase_ms_per_step": {"act": act_ms, "env_kernel": env_ms, "learn_k": learn_ms}},
             "updates_per_s": K * args.steps * world / t_max,
             "k_sweep": sweep,
             "fp32_companion": companion,
-            "roofline": {"kernel": "env_train_kernel (fused env step + replay insert + reset)",
-                         "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms,
-                         "timing": "HIP events attached to every env_train_kernel dispatch of the timed region "
-                                   "(hipExtLaunchKernelGGL start/stop: the dispatch's own begin/end)"},
+            "roofline": roofline,
+            "roofline_fused_kernel": roofline_fused,
             "roofline_mfma": {"kernel": f"learn phase (K {cfg['algo']} updates, all kernels)", "bound": "mfma",
                               "achieved": mfma_tf, "peak": BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3,
                               "unit": "TFLOP/s", "frac": (mfma_tf or 0) / (BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3),

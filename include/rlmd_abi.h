@@ -276,6 +276,11 @@ int rlmd_status_poll(rlmd_agent_t ag, int32_t* flags_host, int32_t* nan_update_h
 
 /* Device scalars: [cauchy_1, cauchy_2, log_alpha, learn_step_cntr, nan_flag]. */
 int rlmd_agent_scalars(rlmd_agent_t ag, double* out_host5);
+/* The host wrote parameters (or targets) through the tensors it handed to
+ * rlmd_agent_create (load_models, a state_dict copy): the next act / learn call
+ * re-derives the bf16 / f32 MFMA compute copies from them.  The optimiser keeps
+ * the copies current otherwise, so they are not rebuilt every step. */
+int rlmd_agent_params_written(rlmd_agent_t ag);
 
 /* ---------------------------------------------------------------- training */
 /* One fused vector step of rl_multiplicative.py:190-227 over all lanes:
@@ -319,11 +324,21 @@ int rlmd_train_episode_log(rlmd_env_t env, int32_t cap_per_wave);
 int rlmd_train_episode_drain(rlmd_env_t env, float* out_dev, int64_t out_cap, int64_t* n_out_host,
                              int64_t* appended_host, void* stream);
 
+/* Post-window policy steps of rlmd_train_step run acting + env step + replay
+ * insert + reset as ONE kernel when the env / net shapes allow (one gamble,
+ * S <= 8, A <= 2, the headline nets; RLMD_NO_FUSED_ENV=1 or on = 0 here selects
+ * the separate launches).  rlmd_train_last_fused: 1 if the last step fused. */
+int rlmd_train_set_fused(int32_t on);
+int rlmd_train_last_fused(void);
+
 /* Initialise obs_dev f32 [N, S] with every lane reset (episode start). */
 int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
 
 /* Live phase timing of rlmd_train_step with HIP events recorded on the step's
  * stream around its three phases (0 acting, 1 fused env kernel, 2 learn).
+ * Phase 1 is the env kernel's own begin / end (the fused acting + env kernel
+ * when the step fused); rlmd_agent_act's fused acting kernel adds its own
+ * begin / end to phase 0.
  * enable(1) resets the counters; read() synchronises and returns the summed
  * milliseconds and the number of timed launches per phase. */
 int rlmd_profile_enable(int32_t on);

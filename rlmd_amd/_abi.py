@@ -87,11 +87,14 @@ SIGNATURES = {
     "rlmd_agent_learn": (C.c_int, [P, P, I32, P, P]),
     "rlmd_agent_learn_batch": (C.c_int, [P, P, P, P, P, P, P, P, P, P, P]),
     "rlmd_agent_scalars": (C.c_int, [P, P]),
+    "rlmd_agent_params_written": (C.c_int, [P]),
     "rlmd_status_poll": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), P]),
     "rlmd_train_step": (C.c_int, [P, P, P, C.POINTER(TrainCfg), P, P, P, P, P]),
     "rlmd_train_reset": (C.c_int, [P, P, P]),
     "rlmd_train_flush_stats": (C.c_int, [P, P]),
     "rlmd_train_episode_log": (C.c_int, [P, C.c_int32]),
+    "rlmd_train_set_fused": (C.c_int, [C.c_int32]),
+    "rlmd_train_last_fused": (C.c_int, []),
     "rlmd_train_episode_drain": (C.c_int, [P, P, C.c_int64, P, P, P]),
     "rlmd_env_lane_start": (C.c_int, [P, P]),
     "rlmd_shadow_means": (C.c_int, [P, I32, I32, C.c_float, C.c_float, P, I32, P]),

@@ -192,6 +192,12 @@ class DeviceAgent:
             sd = torch.load(f"{prefix}_{net}.pt", weights_only=True)
             for k, v in self.state_dict(net).items():
                 v.copy_(sd[k])
+        self.params_written()
+
+    def params_written(self):
+        """Call after writing parameters through state_dict() / the flat tensors:
+        the device re-derives its MFMA compute copies before the next act / learn."""
+        check(_abi.lib().rlmd_agent_params_written(self.h))
 
     def scalars(self):
         out = (C.c_double * 5)()

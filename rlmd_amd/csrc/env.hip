@@ -23,6 +23,7 @@
 // happens where NumPy's does.
 #pragma clang fp contract(off)
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 #include <hip/hip_ext.h>
 
@@ -30,6 +31,8 @@
 #include <vector>
 
 #include "../../include/rlmd_abi.h"
+#include "learn_kernels.h"
+#include "rlmd_act_rows.h"
 #include "rlmd_common.h"
 #include "rlmd_internal.h"
 
@@ -59,6 +62,21 @@ constexpr double kGbmDrift = 0.0540025395205692;
 constexpr double kGbmVol = 0.1897916175617430;
 // dice_sh: I_LEV_FACTOR = (-1 - 5) / (-0.5 - 5) (envs/dice_roll_sh_envs.py:70)
 constexpr double kShILev = (-1.0 - 5.0) / (-0.5 - 5.0);
+
+#ifdef RLMD_TIMING
+// experiment builds only (tools/ts_probe.py env): per-workgroup s_memrealtime at
+// entry / exit of env_train_kernel and act_env_kernel, and thread 0's s_memtime
+// phase stamps of block 0
+__device__ unsigned long long g_ts_env[2048][8];
+#define RLMD_TSE(i, v)                                                                  \
+  do {                                                                                  \
+    if (threadIdx.x == 0 && blockIdx.x < 2048) g_ts_env[blockIdx.x][i] = (v);           \
+  } while (0)
+#else
+#define RLMD_TSE(i, v) \
+  do {                 \
+  } while (0)
+#endif
 
 struct EnvParams {
   int fam, inv, n_lanes, n, obs_days, time_length, action_days, shuffle_days;
@@ -476,6 +494,16 @@ __global__ void __launch_bounds__(256) env_step_kernel(EnvParams P, uint32_t ste
 
 // Upper bound of the action count when it is known at compile time (dice_sh:
 // <= 4; NG > 0: NG + 2 for InvC), else 0 (read through memory per use).
+// ring row of a lane: the host hands ring_base already reduced mod capacity, so
+// one conditional subtract replaces the 64-bit remainder (a long software
+// sequence on the lane's critical path); rings smaller than the lane count wrap
+// more than once and keep the remainder
+__device__ __forceinline__ int64_t ring_row(int64_t base, int64_t lane, int64_t cap) {
+  int64_t r = base + lane;
+  if (r >= cap) r = r - cap < cap ? r - cap : r % cap;
+  return r;
+}
+
 template <int FAM, int NG>
 constexpr int kActRegs = FAM == RLMD_DICE_SH ? 4 : (NG > 0 ? NG + 2 : 0);
 
@@ -497,6 +525,8 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
                                                         double clip_hi, float* obs, rlmd::ReplayView rb,
                                                         int64_t ring_base, StatFold sf) {
   const int lane = blockIdx.x * blockDim.x + threadIdx.x;
+  RLMD_TSE(0, __builtin_amdgcn_s_memrealtime());
+  RLMD_TSE(1, __builtin_amdgcn_s_memtime());
   // block 0 folds the previous launch's per-block rows into the caller's
   // accumulator first (its rows are complete: that launch has ended)
   if (blockIdx.x == 0 && sf.fold_src) fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst);
@@ -541,7 +571,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
         return act_of(i);
       }
     };
-    const int64_t row = (ring_base + lane) % rb.capacity;
+    const int64_t row = ring_row(ring_base, lane, rb.capacity);
     // s (the current obs) goes to the ring unchanged.  gfx9 counts stores in
     // vmcnt, so a store issued before the compute would be waited on at the first
     // use of a loaded value: the first 8 obs elements are loaded now and stored
@@ -560,8 +590,14 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
         if (k0 + j < S) rb.state[row * S + k0 + j] = v[j];
     }
 
+    // the one draw of a single-gamble lane depends on (seed, lane, step) only: its
+    // Philox + f64 Box-Muller chain runs while the lane-state loads are in flight
+    constexpr bool one_draw = NG == 1 && FAM != RLMD_MARKET;
+    const double dr0 = one_draw ? philox_draw<FAM>(P, lane, step, 0) : 0.0;
+    RLMD_TSE(2, __builtin_amdgcn_s_memtime());
     StepOut o = env_step_lane<FAM, NG, AT>(
-        P, lane, w0, t, start, ep, act, [&](int j) { return philox_draw<FAM>(P, lane, step, j); },
+        P, lane, w0, t, start, ep, act,
+        [&](int j) { return one_draw ? dr0 : philox_draw<FAM>(P, lane, step, j); },
         [&](int k, double v) {
           const float f = (float)v;
           rb.next_state[row * S + k] = f;
@@ -583,6 +619,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
           }
           if (lid == __ffsll((unsigned long long)m) - 1) P.ep_cnt[lane >> 6] = ep_base + (uint32_t)__popcll(m);
         });
+    RLMD_TSE(3, __builtin_amdgcn_s_memtime());
     if (ep_slot >= 0) {
       float* er = P.ep_rows + ep_slot * P.ep_w;
       er[0] = (float)step;
@@ -606,12 +643,124 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
       P.wealth[lane] = o.W;
       P.time[lane] = t + 1;
     }
+    RLMD_TSE(4, __builtin_amdgcn_s_memtime());
   }
   // episode statistics: a fixed-order block reduction into this block's row of
   // the launch's partial buffer (plain stores; device-scope atomics on one
   // address from every wave serialise across the XCDs and cost more than the
   // whole env step)
   if (sf.part_out) {
+    __shared__ double red[3][256 / 64];
+#pragma unroll
+    for (int m = 32; m > 0; m >>= 1) {
+      st_n += __shfl_xor(st_n, m, 64);
+      st_r += __shfl_xor(st_r, m, 64);
+      st_t += __shfl_xor(st_t, m, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+      red[0][w] = st_n;
+      red[1][w] = st_r;
+      red[2][w] = st_t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+      const int q = threadIdx.x;
+      double v = 0.0;
+      for (int i = 0; i < (int)(blockDim.x >> 6); ++i) v += red[q][i];
+      sf.part_out[(int64_t)blockIdx.x * 4 + q] = v;
+    }
+  }
+  RLMD_TSE(5, __builtin_amdgcn_s_memtime());
+  RLMD_TSE(6, __builtin_amdgcn_s_memrealtime());
+}
+
+// ---------------------------------------------------------------------------
+// fused acting + env step (post-window policy steps of the training loop):
+// rlmd_act_rows.h's 64-row acting body, then, on the row's own thread, the env
+// step of env_train_kernel with the action still in registers and the
+// observation still in LDS — one launch per vector step instead of two, and the
+// actions never round-trip through HBM.  This file compiles with FP contraction
+// off (the env's NumPy rounding), so the acting body here rounds the sampler's
+// few multiply-adds separately where act.hip fuses them (<= 1 ulp of an action).
+// ---------------------------------------------------------------------------
+template <int FAM, int NG, int H1P, int NB, int SP>
+__global__ void __launch_bounds__(256) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
+                                                      float* obs, rlmd::ReplayView rb, int64_t ring_base,
+                                                      StatFold sf) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  if (blockIdx.x == 0 && sf.fold_src) fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst);
+  const int tid = threadIdx.x;
+  const int lane = blockIdx.x * rlmd::actrows::kRows + tid;  // this thread's env lane (tid < 64)
+  const bool mine = tid < rlmd::actrows::kRows && lane < P.n_lanes;
+  double w0 = 0.0, dr0 = 0.0;
+  int t = 1, start = 0;
+  uint32_t ep = 0, ep_base = 0;
+  double st_n = 0.0, st_r = 0.0, st_t = 0.0;
+  constexpr bool one_draw = NG == 1 && FAM != RLMD_MARKET;
+  // the lane state, loaded with the acting body's first load round, and the
+  // lane's draw (independent of the action: its f64 Box-Muller / uniform chain
+  // runs under the acting body instead of in the epilogue's tail)
+  auto pro = [&] {
+    if (mine) {
+      if (one_draw) dr0 = philox_draw<FAM>(P, lane, step, 0);
+      w0 = P.wealth[lane];
+      t = P.time[lane];
+      if (FAM == RLMD_MARKET) start = P.start[lane];
+      ep = P.episode[lane];
+      ep_base = P.ep_rows ? P.ep_cnt[lane >> 6] : 0u;
+    }
+  };
+  auto epi = [&](int, int b, const float* acts, const float* obs_row) {
+    const int S = P.state_dim, A = P.action_dim;
+    auto act = [&](int i) -> float { return i == 0 ? acts[0] : acts[1]; };  // A <= 2
+    const int64_t row = ring_row(ring_base, b, rb.capacity);
+    int64_t ep_slot = -1;
+    const StepOut o = env_step_lane<FAM, NG, float>(
+        P, b, w0, t, start, ep, act, [&](int j) { return one_draw ? dr0 : philox_draw<FAM>(P, b, step, j); },
+        [&](int k, double v) {
+          const float f = (float)v;
+          rb.next_state[row * S + k] = f;
+          obs[(int64_t)b * S + k] = f;
+        },
+        [&](int k, double v) {
+          if (ep_slot >= 0 && k < P.ep_w - 4) P.ep_rows[ep_slot * P.ep_w + 4 + k] = (float)v;
+        },
+        [&](const StepOut& so) {
+          if (!P.ep_rows) return;
+          const uint64_t m = __ballot(so.done);
+          if (m == 0) return;
+          const int lid = threadIdx.x & 63;
+          if (so.done) {
+            const uint32_t at = ep_base + (uint32_t)__popcll(m & ((1ull << lid) - 1ull));
+            if (at < (uint32_t)P.ep_cap) ep_slot = (int64_t)(b >> 6) * P.ep_cap + at;
+          }
+          if (lid == __ffsll((unsigned long long)m) - 1) P.ep_cnt[b >> 6] = ep_base + (uint32_t)__popcll(m);
+        });
+    if (ep_slot >= 0) {
+      float* er = P.ep_rows + ep_slot * P.ep_w;
+      er[0] = (float)step;
+      er[1] = (float)b;
+      er[2] = (float)o.reward;
+      er[3] = (float)t;
+    }
+    for (int j = 0; j < S; ++j) rb.state[row * S + j] = obs_row[j];
+    for (int i = 0; i < A; ++i) rb.action[row * A + i] = act(i);
+    rb.reward[row] = (float)o.reward;
+    rb.done[row] = o.learn_done;
+    if (rb.n_steps > 1) rlmd::ms_record(rb, b, row, o.learn_done);
+    if (o.done) {
+      st_n = 1.0;
+      st_r = o.reward;
+      st_t = (double)t;
+      env_reset_lane<FAM>(P, b, [&](int k, double v) { obs[(int64_t)b * S + k] = (float)v; });
+    } else {
+      P.wealth[b] = o.W;
+      P.time[b] = t + 1;
+    }
+  };
+  rlmd::actrows::act_rows<H1P, NB, SP>(a, smem, pro, epi);
+  if (sf.part_out) {  // the block's finished-episode statistics, as env_train_kernel
     __shared__ double red[3][256 / 64];
 #pragma unroll
     for (int m = 32; m > 0; m >>= 1) {
@@ -838,7 +987,8 @@ struct rlmd_env_s {
   // of per-block rows, the parity of the next launch, and the accumulator the
   // last launch's rows still owe (nullptr when nothing is pending)
   double* d_part = nullptr;
-  int part_rows = 0, part_parity = 0;
+  int part_rows = 0, part_parity = 0;  // part_rows: per-parity capacity (64-lane blocks)
+  int pend_rows = 0;                   // rows the pending launch wrote
   double* pending_dst = nullptr;
   // per-episode log (EnvParams::ep_rows / ep_cnt) and the drain's scratch
   int64_t* ep_offs = nullptr;
@@ -876,7 +1026,7 @@ void env_train_launch_params(rlmd_env_t env, EnvParams*& P);
 int flush_stats(rlmd_env_t env, hipStream_t stream) {
   if (!env->pending_dst) return 0;
   const double* rows = env->d_part + (size_t)(env->part_parity ^ 1) * env->part_rows * 4;
-  hipLaunchKernelGGL(stat_fold_kernel, dim3(1), dim3(256), 0, stream, rows, env->part_rows, env->pending_dst);
+  hipLaunchKernelGGL(stat_fold_kernel, dim3(1), dim3(256), 0, stream, rows, env->pend_rows, env->pending_dst);
   RLMD_LAUNCH_CHECK();
   env->pending_dst = nullptr;
   return 0;
@@ -885,10 +1035,11 @@ int flush_stats(rlmd_env_t env, hipStream_t stream) {
 int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uint32_t step,
               float* actions, int random_actions, int abs_actions, int window, double clip_lo, double clip_hi,
               float* obs, double* ep_stats, hipStream_t stream, hipEvent_t ev_start, hipEvent_t ev_stop) {
+  ring_base %= rb.capacity;
   const int N = env->P.n_lanes;
   const dim3 grid((N + 255) / 256), block(256);
   const bool f64 = window || random_actions;
-  StatFold sf{nullptr, nullptr, nullptr, env->part_rows};
+  StatFold sf{nullptr, nullptr, nullptr, env->pend_rows};
   double* const last_rows = env->d_part + (size_t)(env->part_parity ^ 1) * env->part_rows * 4;
   if (env->pending_dst && env->pending_dst != ep_stats) {  // different accumulator: settle it now
     const int r = flush_stats(env, stream);
@@ -914,7 +1065,68 @@ int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uin
 #undef TRAIN
   RLMD_LAUNCH_CHECK();
   env->pending_dst = ep_stats;
-  if (ep_stats) env->part_parity ^= 1;
+  if (ep_stats) {
+    env->part_parity ^= 1;
+    env->pend_rows = (int)grid.x;
+  }
+  return 0;
+}
+
+// the fused instantiations: one gamble / asset (market: one observed day), S <= 8,
+// A <= 2; RLMD_NO_FUSED_ENV=1 turns the fusion off (separate acting and env launches)
+int g_fuse_env = -1;  // -1: from RLMD_NO_FUSED_ENV at first use; rlmd_train_set_fused sets it
+
+bool env_act_fusable(rlmd_env_t env) {
+  const EnvParams& P = env->P;
+  if (g_fuse_env < 0) g_fuse_env = getenv("RLMD_NO_FUSED_ENV") != nullptr ? 0 : 1;
+  return g_fuse_env == 1 && P.n == 1 && (P.fam != RLMD_MARKET || P.obs_days == 1) && P.action_dim <= actrows::kMaxA &&
+         P.state_dim <= 8;
+}
+
+int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step, const FusedActArgs& a,
+                  int h1p, int nb, int sp, float* obs, double* ep_stats, hipStream_t stream, hipEvent_t ev_start,
+                  hipEvent_t ev_stop, bool* launched) {
+  *launched = false;
+  ring_base %= rb.capacity;
+  const EnvParams& P = env->P;
+  const bool shape = sp == 8 && ((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5));
+  if (!env_act_fusable(env) || !shape || a.n != P.n_lanes) return 0;
+  const int N = P.n_lanes;
+  const dim3 grid((N + actrows::kRows - 1) / actrows::kRows), block(256);
+  StatFold sf{nullptr, nullptr, nullptr, env->pend_rows};
+  double* const last_rows = env->d_part + (size_t)(env->part_parity ^ 1) * env->part_rows * 4;
+  if (env->pending_dst && env->pending_dst != ep_stats) {
+    const int r = flush_stats(env, stream);
+    if (r) return r;
+  } else if (env->pending_dst) {
+    sf.fold_src = last_rows;
+    sf.fold_dst = env->pending_dst;
+  }
+  if (ep_stats) sf.part_out = env->d_part + (size_t)env->part_parity * env->part_rows * 4;
+#define FUSED(F, H, B)                                                                                         \
+  hipExtLaunchKernelGGL((act_env_kernel<F, 1, H, B, 8>), grid, block, actrows::act_lds_bytes(H, 8), stream,    \
+                        ev_start, ev_stop, 0, a, env->P, step, obs, rb, ring_base, sf)
+#define FUSED_FAM(F)                          \
+  {                                           \
+    if (h1p == 256) FUSED(F, 256, 4);         \
+    else FUSED(F, 416, 5);                    \
+  }
+  switch (P.fam) {
+    case RLMD_COIN: FUSED_FAM(RLMD_COIN); break;
+    case RLMD_DICE: FUSED_FAM(RLMD_DICE); break;
+    case RLMD_GBM: FUSED_FAM(RLMD_GBM); break;
+    case RLMD_DICE_SH: FUSED_FAM(RLMD_DICE_SH); break;
+    default: FUSED_FAM(RLMD_MARKET); break;
+  }
+#undef FUSED_FAM
+#undef FUSED
+  RLMD_LAUNCH_CHECK();
+  env->pending_dst = ep_stats;
+  if (ep_stats) {
+    env->part_parity ^= 1;
+    env->pend_rows = (int)grid.x;
+  }
+  *launched = true;
   return 0;
 }
 
@@ -1011,7 +1223,7 @@ int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t 
   RLMD_HIP(hipMalloc(&P.time, sizeof(int32_t) * N));
   RLMD_HIP(hipMalloc(&P.start, sizeof(int32_t) * N));
   RLMD_HIP(hipMalloc(&P.episode, sizeof(uint32_t) * N));
-  e->part_rows = (int)((N + 255) / 256);
+  e->part_rows = (int)((N + 63) / 64);  // the fused kernel's 64-lane blocks; 256-lane launches use fewer
   RLMD_HIP(hipMalloc(&e->d_part, sizeof(double) * 8 * e->part_rows));
   RLMD_HIP(hipMemset(P.episode, 0xff, sizeof(uint32_t) * N));  // first reset -> episode 0
   RLMD_HIP(hipMemset(P.start, 0, sizeof(int32_t) * N));
@@ -1139,6 +1351,17 @@ int rlmd_env_lane_start(rlmd_env_t env, int32_t* start_host) {
 int rlmd_train_flush_stats(rlmd_env_t env, void* stream) {
   RLMD_CHECK(env, "null env");
   return rlmd::flush_stats(env, (hipStream_t)stream);
+}
+
+#ifdef RLMD_TIMING
+int rlmd_debug_ts_env(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_env), sizeof(unsigned long long) * 8 * n) != hipSuccess;
+}
+#endif
+
+int rlmd_train_set_fused(int32_t on) {
+  rlmd::g_fuse_env = on ? 1 : 0;
+  return 0;
 }
 
 int rlmd_train_episode_log(rlmd_env_t env, int32_t cap_per_wave) {

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "learn_kernels.h"
+#include "rlmd_act_rows.h"
 #include "rlmd_block.h"
 #include "rlmd_loss.h"
 #include "rlmd_policy.h"
@@ -273,6 +274,10 @@ struct rlmd_agent_s {
   int32_t max_tiles = 0;
   bool fuse_adam = false;
   int fuse_splits = RLMD_GRAD_SPLITS;
+  // the compute copies may differ from the f32 masters: set at creation and by
+  // rlmd_agent_params_written (host writes through the parameter tensors);
+  // the optimiser keeps them current otherwise
+  bool copies_dirty = true;
 };
 
 namespace rlmd {
@@ -428,9 +433,12 @@ RowNet row_net(rlmd_agent_s* ag, int slot) {
   return RowNet{base + off, copy_wc(ag, slot), copy_wt(ag, slot)};
 }
 
-// Re-derive every compute copy from the f32 masters (start of each learn call:
-// the host may have written parameters through the tensor views in between).
+// Re-derive every compute copy from the f32 masters when the host has written
+// parameters since the last refresh (rlmd_agent_params_written); Adam keeps
+// them current between host writes, so a clean agent skips the six copies.
 int refresh_copies(rlmd_agent_s* ag, hipStream_t st) {
+  if (!ag->copies_dirty) return 0;
+  ag->copies_dirty = false;
   CopyJob jobs[6];
   for (int slot = 0; slot < 6; ++slot) {
     const RowNet n = row_net(ag, slot);
@@ -771,20 +779,21 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
 // training step refreshes them once at its start); otherwise the actor's copy is
 // re-derived first, as the host may have written parameters since the last update.
 int agent_act(rlmd_agent_s* ag, const float* obs, int64_t n, float* actions, int mode,
-              uint64_t noise_ctr, const float* eps, hipStream_t st, bool copies_current = false) {
+              uint64_t noise_ctr, const float* eps, hipStream_t st, bool copies_current = false,
+              hipEvent_t ev_start = nullptr, hipEvent_t ev_stop = nullptr) {
   const rlmd_agent_cfg& c = ag->cfg;
   if (n <= 0) return 0;
   RLMD_CHECK(n <= INT32_MAX, "too many rows");
   static const bool fused_ok = getenv("RLMD_NO_FUSED_ACT") == nullptr;
   if (fused_ok && fused_act_supported(c)) {
-    if (!copies_current) {
+    if (!copies_current && ag->copies_dirty) {
       const RowNet an = row_net(ag, SLOT_ACTOR);
       const CopyJob job{an.p + ag->actor.w2, copy_wc(ag, SLOT_ACTOR), copy_wt(ag, SLOT_ACTOR)};
       RLMD_TRY(w2_copies_launch(&job, 1, row_dims(ag), st));
     }
     return fused_act_launch(c, obs, n, actions, ag->params + ag->off_actor, ag->actor,
                             static_cast<const unsigned short*>(copy_wc(ag, SLOT_ACTOR)), mode,
-                            c.seed ^ 0xac7ac7ac7ull, (uint32_t)noise_ctr, eps, st);
+                            c.seed ^ 0xac7ac7ac7ull, (uint32_t)noise_ctr, eps, st, ev_start, ev_stop);
   }
   if (n > ag->act_cap) {
     if (ag->act_h1) {
@@ -796,6 +805,7 @@ int agent_act(rlmd_agent_s* ag, const float* obs, int64_t n, float* actions, int
     ag->act_cap = n;
   }
   RLMD_CHECK(n <= INT32_MAX, "too many rows");
+  if (ev_start) RLMD_HIP(hipEventRecord(ev_start, st));  // the generic path: several launches
   const float* Pa = ag->params + ag->off_actor;
   const NetOff& ao = ag->actor;
   const float* x[1] = {obs};
@@ -819,7 +829,9 @@ int agent_act(rlmd_agent_s* ag, const float* obs, int64_t n, float* actions, int
     h.noise_std = c.policy_noise;
     h.clamp_noise = 0;
   }
-  return launch_head(h, st);
+  RLMD_TRY(launch_head(h, st));
+  if (ev_stop) RLMD_HIP(hipEventRecord(ev_stop, st));
+  return 0;
 }
 
 }  // namespace
@@ -991,11 +1003,16 @@ int rlmd_eval_market(rlmd_env_t env, rlmd_agent_t ag, const int32_t* start_dev, 
   return 0;
 }
 
+static int prof_pair(int phase, hipEvent_t* start, hipEvent_t* stop);
+
 int rlmd_agent_act(rlmd_agent_t ag, const float* obs, int64_t n, float* actions, int32_t mode,
                    uint64_t noise_ctr, const float* eps, void* stream) {
   RLMD_CHECK(ag && obs && actions, "null argument");
   RLMD_CHECK(mode == 0 || mode == 1, "mode must be 0 (stochastic) or 1 (deterministic)");
-  return rlmd::agent_act(ag, obs, n, actions, mode, noise_ctr, eps, (hipStream_t)stream);
+  // with rlmd_profile_enable, the fused acting kernel's own begin / end land in phase 0
+  hipEvent_t e0, e1;
+  RLMD_TRY(prof_pair(0, &e0, &e1));
+  return rlmd::agent_act(ag, obs, n, actions, mode, noise_ctr, eps, (hipStream_t)stream, false, e0, e1);
 }
 
 int rlmd_agent_learn(rlmd_agent_t ag, rlmd_replay_t rb, int32_t k, float* stats, void* stream) {
@@ -1031,6 +1048,12 @@ int rlmd_debug_ts(unsigned long long* out) {
   return 0;
 }
 #endif
+
+int rlmd_agent_params_written(rlmd_agent_t ag) {
+  RLMD_CHECK(ag, "null agent");
+  ag->copies_dirty = true;
+  return 0;
+}
 
 int rlmd_agent_scalars(rlmd_agent_t ag, double* out) {
   RLMD_CHECK(ag && out, "null argument");
@@ -1100,6 +1123,8 @@ struct PhaseProfiler {
 PhaseProfiler g_prof;
 }  // namespace
 
+static int prof_pair(int phase, hipEvent_t* start, hipEvent_t* stop) { return g_prof.pair(phase, start, stop); }
+
 int rlmd_profile_enable(int32_t on) {
   RLMD_HIP(hipDeviceSynchronize());
   g_prof.enabled = on != 0;
@@ -1123,6 +1148,12 @@ int rlmd_profile_read(double* ms_out3, int64_t* count_out3) {
   return 0;
 }
 
+namespace {
+int g_last_fused = 0;  // whether the last rlmd_train_step ran the fused acting + env kernel
+}
+
+int rlmd_train_last_fused(void) { return g_last_fused; }
+
 int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlmd_train_cfg* cfg,
                     float* obs, float* actions, double* ep_stats, float* stats, void* stream) {
   RLMD_CHECK(env && rb && cfg && obs && actions, "null argument");
@@ -1135,17 +1166,31 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
              "replay / env dims differ");
   const int64_t cs = cfg->cum_step;
   const bool random = cs < cfg->warmup_steps;
+  // action_window (tools/utils.py:345-373): only warmup < cum_step <= smoothing_window
+  const bool window = cs <= cfg->smoothing_window && cs > cfg->warmup_steps;
+  // post-window policy steps (the steady state): acting + env step in one launch
+  // (env.hip act_env_kernel) when the env / net shapes have an instantiation
+  int h1p = 0, nb = 0, sp = 0;
+  rlmd::FusedActArgs fa{};
+  bool fused = false;
+  if (!random && !window && ag && rlmd::fused_act_supported(ag->cfg) && rlmd::env_act_fusable(env)) {
+    rlmd::actrows::fused_shape(ag->cfg, h1p, nb);
+    sp = ag->cfg.state_dim <= 8 ? 8 : 16;
+    fused = sp == 8 && ((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5));
+    if (fused)
+      fa = rlmd::fused_act_args(ag->cfg, obs, N, actions, ag->params + ag->off_actor, ag->actor,
+                                (const unsigned short*)rlmd::copy_wc(ag, rlmd::SLOT_ACTOR), 0,
+                                ag->cfg.seed ^ 0xac7ac7ac7ull, (uint32_t)cs, nullptr);
+  }
   if (!random) {
     RLMD_CHECK(ag, "policy acting needs an agent");
     RLMD_TRY(g_prof.record(0, 0, st));
     // one refresh of every compute copy serves the acting and the K updates below
     RLMD_TRY(rlmd::refresh_copies(ag, st));
-    RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st, true));
+    if (!fused) RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st, true));
     RLMD_TRY(g_prof.record(0, 1, st));
   }
-  // action_window (tools/utils.py:345-373): only warmup < cum_step <= smoothing_window
   double lo = -INFINITY, hi = INFINITY;
-  const bool window = cs <= cfg->smoothing_window && cs > cfg->warmup_steps;
   if (window) {
     const double ratio = (double)cs / (double)cfg->smoothing_window;
     const double width = (sin(M_PI * (ratio - 0.5)) + 1.0) / 2.0;
@@ -1155,8 +1200,16 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   const int64_t base = rlmd::replay_mem_idx(rb);
   hipEvent_t e0, e1;
   RLMD_TRY(g_prof.pair(1, &e0, &e1));
-  RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, window ? 1 : 0,
-                           lo, hi, obs, ep_stats, st, e0, e1));
+  g_last_fused = fused ? 1 : 0;
+  if (!fused) {
+    RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, window ? 1 : 0,
+                             lo, hi, obs, ep_stats, st, e0, e1));
+  } else {
+    bool launched = false;
+    RLMD_TRY(rlmd::env_act_train(env, v, base, (uint32_t)cs, fa, h1p, nb, sp, obs, ep_stats, st, e0, e1,
+                                 &launched));
+    RLMD_CHECK(launched, "fused acting + env step: no instantiation");
+  }
   rlmd::replay_advance(rb, N);
   if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch) {
     RLMD_TRY(g_prof.record(2, 0, st));

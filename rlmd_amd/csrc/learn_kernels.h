@@ -31,6 +31,21 @@ struct NetOff {
   int64_t size;
 };
 
+// Arguments of the fused acting body (rlmd_act_rows.h, act.hip, env.hip).
+struct FusedActArgs {
+  const float* obs;             // [n, S]
+  const float* params;          // actor params (f32 masters)
+  const unsigned short* w2bf;   // fc2.weight as the bf16 compute copy [H2p][H1p], fragment-major
+  NetOff off;
+  float* actions;               // [n, A]
+  int32_t n, S, A, algo, mode, H1, H2;
+  uint64_t seed;
+  uint32_t tag, ctr;
+  const float* eps_in;          // injected noise [n, A] (nullable)
+  float max_action, ls_min, ls_max, noise_std;
+  int32_t dist;  // SAC sampler (rlmd_policy.h)
+};
+
 struct HeadArgs {
   const float* h2;      // [n, H2] actor layer-2 activations
   const float* params;  // actor params base
@@ -238,8 +253,20 @@ int w2_copies_launch(const CopyJob* jobs, int n, const RowDims& d, hipStream_t s
 // act.hip: fused bf16 acting (obs -> actions in one launch) for the headline nets;
 // w2bf = the actor's bf16 compute copy wc (fragment-major [H2p][H1p]).
 bool fused_act_supported(const rlmd_agent_cfg& c);
+FusedActArgs fused_act_args(const rlmd_agent_cfg& c, const float* obs, int64_t n, float* actions,
+                            const float* actor_params, const NetOff& off, const unsigned short* w2bf, int mode,
+                            uint64_t seed, uint32_t ctr, const float* eps);
+// env.hip: acting + env step + replay insert + auto-reset in ONE launch for the
+// post-window policy steps of rlmd_train_step (FusedActArgs of fused_act_args;
+// h1p / nb / sp: the acting shape).  Returns 1 (nothing launched) when this env /
+// net combination has no fused instantiation.
+bool env_act_fusable(rlmd_env_t env);
+int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step, const FusedActArgs& a,
+                  int h1p, int nb, int sp, float* obs, double* ep_stats, hipStream_t stream, hipEvent_t ev_start,
+                  hipEvent_t ev_stop, bool* launched);
 int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float* actions,
                      const float* actor_params, const NetOff& off, const unsigned short* w2bf, int mode,
-                     uint64_t seed, uint32_t ctr, const float* eps, hipStream_t st);
+                     uint64_t seed, uint32_t ctr, const float* eps, hipStream_t st, hipEvent_t ev_start = nullptr,
+                     hipEvent_t ev_stop = nullptr);
 
 }  // namespace rlmd

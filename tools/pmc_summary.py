@@ -70,15 +70,30 @@ def main(tag):
         n, t = int(r["Calls"]), float(r["TotalDurationNs"])
         lines.append(f"{n:6d} {t / n / 1e3:9.2f} {t / 1e6:9.3f} {100 * t / tot:6.2f}  {r['Name'][:120]}")
     open(os.path.join(dst, f"{tag}_kernel_summary.txt"), "w").write("\n".join(lines) + "\n")
-    fetch, g1 = counter(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
-    write, g2 = counter(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
-    fetch_b = 2.0 * 1024.0 * statistics.median(fetch)
-    write_b = 1024.0 * statistics.median(write)
-    out = {"kernel": "env_train_kernel", "lanes": sorted(g1 | g2)[0], "launches": [len(fetch), len(write)],
-           "fetch_bytes_per_launch": fetch_b, "write_bytes_per_launch": write_b,
-           "hbm_bytes_per_launch": fetch_b + write_b,
-           "method": "median over launches of separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes; KiB x 1024; "
-                     "FETCH_SIZE doubled (gfx950 half-count of wide coalesced reads)"}
+    fpath = os.path.join(src, "fetch", "fetch_counter_collection.csv")
+    wpath = os.path.join(src, "write", "write_counter_collection.csv")
+    per = {}
+    for k in ("act_env_kernel", "fused_act_kernel", "env_train_kernel"):
+        fetch, g1 = counter(fpath, "FETCH_SIZE", k)
+        write, g2 = counter(wpath, "WRITE_SIZE", k)
+        if fetch and write:
+            per[k] = {"launches": [len(fetch), len(write)], "grid": sorted(g1 | g2)[0],
+                      "fetch_bytes": 2.0 * 1024.0 * statistics.median(fetch),
+                      "write_bytes": 1024.0 * statistics.median(write)}
+            per[k]["hbm_bytes"] = per[k]["fetch_bytes"] + per[k]["write_bytes"]
+    if "act_env_kernel" in per and "fused_act_kernel" in per:
+        a, b = per["act_env_kernel"], per["fused_act_kernel"]
+        out = {"kernel": "act_env_kernel - fused_act_kernel (the env step's marginal traffic)",
+               "lanes": a["grid"] // 4, "hbm_bytes_per_launch": a["hbm_bytes"] - b["hbm_bytes"],
+               "fetch_bytes_per_launch": a["fetch_bytes"] - b["fetch_bytes"],
+               "write_bytes_per_launch": a["write_bytes"] - b["write_bytes"], "per_kernel": per}
+    else:
+        e = per["env_train_kernel"]
+        out = {"kernel": "env_train_kernel", "lanes": e["grid"], "launches": e["launches"],
+               "fetch_bytes_per_launch": e["fetch_bytes"], "write_bytes_per_launch": e["write_bytes"],
+               "hbm_bytes_per_launch": e["hbm_bytes"], "per_kernel": per}
+    out["method"] = ("median over launches of separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes; KiB x 1024; "
+                     "FETCH_SIZE doubled (gfx950 half-count of wide coalesced reads)")
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc_env.json"), "w"), indent=1)
     mf = os.path.join(src, "mfma", "mfma_counter_collection.csv")
     if os.path.exists(mf):

@@ -21,7 +21,7 @@ def build():
 
     b.build()
     os.makedirs(OUT, exist_ok=True)
-    timed = ("learn.hip", "rows.hip", "act.hip")
+    timed = ("learn.hip", "rows.hip", "act.hip", "env.hip")
     tobjs = []
     for src in timed:
         obj = os.path.join(OUT, src.replace(".hip", "_ts.o"))
@@ -118,5 +118,42 @@ def run_act():
         print(f"  {name:9s} cycles median {np.median(ph[:, i]):8.0f}  p90 {np.percentile(ph[:, i], 90):8.0f}")
 
 
+def run_env():
+    """Per-workgroup timeline of env_train_kernel (C2: 65,536 GBM lanes, 256
+    blocks): block start spread, spans, block 0's phases (cycles)."""
+    import numpy as np
+    import torch
+
+    from rlmd_amd import _abi
+
+    _abi._LIB = _abi.load(LIB)
+    lib = _abi._LIB
+    lib.rlmd_debug_ts_env.restype = C.c_int
+    lib.rlmd_debug_ts_env.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    lib.rlmd_train_set_fused(0)
+    from rlmd_amd.trainer import VecTrainer
+
+    tr = VecTrainer("gbm", "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
+                    replay_capacity=1 << 20, k_updates=1, device="cuda:0")
+    nb = 256
+    buf = (C.c_ulonglong * (8 * nb))()
+    spans, starts, ph = [], [], []
+    for it in range(12):
+        tr.step()
+        torch.cuda.synchronize()
+        lib.rlmd_debug_ts_env(buf, nb)
+        t = np.array(buf[:], dtype=np.int64).reshape(nb, 8)
+        if it < 2:
+            continue
+        st, en = t[:, 0] - t[:, 0].min(), t[:, 6] - t[:, 0].min()
+        starts.append(np.percentile(st, [0, 50, 100]))
+        spans.append(np.percentile(en - st, [0, 50, 100]))
+        ph.append(np.diff(t[0, 1:6]))
+    print("env_train_kernel: 256 blocks, realtime ticks (100 MHz = 10 ns)")
+    print("  block start spread pct 0/50/100:", np.median(starts, 0))
+    print("  block span         pct 0/50/100:", np.median(spans, 0))
+    print("  block-0 phases (cycles) entry->draw, draw->step, step->stores, stores->end:", np.median(ph, 0))
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run, "act": run_act}[sys.argv[1]]()
+    {"build": build, "run": run, "act": run_act, "env": run_env}[sys.argv[1]]()
