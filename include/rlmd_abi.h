@@ -139,6 +139,24 @@ int rlmd_lev_coin_sweep(const uint8_t* outcomes_dev, int64_t investors, int32_t 
                         void* workspace_dev, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
                         void* stream);
 
+/* Replaces dice_smart_lev (lev/lev_exp.py:586-705), dice_sh_smart_lev
+ * (:1209-1332) and gbm_smart_lev (:1008-1119): per leverage, every investor's
+ * f32 value times its gamble factor each step, then the step's values sorted
+ * descending (top / adjusted groups) into data_dev f32 [n_lev][13][horizon - 1]
+ * (mean x3, mad x3, std x3, lower median x3 of all / top / adjusted, lev) and the
+ * final values into data_T_dev f32 [n_lev][investors] (nullable).
+ * kind 0 (dice, dice_sh): outcomes_dev u8 [investors][ld] in {0 up, 1 down, 2 mid},
+ *   table_host f32 [n_lev][3] the factors per outcome (the reference's
+ *   1 + lev*r (+ (1 - lev)*r_sh) in its f32 arithmetic);
+ * kind 1 (gbm): outcomes_dev f32 [investors][ld], factor expf(lev * outcome).
+ * levs_host f32 [n_lev] (as the reference's lev_range, negation included);
+ * workspace of rlmd_lev_sorted_workspace_bytes(investors, n_lev) bytes. */
+int64_t rlmd_lev_sorted_workspace_bytes(int64_t investors, int32_t n_lev);
+int rlmd_lev_sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
+                          int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
+                          void* workspace, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
+                          void* stream);
+
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);
 /* Market lanes' episode start rows (i32 [N]) read back (eval_market's

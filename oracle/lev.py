@@ -3,7 +3,8 @@
 TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker of
 rlmd_lev_coin_sweep; never called by the product path.
 
-Follows lev/lev_exp.py:29-53 (param_range) and :128-237 (coin_smart_lev):
+Follows lev/lev_exp.py:29-53 (param_range) and :128-237 (coin_smart_lev),
+and (sorted_smart_lev below) :586-705 dice, :1008-1119 GBM, :1209-1332 dice_sh:
 for each leverage l (negated when -down_r > up_r), every investor's value
 is multiplied step by step by 1 + l*up_r (outcome 1) or 1 + l*down_r (0) in
 float32; after each step t >= 1 the values are sorted descending, the first
@@ -57,3 +58,57 @@ def coin_smart_lev(outcomes, top, value_0, up_r, down_r, lev_low, lev_high, lev_
             data[i, :, t] = [a[0], tp[0], ad[0], a[1], tp[1], ad[1], a[2], tp[2], ad[2], a[3], tp[3], ad[3], lev]
         data_T[i] = val
     return data, data_T
+
+
+def sorted_smart_lev(g_of_lev, levs, top, value_0, hor):
+    """The shared loop of dice_smart_lev (lev/lev_exp.py:586-705), gbm_smart_lev
+    (:1008-1119) and dice_sh_smart_lev (:1209-1332): g_of_lev(lev) -> the f32
+    gamble factors [investors, horizon]; sequential f32 products, per-step sort."""
+    data = np.zeros((len(levs), 13, hor - 1), dtype=np.float32)
+    data_T = None
+    for i, lev in enumerate(levs):
+        g = g_of_lev(lev)
+        if data_T is None:
+            data_T = np.zeros((len(levs), g.shape[0]), dtype=np.float32)
+        val = (np.float32(value_0) * g[:, 0]).astype(np.float32)
+        for t in range(hor - 1):
+            val = (val * g[:, t + 1]).astype(np.float32)
+            s = np.sort(val)[::-1]
+            a, tp, ad = _group(val), _group(s[:top]), _group(s[top:])
+            data[i, :, t] = [a[0], tp[0], ad[0], a[1], tp[1], ad[1], a[2], tp[2], ad[2], a[3], tp[3], ad[3], lev]
+        data_T[i] = val
+    return data, data_T
+
+
+def _levs(lev_low, lev_high, lev_incr, negate):
+    levs = np.array(param_range(lev_low, lev_high, lev_incr), dtype=np.float32)
+    return -levs if negate else levs
+
+
+def dice_smart_lev(outcomes, top, value_0, up_r, down_r, mid_r, lev_low, lev_high, lev_incr):
+    """lev/lev_exp.py:586-705 on a [investors, horizon] {0 up, 1 down, 2 mid}
+    matrix; factors 1 + lev * r in float32."""
+    levs = _levs(lev_low, lev_high, lev_incr, -down_r > up_r)
+    f = lambda lev, r: np.float32(1) + lev * np.float32(r)  # noqa: E731
+    g = lambda lev: np.where(outcomes == 0, f(lev, up_r), np.where(outcomes == 1, f(lev, down_r),  # noqa: E731
+                                                                    f(lev, mid_r))).astype(np.float32)
+    return sorted_smart_lev(g, levs, top, value_0, outcomes.shape[1])
+
+
+def dice_sh_smart_lev(outcomes, top, value_0, up_r, down_r, mid_r, sh_up_r, sh_down_r, sh_mid_r, lev_low, lev_high,
+                      lev_incr):
+    """lev/lev_exp.py:1209-1332: factors 1 + lev * r + (1 - lev) * r_sh (float32)."""
+    levs = _levs(lev_low, lev_high, lev_incr, -down_r > up_r)
+    f = lambda lev, r, rs: (np.float32(1) + lev * np.float32(r)) + (np.float32(1) - lev) * np.float32(rs)  # noqa
+    g = lambda lev: np.where(outcomes == 0, f(lev, up_r, sh_up_r),  # noqa: E731
+                             np.where(outcomes == 1, f(lev, down_r, sh_down_r),
+                                      f(lev, mid_r, sh_mid_r))).astype(np.float32)
+    return sorted_smart_lev(g, levs, top, value_0, outcomes.shape[1])
+
+
+def gbm_smart_lev(outcomes, top, value_0, lev_low, lev_high, lev_incr):
+    """lev/lev_exp.py:1008-1119: factors exp(lev * outcome) in float32."""
+    levs = _levs(lev_low, lev_high, lev_incr, False)
+    o = outcomes.astype(np.float32)
+    g = lambda lev: np.exp(lev * o).astype(np.float32)  # noqa: E731
+    return sorted_smart_lev(g, levs, top, value_0, outcomes.shape[1])

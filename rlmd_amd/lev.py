@@ -1,11 +1,14 @@
 """Fixed-leverage Monte-Carlo sweeps on the device.
 
-Mirrors lev/lev_exp.py:29-53 (param_range) and :128-237 (coin_smart_lev) with
+Mirrors lev/lev_exp.py:29-53 (param_range), :128-237 (coin_smart_lev), :586-705
+(dice_smart_lev), :1008-1119 (gbm_smart_lev) and :1209-1332 (dice_sh_smart_lev) with
 the reference's argument order and return values: `data` [n_lev, 13,
 horizon - 1] (mean / mean_top / mean_adj, mad x3, std x3, median x3, lev after
-each step) and `data_T` [n_lev, investors] (final values).  The sweep runs in
-rlmd_lev_coin_sweep (rlmd_amd/csrc/lev.hip): up-count histograms instead of
-one sort per (leverage, step).
+each step) and `data_T` [n_lev, investors] (final values).  The coin sweep runs
+in rlmd_lev_coin_sweep (rlmd_amd/csrc/lev.hip: up-count histograms instead of
+one sort per (leverage, step)); the die, safe-haven and GBM sweeps, whose values
+are not monotone in one count, in rlmd_lev_sweep_sorted (lev_sort.hip: a device
+radix sort per (step, leverage)).
 """
 import numpy as np
 import torch
@@ -54,3 +57,75 @@ def coin_smart_lev(device, outcomes, investors, horizon, top, value_0, up_r, dow
                                        float(down_r), levs.ctypes.data, n_lev, P(ws), ws.numel(), P(data),
                                        P(data_T) if data_T is not None else None, _abi.stream_ptr()))
     return data, data_T
+
+
+def _lev_range(lev_low, lev_high, lev_incr, negate):
+    """The reference's lev_range tensor (torch f32, negated for dice / dice_sh when
+    -down_r > up_r, lev_exp.py:623-624, :1249-1250)."""
+    r = torch.tensor([float(x) for x in param_range(float(lev_low), float(lev_high), float(lev_incr))],
+                     dtype=torch.float32)
+    return -r if negate else r
+
+
+def _sorted_sweep(kind, dev, outc, inv, hor, top, value_0, table, levs, final_values):
+    lib = _abi.lib()
+    n_lev = int(levs.numel())
+    ws = torch.empty(int(lib.rlmd_lev_sorted_workspace_bytes(int(inv), n_lev)), dtype=torch.uint8, device=dev)
+    data = torch.empty((n_lev, 13, hor - 1), dtype=torch.float32, device=dev)
+    data_T = torch.empty((n_lev, inv), dtype=torch.float32, device=dev) if final_values else None
+    lv = np.ascontiguousarray(levs.numpy(), dtype=np.float32)
+    assert table is None or table.dtype == np.float32, "factor table must be the reference's f32 arithmetic"
+    tb = None if table is None else np.ascontiguousarray(table, dtype=np.float32)
+    P = _abi.ptr
+    _abi.check(lib.rlmd_lev_sweep_sorted(kind, P(outc), int(inv), int(hor), outc.stride(0), int(top), float(value_0),
+                                         None if tb is None else tb.ctypes.data, lv.ctypes.data, n_lev, P(ws),
+                                         ws.numel(), P(data), P(data_T) if data_T is not None else None,
+                                         _abi.stream_ptr()))
+    return data, data_T
+
+
+def _categorical(outcomes, inv, hor, dev):
+    o = torch.as_tensor(outcomes)
+    if tuple(o.shape) != (int(inv), int(hor)):
+        raise ValueError("outcomes shape does not match investors x horizon")
+    return o.to(device=dev, dtype=torch.uint8).contiguous()
+
+
+def dice_smart_lev(device, outcomes, investors, horizon, top, value_0, up_r, down_r, mid_r, lev_low, lev_high,
+                   lev_incr, final_values=True):
+    """lev/lev_exp.py:586-705 on the device (rlmd_lev_sweep_sorted, kind 0):
+    outcomes [investors, horizon] in {0 up, 1 down, 2 mid}; the factor of each
+    outcome is the reference's f32 torch arithmetic 1 + lev * r."""
+    dev = torch.device(device)
+    up_r, down_r, mid_r = float(up_r), float(down_r), float(mid_r)  # Python scalars: torch keeps f32
+    levs = _lev_range(lev_low, lev_high, lev_incr, -down_r > up_r)
+    table = torch.stack([torch.stack([1 + lev * up_r, 1 + lev * down_r, 1 + lev * mid_r]) for lev in levs])
+    outc = _categorical(outcomes, investors, horizon, dev)
+    return _sorted_sweep(0, dev, outc, int(investors), int(horizon), top, value_0, table.numpy(), levs, final_values)
+
+
+def dice_sh_smart_lev(device, outcomes, investors, horizon, top, value_0, up_r, down_r, mid_r, sh_up_r, sh_down_r,
+                      sh_mid_r, lev_low, lev_high, lev_incr, final_values=True):
+    """lev/lev_exp.py:1209-1332 on the device: die + safe haven, factor
+    1 + lev * r + (1 - lev) * r_sh per outcome (f32 torch arithmetic)."""
+    dev = torch.device(device)
+    up_r, down_r, mid_r = float(up_r), float(down_r), float(mid_r)  # Python scalars: torch keeps f32
+    sh_up_r, sh_down_r, sh_mid_r = float(sh_up_r), float(sh_down_r), float(sh_mid_r)
+    levs = _lev_range(lev_low, lev_high, lev_incr, -down_r > up_r)
+    table = torch.stack([torch.stack([1 + lev * up_r + (1 - lev) * sh_up_r, 1 + lev * down_r + (1 - lev) * sh_down_r,
+                                      1 + lev * mid_r + (1 - lev) * sh_mid_r]) for lev in levs])
+    outc = _categorical(outcomes, investors, horizon, dev)
+    return _sorted_sweep(0, dev, outc, int(investors), int(horizon), top, value_0, table.numpy(), levs, final_values)
+
+
+def gbm_smart_lev(device, outcomes, investors, horizon, top, value_0, lev_low, lev_high, lev_incr,
+                  final_values=True):
+    """lev/lev_exp.py:1008-1119 on the device (kind 1): outcomes f32 log-returns
+    [investors, horizon], factor expf(lev * outcome)."""
+    dev = torch.device(device)
+    levs = _lev_range(lev_low, lev_high, lev_incr, False)
+    o = torch.as_tensor(outcomes, dtype=torch.float32)
+    if tuple(o.shape) != (int(investors), int(horizon)):
+        raise ValueError("outcomes shape does not match investors x horizon")
+    outc = o.to(dev).contiguous()
+    return _sorted_sweep(1, dev, outc, int(investors), int(horizon), top, value_0, None, levs, final_values)

@@ -864,6 +864,35 @@ def lev_fixtures(seed=41):
         out[name + "_levs"] = np.array(lev_exp.param_range(lo, hi, inc), dtype=np.float64)
         out[name + "_data"] = data.numpy()
         out[name + "_data_T"] = data_T.numpy()
+    # dice / dice_sh: categorical {0 up, 1 down, 2 mid} outcomes with the envs'
+    # probabilities (lev/dice_roll.py, lev/dice_roll_sh.py draw them the same way);
+    # gbm: N(mu, sigma) log-returns (lev/gbm.py); torch CPU, float32
+    for name, inv, hor, top, v0, rets, lo, hi, inc in (
+            ("dice", 1200, 36, 12, 100.0, (0.5, -0.5, 0.05), 0.1, 0.9, 0.2),
+            ("diceneg", 900, 30, 5, 100.0, (0.3, -0.6, 0.05), 0.25, 1.0, 0.25),
+            ("dicesh", 1100, 32, 9, 100.0, (0.5, -0.5, 0.05, -1.0, 5.0, -1.0), 0.1, 0.9, 0.2),
+            ("gbm", 1000, 40, 10, 100.0, None, 0.5, 2.5, 0.5)):
+        g = T.Generator().manual_seed(seed + inv)
+        if name == "gbm":
+            outc = 0.0540025395205692 - 0.1897916175617430 ** 2 / 2 + 0.1897916175617430 * T.randn(
+                (inv, hor), generator=g)
+        else:
+            u = T.rand((inv, hor), generator=g)
+            outc = T.where(u < 1 / 6, 0.0, T.where(u < 2 / 6, 1.0, 2.0))
+        with contextlib.redirect_stdout(io.StringIO()):
+            if name == "gbm":
+                data, data_T = lev_exp.gbm_smart_lev(T.device("cpu"), outc, inv, hor, top, v0, lo, hi, inc)
+            elif name == "dicesh":
+                data, data_T = lev_exp.dice_sh_smart_lev(T.device("cpu"), outc.numpy(), inv, hor, top, v0, *rets, lo,
+                                                         hi, inc)
+            else:
+                data, data_T = lev_exp.dice_smart_lev(T.device("cpu"), outc.numpy(), inv, hor, top, v0, *rets, lo, hi,
+                                                      inc)
+        out[name + "_outcomes"] = outc.numpy().astype(np.float32)
+        out[name + "_args"] = np.array([inv, hor, top, v0, lo, hi, inc], dtype=np.float64)
+        out[name + "_rets"] = np.array(rets if rets else [], dtype=np.float64)
+        out[name + "_data"] = data.numpy()
+        out[name + "_data_T"] = data_T.numpy()
     return out
 
 

@@ -40,3 +40,35 @@ def test_facade_param_range_is_the_oracle_grid():
 
     for args in [(0.05, 1.0, 0.05), (0.1, 1.0, 0.1), (0.0, 0.0, 0.1), (0.25, 1.0, 0.25)]:
         assert lev.param_range(*args) == olev.param_range(*args)
+
+
+SORTED = ["dice", "diceneg", "dicesh", "gbm"]
+
+
+def sorted_oracle(case, outcomes=None):
+    """oracle/lev.py's dice / dice_sh / gbm sweeps on a fixture case's inputs."""
+    a, rets = Z[case + "_args"], Z[case + "_rets"]
+    top, v0, lo, hi, inc = int(a[2]), a[3], a[4], a[5], a[6]
+    o = Z[case + "_outcomes"] if outcomes is None else outcomes
+    if case == "gbm":
+        return olev.gbm_smart_lev(o, top, v0, lo, hi, inc)
+    if case == "dicesh":
+        return olev.dice_sh_smart_lev(o, top, v0, *rets, lo, hi, inc)
+    return olev.dice_smart_lev(o, top, v0, *rets, lo, hi, inc)
+
+
+@pytest.mark.parametrize("case", SORTED)
+def test_sorted_oracle_matches_reference(case):
+    """dice_smart_lev / dice_sh_smart_lev / gbm_smart_lev (lev_exp.py:586, :1209,
+    :1008) run by the reference on torch CPU: final values bit-equal for the
+    categorical gambles (the same f32 factors and products) and within 2 f32 ulps
+    for GBM (NumPy's vs torch's expf); the table within 2e-6 / 2e-5."""
+    d, dT = sorted_oracle(case)
+    ref_d, ref_dT = Z[case + "_data"], Z[case + "_data_T"]
+    assert d.shape == ref_d.shape and dT.shape == ref_dT.shape
+    if case == "gbm":
+        np.testing.assert_allclose(dT, ref_dT, rtol=2e-5, atol=0)
+        assert close_table(d, ref_d, 2e-5).all()
+    else:
+        np.testing.assert_array_equal(dT, ref_dT)
+        assert close_table(d, ref_d, 2e-6).all()

@@ -97,3 +97,78 @@ def test_bad_arguments_fail_loudly():
     with pytest.raises(ValueError):
         lev.coin_smart_lev("cuda:0", o, 9, 10, 1, 1.0, 0.5, -0.4, 0.5, 0.5, 0.5)
     assert _abi.lib().rlmd_lev_workspace_bytes(10, 0) == -1
+
+
+from tests.test_lev_cpu import SORTED, sorted_oracle  # noqa: E402
+
+
+def _sorted_device(case, outcomes=None, top=None):
+    from rlmd_amd import lev
+
+    a, rets = Z[case + "_args"], Z[case + "_rets"]
+    inv, hor = int(a[0]), int(a[1])
+    top = int(a[2]) if top is None else top
+    v0, lo, hi, inc = a[3], a[4], a[5], a[6]
+    o = torch.from_numpy(Z[case + "_outcomes"] if outcomes is None else outcomes)
+    inv, hor = o.shape
+    if case == "gbm":
+        d, dT = lev.gbm_smart_lev("cuda:0", o, inv, hor, top, v0, lo, hi, inc)
+    elif case == "dicesh":
+        d, dT = lev.dice_sh_smart_lev("cuda:0", o, inv, hor, top, v0, *rets, lo, hi, inc)
+    else:
+        d, dT = lev.dice_smart_lev("cuda:0", o, inv, hor, top, v0, *rets, lo, hi, inc)
+    return d.cpu().numpy(), dT.cpu().numpy()
+
+
+@pytest.mark.parametrize("case", SORTED)
+def test_sorted_sweep_matches_reference(case):
+    """rlmd_lev_sweep_sorted vs the reference's dice / dice_sh / gbm sweeps
+    (tests/golden/lev.npz): categorical final values bit-exact (the same f32
+    factors and sequential products), GBM within 2e-5 (device vs torch expf);
+    the table within 2e-6 / 2e-5 (f64 group sums of the sorted values)."""
+    d, dT = _sorted_device(case)
+    ref_d, ref_dT = Z[case + "_data"], Z[case + "_data_T"]
+    assert d.shape == ref_d.shape
+    if case == "gbm":
+        np.testing.assert_allclose(dT, ref_dT, rtol=2e-5, atol=0)
+        ok = close_table(d, ref_d, 2e-5)
+    else:
+        np.testing.assert_array_equal(dT, ref_dT)
+        ok = close_table(d, ref_d, 2e-6)
+    assert ok.all(), np.argwhere(~ok)[:5]
+
+
+@pytest.mark.parametrize("case,inv,hor,top", [("dice", 60000, 120, 600), ("dicesh", 40000, 90, 0),
+                                              ("gbm", 50000, 100, 50000), ("diceneg", 7777, 60, 3)])
+def test_sorted_sweep_matches_oracle_larger(case, inv, hor, top):
+    """Larger outcome matrices (incl. top = 0 and top = investors: one group
+    empty, NaN rows) against oracle/lev.py."""
+    rng = np.random.default_rng(inv)
+    if case == "gbm":
+        o = (0.0540025395205692 - 0.1897916175617430 ** 2 / 2
+             + 0.1897916175617430 * rng.standard_normal((inv, hor))).astype(np.float32)
+    else:
+        u = rng.random((inv, hor))
+        o = np.where(u < 1 / 6, 0, np.where(u < 2 / 6, 1, 2)).astype(np.float32)
+    d, dT = _sorted_device(case, o, top)
+    od, odT = sorted_oracle_top(case, o, top)
+    fin = np.isfinite(od)
+    assert (np.isfinite(d) == fin).all()
+    if case == "gbm":
+        np.testing.assert_allclose(dT, odT, rtol=2e-5, atol=0)
+        assert close_table(np.where(fin, d, 0), np.where(fin, od, 0), 2e-5).all()
+    else:
+        np.testing.assert_array_equal(dT, odT)
+        assert close_table(np.where(fin, d, 0), np.where(fin, od, 0), 2e-6).all()
+
+
+def sorted_oracle_top(case, o, top):
+    from oracle import lev as olev
+
+    a, rets = Z[case + "_args"], Z[case + "_rets"]
+    v0, lo, hi, inc = a[3], a[4], a[5], a[6]
+    if case == "gbm":
+        return olev.gbm_smart_lev(o, top, v0, lo, hi, inc)
+    if case == "dicesh":
+        return olev.dice_sh_smart_lev(o, top, v0, *rets, lo, hi, inc)
+    return olev.dice_smart_lev(o, top, v0, *rets, lo, hi, inc)

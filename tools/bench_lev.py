@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--horizon", type=int, default=3000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kind", default="coin", choices=["coin", "dice", "dice_sh", "gbm"])
     a = ap.parse_args()
+    if a.kind != "coin":
+        return sorted_main(a)
     dev = torch.device("cuda:0")
     inv, hor = a.investors, a.horizon
     g = torch.Generator(device=dev).manual_seed(420)
@@ -58,6 +61,57 @@ def main():
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": 20000 * 200 * 10 / dt, "unit": "1/s", "cores": 1, "kind": "port",
                                "sample": "20000 investors x 200 steps x 10 leverages, sort per step (NumPy)"}
+    print(json.dumps(out))
+
+
+def sorted_main(a):
+    """dice_smart_lev / dice_sh_smart_lev / gbm_smart_lev (rlmd_lev_sweep_sorted:
+    a device radix sort per (step, leverage)) at the given size, 10 leverages
+    (lev/dice_roll.py, dice_roll_sh.py, gbm.py grids 0.1..1.0)."""
+    dev = torch.device("cuda:0")
+    inv, hor = a.investors, a.horizon
+    g = torch.Generator(device=dev).manual_seed(420)
+    if a.kind == "gbm":
+        o = (0.0540025395205692 - 0.1897916175617430 ** 2 / 2
+             + 0.1897916175617430 * torch.randn((inv, hor), generator=g, device=dev))
+    else:
+        u = torch.rand((inv, hor), generator=g, device=dev)
+        o = torch.where(u < 1 / 6, 0.0, torch.where(u < 2 / 6, 1.0, 2.0))
+    top = int(inv * 1e-4)
+    if a.kind == "dice":
+        run = lambda: lev.dice_smart_lev(dev, o, inv, hor, top, 100.0, 0.5, -0.5, 0.05, 0.1, 1.0, 0.1)  # noqa
+    elif a.kind == "dice_sh":
+        run = lambda: lev.dice_sh_smart_lev(dev, o, inv, hor, top, 100.0, 0.5, -0.5, 0.05, -1.0, 5.0, -1.0,  # noqa
+                                            0.1, 1.0, 0.1)
+    else:
+        run = lambda: lev.gbm_smart_lev(dev, o, inv, hor, top, 100.0, 0.1, 1.0, 0.1)  # noqa
+    data, _ = run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(a.reps):
+        data, data_T = run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    n_lev = data.shape[0]
+    out = {"metric": f"{a.kind}_smart_lev investor-steps-leverages/s", "value": inv * hor * n_lev / (ms / 1e3),
+           "unit": "1/s", "ms_per_sweep": ms, "ms_per_step": ms / (hor - 1),
+           "config": {"investors": inv, "horizon": hor, "n_lev": n_lev, "top": top}}
+    if not a.no_cpu_baseline:
+        from oracle import lev as olev
+
+        oc = o[:20000, :100].cpu().numpy()
+        t0 = time.perf_counter()
+        if a.kind == "gbm":
+            olev.gbm_smart_lev(oc, 2, 100.0, 0.1, 1.0, 0.1)
+        elif a.kind == "dice":
+            olev.dice_smart_lev(oc, 2, 100.0, 0.5, -0.5, 0.05, 0.1, 1.0, 0.1)
+        else:
+            olev.dice_sh_smart_lev(oc, 2, 100.0, 0.5, -0.5, 0.05, -1.0, 5.0, -1.0, 0.1, 1.0, 0.1)
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": 20000 * 100 * 10 / dt, "unit": "1/s", "cores": 1, "kind": "port",
+                               "sample": "20000 investors x 100 steps x 10 leverages, sort per step (NumPy)"}
     print(json.dumps(out))
 
 
