@@ -156,6 +156,17 @@ int rlmd_lev_sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t invest
                           int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
                           void* workspace, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
                           void* stream);
+/* Replaces the *_fixed_final_lev family (coin :56-127, dice :508-585, gbm
+ * :935-1007, dice_sh :1121-1208), which reports the statistics of the values at
+ * maturity only: the same inputs (coin: kind 0 with outcome 0 = down, 1 = up),
+ * stats_dev f32 [n_lev][13] (the column of rlmd_lev_sweep_sorted at maturity)
+ * and the final values values_dev f32 [n_lev][investors] (nullable).  The
+ * values are sequential f32 products; the reference's gambles.prod(dim=1) rounds
+ * in torch's reduction order. */
+int rlmd_lev_final_sorted(int32_t kind, const void* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
+                          int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
+                          void* workspace, int64_t workspace_bytes, float* stats_dev, float* values_dev,
+                          void* stream);
 
 /* Lane wealth (f64 [N]) and time (i32 [N]) read back for tests/logging. */
 int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host);

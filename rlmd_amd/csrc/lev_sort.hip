@@ -1,7 +1,9 @@
 // lev_sort.hip — fixed-leverage sweeps with per-step sorts (gfx950).
 //
 // Replaces dice_smart_lev (lev/lev_exp.py:586-705), gbm_smart_lev (:1008-1119)
-// and dice_sh_smart_lev (:1209-1332): for every leverage l each investor's value
+// and dice_sh_smart_lev (:1209-1332) — and, statistics of the final values only,
+// the *_fixed_final_lev family (:56-127, :508-585, :935-1007, :1121-1208):
+// for every leverage l each investor's value
 // is multiplied step by step by its gamble factor (float32, as the reference's
 // torch tensors), and after each step t >= 1 the values are sorted descending:
 // the first `top` form the top group, the rest the adjusted group, and the
@@ -141,13 +143,14 @@ int64_t rlmd_lev_sorted_workspace_bytes(int64_t investors, int32_t n_lev) {
   return ((vals + 255) & ~255ll) + ((sums + 255) & ~255ll) + (int64_t)sort_temp_bytes(investors);
 }
 
-int rlmd_lev_sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
-                          int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
-                          void* workspace, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
-                          void* stream) {
+static int sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
+                        int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
+                        void* workspace, int64_t workspace_bytes, float* data_dev, float* data_T_dev, void* stream,
+                        bool final_only) {
   RLMD_CHECK(kind == 0 || kind == 1, "kind: 0 categorical, 1 gbm");
   RLMD_CHECK(outcomes_dev && workspace && data_dev && levs_host, "null argument");
-  RLMD_CHECK(investors > 0 && investors <= INT32_MAX && horizon >= 2 && ld >= horizon, "bad sizes");
+  RLMD_CHECK(investors > 0 && investors <= INT32_MAX && horizon >= (final_only ? 1 : 2) && ld >= horizon,
+             "bad sizes");
   RLMD_CHECK(n_lev > 0 && n_lev <= 1024, "n_lev out of range");
   RLMD_CHECK(kind == 1 || table_host, "categorical sweep needs the factor table");
   const int64_t need = rlmd_lev_sorted_workspace_bytes(investors, n_lev);
@@ -179,11 +182,11 @@ int rlmd_lev_sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t invest
   a.table = small + n_lev;
   a.val = val;
   const dim3 grid_adv((unsigned)((investors + kT - 1) / kT), (unsigned)n_lev);
-  const int steps = horizon - 1;
+  const int steps = final_only ? 1 : horizon - 1;
   for (int t = 0; t < horizon; ++t) {
     hipLaunchKernelGGL(lev_advance_kernel, grid_adv, dim3(kT), 0, st, a, t, value_0);
     RLMD_LAUNCH_CHECK();
-    if (t == 0) continue;
+    if (final_only ? t < horizon - 1 : t == 0) continue;
     for (int l = 0; l < n_lev; ++l) {
       RLMD_HIP(hipcub::DeviceRadixSort::SortKeysDescending(tmp, tmp_bytes, val + (int64_t)l * investors,
                                                            sorted + (int64_t)l * investors, (int)investors, 0, 32,
@@ -194,13 +197,29 @@ int rlmd_lev_sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t invest
                          means, pass, part);
       RLMD_LAUNCH_CHECK();
       hipLaunchKernelGGL(lev_sorted_fold_kernel, dim3((n_lev + 63) / 64), dim3(64), 0, st, sorted, investors, tp,
-                         n_lev, part, pass, means, small, data_dev, steps, t - 1);
+                         n_lev, part, pass, means, small, data_dev, steps, final_only ? 0 : t - 1);
       RLMD_LAUNCH_CHECK();
     }
   }
   if (data_T_dev)
     RLMD_HIP(hipMemcpyAsync(data_T_dev, val, sizeof(float) * n_lev * investors, hipMemcpyDeviceToDevice, st));
   return 0;
+}
+
+int rlmd_lev_sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
+                          int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
+                          void* workspace, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
+                          void* stream) {
+  return sweep_sorted(kind, outcomes_dev, investors, horizon, ld, top, value_0, table_host, levs_host, n_lev,
+                      workspace, workspace_bytes, data_dev, data_T_dev, stream, false);
+}
+
+int rlmd_lev_final_sorted(int32_t kind, const void* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
+                          int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
+                          void* workspace, int64_t workspace_bytes, float* stats_dev, float* values_dev,
+                          void* stream) {
+  return sweep_sorted(kind, outcomes_dev, investors, horizon, ld, top, value_0, table_host, levs_host, n_lev,
+                      workspace, workspace_bytes, stats_dev, values_dev, stream, true);
 }
 
 }  // extern "C"

@@ -129,3 +129,97 @@ def gbm_smart_lev(device, outcomes, investors, horizon, top, value_0, lev_low, l
         raise ValueError("outcomes shape does not match investors x horizon")
     outc = o.to(dev).contiguous()
     return _sorted_sweep(1, dev, outc, int(investors), int(horizon), top, value_0, None, levs, final_values)
+
+
+# ---------------------------------------------------------------------------
+# *_fixed_final_lev: statistics of the values at maturity (rlmd_lev_final_sorted)
+# ---------------------------------------------------------------------------
+STAT_NAMES = ["mean", "mean_top", "mean_adj", "mad", "mad_top", "mad_adj", "std", "std_top", "std_adj", "med",
+              "med_top", "med_adj", "lev"]
+
+
+def _final(kind, dev, outc, inv, hor, top, value_0, table, levs, verbose):
+    lib = _abi.lib()
+    n_lev = int(levs.numel())
+    ws = torch.empty(int(lib.rlmd_lev_sorted_workspace_bytes(int(inv), n_lev)), dtype=torch.uint8, device=dev)
+    stats = torch.empty((n_lev, 13), dtype=torch.float32, device=dev)
+    values = torch.empty((n_lev, inv), dtype=torch.float32, device=dev)
+    lv = np.ascontiguousarray(levs.numpy(), dtype=np.float32)
+    tb = None if table is None else np.ascontiguousarray(table, dtype=np.float32)
+    P = _abi.ptr
+    _abi.check(lib.rlmd_lev_final_sorted(kind, P(outc), int(inv), int(hor), outc.stride(0), int(top), float(value_0),
+                                         None if tb is None else tb.ctypes.data, lv.ctypes.data, n_lev, P(ws),
+                                         ws.numel(), P(stats), P(values), _abi.stream_ptr()))
+    if verbose:  # the reference's summary lines (lev_exp.py:103-125)
+        for row in stats.cpu().numpy():
+            m, mt, ma, d, dt, da, s, st, sa, md, mdt, mda, lev = row
+            print(f"       lev {lev * 100:1.0f}%:\n"
+                  f"                 avg mean/med/mad/std:  $ {m:1.2e} / {md:1.2e} / {d:1.1e} / {s:1.1e}\n"
+                  f"                 top mean/med/mad/std:  $ {mt:1.2e} / {mdt:1.2e} / {dt:1.1e} / {st:1.1e}\n"
+                  f"                 adj mean/med/mad/std:  $ {ma:1.2e} / {mda:1.2e} / {da:1.1e} / {sa:1.1e}")
+    return stats, values
+
+
+def coin_fixed_final_lev(device, outcomes, top, value_0, up_r, down_r, lev_low, lev_high, lev_incr, verbose=False):
+    """lev/lev_exp.py:56-127: statistics of value_0 * prod(1 + lev * r) per leverage
+    (outcome 1 up, else down).  Returns (stats [n_lev, 13] in STAT_NAMES order,
+    final values [n_lev, investors]); the reference prints the statistics only."""
+    dev = torch.device(device)
+    up_r, down_r = float(up_r), float(down_r)
+    levs = _lev_range(lev_low, lev_high, lev_incr, -down_r > up_r)
+    table = torch.stack([torch.stack([1 + lev * down_r, 1 + lev * up_r, 1 + lev * up_r]) for lev in levs])
+    o = torch.as_tensor(outcomes)
+    inv, hor = o.shape
+    outc = (o == 1).to(device=dev, dtype=torch.uint8).contiguous()
+    return _final(0, dev, outc, inv, hor, top, value_0, table.numpy(), levs, verbose)
+
+
+def dice_fixed_final_lev(device, outcomes, top, value_0, up_r, down_r, mid_r, lev_low, lev_high, lev_incr,
+                         verbose=False):
+    """lev/lev_exp.py:508-585 (outcomes {0 up, 1 down, 2 mid})."""
+    dev = torch.device(device)
+    up_r, down_r, mid_r = float(up_r), float(down_r), float(mid_r)
+    levs = _lev_range(lev_low, lev_high, lev_incr, -down_r > up_r)
+    table = torch.stack([torch.stack([1 + lev * up_r, 1 + lev * down_r, 1 + lev * mid_r]) for lev in levs])
+    o = torch.as_tensor(outcomes)
+    inv, hor = o.shape
+    return _final(0, dev, _categorical(o, inv, hor, dev), inv, hor, top, value_0, table.numpy(), levs, verbose)
+
+
+def dice_sh_fixed_final_lev(device, outcomes, top, value_0, up_r, down_r, mid_r, sh_up_r, sh_down_r, sh_mid_r,
+                            lev_low, lev_high, lev_incr, verbose=False):
+    """lev/lev_exp.py:1121-1208 (die + safe haven)."""
+    dev = torch.device(device)
+    up_r, down_r, mid_r = float(up_r), float(down_r), float(mid_r)
+    sh_up_r, sh_down_r, sh_mid_r = float(sh_up_r), float(sh_down_r), float(sh_mid_r)
+    levs = _lev_range(lev_low, lev_high, lev_incr, -down_r > up_r)
+    table = torch.stack([torch.stack([1 + lev * up_r + (1 - lev) * sh_up_r, 1 + lev * down_r + (1 - lev) * sh_down_r,
+                                      1 + lev * mid_r + (1 - lev) * sh_mid_r]) for lev in levs])
+    o = torch.as_tensor(outcomes)
+    inv, hor = o.shape
+    return _final(0, dev, _categorical(o, inv, hor, dev), inv, hor, top, value_0, table.numpy(), levs, verbose)
+
+
+def gbm_fixed_final_lev(device, outcomes, top, value_0, lev_low, lev_high, lev_incr, verbose=False):
+    """lev/lev_exp.py:935-1007: factors exp(lev * outcome)."""
+    dev = torch.device(device)
+    levs = _lev_range(lev_low, lev_high, lev_incr, False)
+    o = torch.as_tensor(outcomes, dtype=torch.float32)
+    inv, hor = o.shape
+    return _final(1, dev, o.to(dev).contiguous(), inv, hor, top, value_0, None, levs, verbose)
+
+
+def coin_galaxy_brain_lev(device, ru_min, ru_max, ru_incr, rd_min, rd_max, rd_incr, pu_min, pu_max, pu_incr):
+    """lev/lev_exp.py:455-505: the Kelly fraction pu / rd - (1 - pu) / ru over a
+    (pu, ru, rd) grid, [n_pu, n_ru, n_ru, 4] = (pu, ru, rd, kelly) (the reference
+    sizes the third axis by ru's grid and fills it from rd's).  A few hundred
+    scalars: evaluated on the host in the reference's Python floats, stored f32."""
+    ru_range = param_range(ru_min, ru_max, ru_incr)
+    rd_range = param_range(rd_min, rd_max, rd_incr)
+    pu_range = param_range(pu_min, pu_max, pu_incr)
+    data = torch.zeros((len(pu_range), len(ru_range), len(ru_range), 4))
+    for i, pu in enumerate(pu_range):
+        for j, ru in enumerate(ru_range):
+            for k, rd in enumerate(rd_range):
+                data[i, j, k, :] = torch.tensor([pu, ru, rd, pu / rd - (1 - pu) / ru])
+    return data.to(torch.device(device))

@@ -1027,6 +1027,99 @@ def c1_trace(n_steps=2500, seed=0):
 
 
 # ----------------------------------------------------------------------------
+# F10: *_fixed_final_lev (statistics captured at the reference's torch calls)
+#      and coin_galaxy_brain_lev
+# ----------------------------------------------------------------------------
+class _StatRecorder(types.ModuleType):
+    """``T`` of lev_exp recording what its fixed-final statistics return:
+    std_mean (std, mean), median and mean, in call order."""
+
+    def __init__(self):
+        super().__init__("torch_proxy")
+        self.calls = []
+
+    def __getattr__(self, name):
+        return getattr(T, name)
+
+    def std_mean(self, x, *a, **kw):
+        r = T.std_mean(x, *a, **kw)
+        self.calls.append(("std_mean", float(r[0]), float(r[1]), x.detach().clone()))
+        return r
+
+    def median(self, x, *a, **kw):
+        r = T.median(x, *a, **kw)
+        self.calls.append(("median", float(r)))
+        return r
+
+    def mean(self, x, *a, **kw):
+        r = T.mean(x, *a, **kw)
+        self.calls.append(("mean", float(r)))
+        return r
+
+
+def _final_stats(calls, n_lev):
+    """[n_lev, 12] in STAT_NAMES order from the recorded calls (per leverage: the
+    all / top / adjusted groups' std_mean, median, mean(|.|) in that order) and
+    the recorded final values [n_lev, investors]."""
+    per = len(calls) // n_lev
+    out, vals = np.zeros((n_lev, 12)), []
+    for i in range(n_lev):
+        c = calls[i * per:(i + 1) * per]
+        sm = [x for x in c if x[0] == "std_mean"]
+        md = [x[1] for x in c if x[0] == "median"]
+        mn = [x[1] for x in c if x[0] == "mean"]
+        out[i] = [sm[0][2], sm[1][2], sm[2][2], mn[0], mn[1], mn[2], sm[0][1], sm[1][1], sm[2][1], md[0], md[1], md[2]]
+        vals.append(sm[0][3].numpy())
+    return out, np.stack(vals)
+
+
+def lev_final_fixtures(seed=43):
+    import contextlib
+    import io
+
+    from lev import lev_exp
+
+    out = {}
+    cases = [("coin", 900, 30, 11, 100.0, (0.5, -0.4), 0.1, 1.0, 0.3),
+             ("dice", 800, 25, 7, 100.0, (0.5, -0.5, 0.05), 0.2, 0.8, 0.3),
+             ("dicesh", 700, 20, 5, 100.0, (0.5, -0.5, 0.05, -1.0, 5.0, -1.0), 0.1, 0.9, 0.4),
+             ("gbm", 600, 35, 6, 100.0, (), 0.5, 2.0, 0.5)]
+    saved = lev_exp.T
+    try:
+        for name, inv, hor, top, v0, rets, lo, hi, inc in cases:
+            g = T.Generator().manual_seed(seed + inv)
+            if name == "coin":
+                outc = T.bernoulli(T.full((inv, hor), 0.5), generator=g)
+            elif name == "gbm":
+                outc = 0.0540025395205692 - 0.1897916175617430 ** 2 / 2 + 0.1897916175617430 * T.randn(
+                    (inv, hor), generator=g)
+            else:
+                u = T.rand((inv, hor), generator=g)
+                outc = T.where(u < 1 / 6, 0.0, T.where(u < 2 / 6, 1.0, 2.0))
+            rec = _StatRecorder()
+            lev_exp.T = rec
+            with contextlib.redirect_stdout(io.StringIO()):
+                fn = {"coin": lev_exp.coin_fixed_final_lev, "dice": lev_exp.dice_fixed_final_lev,
+                      "dicesh": lev_exp.dice_sh_fixed_final_lev, "gbm": lev_exp.gbm_fixed_final_lev}[name]
+                o_arg = outc.numpy() if name == "dicesh" else outc
+                fn(T.device("cpu"), o_arg, top, v0, *rets, lo, hi, inc)
+            lev_exp.T = saved
+            n_lev = len(lev_exp.param_range(lo, hi, inc))
+            st, vals = _final_stats(rec.calls, n_lev)
+            out[name + "_outcomes"] = outc.numpy().astype(np.float32)
+            out[name + "_args"] = np.array([inv, hor, top, v0, lo, hi, inc], dtype=np.float64)
+            out[name + "_rets"] = np.array(rets, dtype=np.float64)
+            out[name + "_stats"] = st
+            out[name + "_values"] = vals
+        grid = (0.1, 0.5, 0.1, 0.1, 0.4, 0.1, 0.4, 0.6, 0.1)  # len(rd) <= len(ru): the reference indexes rd by ru's size
+        out["galaxy_args"] = np.array(grid, dtype=np.float64)
+        out["galaxy"] = lev_exp.coin_galaxy_brain_lev(T.device("cpu"), *grid).numpy()
+    finally:
+        lev_exp.T = saved
+    return out
+
+
+# ----------------------------------------------------------------------------
 # F9: the reference's readers (tools/aggregate_data.py) on the build's log files
 # ----------------------------------------------------------------------------
 def _logs_mod():
@@ -1074,6 +1167,7 @@ def main():
         "lev.npz": lev_fixtures,
         "c1_trace.npz": c1_trace,
         "aggregate.npz": aggregate_fixtures,
+        "lev_final.npz": lev_final_fixtures,
     }
     only = sys.argv[1:]
     for fn, job in jobs.items():

@@ -72,3 +72,15 @@ def test_sorted_oracle_matches_reference(case):
     else:
         np.testing.assert_array_equal(dT, ref_dT)
         assert close_table(d, ref_d, 2e-6).all()
+
+
+ZF = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lev_final.npz"))
+
+
+def test_galaxy_brain_matches_reference():
+    """coin_galaxy_brain_lev (lev_exp.py:455-505) run by the reference: the
+    Kelly-fraction grid, bit-equal (host arithmetic in Python floats, f32 table)."""
+    from rlmd_amd import lev
+
+    got = lev.coin_galaxy_brain_lev("cpu", *ZF["galaxy_args"]).numpy()
+    np.testing.assert_array_equal(got, ZF["galaxy"])

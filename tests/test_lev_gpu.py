@@ -4,6 +4,8 @@ reference's sequential float32 products, bit-exact; the summary table is
 computed from up-count histograms with each bin's value rounded once, so it
 agrees with the reference's step-by-step products to a few f32 ulps
 (rtol 1e-5; mad / std rows also within 1e-5 of their group mean)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -172,3 +174,30 @@ def sorted_oracle_top(case, o, top):
     if case == "dicesh":
         return olev.dice_sh_smart_lev(o, top, v0, *rets, lo, hi, inc)
     return olev.dice_smart_lev(o, top, v0, *rets, lo, hi, inc)
+
+
+ZF = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "lev_final.npz"))
+
+
+@pytest.mark.parametrize("case", ["coin", "dice", "dicesh", "gbm"])
+def test_fixed_final_matches_reference(case):
+    """*_fixed_final_lev (lev_exp.py:56, :508, :935, :1121): the statistics the
+    reference computed (recorded at its torch calls, make_golden.lev_final_fixtures)
+    and its final values.  The device multiplies sequentially where the reference
+    reduces with gambles.prod(dim=1) (torch's order): rtol 1e-5 on values and
+    statistics (the dispersion rows also 1e-5 of the group mean)."""
+    from rlmd_amd import lev
+
+    a, rets = ZF[case + "_args"], [float(x) for x in ZF[case + "_rets"]]
+    inv, hor, top, v0, lo, hi, inc = int(a[0]), int(a[1]), int(a[2]), a[3], a[4], a[5], a[6]
+    o = torch.from_numpy(ZF[case + "_outcomes"])
+    fn = {"coin": lev.coin_fixed_final_lev, "dice": lev.dice_fixed_final_lev, "dicesh": lev.dice_sh_fixed_final_lev,
+          "gbm": lev.gbm_fixed_final_lev}[case]
+    st, vals = fn("cuda:0", o, top, v0, *rets, lo, hi, inc)
+    st, vals = st.cpu().numpy(), vals.cpu().numpy()
+    np.testing.assert_allclose(vals, ZF[case + "_values"], rtol=1e-5, atol=0)
+    ref = ZF[case + "_stats"]
+    means = ref[:, [0, 1, 2, 0, 1, 2, 0, 1, 2, 0, 1, 2]]
+    disp = (np.arange(12) >= 3) & (np.arange(12) < 9)
+    tol = 1e-5 * np.abs(ref) + 1e-5 * np.abs(means) * disp[None, :]
+    assert (np.abs(st[:, :12] - ref) <= tol + 1e-30).all(), (st[:, :12], ref)
