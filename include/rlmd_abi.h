@@ -156,6 +156,20 @@ int rlmd_lev_sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t invest
                           int64_t top, float value_0, const float* table_host, const float* levs_host, int32_t n_lev,
                           void* workspace, int64_t workspace_bytes, float* data_dev, float* data_T_dev,
                           void* stream);
+/* Replaces coin_big_brain_lev (lev/lev_exp.py:270-452) and dice_big_brain_lev
+ * (:741-932): per configuration c = (roll, stop) every investor re-levers each
+ * step from its own value (coin_optimal_lev :240-267 / dice_optimal_lev
+ * :704-738, f32).  outcomes_dev u8 codes [investors][ld] with rets_host3 the
+ * return of each code; cfg_host f32 [n_cfg][5] = {stop * value_0, roll, the
+ * initial leverage, roll > 0, stop}; data_dev f32 [n_cfg][26][horizon - 1]: value
+ * statistics (rows 0-11), leverage statistics (12-23), stop, roll; the caller
+ * orders configurations roll-major, as the reference's [n_roll][n_stop].
+ * f64 = 0: coin (every quantity f32); 1: dice (the reference casts the outcomes
+ * to float64, so values — and with roll 0 the leverages — are f64). */
+int64_t rlmd_lev_brain_workspace_bytes(int64_t investors, int32_t n_cfg);
+int rlmd_lev_brain(int32_t f64, const uint8_t* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
+                   int64_t top, float value_0, const double* rets_host3, float lev_factor, const float* cfg_host,
+                   int32_t n_cfg, void* workspace, int64_t workspace_bytes, float* data_dev, void* stream);
 /* Replaces the *_fixed_final_lev family (coin :56-127, dice :508-585, gbm
  * :935-1007, dice_sh :1121-1208), which reports the statistics of the values at
  * maturity only: the same inputs (coin: kind 0 with outcome 0 = down, 1 = up),

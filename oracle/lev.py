@@ -112,3 +112,45 @@ def gbm_smart_lev(outcomes, top, value_0, lev_low, lev_high, lev_incr):
     o = outcomes.astype(np.float32)
     g = lambda lev: np.exp(lev * o).astype(np.float32)  # noqa: E731
     return sorted_smart_lev(g, levs, top, value_0, outcomes.shape[1])
+
+
+def brain_lev(codes, rets3, top, value_0, lev_factor, stops, rolls, f64=False):
+    """coin_big_brain_lev / dice_big_brain_lev (lev/lev_exp.py:270-452, :741-932)
+    on outcome codes [investors, horizon] with rets3[code] the step return: per
+    (roll, stop) the leverage re-set from each investor's value every step
+    (coin_optimal_lev :240-267 / dice_optimal_lev :704-738).  Coin: float32
+    throughout.  Dice (f64): the reference casts the outcomes to float64 (:751),
+    so values are f64; with roll 0 the leverage is f64 (f32 lev_factor and floor
+    against the f64 value), with roll > 0 dice_optimal_lev casts the values to
+    float32 first and the leverage is f32."""
+    inv, hor = codes.shape
+    f = np.float32
+    vt = np.float64 if f64 else np.float32
+    r = np.asarray(rets3, dtype=vt)[codes]
+    lf = f(lev_factor)
+    data = np.zeros((len(rolls), len(stops), 26, hor - 1), dtype=np.float32)
+
+    def opt(v, vmin, roll):
+        if roll == 0:
+            return (vt(lf) * (vt(1) - vt(vmin) / v)).astype(vt)
+        vf = v.astype(np.float32)
+        loss = np.where(vf <= f(value_0), vmin, f(value_0) + roll * (vf - f(value_0))).astype(np.float32)
+        return (lf * (f(1) - loss / vf)).astype(np.float32).astype(vt)
+
+    for j, roll in enumerate(np.asarray(rolls, dtype=np.float32)):
+        for i, stop in enumerate(np.asarray(stops, dtype=np.float32)):
+            vmin = stop * f(value_0)
+            lev0 = lf * (f(1) - vmin / f(value_0))
+            val = (vt(value_0) * (vt(1) + vt(lev0) * r[:, 0])).astype(vt)
+            lev = opt(val, vmin, roll)
+            for t in range(hor - 1):
+                sl = np.sort(lev)[::-1]
+                a, tp, ad = _group(lev), _group(sl[:top]), _group(sl[top:])
+                data[j, i, 12:26, t] = [a[0], tp[0], ad[0], a[1], tp[1], ad[1], a[2], tp[2], ad[2], a[3], tp[3],
+                                        ad[3], stop, roll]
+                val = (val * (vt(1) + lev * r[:, t + 1])).astype(vt)
+                lev = opt(val, vmin, roll)
+                s = np.sort(val)[::-1]
+                a, tp, ad = _group(val), _group(s[:top]), _group(s[top:])
+                data[j, i, 0:12, t] = [a[0], tp[0], ad[0], a[1], tp[1], ad[1], a[2], tp[2], ad[2], a[3], tp[3], ad[3]]
+    return data

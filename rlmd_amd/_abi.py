@@ -102,6 +102,8 @@ SIGNATURES = {
     "rlmd_lev_workspace_bytes": (I64, [I64, I32]),
     "rlmd_lev_sorted_workspace_bytes": (I64, [I64, I32]),
     "rlmd_lev_sweep_sorted": (C.c_int, [I32, P, I64, I32, I64, I64, C.c_float, P, P, I32, P, I64, P, P, P]),
+    "rlmd_lev_brain_workspace_bytes": (I64, [I64, I32]),
+    "rlmd_lev_brain": (C.c_int, [I32, P, I64, I32, I64, I64, C.c_float, P, C.c_float, P, I32, P, I64, P, P]),
     "rlmd_lev_final_sorted": (C.c_int, [I32, P, I64, I32, I64, I64, C.c_float, P, P, I32, P, I64, P, P, P]),
     "rlmd_lev_coin_sweep": (C.c_int, [P, I64, I32, I64, I64, C.c_float, C.c_float, C.c_float, P, I32, P, I64, P, P,
                                        P]),

@@ -27,8 +27,17 @@
 #include <hipcub/hipcub.hpp>
 #include <math.h>
 
+#include <algorithm>
+#include <vector>
+
 #include "../../include/rlmd_abi.h"
 #include "rlmd_common.h"
+
+#define RLMD_TRY_INT(x)    \
+  do {                     \
+    const int _r = (x);    \
+    if (_r) return _r;     \
+  } while (0)
 
 namespace {
 
@@ -66,10 +75,11 @@ __global__ void __launch_bounds__(kT) lev_advance_kernel(SortedArgs a, int t, fl
 
 // group sums over sorted-descending values s[0, N): all, top = [0, top), adj =
 // [top, N).  pass 0: sums; pass 1: |v - m| and (v - m)^2 with the means m.
-__global__ void __launch_bounds__(kT) lev_sorted_sums_kernel(const float* sorted, int64_t N, int64_t top,
+template <typename VT>
+__global__ void __launch_bounds__(kT) lev_sorted_sums_kernel(const VT* sorted, int64_t N, int64_t top,
                                                              const double* means, int pass, double* part) {
   const int l = blockIdx.y, c = blockIdx.x;
-  const float* s = sorted + (int64_t)l * N;
+  const VT* s = sorted + (int64_t)l * N;
   const int64_t per = (N + kChunks - 1) / kChunks, b0 = c * per, b1 = b0 + per < N ? b0 + per : N;
   double acc[6] = {0, 0, 0, 0, 0, 0};  // pass 0: all, top, adj ; pass 1: |.| all/top/adj, sq all/top/adj
   const double ma = pass ? means[l * 3 + 0] : 0.0, mt = pass ? means[l * 3 + 1] : 0.0,
@@ -100,8 +110,13 @@ __global__ void __launch_bounds__(kT) lev_sorted_sums_kernel(const float* sorted
 }
 
 // pass 0: means of the three groups; pass 1: the table column at step t
-__global__ void lev_sorted_fold_kernel(const float* sorted, int64_t N, int64_t top, int n_lev, const double* part,
-                                       int pass, double* means, const float* levs, float* data, int steps, int t) {
+// rows: table rows per configuration; row0: where the 12 statistics go; the
+// n_extra constants extra[l][*] fill rows row0 + 12 ... (the sweeps' lev row,
+// the big-brain stop / roll rows)
+template <typename VT>
+__global__ void lev_sorted_fold_kernel(const VT* sorted, int64_t N, int64_t top, int n_lev, const double* part,
+                                       int pass, double* means, const float* extra, int n_extra, float* data,
+                                       int rows, int row0, int steps, int t) {
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
   if (l >= n_lev) return;
   double s[6] = {0, 0, 0, 0, 0, 0};
@@ -114,21 +129,73 @@ __global__ void lev_sorted_fold_kernel(const float* sorted, int64_t N, int64_t t
     means[l * 3 + 2] = s[2] / nd;
     return;
   }
-  const float* v = sorted + (int64_t)l * N;
+  const VT* v = sorted + (int64_t)l * N;
   // lower medians: ascending index (n - 1) / 2 of each group, read from the
   // descending order
   auto med = [&](int64_t lo, int64_t n) -> double { return n > 0 ? (double)v[lo + n - 1 - (n - 1) / 2] : NAN; };
-  float col[13] = {(float)means[l * 3 + 0], (float)means[l * 3 + 1], (float)means[l * 3 + 2],
-                   (float)(s[0] / na), (float)(s[1] / nt), (float)(s[2] / nd),
-                   (float)sqrt(s[3] / na), (float)sqrt(s[4] / nt), (float)sqrt(s[5] / nd),
-                   (float)med(0, N), (float)med(0, top), (float)med(top, N - top), levs[l]};
-  for (int r = 0; r < 13; ++r) data[((int64_t)l * 13 + r) * steps + t] = col[r];
+  const float col[12] = {(float)means[l * 3 + 0], (float)means[l * 3 + 1], (float)means[l * 3 + 2],
+                         (float)(s[0] / na), (float)(s[1] / nt), (float)(s[2] / nd),
+                         (float)sqrt(s[3] / na), (float)sqrt(s[4] / nt), (float)sqrt(s[5] / nd),
+                         (float)med(0, N), (float)med(0, top), (float)med(top, N - top)};
+  for (int r = 0; r < 12; ++r) data[((int64_t)l * rows + row0 + r) * steps + t] = col[r];
+  for (int e = 0; e < n_extra; ++e) data[((int64_t)l * rows + row0 + 12 + e) * steps + t] = extra[l * n_extra + e];
 }
 
+// ---------------------------------------------------------------------------
+// big-brain investors (coin_big_brain_lev :270-452, dice_big_brain_lev :741-932):
+// configuration c = (roll, stop) sets each investor's leverage from its own
+// value every step — lev = lev_factor (1 - L / v) with L the stop-loss floor
+// stop * value_0, or, when roll > 0 and v > value_0, the rolling floor
+// value_0 + roll (v - value_0) (coin_optimal_lev :240-267, dice_optimal_lev
+// :704-738) — in the reference's arithmetic (coin f32; dice f64 values, see
+// optimal_lev; this file compiles with FP contraction off).  Per step: the leverages' statistics (rows 12-23, then stop
+// and roll), the value step v = v (1 + lev r), the new leverages, the values'
+// statistics (rows 0-11).
+// ---------------------------------------------------------------------------
+struct BrainArgs {
+  const uint8_t* cat;  // outcome codes [investors][ld]
+  int64_t investors, ld;
+  double ret[3];       // return per outcome code (f32 values for coin, f64 for dice)
+  float value_0, lev_factor;
+  const float* cfg;    // [n_cfg][5]: stop floor value_min, roll, initial leverage, roll > 0, stop level
+  void* val;           // [n_cfg][investors] VT
+  void* lev;           // [n_cfg][investors] VT
+};
+
+// coin (VT float, lev_exp.py:240-267): every quantity f32.  dice (VT double,
+// :704-738, :741-932): outcomes are cast to float64, so values are f64; with
+// roll 0 the leverage is f64 too (f32 lev_factor / value_min against the f64
+// value), with roll > 0 dice_optimal_lev first casts the values to f32 and the
+// leverage is all f32.
+template <typename VT>
+__device__ __forceinline__ VT optimal_lev(VT v, float v0, float vmin, float roll, bool rolling, float lf) {
+  if (!rolling) return (VT)lf * ((VT)1 - (VT)vmin / v);
+  const float vf = (float)v;
+  const float loss = vf <= v0 ? vmin : v0 + roll * (vf - v0);
+  return (VT)(lf * (1.f - loss / vf));
+}
+
+// t == 0: v = value_0 (1 + lev0 r[0]); else v = v (1 + lev r[t]); then lev = optimal(v)
+template <typename VT>
+__global__ void __launch_bounds__(kT) lev_brain_advance_kernel(BrainArgs a, int t) {
+  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
+  const int c = blockIdx.y;
+  if (i >= a.investors) return;
+  const float* k = a.cfg + 5 * c;
+  const int o = a.cat[i * a.ld + t];
+  const VT r = (VT)a.ret[o > 2 ? 2 : o];
+  const int64_t j = (int64_t)c * a.investors + i;
+  VT* val = static_cast<VT*>(a.val);
+  VT* lev = static_cast<VT*>(a.lev);
+  const VT v = t == 0 ? (VT)a.value_0 * ((VT)1 + (VT)k[2] * r) : val[j] * ((VT)1 + lev[j] * r);
+  val[j] = v;
+  lev[j] = optimal_lev<VT>(v, a.value_0, k[0], k[1], k[3] != 0.f, a.lev_factor);
+}
+
+template <typename VT = float>
 size_t sort_temp_bytes(int64_t investors) {
   size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortKeysDescending(nullptr, bytes, (const float*)nullptr, (float*)nullptr,
-                                                    (int)investors);
+  (void)hipcub::DeviceRadixSort::SortKeysDescending(nullptr, bytes, (const VT*)nullptr, (VT*)nullptr, (int)investors);
   return (bytes + 255) & ~(size_t)255;
 }
 
@@ -193,11 +260,11 @@ static int sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investor
                                                            st));
     }
     for (int pass = 0; pass < 2; ++pass) {
-      hipLaunchKernelGGL(lev_sorted_sums_kernel, dim3(kChunks, n_lev), dim3(kT), 0, st, sorted, investors, tp,
+      hipLaunchKernelGGL(lev_sorted_sums_kernel<float>, dim3(kChunks, n_lev), dim3(kT), 0, st, sorted, investors, tp,
                          means, pass, part);
       RLMD_LAUNCH_CHECK();
-      hipLaunchKernelGGL(lev_sorted_fold_kernel, dim3((n_lev + 63) / 64), dim3(64), 0, st, sorted, investors, tp,
-                         n_lev, part, pass, means, small, data_dev, steps, final_only ? 0 : t - 1);
+      hipLaunchKernelGGL(lev_sorted_fold_kernel<float>, dim3((n_lev + 63) / 64), dim3(64), 0, st, sorted, investors,
+                         tp, n_lev, part, pass, means, small, 1, data_dev, 13, 0, steps, final_only ? 0 : t - 1);
       RLMD_LAUNCH_CHECK();
     }
   }
@@ -220,6 +287,96 @@ int rlmd_lev_final_sorted(int32_t kind, const void* outcomes_dev, int64_t invest
                           void* stream) {
   return sweep_sorted(kind, outcomes_dev, investors, horizon, ld, top, value_0, table_host, levs_host, n_lev,
                       workspace, workspace_bytes, stats_dev, values_dev, stream, true);
+}
+
+int64_t rlmd_lev_brain_workspace_bytes(int64_t investors, int32_t n_cfg) {
+  if (investors <= 0 || investors > INT32_MAX || n_cfg <= 0) return -1;
+  const int64_t vals = 3 * (int64_t)n_cfg * investors * 8;  // values, leverages, sorted copy (f64 at most)
+  const int64_t sums = (int64_t)n_cfg * kChunks * 6 * 8 + (int64_t)n_cfg * 3 * 8 + (int64_t)n_cfg * 8 * 4;
+  const int64_t tmp = (int64_t)std::max(sort_temp_bytes<float>(investors), sort_temp_bytes<double>(investors));
+  return ((vals + 255) & ~255ll) + ((sums + 255) & ~255ll) + tmp;
+}
+
+}  // extern "C"
+
+template <typename VT>
+static int lev_brain(const uint8_t* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld, int64_t top,
+                     float value_0, const double* rets3, float lev_factor, const float* cfg_host, int32_t n_cfg,
+                     void* workspace, float* data_dev, hipStream_t st) {
+  const int64_t tp = top < investors ? (top > 0 ? top : 0) : investors;
+  unsigned char* w = static_cast<unsigned char*>(workspace);
+  const int64_t NC = (int64_t)n_cfg * investors;
+  VT* val = reinterpret_cast<VT*>(w);
+  VT* lev = val + NC;
+  VT* sorted = lev + NC;
+  unsigned char* w2 = w + ((3 * NC * 8 + 255) & ~255ll);
+  double* part = reinterpret_cast<double*>(w2);
+  double* means = part + (int64_t)n_cfg * kChunks * 6;
+  float* cfg = reinterpret_cast<float*>(means + (int64_t)n_cfg * 3);  // [n_cfg][5] | extra [n_cfg][2]
+  float* extra = cfg + 5 * n_cfg;
+  const int64_t sums = (int64_t)n_cfg * kChunks * 6 * 8 + (int64_t)n_cfg * 3 * 8 + (int64_t)n_cfg * 8 * 4;
+  void* tmp = w2 + ((sums + 255) & ~255ll);
+  size_t tmp_bytes = sort_temp_bytes<VT>(investors);
+  std::vector<float> ex(2 * (size_t)n_cfg);
+  for (int c = 0; c < n_cfg; ++c) {  // rows 24 / 25: stop level and roll
+    ex[2 * c] = cfg_host[5 * c + 4];
+    ex[2 * c + 1] = cfg_host[5 * c + 1];
+  }
+  RLMD_HIP(hipMemcpyAsync(cfg, cfg_host, sizeof(float) * 5 * n_cfg, hipMemcpyHostToDevice, st));
+  RLMD_HIP(hipMemcpyAsync(extra, ex.data(), sizeof(float) * 2 * n_cfg, hipMemcpyHostToDevice, st));
+  BrainArgs a{};
+  a.cat = outcomes_dev;
+  a.investors = investors;
+  a.ld = ld;
+  for (int q = 0; q < 3; ++q) a.ret[q] = rets3[q];
+  a.value_0 = value_0;
+  a.lev_factor = lev_factor;
+  a.cfg = cfg;
+  a.val = val;
+  a.lev = lev;
+  const dim3 grid_adv((unsigned)((investors + kT - 1) / kT), (unsigned)n_cfg);
+  const int steps = horizon - 1;
+  auto stats = [&](const VT* src, int row0, const float* ext, int n_ext, int t) -> int {
+    for (int c = 0; c < n_cfg; ++c)
+      RLMD_HIP(hipcub::DeviceRadixSort::SortKeysDescending(tmp, tmp_bytes, src + (int64_t)c * investors,
+                                                           sorted + (int64_t)c * investors, (int)investors, 0,
+                                                           (int)(8 * sizeof(VT)), st));
+    for (int pass = 0; pass < 2; ++pass) {
+      hipLaunchKernelGGL(lev_sorted_sums_kernel<VT>, dim3(kChunks, n_cfg), dim3(kT), 0, st, sorted, investors, tp,
+                         means, pass, part);
+      RLMD_LAUNCH_CHECK();
+      hipLaunchKernelGGL(lev_sorted_fold_kernel<VT>, dim3((n_cfg + 63) / 64), dim3(64), 0, st, sorted, investors,
+                         tp, n_cfg, part, pass, means, ext, n_ext, data_dev, 26, row0, steps, t);
+      RLMD_LAUNCH_CHECK();
+    }
+    return 0;
+  };
+  hipLaunchKernelGGL(lev_brain_advance_kernel<VT>, grid_adv, dim3(kT), 0, st, a, 0);
+  RLMD_LAUNCH_CHECK();
+  for (int t = 0; t < steps; ++t) {
+    RLMD_TRY_INT(stats(lev, 12, extra, 2, t));
+    hipLaunchKernelGGL(lev_brain_advance_kernel<VT>, grid_adv, dim3(kT), 0, st, a, t + 1);
+    RLMD_LAUNCH_CHECK();
+    RLMD_TRY_INT(stats(val, 0, nullptr, 0, t));
+  }
+  return 0;
+}
+
+extern "C" {
+
+int rlmd_lev_brain(int32_t f64, const uint8_t* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
+                   int64_t top, float value_0, const double* rets_host3, float lev_factor, const float* cfg_host,
+                   int32_t n_cfg, void* workspace, int64_t workspace_bytes, float* data_dev, void* stream) {
+  RLMD_CHECK(outcomes_dev && rets_host3 && cfg_host && workspace && data_dev, "null argument");
+  RLMD_CHECK(investors > 0 && investors <= INT32_MAX && horizon >= 2 && ld >= horizon, "bad sizes");
+  RLMD_CHECK(n_cfg > 0 && n_cfg <= 4096, "n_cfg out of range");
+  RLMD_CHECK(workspace_bytes >= rlmd_lev_brain_workspace_bytes(investors, n_cfg),
+             "workspace smaller than rlmd_lev_brain_workspace_bytes");
+  if (f64)
+    return lev_brain<double>(outcomes_dev, investors, horizon, ld, top, value_0, rets_host3, lev_factor, cfg_host,
+                             n_cfg, workspace, data_dev, (hipStream_t)stream);
+  return lev_brain<float>(outcomes_dev, investors, horizon, ld, top, value_0, rets_host3, lev_factor, cfg_host, n_cfg,
+                          workspace, data_dev, (hipStream_t)stream);
 }
 
 }  // extern "C"

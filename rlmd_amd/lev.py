@@ -223,3 +223,62 @@ def coin_galaxy_brain_lev(device, ru_min, ru_max, ru_incr, rd_min, rd_max, rd_in
             for k, rd in enumerate(rd_range):
                 data[i, j, k, :] = torch.tensor([pu, ru, rd, pu / rd - (1 - pu) / ru])
     return data.to(torch.device(device))
+
+
+# ---------------------------------------------------------------------------
+# *_big_brain_lev: investors that re-lever from their own value every step
+# ---------------------------------------------------------------------------
+def _brain(device, codes, inv, hor, top, value_0, rets3, lev_factor, stops, rolls, f64):
+    dev = torch.device(device)
+    lf = torch.as_tensor(lev_factor, dtype=torch.float32).reshape(())
+    cfg = []
+    for roll in rolls:  # roll-major, as the reference's data[j = roll, i = stop]
+        for stop in stops:
+            value_min = stop * value_0
+            v0 = torch.tensor(value_0, dtype=torch.float32)
+            # optimal leverage at value_0 (lev_exp.py:240-267, :704-738): the floor is
+            # value_min either way (value_t <= value_0)
+            lev0 = lf * (1 - value_min / v0)
+            cfg.append([float(value_min), float(roll), float(lev0), 1.0 if float(roll) != 0 else 0.0, float(stop)])
+    cfg = np.ascontiguousarray(cfg, dtype=np.float32)
+    n_cfg = len(cfg)
+    lib = _abi.lib()
+    ws = torch.empty(int(lib.rlmd_lev_brain_workspace_bytes(int(inv), n_cfg)), dtype=torch.uint8, device=dev)
+    data = torch.empty((len(rolls), len(stops), 26, hor - 1), dtype=torch.float32, device=dev)
+    # coin: T.where(outcomes == 1, up_r, down_r) is f32; dice's outcomes are f64
+    r3 = np.ascontiguousarray([float(r) if f64 else float(np.float32(r)) for r in rets3], dtype=np.float64)
+    P = _abi.ptr
+    _abi.check(lib.rlmd_lev_brain(1 if f64 else 0, P(codes), int(inv), int(hor), codes.stride(0), int(top), float(value_0),
+                                  r3.ctypes.data, float(lf), cfg.ctypes.data, n_cfg, P(ws), ws.numel(), P(data),
+                                  _abi.stream_ptr()))
+    return data
+
+
+def coin_big_brain_lev(device, outcomes, investors, horizon, top, value_0, up_r, down_r, lev_factor, stop_min,
+                       stop_max, stop_incr, roll_min, roll_max, roll_incr):
+    """lev/lev_exp.py:270-452 on the device (rlmd_lev_brain): data [n_roll,
+    n_stop, 26, horizon - 1] = value statistics (rows 0-11), leverage statistics
+    (12-23), stop, roll.  Outcome 1 up (return up_r), else down_r.  With a
+    retention ratio > 0 the reference's coin_optimal_lev is handed the Python
+    float value_0 for the first leverage and torch.where rejects its bool
+    condition (TypeError); the build applies dice_optimal_lev's reading (the
+    floor at value_0 is the stop-loss), which the reference uses for dice."""
+    dev = torch.device(device)
+    stops = torch.tensor(param_range(stop_min, stop_max, stop_incr), dtype=torch.float32)
+    rolls = torch.tensor(param_range(roll_min, roll_max, roll_incr), dtype=torch.float32)
+    o = torch.as_tensor(outcomes)
+    codes = (o == 1).to(device=dev, dtype=torch.uint8).contiguous()  # code 0 down, 1 up
+    return _brain(dev, codes, int(investors), int(horizon), top, value_0, [float(down_r), float(up_r), float(up_r)],
+                  lev_factor, stops, rolls, False)
+
+
+def dice_big_brain_lev(device, outcomes, investors, horizon, top, value_0, up_r, down_r, mid_r, lev_factor, stop_min,
+                       stop_max, stop_incr, roll_min, roll_max, roll_incr):
+    """lev/lev_exp.py:741-932 on the device: outcomes {0 up, 1 down, 2 mid}; the
+    reference casts them to float64 (:751), so values are f64 (see rlmd_lev_brain)."""
+    dev = torch.device(device)
+    stops = torch.tensor(param_range(stop_min, stop_max, stop_incr), dtype=torch.float32)
+    rolls = torch.tensor(param_range(roll_min, roll_max, roll_incr), dtype=torch.float32)
+    codes = _categorical(outcomes, investors, horizon, dev)
+    return _brain(dev, codes, int(investors), int(horizon), top, value_0, [float(up_r), float(down_r), float(mid_r)],
+                  lev_factor, stops, rolls, True)

@@ -1111,6 +1111,26 @@ def lev_final_fixtures(seed=43):
             out[name + "_rets"] = np.array(rets, dtype=np.float64)
             out[name + "_stats"] = st
             out[name + "_values"] = vals
+        # big-brain investors: coin with retention 0 only (a ratio > 0 raises a
+        # TypeError in the reference's coin_optimal_lev), dice with 0 and > 0
+        for name, inv, hor, top, v0, rets, lf, stop, roll in (
+                ("coinbrain", 600, 24, 9, 100.0, (0.5, -0.4), 1.8, (0.1, 0.5, 0.2), (0.0, 0.0, 0.1)),
+                ("dicebrain", 500, 20, 7, 100.0, (0.5, -0.5, 0.05), 1.6, (0.2, 0.6, 0.2), (0.5, 0.9, 0.2)),
+                ("dicebrain0", 400, 18, 3, 100.0, (0.5, -0.5, 0.05), 1.6, (0.3, 0.3, 0.1), (0.0, 0.0, 0.1))):
+            g = T.Generator().manual_seed(seed + inv + hor)
+            if name == "coinbrain":
+                outc = T.bernoulli(T.full((inv, hor), 0.5), generator=g)
+                fn = lev_exp.coin_big_brain_lev
+            else:
+                u = T.rand((inv, hor), generator=g)
+                outc = T.where(u < 1 / 6, 0.0, T.where(u < 2 / 6, 1.0, 2.0))
+                fn = lev_exp.dice_big_brain_lev
+            with contextlib.redirect_stdout(io.StringIO()):
+                data = fn(T.device("cpu"), outc, inv, hor, top, v0, *rets, T.tensor(lf), *stop, *roll)
+            out[name + "_outcomes"] = outc.numpy().astype(np.float32)
+            out[name + "_args"] = np.array([inv, hor, top, v0, lf, *stop, *roll], dtype=np.float64)
+            out[name + "_rets"] = np.array(rets, dtype=np.float64)
+            out[name + "_data"] = data.numpy()
         grid = (0.1, 0.5, 0.1, 0.1, 0.4, 0.1, 0.4, 0.6, 0.1)  # len(rd) <= len(ru): the reference indexes rd by ru's size
         out["galaxy_args"] = np.array(grid, dtype=np.float64)
         out["galaxy"] = lev_exp.coin_galaxy_brain_lev(T.device("cpu"), *grid).numpy()

@@ -84,3 +84,40 @@ def test_galaxy_brain_matches_reference():
 
     got = lev.coin_galaxy_brain_lev("cpu", *ZF["galaxy_args"]).numpy()
     np.testing.assert_array_equal(got, ZF["galaxy"])
+
+
+BRAIN = ["coinbrain", "dicebrain", "dicebrain0"]
+
+
+def close26(d, ref, rtol):
+    """close_table for the big-brain tables (value rows 0-11, leverage rows 12-23)."""
+    idx = [0, 1, 2] * 4
+    means = np.concatenate([ref[:, :, idx, :], ref[:, :, [12 + i for i in idx], :], ref[:, :, 24:26, :]], 2)
+    disp = np.zeros(26, bool)
+    disp[3:9] = disp[15:21] = True
+    tol = rtol * np.abs(ref) + rtol * np.abs(means) * disp[None, None, :, None]
+    return np.abs(d - ref) <= tol + 1e-30
+
+
+def brain_inputs(case):
+    a, rets = ZF[case + "_args"], ZF[case + "_rets"]
+    inv, hor, top, v0, lf = int(a[0]), int(a[1]), int(a[2]), a[3], a[4]
+    o = ZF[case + "_outcomes"]
+    return inv, hor, top, v0, lf, tuple(a[5:8]), tuple(a[8:11]), rets, o
+
+
+@pytest.mark.parametrize("case", BRAIN)
+def test_brain_oracle_matches_reference(case):
+    """coin_big_brain_lev (roll 0: a ratio > 0 raises TypeError in the reference)
+    and dice_big_brain_lev (f64 values; roll 0 and > 0) run by the reference:
+    the oracle within 2e-6 (dispersion rows 2e-6 of their group mean)."""
+    inv, hor, top, v0, lf, st, rl, rets, o = brain_inputs(case)
+    stops = np.array(olev.param_range(*st), np.float32)
+    rolls = np.array(olev.param_range(*rl), np.float32)
+    if case == "coinbrain":
+        d = olev.brain_lev((o == 1).astype(np.int64), [np.float32(rets[1]), np.float32(rets[0]), np.float32(rets[0])],
+                           top, v0, np.float32(lf), stops, rolls)
+    else:
+        d = olev.brain_lev(o.astype(np.int64), list(rets), top, v0, np.float32(lf), stops, rolls, f64=True)
+    assert d.shape == ZF[case + "_data"].shape
+    assert close26(d, ZF[case + "_data"], 2e-6).all()

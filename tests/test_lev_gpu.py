@@ -201,3 +201,46 @@ def test_fixed_final_matches_reference(case):
     disp = (np.arange(12) >= 3) & (np.arange(12) < 9)
     tol = 1e-5 * np.abs(ref) + 1e-5 * np.abs(means) * disp[None, :]
     assert (np.abs(st[:, :12] - ref) <= tol + 1e-30).all(), (st[:, :12], ref)
+
+
+from tests.test_lev_cpu import BRAIN, brain_inputs, close26  # noqa: E402
+
+
+@pytest.mark.parametrize("case", BRAIN)
+def test_big_brain_matches_reference(case):
+    """rlmd_lev_brain vs the reference's coin / dice big-brain tables: 2e-6 (the
+    same arithmetic per investor; f64 group sums of the sorted values)."""
+    from rlmd_amd import lev
+
+    inv, hor, top, v0, lf, st, rl, rets, o = brain_inputs(case)
+    fn = lev.coin_big_brain_lev if case == "coinbrain" else lev.dice_big_brain_lev
+    d = fn("cuda:0", torch.from_numpy(o), inv, hor, top, v0, *rets, torch.tensor(lf), *st, *rl).cpu().numpy()
+    ok = close26(d, ZF[case + "_data"], 2e-6)
+    assert ok.all(), np.argwhere(~ok)[:5]
+
+
+@pytest.mark.parametrize("case,inv,hor", [("coin", 30000, 60), ("dice", 20000, 50)])
+def test_big_brain_rolling_matches_oracle(case, inv, hor):
+    """Larger matrices with retention ratios > 0 (coin included: the build's
+    reading of the reference's TypeError path) against oracle/lev.py."""
+    from oracle import lev as olev
+    from rlmd_amd import lev
+
+    rng = np.random.default_rng(inv)
+    u = rng.random((inv, hor))
+    stops, rolls = (0.1, 0.5, 0.2), (0.0, 0.9, 0.3)
+    if case == "coin":
+        o = (u < 0.5).astype(np.float32)
+        d = lev.coin_big_brain_lev("cuda:0", o, inv, hor, 30, 100.0, 0.5, -0.4, 1.8, *stops, *rolls).cpu().numpy()
+        od = olev.brain_lev((o == 1).astype(np.int64), [np.float32(-0.4), np.float32(0.5), np.float32(0.5)], 30, 100.0,
+                            np.float32(1.8), np.array(olev.param_range(*stops), np.float32),
+                            np.array(olev.param_range(*rolls), np.float32))
+    else:
+        o = np.where(u < 1 / 6, 0, np.where(u < 2 / 6, 1, 2)).astype(np.float32)
+        d = lev.dice_big_brain_lev("cuda:0", o, inv, hor, 30, 100.0, 0.5, -0.5, 0.05, 1.6, *stops, *rolls).cpu().numpy()
+        od = olev.brain_lev(o.astype(np.int64), [0.5, -0.5, 0.05], 30, 100.0, np.float32(1.6),
+                            np.array(olev.param_range(*stops), np.float32),
+                            np.array(olev.param_range(*rolls), np.float32), f64=True)
+    assert d.shape == od.shape
+    ok = close26(d, od, 2e-6)
+    assert ok.all(), np.argwhere(~ok)[:5]
