@@ -39,7 +39,7 @@ namespace {
 using namespace actrows;
 
 template <int H1P, int NB, int SP>
-__global__ void __launch_bounds__(256) fused_act_kernel(FusedActArgs a) {
+__global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) fused_act_kernel(FusedActArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   act_rows<H1P, NB, SP>(
       a, smem, [] {},

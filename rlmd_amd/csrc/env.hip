@@ -685,7 +685,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
 // few multiply-adds separately where act.hip fuses them (<= 1 ulp of an action).
 // ---------------------------------------------------------------------------
 template <int FAM, int NG, int H1P, int NB, int SP>
-__global__ void __launch_bounds__(256) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
+__global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
                                                       StatFold sf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -887,6 +887,210 @@ __global__ void __launch_bounds__(256) eval_market_step_kernel(EnvParams P, cons
   } else {
     P.wealth[lane] = o.W;
     P.time[lane] = t + 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// market evaluation as ONE launch: each 16-lane workgroup runs its lanes' whole
+// test slice in a day loop — the deterministic policy (the arithmetic of
+// rlmd_act_rows.h's body at one 16-row MFMA tile: layer 1 on the f32 MFMA, bf16
+// layer 2, DPP head sums, tanh) and then, on the lane's own thread, the market
+// step of eval_market_step_kernel with the action in registers and the next
+// observation written straight into LDS.  W1 / b1 are staged into LDS once,
+// the head weights and biases sit in registers for the whole episode, and the
+// fc2 fragments too where they fit (SAC 256/256: 32 x 16 B per lane); only the
+// price rows are read per day.  Replaces the host loop of one acting and one
+// step launch per day.  The loop ends when every lane of the block is done.
+// ---------------------------------------------------------------------------
+template <int NG, typename AT, int H1P, int NB, int SP>
+__global__ void __launch_bounds__(256) eval_market_loop_kernel(rlmd::FusedActArgs a, EnvParams P, int T,
+                                                               double clip_lo, double clip_hi, double* reward_out,
+                                                               int32_t* steps_out, double* risk_out, uint8_t* live_io,
+                                                               float* obs_out) {
+  using namespace rlmd::actrows;
+  constexpr int kR = 16;
+  constexpr int HP = H1P + 8;
+  constexpr int NT = L1Tiles<H1P>::NT, NTP = L1Tiles<H1P>::NTP;
+  constexpr int nS = H1P / 32;
+  constexpr bool kRegW2 = NB * nS <= 32;
+  __shared__ __attribute__((aligned(16))) unsigned short h1s[kR * HP];
+  __shared__ float part[4 * kR * 2 * kMaxA];
+  __shared__ float w1s[SP * 16 * NTP + H1P];  // w1g [SP][16][NTP], then b1 [H1P]
+  __shared__ float obs_s[kR * SP];
+  __shared__ double risk_s[kR * 8];  // the lanes' last risk rows (risk_dim <= 8), written out once
+  __shared__ double sink_s[kR];
+  float* const b1s = w1s + SP * 16 * NTP;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int row0 = blockIdx.x * kR;
+  const rlmd::NetOff& o = a.off;
+  const int S = a.S, A = a.A, H1 = a.H1, H2 = a.H2;
+  const int nh = a.algo == RLMD_SAC ? 2 * A : A;
+  // ---- once per episode: head weights / fc2 bias of this wave's columns, the
+  //      head biases, W1 / b1 / the first observations into LDS, lane state
+  const int col0 = 16 * NB * wave;
+  float hw[NB][2 * kMaxA];
+  float b2v[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int c = col0 + 16 * nb + (lane & 15);
+    const bool live = c < H2;
+    b2v[nb] = live ? a.params[o.b2 + c] : 0.f;
+#pragma unroll
+    for (int h = 0; h < 2 * kMaxA; ++h) {
+      const int64_t base = h < A ? o.w3 + (int64_t)h * H2 : o.w4 + (int64_t)(h - A) * H2;
+      hw[nb][h] = live && h < nh ? a.params[base + c] : 0.f;
+    }
+  }
+  const bf16x8* wf = reinterpret_cast<const bf16x8*>(a.w2bf) + (int64_t)(NB * wave) * nS * 64 + lane;
+  bf16x8 wreg[kRegW2 ? NB : 1][kRegW2 ? nS : 1];
+  if constexpr (kRegW2) {
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int s = 0; s < nS; ++s) wreg[nb][s] = wf[(nb * nS + s) * 64];
+  }
+  const bool mine = tid < kR && row0 + tid < a.n;
+  const int b = row0 + tid;
+  float mu_b[kMaxA], ls_b[kMaxA];
+#pragma unroll
+  for (int j = 0; j < kMaxA; ++j) {
+    mu_b[j] = mine && j < A ? a.params[o.b3 + j] : 0.f;
+    ls_b[j] = mine && j < A && a.algo == RLMD_SAC ? a.params[o.b4 + j] : 0.f;
+  }
+  bool alive = false;
+  double w = 0.0, last_r = 0.0;
+  int t = 0, start = 0, last_t = 0;
+  uint32_t ep = 0;
+  if (mine) {
+    alive = live_io[b] != 0;
+    w = P.wealth[b];
+    t = P.time[b];
+    start = P.start[b];
+    ep = P.episode[b];
+    last_r = reward_out[b];
+    last_t = steps_out[b];
+  }
+  for (int e = tid; e < SP * 16 * NTP + H1P; e += 256) {
+    const bool isb = e >= SP * 16 * NTP;
+    const int k = e / (16 * NTP), jt = e - k * (16 * NTP);
+    const int jj = jt / NTP, tt = jt - jj * NTP;
+    const int c = isb ? e - SP * 16 * NTP : 16 * tt + jj;
+    const bool ok = c < H1 && (isb || (tt < NT && k < S));
+    w1s[e] = ok ? a.params[o.w1 + (isb ? H1 * S + c : c * S + k)] : 0.f;
+  }
+  for (int e = tid; e < kR * SP; e += 256) {
+    const int r = e / SP, k = e - r * SP;
+    obs_s[e] = (k < S && row0 + r < a.n) ? a.obs[(int64_t)(row0 + r) * S + k] : 0.f;
+  }
+  if (!__syncthreads_or(alive)) return;
+  if (mine && risk_out)
+    for (int k = 0; k < P.risk_dim; ++k) risk_s[tid * 8 + k] = risk_out[(int64_t)b * P.risk_dim + k];
+  const int j = lane & 15, kl = lane >> 4;
+  for (int day = 0; day < T; ++day) {
+    // today's first price row is action-independent: its load is issued now and
+    // lands under the policy forward (the step's own read then hits the cache)
+    double pf = 0.0;
+    if (alive) pf = market_obs(P, b, start, ep, t, 0);
+    // ---- layer 1: wave w computes tiles w, w + 4, ... for the 16 rows
+    for (int tt = wave; tt < NT; tt += 4) {
+      f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < SP / 4; ++ks)
+        h = __builtin_amdgcn_mfma_f32_16x16x4f32(w1s[((4 * ks + kl) * 16 + j) * NTP + tt], obs_s[j * SP + 4 * ks + kl],
+                                                 h, 0, 0, 0);
+      const f32x4 bias = *reinterpret_cast<const f32x4*>(&b1s[16 * tt + 4 * kl]);
+      uint2 pk;
+      pk.x = (uint32_t)f2bf_rne(fmaxf(h[0] + bias[0], 0.f)) | ((uint32_t)f2bf_rne(fmaxf(h[1] + bias[1], 0.f)) << 16);
+      pk.y = (uint32_t)f2bf_rne(fmaxf(h[2] + bias[2], 0.f)) | ((uint32_t)f2bf_rne(fmaxf(h[3] + bias[3], 0.f)) << 16);
+      *reinterpret_cast<uint2*>(&h1s[j * HP + 16 * tt + 4 * kl]) = pk;
+    }
+    __syncthreads();
+    // ---- layer 2: 16 rows x 16 NB columns per wave, K = H1P in steps of 32
+    f32x4 acc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int kq = 8 * (lane >> 4);
+#pragma unroll
+    for (int s = 0; s < nS; ++s) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(&h1s[j * HP + 32 * s + kq]);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        bf16x8 bf;
+        if constexpr (kRegW2) bf = wreg[nb][s];
+        else bf = wf[(nb * nS + s) * 64];
+        acc[nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[nb], 0, 0, 0);
+      }
+    }
+    // ---- relu(h2 + b2) . heads, partial per row over this wave's columns
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg) {
+      float ph[2 * kMaxA];
+#pragma unroll
+      for (int h = 0; h < 2 * kMaxA; ++h) ph[h] = 0.f;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const float v = fmaxf(acc[nb][rg] + b2v[nb], 0.f);
+#pragma unroll
+        for (int h = 0; h < 2 * kMaxA; ++h) ph[h] = fmaf(v, hw[nb][h], ph[h]);
+      }
+#pragma unroll
+      for (int h = 0; h < 2 * kMaxA; ++h)
+        if (h < nh) ph[h] = rlmd_row16_sum(ph[h]);
+      if ((lane & 15) == 0) {
+        const int r = 4 * (lane >> 4) + rg;
+#pragma unroll
+        for (int h = 0; h < 2 * kMaxA; ++h)
+          if (h < nh) part[(wave * kR + r) * 2 * kMaxA + h] = ph[h];
+      }
+    }
+    __syncthreads();
+    // ---- per lane: the deterministic action (eval_next_action), the market step
+    if (alive) {
+      sink_s[tid] = pf;
+      float acts[kMaxA] = {0.f, 0.f};
+#pragma unroll
+      for (int jj = 0; jj < kMaxA; ++jj) {
+        if (jj >= A) break;
+        float mu = mu_b[jj], ls_raw = 0.f;
+        for (int q = 0; q < 4; ++q) mu += part[(q * kR + tid) * 2 * kMaxA + jj];
+        if (a.algo == RLMD_SAC) {
+          ls_raw = ls_b[jj];
+          for (int q = 0; q < 4; ++q) ls_raw += part[(q * kR + tid) * 2 * kMaxA + A + jj];
+          const rlmd::PolicyComp pc = rlmd::policy_comp(a.dist, mu, ls_raw, 0.f, a.ls_min, a.ls_max);
+          acts[jj] = tanhf(pc.mu) * a.max_action;
+        } else {
+          acts[jj] = tanhf(mu) * a.max_action;
+        }
+      }
+      auto act = [&](int i) -> AT {
+        const double v = (double)(i == 0 ? acts[0] : acts[1]);
+        if (sizeof(AT) == 4) return (AT)v;
+        return (AT)fmin(fmax(v, clip_lo), clip_hi);
+      };
+      const StepOut so = env_step_lane<RLMD_MARKET, NG, AT>(
+          P, b, w, t, start, ep, act, [&](int) { return 0.0; },
+          [&](int k, double v) { obs_s[tid * SP + k] = (float)v; },
+          [&](int k, double v) { risk_s[tid * 8 + k] = v; });
+      last_r = so.reward;
+      last_t = t;
+      if (so.done) {
+        alive = false;
+      } else {
+        w = so.W;
+        ++t;
+      }
+    }
+    if (!__syncthreads_or(alive)) break;
+  }
+  if (mine) {
+    P.wealth[b] = w;
+    P.time[b] = t;
+    reward_out[b] = last_r;
+    steps_out[b] = last_t;
+    live_io[b] = alive ? 1 : 0;
+    for (int k = 0; k < S; ++k) obs_out[(int64_t)b * S + k] = obs_s[tid * SP + k];
+    if (risk_out)
+      for (int k = 0; k < P.risk_dim; ++k) risk_out[(int64_t)b * P.risk_dim + k] = risk_s[tid * 8 + k];
   }
 }
 
@@ -1156,6 +1360,46 @@ int env_market_eval_step(rlmd_env_t env, const float* actions, int window, doubl
   }
 #undef MSTEP
   RLMD_LAUNCH_CHECK();
+  return 0;
+}
+
+// the whole market evaluation in one launch (eval_market_loop_kernel) for the
+// acting shapes with an instantiation; *launched = false leaves it to the
+// caller's per-day loop.  Off with the acting + env fusion (RLMD_NO_FUSED_ENV=1,
+// rlmd_train_set_fused(0)).
+int env_act_market_eval(rlmd_env_t env, const FusedActArgs& a, int h1p, int nb, int T, int window, double lo,
+                        double hi, float* obs, double* reward, int32_t* steps, double* risk, uint8_t* live,
+                        hipStream_t stream, bool* launched) {
+  *launched = false;
+  if (g_fuse_env < 0) g_fuse_env = getenv("RLMD_NO_FUSED_ENV") != nullptr ? 0 : 1;
+  const bool off = g_fuse_env == 0;
+  const EnvParams& P = env->P;
+  const int sp = a.S <= 8 ? 8 : 16;
+  if (off || P.fam != RLMD_MARKET || a.n != P.n_lanes || a.S > 16 || a.A > actrows::kMaxA || P.risk_dim > 8 ||
+      !((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5)))
+    return 0;
+  const dim3 grid((P.n_lanes + 15) / 16), block(256);
+#define MLOOP(NG, AT, H, B, SPV)                                                                                   \
+  hipLaunchKernelGGL((eval_market_loop_kernel<NG, AT, H, B, SPV>), grid, block, 0, stream, a, env->P, T, lo, hi, \
+                     reward, steps, risk, live, obs)
+#define MLOOP_SHAPE(NG, AT)                   \
+  {                                           \
+    if (h1p == 256 && sp == 8) MLOOP(NG, AT, 256, 4, 8);       \
+    else if (h1p == 256) MLOOP(NG, AT, 256, 4, 16);            \
+    else if (sp == 8) MLOOP(NG, AT, 416, 5, 8);                \
+    else MLOOP(NG, AT, 416, 5, 16);                            \
+  }
+  if (P.n == 1) {
+    if (window) MLOOP_SHAPE(1, double)
+    else MLOOP_SHAPE(1, float)
+  } else {
+    if (window) MLOOP_SHAPE(0, double)
+    else MLOOP_SHAPE(0, float)
+  }
+#undef MLOOP_SHAPE
+#undef MLOOP
+  RLMD_LAUNCH_CHECK();
+  *launched = true;
   return 0;
 }
 

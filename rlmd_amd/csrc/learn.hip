@@ -995,6 +995,17 @@ int rlmd_eval_market(rlmd_env_t env, rlmd_agent_t ag, const int32_t* start_dev, 
   RLMD_TRY(rlmd::env_market_eval_reset(env, start_dev, obs_dev, reward_dev, steps_dev, live_dev, st));
   const int T = rlmd::env_episode_steps(env);
   RLMD_TRY(rlmd::refresh_copies(ag, st));
+  if (rlmd::fused_act_supported(ag->cfg)) {  // the whole test slice in one launch
+    int h1p = 0, nb = 0;
+    rlmd::actrows::fused_shape(ag->cfg, h1p, nb);
+    const rlmd::FusedActArgs fa =
+        rlmd::fused_act_args(ag->cfg, obs_dev, N, actions_dev, ag->params + ag->off_actor, ag->actor,
+                             (const unsigned short*)rlmd::copy_wc(ag, rlmd::SLOT_ACTOR), 1, 0, 0, nullptr);
+    bool launched = false;
+    RLMD_TRY(rlmd::env_act_market_eval(env, fa, h1p, nb, T, window ? 1 : 0, lo, hi, obs_dev, reward_dev, steps_dev,
+                                       risk_dev, live_dev, st, &launched));
+    if (launched) return 0;
+  }
   for (int t = 0; t < T; ++t) {
     RLMD_TRY(rlmd::agent_act(ag, obs_dev, N, actions_dev, 1, 0, nullptr, st, true));  // eval_next_action
     RLMD_TRY(rlmd::env_market_eval_step(env, actions_dev, window ? 1 : 0, lo, hi, obs_dev, reward_dev, steps_dev,

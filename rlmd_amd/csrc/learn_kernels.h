@@ -261,6 +261,11 @@ FusedActArgs fused_act_args(const rlmd_agent_cfg& c, const float* obs, int64_t n
 // h1p / nb / sp: the acting shape).  Returns 1 (nothing launched) when this env /
 // net combination has no fused instantiation.
 bool env_act_fusable(rlmd_env_t env);
+// env.hip: rlmd_eval_market's day loop in one launch (eval_market_loop_kernel);
+// *launched = false when the env / net shapes have no instantiation.
+int env_act_market_eval(rlmd_env_t env, const FusedActArgs& a, int h1p, int nb, int T, int window, double lo,
+                        double hi, float* obs, double* reward, int32_t* steps, double* risk, uint8_t* live,
+                        hipStream_t stream, bool* launched);
 int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step, const FusedActArgs& a,
                   int h1p, int nb, int sp, float* obs, double* ep_stats, hipStream_t stream, hipEvent_t ev_start,
                   hipEvent_t ev_stop, bool* launched);

@@ -158,3 +158,74 @@ def test_trainer_evaluate_market(golden, dev):
     assert ev["steps"].min() >= 1 and ev["steps"].max() <= 15
     assert np.isfinite(ev["reward"]).all() and np.isfinite(ev["stats"]).all()
     assert ev["stats"].shape == (14,)
+
+
+@pytest.mark.parametrize("algo,h1,h2", [("SAC", 256, 256), ("TD3", 400, 300)])
+@pytest.mark.parametrize("inv,n,d", [("A", 1, 1), ("B", 1, 5), ("A", 2, 3)])
+@pytest.mark.parametrize("window", [False, True])
+def test_eval_market_one_launch_matches_day_loop(golden, dev, algo, h1, h2, inv, n, d, window):
+    """rlmd_eval_market's one-launch form (eval_market_loop_kernel: bf16 policy +
+    market step per lane, a day loop in the kernel) against the per-day host loop
+    of fused acting + step launches (rlmd_train_set_fused(0)) on the same bf16
+    agent: the same arithmetic, so rewards, steps and risk are bit-equal; D1 and
+    Dx (S = 5, 9, 10: both LDS observation pitches), one and two assets, float32
+    and (inside the action window) float64 actions, ragged 16-lane blocks, shuffled
+    slices."""
+    from rlmd_amd import _abi
+    from rlmd_amd.agent import DeviceAgent
+    from rlmd_amd.trainer import market_evaluate
+
+    prices = golden("market.npz")["prices"][:, :n]
+    S, A = 4 + d * n, n + (1 if inv == "B" else 0)
+    ag = DeviceAgent(algo, S, A, h1, h2, 16, 8, precision="bf16", seed=5, device=dev)
+    test_days = 40
+    starts = np.random.default_rng(7).integers(0, prices.shape[0] - test_days - d - 1, size=203)
+    cum, warm, sw = (50, 10, 100) if window else (500, 10, 100)
+    lib = _abi.lib()
+    outs = []
+    try:
+        for fused in (1, 0):
+            lib.rlmd_train_set_fused(fused)
+            outs.append(market_evaluate(ag, prices, inv, d, test_days, starts, cum, warm, sw, shuffle_days=3, seed=11,
+                                        device=dev))
+    finally:
+        lib.rlmd_train_set_fused(1)
+    a, b = outs
+    np.testing.assert_array_equal(a["steps"], b["steps"])
+    np.testing.assert_array_equal(a["reward"], b["reward"])
+    np.testing.assert_array_equal(a["risk"], b["risk"])
+    np.testing.assert_array_equal(a["stats"], b["stats"])
+    assert a["steps"].max() == test_days and np.isfinite(a["reward"]).all()
+
+
+def test_eval_market_one_launch_time(dev):
+    """C4's evaluation event (100 episodes x 250 test days, SAC 256/256 bf16,
+    Market_InvA_D1) on a synthetic 9,167-day table: the one-launch form and the
+    per-day loop, timed with events; the one-launch form must be faster."""
+    from rlmd_amd import _abi
+    from rlmd_amd.agent import DeviceAgent
+    from rlmd_amd.trainer import market_evaluate
+
+    rng = np.random.default_rng(3)
+    prices = 100.0 * np.exp(np.cumsum(0.01 * rng.standard_normal((9167, 1)), axis=0))
+    ag = DeviceAgent("SAC", 5, 1, 256, 256, 16, 8, precision="bf16", seed=1, device=dev)
+    starts = rng.integers(0, 9167 - 260, size=100)
+    lib = _abi.lib()
+    ms = {}
+    try:
+        for fused in (1, 0):
+            lib.rlmd_train_set_fused(fused)
+            market_evaluate(ag, prices, "A", 1, 250, starts, 5000, 10, 100, device=dev)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                out = market_evaluate(ag, prices, "A", 1, 250, starts, 5000, 10, 100, device=dev)
+            e1.record()
+            torch.cuda.synchronize()
+            ms[fused] = e0.elapsed_time(e1) / 5
+            assert out["steps"].max() == 250
+    finally:
+        lib.rlmd_train_set_fused(1)
+    print(f"C4 eval event: one launch {ms[1]:.3f} ms, per-day loop {ms[0]:.3f} ms")
+    assert ms[1] < ms[0]
