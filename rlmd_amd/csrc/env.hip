@@ -189,6 +189,18 @@ struct NoDoneHook {
   __device__ void operator()(const StepOut&) const {}
 };
 
+// market: the action-independent relative prices obs(t, k) / obs(0, k) - 1 of a
+// step, when a caller has them precomputed (kOn); otherwise read in the step
+struct NoMrel {
+  static constexpr bool kOn = false;
+  __device__ double operator()(int) const { return 0.0; }
+};
+struct MrelRow {
+  static constexpr bool kOn = true;
+  const double* row;
+  __device__ double operator()(int k) const { return row[k]; }
+};
+
 // One env step for one lane.  `act(i)` yields action i as AT, `draw(j)` the
 // j-th uniform/normal.  Writes state element k through st(k, v) and risk
 // element k through rk(k, v).
@@ -203,10 +215,10 @@ struct NoDoneHook {
 // only its own code; NG > 0 fixes n_gambles / n_assets at compile time (the
 // n == 1 configurations), NG == 0 reads it from P.
 template <int FAM, int NG, typename AT, typename ActF, typename DrawF, typename StF, typename RkF,
-          typename DoneF = NoDoneHook>
+          typename DoneF = NoDoneHook, typename MrelF = NoMrel>
 __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, double w0, int t,
                                         int start, uint32_t ep, ActF act, DrawF draw, StF st,
-                                        RkF rk, DoneF on_done = DoneF{}) {
+                                        RkF rk, DoneF on_done = DoneF{}, MrelF mrel = MrelF{}) {
   constexpr FamConst C = fam_const(FAM);
   constexpr int fam = FAM;
   const int inv = P.inv, n = NG ? NG : P.n;
@@ -256,6 +268,7 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
       if (fam == RLMD_COIN) return coin_outcome(draw(j));
       if (fam == RLMD_DICE) return dice_value(dice_index(draw(j)));
       if (fam == RLMD_GBM) return (kGbmDrift - kGbmVol * kGbmVol / 2) + kGbmVol * draw(j);
+      if constexpr (MrelF::kOn) return mrel(j);
       return market_obs(P, lane, start, ep, t, j) / market_obs(P, lane, start, ep, 0, j) - 1.0;
     };
     auto lev_of = [&](int j) -> double {
@@ -329,7 +342,8 @@ __device__ inline StepOut env_step_lane(const EnvParams& P, uint32_t lane, doubl
   } else if (fam == RLMD_MARKET) {
     const int m = P.obs_days * n;
     for (int k = 0; k < m; ++k)
-      put(4 + k, market_obs(P, lane, start, ep, t, k) / market_obs(P, lane, start, ep, 0, k) - 1.0);
+      put(4 + k, MrelF::kOn ? mrel(k)
+                            : market_obs(P, lane, start, ep, t, k) / market_obs(P, lane, start, ep, 0, k) - 1.0);
   } else {
     for (int j = 0; j < n; ++j) {
       double r;
@@ -918,7 +932,8 @@ __global__ void __launch_bounds__(256) eval_market_loop_kernel(rlmd::FusedActArg
   __shared__ float w1s[SP * 16 * NTP + H1P];  // w1g [SP][16][NTP], then b1 [H1P]
   __shared__ float obs_s[kR * SP];
   __shared__ double risk_s[kR * 8];  // the lanes' last risk rows (risk_dim <= 8), written out once
-  __shared__ double sink_s[kR];
+  __shared__ double p0_s[kR * 16];   // the episode's first observed prices obs(0, k), k < m <= 16
+  __shared__ double mrel_s[2 * kR * 16];  // obs(t, k) / obs(0, k) - 1, double-buffered by day parity
   float* const b1s = w1s + SP * 16 * NTP;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * kR;
@@ -985,26 +1000,51 @@ __global__ void __launch_bounds__(256) eval_market_loop_kernel(rlmd::FusedActArg
   if (!__syncthreads_or(alive)) return;
   if (mine && risk_out)
     for (int k = 0; k < P.risk_dim; ++k) risk_s[tid * 8 + k] = risk_out[(int64_t)b * P.risk_dim + k];
+  const int m = P.obs_days * (NG ? NG : P.n);  // observed prices per state (<= 16: host check)
+  // wave 1's threads 64 + r precompute lane r's relative prices; p0_s is theirs
+  const bool pre = tid >= 64 && tid < 64 + kR && row0 + tid - 64 < a.n && live_io[row0 + tid - 64] != 0;
+  const int r1 = tid - 64, b1 = row0 + r1;
+  int t1 = 0, start1 = 0;
+  uint32_t ep1 = 0;
+  if (pre) {
+    t1 = P.time[b1];
+    start1 = P.start[b1];
+    ep1 = P.episode[b1];
+    for (int k = 0; k < m; ++k) p0_s[r1 * 16 + k] = market_obs(P, b1, start1, ep1, 0, k);
+  }
+  auto mrel_fill = [&](int tday, int par) {
+    double* dst = mrel_s + (par * kR + r1) * 16;
+    for (int k = 0; k < m; ++k) dst[k] = market_obs(P, b1, start1, ep1, tday, k) / p0_s[r1 * 16 + k] - 1.0;
+  };
+  if (pre && t1 <= T) mrel_fill(t1, 0);
+  __syncthreads();
+
   const int j = lane & 15, kl = lane >> 4;
   for (int day = 0; day < T; ++day) {
     // today's first price row is action-independent: its load is issued now and
     // lands under the policy forward (the step's own read then hits the cache)
-    double pf = 0.0;
-    if (alive) pf = market_obs(P, b, start, ep, t, 0);
-    // ---- layer 1: wave w computes tiles w, w + 4, ... for the 16 rows
-    for (int tt = wave; tt < NT; tt += 4) {
-      f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool probe = day == 10;
+    if (probe) RLMD_TSE(0, __builtin_amdgcn_s_memtime());
+    // ---- layer 1: wave w computes tiles w, w + 4, ... for the 16 rows (all of a
+    //      wave's tiles issued together)
 #pragma unroll
-      for (int ks = 0; ks < SP / 4; ++ks)
-        h = __builtin_amdgcn_mfma_f32_16x16x4f32(w1s[((4 * ks + kl) * 16 + j) * NTP + tt], obs_s[j * SP + 4 * ks + kl],
-                                                 h, 0, 0, 0);
-      const f32x4 bias = *reinterpret_cast<const f32x4*>(&b1s[16 * tt + 4 * kl]);
-      uint2 pk;
-      pk.x = (uint32_t)f2bf_rne(fmaxf(h[0] + bias[0], 0.f)) | ((uint32_t)f2bf_rne(fmaxf(h[1] + bias[1], 0.f)) << 16);
-      pk.y = (uint32_t)f2bf_rne(fmaxf(h[2] + bias[2], 0.f)) | ((uint32_t)f2bf_rne(fmaxf(h[3] + bias[3], 0.f)) << 16);
-      *reinterpret_cast<uint2*>(&h1s[j * HP + 16 * tt + 4 * kl]) = pk;
+    for (int q = 0; q < (NT + 3) / 4; ++q) {
+      const int tt = wave + 4 * q;
+      if (NT % 4 == 0 || tt < NT) {  // no branch between the reads where 4 | NT
+        f32x4 h = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < SP / 4; ++ks)
+          h = __builtin_amdgcn_mfma_f32_16x16x4f32(w1s[((4 * ks + kl) * 16 + j) * NTP + tt],
+                                                   obs_s[j * SP + 4 * ks + kl], h, 0, 0, 0);
+        const f32x4 bias = *reinterpret_cast<const f32x4*>(&b1s[16 * tt + 4 * kl]);
+        uint2 pk;
+        pk.x = (uint32_t)f2bf_rne(fmaxf(h[0] + bias[0], 0.f)) | ((uint32_t)f2bf_rne(fmaxf(h[1] + bias[1], 0.f)) << 16);
+        pk.y = (uint32_t)f2bf_rne(fmaxf(h[2] + bias[2], 0.f)) | ((uint32_t)f2bf_rne(fmaxf(h[3] + bias[3], 0.f)) << 16);
+        *reinterpret_cast<uint2*>(&h1s[j * HP + 16 * tt + 4 * kl]) = pk;
+      }
     }
     __syncthreads();
+    if (probe) RLMD_TSE(1, __builtin_amdgcn_s_memtime());
     // ---- layer 2: 16 rows x 16 NB columns per wave, K = H1P in steps of 32
     f32x4 acc[NB];
 #pragma unroll
@@ -1044,9 +1084,13 @@ __global__ void __launch_bounds__(256) eval_market_loop_kernel(rlmd::FusedActArg
       }
     }
     __syncthreads();
+    if (probe) RLMD_TSE(2, __builtin_amdgcn_s_memtime());
     // ---- per lane: the deterministic action (eval_next_action), the market step
+    // wave 1 (idle while wave 0 steps): tomorrow's relative prices, read by wave 0
+    // after the end-of-day barrier (the lane's day index is t0 + day + 1 while it
+    // is live; rows past the last step are never read)
+    if (pre && t1 + day + 1 <= T) mrel_fill(t1 + day + 1, (day + 1) & 1);
     if (alive) {
-      sink_s[tid] = pf;
       float acts[kMaxA] = {0.f, 0.f};
 #pragma unroll
       for (int jj = 0; jj < kMaxA; ++jj) {
@@ -1067,10 +1111,11 @@ __global__ void __launch_bounds__(256) eval_market_loop_kernel(rlmd::FusedActArg
         if (sizeof(AT) == 4) return (AT)v;
         return (AT)fmin(fmax(v, clip_lo), clip_hi);
       };
+      if (probe) RLMD_TSE(3, __builtin_amdgcn_s_memtime());
       const StepOut so = env_step_lane<RLMD_MARKET, NG, AT>(
           P, b, w, t, start, ep, act, [&](int) { return 0.0; },
           [&](int k, double v) { obs_s[tid * SP + k] = (float)v; },
-          [&](int k, double v) { risk_s[tid * 8 + k] = v; });
+          [&](int k, double v) { risk_s[tid * 8 + k] = v; }, NoDoneHook{}, MrelRow{mrel_s + ((day & 1) * kR + tid) * 16});
       last_r = so.reward;
       last_t = t;
       if (so.done) {
@@ -1079,8 +1124,11 @@ __global__ void __launch_bounds__(256) eval_market_loop_kernel(rlmd::FusedActArg
         w = so.W;
         ++t;
       }
+      if (probe) RLMD_TSE(4, __builtin_amdgcn_s_memtime());
     }
-    if (!__syncthreads_or(alive)) break;
+    const int any_alive = __syncthreads_or(alive);
+    if (probe) RLMD_TSE(5, __builtin_amdgcn_s_memtime());
+    if (!any_alive) break;
   }
   if (mine) {
     P.wealth[b] = w;
@@ -1376,6 +1424,7 @@ int env_act_market_eval(rlmd_env_t env, const FusedActArgs& a, int h1p, int nb, 
   const EnvParams& P = env->P;
   const int sp = a.S <= 8 ? 8 : 16;
   if (off || P.fam != RLMD_MARKET || a.n != P.n_lanes || a.S > 16 || a.A > actrows::kMaxA || P.risk_dim > 8 ||
+      P.obs_days * P.n > 16 ||
       !((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5)))
     return 0;
   const dim3 grid((P.n_lanes + 15) / 16), block(256);

@@ -155,5 +155,39 @@ def run_env():
     print("  block-0 phases (cycles) entry->draw, draw->step, step->stores, stores->end:", np.median(ph, 0))
 
 
+def run_mkt():
+    """eval_market_loop_kernel (C4's evaluation event, 100 lanes x 250 days): block
+    0's phase cycles on day 10 (day start -> layer 1 -> layer 2 + heads -> action
+    -> market step -> end-of-day barrier)."""
+    import numpy as np
+    import torch
+
+    torch.zeros(1, device="cuda:0")
+
+    from rlmd_amd import _abi
+
+    _abi._LIB = _abi.load(LIB)
+    lib = _abi._LIB
+    lib.rlmd_debug_ts_env.restype = C.c_int
+    lib.rlmd_debug_ts_env.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    from rlmd_amd.agent import DeviceAgent
+    from rlmd_amd.trainer import market_evaluate
+
+    rng = np.random.default_rng(3)
+    prices = 100.0 * np.exp(np.cumsum(0.01 * rng.standard_normal((9167, 1)), axis=0))
+    ag = DeviceAgent("SAC", 5, 1, 256, 256, 16, 8, precision="bf16", seed=1, device="cuda:0")
+    starts = rng.integers(0, 9167 - 260, size=100)
+    buf = (C.c_ulonglong * (8 * 7))()
+    ph = []
+    for it in range(8):
+        market_evaluate(ag, prices, "A", 1, 250, starts, 5000, 10, 100, device="cuda:0")
+        lib.rlmd_debug_ts_env(buf, 7)
+        t = np.array(buf[:], dtype=np.int64).reshape(7, 8)
+        if it >= 2:
+            ph.append(np.diff(t[0, 0:6]))
+    print("eval_market_loop_kernel block 0, day 10 (cycles): start->L1, L1->L2+heads, ->action, ->step, ->barrier")
+    print("  ", np.median(ph, 0), "total", np.median(np.sum(ph, 1)))
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run, "act": run_act, "env": run_env}[sys.argv[1]]()
+    {"build": build, "run": run, "act": run_act, "env": run_env, "mkt": run_mkt}[sys.argv[1]]()
