@@ -1,30 +1,39 @@
-// lev_sort.hip — fixed-leverage sweeps with per-step sorts (gfx950).
+// lev_sort.hip — fixed-leverage sweeps whose order statistics need the values
+// themselves (gfx950).
 //
 // Replaces dice_smart_lev (lev/lev_exp.py:586-705), gbm_smart_lev (:1008-1119)
 // and dice_sh_smart_lev (:1209-1332) — and, statistics of the final values only,
-// the *_fixed_final_lev family (:56-127, :508-585, :935-1007, :1121-1208):
-// for every leverage l each investor's value
-// is multiplied step by step by its gamble factor (float32, as the reference's
-// torch tensors), and after each step t >= 1 the values are sorted descending:
-// the first `top` form the top group, the rest the adjusted group, and the
-// table column [mean, mean_top, mean_adj, mad x3, std x3, median x3, lev] is
-// stored (std unbiased=False, median = the lower middle element, torch.median).
+// the *_fixed_final_lev family (:56-127, :508-585, :935-1007, :1121-1208) — and
+// the big-brain investors (coin_big_brain_lev :270-452, dice_big_brain_lev
+// :741-932): for every leverage l each investor's value is multiplied step by
+// step by its gamble factor (float32, as the reference's torch tensors), and
+// after each step t >= 1 the reference SORTS the values descending: the first
+// `top` form the top group, the rest the adjusted group, and the table column
+// [mean, mean_top, mean_adj, mad x3, std x3, median x3, lev] is stored (std
+// unbiased=False, median = the lower middle element, torch.median).
 //
 // Unlike the coin flip (lev.hip: the value is monotone in one up-count, so
-// histograms replace the sorts) a die's value depends on two counts and a GBM
-// path's on a continuous sum, so the order really is sorted here, once per
-// (step, leverage), on the device:
-//   lev_advance_kernel   values *= factor(outcome[i][t]) for every (lev, investor)
-//                        (categorical: factor table [lev][3] from the host,
-//                        computed with the reference's f32 arithmetic; GBM:
-//                        expf(lev * outcome)), one pass over the u8 / f32 column
-//   hipcub DeviceRadixSort::SortKeysDescending per leverage (f32 keys)
-//   lev_sorted_sums_kernel  per (lev, chunk): group sums in f64 (pass 1), then
-//                        |v - mean| and (v - mean)^2 sums (pass 2), fixed
-//                        chunk order — deterministic
-//   lev_sorted_fold_kernel  one thread per lev: fold the chunks, write the column
+// histograms of counts replace the sorts) a die's value depends on two counts
+// and a GBM path's on a continuous sum.  But the column needs only FOUR order
+// statistics of each step's values — the top group's boundary (descending rank
+// top - 1) and the three lower medians — plus group sums, and group membership
+// follows from the boundary value vk alone (v > vk: top; v < vk: adjusted; the
+// top - #(v > vk) copies of vk that the sort puts in the top group are added
+// analytically).  So no sort runs: the four ranks are found together by an
+// 11-bit-digit radix SELECT over order-preserving integer keys (3 passes for
+// f32, 6 for f64), each pass one streaming read:
+//   lev_window_kernel    outcome steps [t0, t0 + 32) transposed to [step][investor]
+//                        once per 32 steps (the per-step column read coalesces)
+//   lev_advance_kernel   values *= factor(outcome[t][i]) for every (lev, investor),
+//                        fused with the select's first digit histogram
+//   sel_hist_kernel      later digits: LDS histograms of the keys whose higher
+//                        bits match a target's prefix (one per distinct prefix)
+//   sel_scan_kernel      per (array, target): the digit bin holding the target
+//                        rank (wave scan of the histogram), the next prefix
+//   sel_sums_kernel      group sums in f64 (pass 0), then |v - mean| and
+//                        (v - mean)^2 (pass 1); fixed chunk order: deterministic
+//   sel_fold_kernel      per array: fold the chunks, write the column
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include <math.h>
 
 #include <algorithm>
@@ -41,61 +50,219 @@
 
 namespace {
 
-constexpr int kChunks = 64;  // partial-sum chunks per leverage
+constexpr int kChunks = 64;     // partial-sum chunks per array
 constexpr int kT = 256;
+constexpr int kSelB = 11;       // radix-select digit bits
+constexpr int kSelBins = 1 << kSelB;
+constexpr int kSelBlocks = 128;  // histogram / advance workgroups per array
+constexpr int kW = 32;          // outcome steps per transposed window
 
-struct SortedArgs {
-  int kind;  // 0 categorical (u8 outcomes 0/1/2), 1 GBM (f32 outcomes)
-  const uint8_t* cat;
-  const float* gbm;
-  int64_t investors, ld;
-  int n_lev;
-  const float* table;  // [n_lev][3] (categorical)
-  const float* levs;   // [n_lev]
-  float* val;          // [n_lev][investors]
+// ---- order-preserving integer keys of f32 / f64 (ascending) ----------------
+__device__ __forceinline__ uint32_t okey(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ uint64_t okey(double v) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  return (u >> 63) ? ~u : (u | (1ull << 63));
+}
+__device__ __forceinline__ float kval(uint32_t k) {
+  return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+__device__ __forceinline__ double kval(uint64_t k) {
+  return __longlong_as_double((long long)((k >> 63) ? (k & ~(1ull << 63)) : ~k));
+}
+template <typename VT>
+struct KeyT {
+  typedef uint32_t K;
+};
+template <>
+struct KeyT<double> {
+  typedef uint64_t K;
 };
 
-__device__ __forceinline__ float factor(const SortedArgs& a, int l, int64_t i, int t) {
-  if (a.kind == 0) {
-    const int o = a.cat[i * a.ld + t];
-    return a.table[l * 3 + (o > 2 ? 2 : o)];
-  }
-  return expf(a.levs[l] * a.gbm[i * a.ld + t]);
+// digit of pass p (most significant first): bits [shift, shift + width)
+__host__ __device__ inline void sel_digit(int bits, int p, int& shift, int& width) {
+  const int hi = bits - kSelB * p;
+  width = hi < kSelB ? hi : kSelB;
+  shift = hi - width;
+}
+inline int sel_passes(int bits) { return (bits + kSelB - 1) / kSelB; }
+
+// per (array, target q): q 0 the top group's boundary (ascending rank N - top),
+// 1 the median of all ((N - 1) / 2), 2 of the top group (N - top + (top - 1) / 2),
+// 3 of the adjusted group ((N - top - 1) / 2).  prefix: the key bits decided so
+// far; rank: the rank left inside that prefix; src: the target whose histogram
+// serves this one in the next pass (equal prefixes share one).
+struct SelState {
+  unsigned long long prefix;
+  long long rank;
+  int valid, src;
+};
+
+// chunk c of n_chunks over [0, N)
+__device__ __forceinline__ void chunk_range(int64_t N, int c, int n_chunks, int64_t& b0, int64_t& b1) {
+  const int64_t per = (N + n_chunks - 1) / n_chunks;
+  b0 = (int64_t)c * per;
+  b1 = b0 + per < N ? b0 + per : N;
+  if (b0 > N) b0 = N;
 }
 
-// t == 0: val = value_0 * factor(t = 0); else val *= factor(t)
-__global__ void __launch_bounds__(kT) lev_advance_kernel(SortedArgs a, int t, float value_0) {
-  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
-  const int l = blockIdx.y;
-  if (i >= a.investors) return;
-  float* v = a.val + (int64_t)l * a.investors + i;
-  const float g = factor(a, l, i, t);
-  *v = t == 0 ? value_0 * g : *v * g;
+// LDS histogram slots flushed into the array's global slots (non-zero bins only)
+__device__ __forceinline__ void flush_hist(const unsigned* h, int n, unsigned* g) {
+  for (int i = threadIdx.x; i < n; i += blockDim.x)
+    if (h[i]) atomicAdd(&g[i], h[i]);
 }
 
-// group sums over sorted-descending values s[0, N): all, top = [0, top), adj =
-// [top, N).  pass 0: sums; pass 1: |v - m| and (v - m)^2 with the means m.
+// pass p >= 1: histogram of digit p over the keys matching a target's prefix
 template <typename VT>
-__global__ void __launch_bounds__(kT) lev_sorted_sums_kernel(const VT* sorted, int64_t N, int64_t top,
-                                                             const double* means, int pass, double* part) {
-  const int l = blockIdx.y, c = blockIdx.x;
-  const VT* s = sorted + (int64_t)l * N;
-  const int64_t per = (N + kChunks - 1) / kChunks, b0 = c * per, b1 = b0 + per < N ? b0 + per : N;
-  double acc[6] = {0, 0, 0, 0, 0, 0};  // pass 0: all, top, adj ; pass 1: |.| all/top/adj, sq all/top/adj
-  const double ma = pass ? means[l * 3 + 0] : 0.0, mt = pass ? means[l * 3 + 1] : 0.0,
-               md = pass ? means[l * 3 + 2] : 0.0;
+__global__ void __launch_bounds__(kT) sel_hist_kernel(const VT* vals, int64_t N, int p, const SelState* sel,
+                                                      unsigned* hist) {
+  typedef typename KeyT<VT>::K K;
+  constexpr int bits = 8 * sizeof(VT);
+  int shift, width;
+  sel_digit(bits, p, shift, width);
+  const int l = blockIdx.y;
+  __shared__ unsigned h[4 * kSelBins];
+  for (int i = threadIdx.x; i < 4 * kSelBins; i += kT) h[i] = 0;
+  K pre[4];
+  bool on[4];
+  bool any = false;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const SelState s = sel[l * 4 + q];
+    on[q] = s.valid && s.src == q;
+    pre[q] = (K)s.prefix;
+    any |= on[q];
+  }
+  __syncthreads();
+  if (!any) return;
+  int64_t b0, b1;
+  chunk_range(N, blockIdx.x, gridDim.x, b0, b1);
+  const VT* v = vals + (int64_t)l * N;
+  const K mask = ((K)1 << width) - 1;
   for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) {
-    const double v = s[i];
-    const bool is_top = i < top;
+    const K key = okey(v[i]);
+    const unsigned d = (unsigned)((key >> shift) & mask);
+    const K hi = key >> (shift + width);
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      if (on[q] && hi == pre[q]) atomicAdd(&h[q * kSelBins + d], 1u);
+  }
+  __syncthreads();
+  flush_hist(h, 4 * kSelBins, hist + (int64_t)l * 4 * kSelBins);
+}
+
+// per array (one workgroup, wave q = target q): the bin of digit p that holds
+// the target's rank; then the array's histogram slots are zeroed for the next
+// pass and equal prefixes are pointed at one histogram
+__global__ void __launch_bounds__(256) sel_scan_kernel(int bits, int p, int64_t N, int64_t top, SelState* sel,
+                                                       unsigned* hist) {
+  const int l = blockIdx.x, q = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int shift, width;
+  sel_digit(bits, p, shift, width);
+  const int per = (1 << width) / 64;
+  SelState s = sel[l * 4 + q];
+  if (p == 0) {
+    const int64_t tp = top;
+    const int64_t ranks[4] = {N - tp, (N - 1) / 2, N - tp + (tp - 1) / 2, (N - tp - 1) / 2};
+    const bool valid[4] = {tp >= 1, N >= 1, tp >= 1, N - tp >= 1};
+    s.prefix = 0;
+    s.rank = ranks[q];
+    s.valid = valid[q] ? 1 : 0;
+    s.src = q;
+  }
+  unsigned* base = hist + (int64_t)l * 4 * kSelBins;
+  if (s.valid) {
+    const unsigned* h = base + (p == 0 ? 0 : s.src) * kSelBins;
+    unsigned long long mine = 0;
+    for (int j = 0; j < per; ++j) mine += h[lane * per + j];
+    unsigned long long incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned long long u = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += u;
+    }
+    const unsigned long long m = __ballot(incl > (unsigned long long)s.rank);
+    if (m == 0) {
+      s.valid = 0;  // (the counts do not reach the rank: never for consistent input)
+    } else {
+      const int L = __ffsll(m) - 1;
+      int bin = 0;
+      unsigned long long below = 0;
+      if (lane == L) {
+        unsigned long long cum = incl - mine;
+        for (int j = 0; j < per; ++j) {
+          const unsigned c = h[lane * per + j];
+          if (cum + c > (unsigned long long)s.rank) {
+            bin = lane * per + j;
+            below = cum;
+            break;
+          }
+          cum += c;
+        }
+      }
+      bin = __shfl(bin, L, 64);
+      below = __shfl(below, L, 64);
+      s.prefix = (s.prefix << width) | (unsigned long long)bin;
+      s.rank -= (long long)below;
+    }
+  }
+  __shared__ SelState ss[4];
+  if (lane == 0) ss[q] = s;
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4 * kSelBins; i += 256) base[i] = 0;
+  if (lane == 0) {
+    int src = q;
+    for (int r = 0; r < q; ++r)
+      if (ss[r].valid && ss[r].prefix == s.prefix) {
+        src = r;
+        break;
+      }
+    s.src = src;
+    sel[l * 4 + q] = s;
+  }
+}
+
+// group sums over the array's values: pass 0 [sum all, sum v > vk, #(v > vk),
+// #(v == vk)], pass 1 [|v - m_all|, (v - m_all)^2, top |.|, top ^2, adj |.|,
+// adj ^2] (v == vk excluded: the fold adds those copies)
+template <typename VT>
+__global__ void __launch_bounds__(kT) sel_sums_kernel(const VT* vals, int64_t N, const SelState* sel,
+                                                      const double* means, int pass, double* part) {
+  typedef typename KeyT<VT>::K K;
+  const int l = blockIdx.y, c = blockIdx.x;
+  const VT* s = vals + (int64_t)l * N;
+  const bool has_top = sel[l * 4].valid != 0;
+  const double vk = has_top ? (double)kval((K)sel[l * 4].prefix) : 0.0;
+  int64_t b0, b1;
+  chunk_range(N, c, kChunks, b0, b1);
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  const double ma = pass ? means[l * 8 + 0] : 0.0, mt = pass ? means[l * 8 + 1] : 0.0,
+               md = pass ? means[l * 8 + 2] : 0.0;
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) {
+    const double v = (double)s[i];
+    const bool gt = has_top && v > vk, lt = !has_top || v < vk;
     if (!pass) {
       acc[0] += v;
-      acc[is_top ? 1 : 2] += v;
+      if (gt) {
+        acc[1] += v;
+        acc[2] += 1.0;
+      }
+      if (has_top && v == vk) acc[3] += 1.0;
     } else {
-      const double da = v - ma, dg = v - (is_top ? mt : md);
+      const double da = v - ma;
       acc[0] += fabs(da);
-      acc[3] += da * da;
-      acc[is_top ? 1 : 2] += fabs(dg);
-      acc[is_top ? 4 : 5] += dg * dg;
+      acc[1] += da * da;
+      if (gt) {
+        const double d = v - mt;
+        acc[2] += fabs(d);
+        acc[3] += d * d;
+      }
+      if (lt) {
+        const double d = v - md;
+        acc[4] += fabs(d);
+        acc[5] += d * d;
+      }
     }
   }
   __shared__ double red[6][kT];
@@ -109,36 +276,165 @@ __global__ void __launch_bounds__(kT) lev_sorted_sums_kernel(const VT* sorted, i
   if ((int)threadIdx.x < 6) part[((int64_t)l * kChunks + c) * 6 + threadIdx.x] = red[threadIdx.x][0];
 }
 
-// pass 0: means of the three groups; pass 1: the table column at step t
-// rows: table rows per configuration; row0: where the 12 statistics go; the
-// n_extra constants extra[l][*] fill rows row0 + 12 ... (the sweeps' lev row,
-// the big-brain stop / roll rows)
+// pass 0: the three groups' means (and the boundary's copies per group); pass 1:
+// the table column at step t.  rows: table rows per array; row0: where the 12
+// statistics go; the n_extra constants extra[l][*] fill rows row0 + 12 ... (the
+// sweeps' lev row, the big-brain stop / roll rows)
 template <typename VT>
-__global__ void lev_sorted_fold_kernel(const VT* sorted, int64_t N, int64_t top, int n_lev, const double* part,
-                                       int pass, double* means, const float* extra, int n_extra, float* data,
-                                       int rows, int row0, int steps, int t) {
+__global__ void sel_fold_kernel(int64_t N, int64_t top, int n_arr, const SelState* sel, const double* part, int pass,
+                                double* means, const float* extra, int n_extra, float* data, int rows, int row0,
+                                int steps, int t) {
+  typedef typename KeyT<VT>::K K;
   const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= n_lev) return;
+  if (l >= n_arr) return;
   double s[6] = {0, 0, 0, 0, 0, 0};
   for (int c = 0; c < kChunks; ++c)
     for (int q = 0; q < 6; ++q) s[q] += part[((int64_t)l * kChunks + c) * 6 + q];
   const double na = (double)N, nt = (double)top, nd = (double)(N - top);
+  const bool has_top = sel[l * 4].valid != 0;
+  const double vk = has_top ? (double)kval((K)sel[l * 4].prefix) : 0.0;
+  double* m = means + l * 8;
   if (!pass) {
-    means[l * 3 + 0] = s[0] / na;
-    means[l * 3 + 1] = s[1] / nt;
-    means[l * 3 + 2] = s[2] / nd;
+    const double tie_top = has_top ? nt - s[2] : 0.0;  // copies of vk in the top group
+    const double tie_adj = has_top ? s[3] - tie_top : 0.0;
+    const double sum_top = has_top ? s[1] + tie_top * vk : 0.0;
+    m[0] = s[0] / na;
+    m[1] = sum_top / nt;
+    m[2] = N > top ? (s[0] - sum_top) / nd : NAN;
+    m[3] = tie_top;
+    m[4] = tie_adj;
     return;
   }
-  const VT* v = sorted + (int64_t)l * N;
-  // lower medians: ascending index (n - 1) / 2 of each group, read from the
-  // descending order
-  auto med = [&](int64_t lo, int64_t n) -> double { return n > 0 ? (double)v[lo + n - 1 - (n - 1) / 2] : NAN; };
-  const float col[12] = {(float)means[l * 3 + 0], (float)means[l * 3 + 1], (float)means[l * 3 + 2],
-                         (float)(s[0] / na), (float)(s[1] / nt), (float)(s[2] / nd),
-                         (float)sqrt(s[3] / na), (float)sqrt(s[4] / nt), (float)sqrt(s[5] / nd),
-                         (float)med(0, N), (float)med(0, top), (float)med(top, N - top)};
+  const double tie_top = m[3], tie_adj = m[4];
+  const double dt = vk - m[1], dd = vk - m[2];
+  auto med = [&](int q) -> double {
+    const SelState& x = sel[l * 4 + q];
+    return x.valid ? (double)kval((K)x.prefix) : NAN;
+  };
+  const float col[12] = {(float)m[0],
+                         (float)m[1],
+                         (float)m[2],
+                         (float)(s[0] / na),
+                         (float)((s[2] + tie_top * fabs(dt)) / nt),
+                         (float)((s[4] + tie_adj * fabs(dd)) / nd),
+                         (float)sqrt(s[1] / na),
+                         (float)sqrt((s[3] + tie_top * dt * dt) / nt),
+                         (float)sqrt((s[5] + tie_adj * dd * dd) / nd),
+                         (float)med(1),
+                         (float)med(2),
+                         (float)med(3)};
   for (int r = 0; r < 12; ++r) data[((int64_t)l * rows + row0 + r) * steps + t] = col[r];
   for (int e = 0; e < n_extra; ++e) data[((int64_t)l * rows + row0 + 12 + e) * steps + t] = extra[l * n_extra + e];
+}
+
+struct SelWork {
+  unsigned* hist;  // [n_arr][4][kSelBins], zero between passes
+  SelState* sel;   // [n_arr][4]
+  double* part;    // [n_arr][kChunks][6]
+  double* means;   // [n_arr][8]
+};
+
+size_t sel_work_bytes(int64_t n_arr) {
+  return (size_t)n_arr * (4 * kSelBins * 4 + 4 * sizeof(SelState) + kChunks * 6 * 8 + 8 * 8) + 1024;
+}
+
+SelWork sel_work(unsigned char* p, int64_t n_arr) {
+  SelWork w;
+  w.hist = reinterpret_cast<unsigned*>(p);
+  w.sel = reinterpret_cast<SelState*>(p + n_arr * 4 * kSelBins * 4);
+  w.part = reinterpret_cast<double*>(w.sel + n_arr * 4);
+  w.means = w.part + n_arr * kChunks * 6;
+  return w;
+}
+
+// the column of every array at step t: the select passes (the first digit's
+// histogram already built when hist0_done), then the two sum passes
+template <typename VT>
+int sel_stats(const VT* vals, int64_t N, int64_t top, int n_arr, const SelWork& w, bool hist0_done, const float* extra,
+              int n_extra, float* data, int rows, int row0, int steps, int t, hipStream_t st) {
+  constexpr int bits = 8 * sizeof(VT);
+  const int P = sel_passes(bits);
+  for (int p = 0; p < P; ++p) {
+    if (p > 0) {
+      hipLaunchKernelGGL(sel_hist_kernel<VT>, dim3(kSelBlocks, n_arr), dim3(kT), 0, st, vals, N, p, w.sel, w.hist);
+      RLMD_LAUNCH_CHECK();
+    } else {
+      RLMD_CHECK(hist0_done, "select: first digit histogram missing");
+    }
+    hipLaunchKernelGGL(sel_scan_kernel, dim3(n_arr), dim3(256), 0, st, bits, p, N, top, w.sel, w.hist);
+    RLMD_LAUNCH_CHECK();
+  }
+  for (int pass = 0; pass < 2; ++pass) {
+    hipLaunchKernelGGL(sel_sums_kernel<VT>, dim3(kChunks, n_arr), dim3(kT), 0, st, vals, N, w.sel, w.means, pass,
+                       w.part);
+    RLMD_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sel_fold_kernel<VT>, dim3((n_arr + 63) / 64), dim3(64), 0, st, N, top, n_arr, w.sel, w.part,
+                       pass, w.means, extra, n_extra, data, rows, row0, steps, t);
+    RLMD_LAUNCH_CHECK();
+  }
+  return 0;
+}
+
+// ---- outcome windows ---------------------------------------------------------
+// win[s][i] = src[i][t0 + s] for s < ns (64 investors x 32 steps per workgroup
+// through an LDS tile: row reads of 32 consecutive steps, coalesced column writes)
+template <typename T>
+__global__ void __launch_bounds__(256) lev_window_kernel(const T* src, int64_t inv, int64_t ld, int t0, int ns,
+                                                         T* win) {
+  __shared__ T tile[64][kW + 1];
+  const int64_t i0 = (int64_t)blockIdx.x * 64;
+  for (int e = threadIdx.x; e < 64 * kW; e += 256) {
+    const int r = e / kW, c = e - r * kW;
+    if (i0 + r < inv && c < ns) tile[r][c] = src[(i0 + r) * ld + t0 + c];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * kW; e += 256) {
+    const int c = e / 64, r = e - c * 64;
+    if (i0 + r < inv && c < ns) win[(int64_t)c * inv + i0 + r] = tile[r][c];
+  }
+}
+
+// ---- the sweeps ----------------------------------------------------------------
+struct SortedArgs {
+  int kind;              // 0 categorical (u8 outcomes 0/1/2), 1 GBM (f32 outcomes)
+  const uint8_t* wcat;   // this window's outcomes [kW][investors]
+  const float* wgbm;
+  int64_t investors;
+  int n_lev;
+  const float* table;  // [n_lev][3] (categorical)
+  const float* levs;   // [n_lev]
+  float* val;          // [n_lev][investors]
+};
+
+__device__ __forceinline__ float factor(const SortedArgs& a, int l, int64_t i, int s) {
+  if (a.kind == 0) {
+    const int o = a.wcat[(int64_t)s * a.investors + i];
+    return a.table[l * 3 + (o > 2 ? 2 : o)];
+  }
+  return expf(a.levs[l] * a.wgbm[(int64_t)s * a.investors + i]);
+}
+
+// t == 0: val = value_0 * factor(t = 0); else val *= factor(t); with hist, the
+// new values' first select digit histogrammed on the way (key bits [21, 32))
+__global__ void __launch_bounds__(kT) lev_advance_kernel(SortedArgs a, int t, int s, float value_0, int hist,
+                                                         unsigned* hist_out) {
+  const int l = blockIdx.y;
+  __shared__ unsigned h[kSelBins];
+  if (hist)
+    for (int i = threadIdx.x; i < kSelBins; i += kT) h[i] = 0;
+  __syncthreads();
+  int64_t b0, b1;
+  chunk_range(a.investors, blockIdx.x, gridDim.x, b0, b1);
+  float* v = a.val + (int64_t)l * a.investors;
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) {
+    const float g = factor(a, l, i, s);
+    const float x = t == 0 ? value_0 * g : v[i] * g;
+    v[i] = x;
+    if (hist) atomicAdd(&h[okey(x) >> (32 - kSelB)], 1u);
+  }
+  if (!hist) return;
+  __syncthreads();
+  flush_hist(h, kSelBins, hist_out + (int64_t)l * 4 * kSelBins);
 }
 
 // ---------------------------------------------------------------------------
@@ -148,18 +444,18 @@ __global__ void lev_sorted_fold_kernel(const VT* sorted, int64_t N, int64_t top,
 // stop * value_0, or, when roll > 0 and v > value_0, the rolling floor
 // value_0 + roll (v - value_0) (coin_optimal_lev :240-267, dice_optimal_lev
 // :704-738) — in the reference's arithmetic (coin f32; dice f64 values, see
-// optimal_lev; this file compiles with FP contraction off).  Per step: the leverages' statistics (rows 12-23, then stop
-// and roll), the value step v = v (1 + lev r), the new leverages, the values'
-// statistics (rows 0-11).
+// optimal_lev; this file compiles with FP contraction off).  Per step: the
+// leverages' statistics (rows 12-23, then stop and roll), the value step
+// v = v (1 + lev r), the new leverages, the values' statistics (rows 0-11).
 // ---------------------------------------------------------------------------
 struct BrainArgs {
-  const uint8_t* cat;  // outcome codes [investors][ld]
-  int64_t investors, ld;
-  double ret[3];       // return per outcome code (f32 values for coin, f64 for dice)
+  const uint8_t* wcat;  // this window's outcome codes [kW][investors]
+  int64_t investors;
+  double ret[3];        // return per outcome code (f32 values for coin, f64 for dice)
   float value_0, lev_factor;
-  const float* cfg;    // [n_cfg][5]: stop floor value_min, roll, initial leverage, roll > 0, stop level
-  void* val;           // [n_cfg][investors] VT
-  void* lev;           // [n_cfg][investors] VT
+  const float* cfg;     // [n_cfg][5]: stop floor value_min, roll, initial leverage, roll > 0, stop level
+  void* val;            // [n_cfg][investors] VT
+  void* lev;            // [n_cfg][investors] VT
 };
 
 // coin (VT float, lev_exp.py:240-267): every quantity f32.  dice (VT double,
@@ -177,12 +473,12 @@ __device__ __forceinline__ VT optimal_lev(VT v, float v0, float vmin, float roll
 
 // t == 0: v = value_0 (1 + lev0 r[0]); else v = v (1 + lev r[t]); then lev = optimal(v)
 template <typename VT>
-__global__ void __launch_bounds__(kT) lev_brain_advance_kernel(BrainArgs a, int t) {
+__global__ void __launch_bounds__(kT) lev_brain_advance_kernel(BrainArgs a, int t, int s) {
   const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
   const int c = blockIdx.y;
   if (i >= a.investors) return;
   const float* k = a.cfg + 5 * c;
-  const int o = a.cat[i * a.ld + t];
+  const int o = a.wcat[(int64_t)s * a.investors + i];
   const VT r = (VT)a.ret[o > 2 ? 2 : o];
   const int64_t j = (int64_t)c * a.investors + i;
   VT* val = static_cast<VT*>(a.val);
@@ -192,11 +488,20 @@ __global__ void __launch_bounds__(kT) lev_brain_advance_kernel(BrainArgs a, int 
   lev[j] = optimal_lev<VT>(v, a.value_0, k[0], k[1], k[3] != 0.f, a.lev_factor);
 }
 
-template <typename VT = float>
-size_t sort_temp_bytes(int64_t investors) {
-  size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortKeysDescending(nullptr, bytes, (const VT*)nullptr, (VT*)nullptr, (int)investors);
-  return (bytes + 255) & ~(size_t)255;
+// the first select digit of an existing array (the brain's arrays)
+template <typename VT>
+__global__ void __launch_bounds__(kT) sel_hist0_kernel(const VT* vals, int64_t N, unsigned* hist) {
+  constexpr int bits = 8 * sizeof(VT);
+  const int l = blockIdx.y;
+  __shared__ unsigned h[kSelBins];
+  for (int i = threadIdx.x; i < kSelBins; i += kT) h[i] = 0;
+  __syncthreads();
+  int64_t b0, b1;
+  chunk_range(N, blockIdx.x, gridDim.x, b0, b1);
+  const VT* v = vals + (int64_t)l * N;
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) atomicAdd(&h[(unsigned)(okey(v[i]) >> (bits - kSelB))], 1u);
+  __syncthreads();
+  flush_hist(h, kSelBins, hist + (int64_t)l * 4 * kSelBins);
 }
 
 }  // namespace
@@ -205,9 +510,10 @@ extern "C" {
 
 int64_t rlmd_lev_sorted_workspace_bytes(int64_t investors, int32_t n_lev) {
   if (investors <= 0 || investors > INT32_MAX || n_lev <= 0) return -1;
-  const int64_t vals = 2 * (int64_t)n_lev * investors * 4;  // values + sorted copy
-  const int64_t sums = (int64_t)n_lev * kChunks * 6 * 8 + (int64_t)n_lev * 3 * 8 + (int64_t)n_lev * 16 * 4;
-  return ((vals + 255) & ~255ll) + ((sums + 255) & ~255ll) + (int64_t)sort_temp_bytes(investors);
+  const int64_t vals = (int64_t)n_lev * investors * 4;
+  const int64_t win = (int64_t)kW * investors * 4;  // f32 or u8 outcome window
+  const int64_t small = (int64_t)n_lev * 16 * 4;
+  return ((vals + 255) & ~255ll) + ((win + 255) & ~255ll) + (int64_t)sel_work_bytes(n_lev) + small + 256;
 }
 
 static int sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investors, int32_t horizon, int64_t ld,
@@ -225,48 +531,47 @@ static int sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investor
   const int64_t tp = top < investors ? (top > 0 ? top : 0) : investors;
   hipStream_t st = (hipStream_t)stream;
   unsigned char* w = static_cast<unsigned char*>(workspace);
-  const int64_t vals = 2 * (int64_t)n_lev * investors * 4;
+  const int64_t vals = (int64_t)n_lev * investors * 4;
+  const int64_t winb = (int64_t)kW * investors * 4;
   float* val = reinterpret_cast<float*>(w);
-  float* sorted = val + (int64_t)n_lev * investors;
-  unsigned char* w2 = w + ((vals + 255) & ~255ll);
-  double* part = reinterpret_cast<double*>(w2);
-  double* means = part + (int64_t)n_lev * kChunks * 6;
-  float* small = reinterpret_cast<float*>(means + (int64_t)n_lev * 3);  // levs [n_lev] | table [n_lev][3]
-  const int64_t sums = (int64_t)n_lev * kChunks * 6 * 8 + (int64_t)n_lev * 3 * 8 + (int64_t)n_lev * 16 * 4;
-  void* tmp = w2 + ((sums + 255) & ~255ll);
-  size_t tmp_bytes = sort_temp_bytes(investors);
+  void* win = w + ((vals + 255) & ~255ll);
+  unsigned char* ws = static_cast<unsigned char*>(win) + ((winb + 255) & ~255ll);
+  const SelWork sw = sel_work(ws, n_lev);
+  float* small = reinterpret_cast<float*>(ws + sel_work_bytes(n_lev));  // levs [n_lev] | table [n_lev][3]
+  RLMD_HIP(hipMemsetAsync(sw.hist, 0, (size_t)n_lev * 4 * kSelBins * 4, st));
   RLMD_HIP(hipMemcpyAsync(small, levs_host, sizeof(float) * n_lev, hipMemcpyHostToDevice, st));
   if (kind == 0)
     RLMD_HIP(hipMemcpyAsync(small + n_lev, table_host, sizeof(float) * 3 * n_lev, hipMemcpyHostToDevice, st));
   SortedArgs a{};
   a.kind = kind;
-  a.cat = static_cast<const uint8_t*>(outcomes_dev);
-  a.gbm = static_cast<const float*>(outcomes_dev);
+  a.wcat = static_cast<const uint8_t*>(win);
+  a.wgbm = static_cast<const float*>(win);
   a.investors = investors;
-  a.ld = ld;
   a.n_lev = n_lev;
   a.levs = small;
   a.table = small + n_lev;
   a.val = val;
-  const dim3 grid_adv((unsigned)((investors + kT - 1) / kT), (unsigned)n_lev);
   const int steps = final_only ? 1 : horizon - 1;
+  const dim3 grid_win((unsigned)((investors + 63) / 64));
   for (int t = 0; t < horizon; ++t) {
-    hipLaunchKernelGGL(lev_advance_kernel, grid_adv, dim3(kT), 0, st, a, t, value_0);
+    if (t % kW == 0) {
+      const int ns = std::min(kW, horizon - t);
+      if (kind == 0)
+        hipLaunchKernelGGL(lev_window_kernel<uint8_t>, grid_win, dim3(256), 0, st,
+                           static_cast<const uint8_t*>(outcomes_dev), investors, ld, t, ns,
+                           static_cast<uint8_t*>(win));
+      else
+        hipLaunchKernelGGL(lev_window_kernel<float>, grid_win, dim3(256), 0, st,
+                           static_cast<const float*>(outcomes_dev), investors, ld, t, ns, static_cast<float*>(win));
+      RLMD_LAUNCH_CHECK();
+    }
+    const bool stats = final_only ? t == horizon - 1 : t > 0;
+    hipLaunchKernelGGL(lev_advance_kernel, dim3(kSelBlocks, n_lev), dim3(kT), 0, st, a, t, t % kW, value_0,
+                       stats ? 1 : 0, sw.hist);
     RLMD_LAUNCH_CHECK();
-    if (final_only ? t < horizon - 1 : t == 0) continue;
-    for (int l = 0; l < n_lev; ++l) {
-      RLMD_HIP(hipcub::DeviceRadixSort::SortKeysDescending(tmp, tmp_bytes, val + (int64_t)l * investors,
-                                                           sorted + (int64_t)l * investors, (int)investors, 0, 32,
-                                                           st));
-    }
-    for (int pass = 0; pass < 2; ++pass) {
-      hipLaunchKernelGGL(lev_sorted_sums_kernel<float>, dim3(kChunks, n_lev), dim3(kT), 0, st, sorted, investors, tp,
-                         means, pass, part);
-      RLMD_LAUNCH_CHECK();
-      hipLaunchKernelGGL(lev_sorted_fold_kernel<float>, dim3((n_lev + 63) / 64), dim3(64), 0, st, sorted, investors,
-                         tp, n_lev, part, pass, means, small, 1, data_dev, 13, 0, steps, final_only ? 0 : t - 1);
-      RLMD_LAUNCH_CHECK();
-    }
+    if (!stats) continue;
+    RLMD_TRY_INT(sel_stats<float>(val, investors, tp, n_lev, sw, true, small, 1, data_dev, 13, 0, steps,
+                                  final_only ? 0 : t - 1, st));
   }
   if (data_T_dev)
     RLMD_HIP(hipMemcpyAsync(data_T_dev, val, sizeof(float) * n_lev * investors, hipMemcpyDeviceToDevice, st));
@@ -291,10 +596,10 @@ int rlmd_lev_final_sorted(int32_t kind, const void* outcomes_dev, int64_t invest
 
 int64_t rlmd_lev_brain_workspace_bytes(int64_t investors, int32_t n_cfg) {
   if (investors <= 0 || investors > INT32_MAX || n_cfg <= 0) return -1;
-  const int64_t vals = 3 * (int64_t)n_cfg * investors * 8;  // values, leverages, sorted copy (f64 at most)
-  const int64_t sums = (int64_t)n_cfg * kChunks * 6 * 8 + (int64_t)n_cfg * 3 * 8 + (int64_t)n_cfg * 8 * 4;
-  const int64_t tmp = (int64_t)std::max(sort_temp_bytes<float>(investors), sort_temp_bytes<double>(investors));
-  return ((vals + 255) & ~255ll) + ((sums + 255) & ~255ll) + tmp;
+  const int64_t vals = 2 * (int64_t)n_cfg * investors * 8;  // values, leverages (f64 at most)
+  const int64_t win = (int64_t)kW * investors;
+  const int64_t small = (int64_t)n_cfg * 8 * 4;
+  return ((vals + 255) & ~255ll) + ((win + 255) & ~255ll) + (int64_t)sel_work_bytes(n_cfg) + small + 256;
 }
 
 }  // extern "C"
@@ -308,26 +613,22 @@ static int lev_brain(const uint8_t* outcomes_dev, int64_t investors, int32_t hor
   const int64_t NC = (int64_t)n_cfg * investors;
   VT* val = reinterpret_cast<VT*>(w);
   VT* lev = val + NC;
-  VT* sorted = lev + NC;
-  unsigned char* w2 = w + ((3 * NC * 8 + 255) & ~255ll);
-  double* part = reinterpret_cast<double*>(w2);
-  double* means = part + (int64_t)n_cfg * kChunks * 6;
-  float* cfg = reinterpret_cast<float*>(means + (int64_t)n_cfg * 3);  // [n_cfg][5] | extra [n_cfg][2]
+  uint8_t* win = w + ((2 * NC * 8 + 255) & ~255ll);
+  unsigned char* ws = win + (((int64_t)kW * investors + 255) & ~255ll);
+  const SelWork sw = sel_work(ws, n_cfg);
+  float* cfg = reinterpret_cast<float*>(ws + sel_work_bytes(n_cfg));  // [n_cfg][5] | extra [n_cfg][2]
   float* extra = cfg + 5 * n_cfg;
-  const int64_t sums = (int64_t)n_cfg * kChunks * 6 * 8 + (int64_t)n_cfg * 3 * 8 + (int64_t)n_cfg * 8 * 4;
-  void* tmp = w2 + ((sums + 255) & ~255ll);
-  size_t tmp_bytes = sort_temp_bytes<VT>(investors);
   std::vector<float> ex(2 * (size_t)n_cfg);
   for (int c = 0; c < n_cfg; ++c) {  // rows 24 / 25: stop level and roll
     ex[2 * c] = cfg_host[5 * c + 4];
     ex[2 * c + 1] = cfg_host[5 * c + 1];
   }
+  RLMD_HIP(hipMemsetAsync(sw.hist, 0, (size_t)n_cfg * 4 * kSelBins * 4, st));
   RLMD_HIP(hipMemcpyAsync(cfg, cfg_host, sizeof(float) * 5 * n_cfg, hipMemcpyHostToDevice, st));
   RLMD_HIP(hipMemcpyAsync(extra, ex.data(), sizeof(float) * 2 * n_cfg, hipMemcpyHostToDevice, st));
   BrainArgs a{};
-  a.cat = outcomes_dev;
+  a.wcat = win;
   a.investors = investors;
-  a.ld = ld;
   for (int q = 0; q < 3; ++q) a.ret[q] = rets3[q];
   a.value_0 = value_0;
   a.lev_factor = lev_factor;
@@ -335,28 +636,27 @@ static int lev_brain(const uint8_t* outcomes_dev, int64_t investors, int32_t hor
   a.val = val;
   a.lev = lev;
   const dim3 grid_adv((unsigned)((investors + kT - 1) / kT), (unsigned)n_cfg);
+  const dim3 grid_win((unsigned)((investors + 63) / 64));
   const int steps = horizon - 1;
   auto stats = [&](const VT* src, int row0, const float* ext, int n_ext, int t) -> int {
-    for (int c = 0; c < n_cfg; ++c)
-      RLMD_HIP(hipcub::DeviceRadixSort::SortKeysDescending(tmp, tmp_bytes, src + (int64_t)c * investors,
-                                                           sorted + (int64_t)c * investors, (int)investors, 0,
-                                                           (int)(8 * sizeof(VT)), st));
-    for (int pass = 0; pass < 2; ++pass) {
-      hipLaunchKernelGGL(lev_sorted_sums_kernel<VT>, dim3(kChunks, n_cfg), dim3(kT), 0, st, sorted, investors, tp,
-                         means, pass, part);
-      RLMD_LAUNCH_CHECK();
-      hipLaunchKernelGGL(lev_sorted_fold_kernel<VT>, dim3((n_cfg + 63) / 64), dim3(64), 0, st, sorted, investors,
-                         tp, n_cfg, part, pass, means, ext, n_ext, data_dev, 26, row0, steps, t);
+    hipLaunchKernelGGL(sel_hist0_kernel<VT>, dim3(kSelBlocks, n_cfg), dim3(kT), 0, st, src, investors, sw.hist);
+    RLMD_LAUNCH_CHECK();
+    return sel_stats<VT>(src, investors, tp, n_cfg, sw, true, ext, n_ext, data_dev, 26, row0, steps, t, st);
+  };
+  auto advance = [&](int t) -> int {
+    if (t % kW == 0) {
+      hipLaunchKernelGGL(lev_window_kernel<uint8_t>, grid_win, dim3(256), 0, st, outcomes_dev, investors, ld, t,
+                         std::min(kW, (int)horizon - t), win);
       RLMD_LAUNCH_CHECK();
     }
+    hipLaunchKernelGGL(lev_brain_advance_kernel<VT>, grid_adv, dim3(kT), 0, st, a, t, t % kW);
+    RLMD_LAUNCH_CHECK();
     return 0;
   };
-  hipLaunchKernelGGL(lev_brain_advance_kernel<VT>, grid_adv, dim3(kT), 0, st, a, 0);
-  RLMD_LAUNCH_CHECK();
+  RLMD_TRY_INT(advance(0));
   for (int t = 0; t < steps; ++t) {
     RLMD_TRY_INT(stats(lev, 12, extra, 2, t));
-    hipLaunchKernelGGL(lev_brain_advance_kernel<VT>, grid_adv, dim3(kT), 0, st, a, t + 1);
-    RLMD_LAUNCH_CHECK();
+    RLMD_TRY_INT(advance(t + 1));
     RLMD_TRY_INT(stats(val, 0, nullptr, 0, t));
   }
   return 0;
