@@ -50,7 +50,7 @@
 
 namespace {
 
-constexpr int kChunks = 64;     // partial-sum chunks per array
+constexpr int kChunks = 128;    // partial-sum chunks per array
 constexpr int kT = 256;
 constexpr int kSelB = 11;       // radix-select digit bits
 constexpr int kSelBins = 1 << kSelB;
@@ -100,12 +100,38 @@ struct SelState {
   int valid, src;
 };
 
-// chunk c of n_chunks over [0, N)
+// arrays of N values are stored with a stride of pad4(N) (16-B aligned rows)
+__host__ __device__ inline int64_t pad4(int64_t n) { return (n + 3) & ~3ll; }
+
+// chunk c of n_chunks over [0, N), chunk starts at multiples of 4
 __device__ __forceinline__ void chunk_range(int64_t N, int c, int n_chunks, int64_t& b0, int64_t& b1) {
-  const int64_t per = (N + n_chunks - 1) / n_chunks;
+  const int64_t per = pad4((N + n_chunks - 1) / n_chunks);
   b0 = (int64_t)c * per;
   b1 = b0 + per < N ? b0 + per : N;
   if (b0 > N) b0 = N;
+}
+
+// f(v) for every value of [b0, b1) (b0 a multiple of 4), 16-B loads, two in
+// flight per thread; loads past b1 stay inside the padded row and are masked
+template <typename VT, typename F>
+__device__ __forceinline__ void for_vals(const VT* v, int64_t b0, int64_t b1, F f) {
+  constexpr int V = 16 / sizeof(VT);
+  typedef VT vec_t __attribute__((ext_vector_type(V)));
+  const int64_t step = (int64_t)V * blockDim.x;
+  for (int64_t i = b0 + (int64_t)V * threadIdx.x; i < b1; i += 2 * step) {
+    const vec_t x0 = *reinterpret_cast<const vec_t*>(v + i);
+    const bool two = i + step < b1;
+    vec_t x1;
+    if (two) x1 = *reinterpret_cast<const vec_t*>(v + i + step);
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      if (i + e < b1) f(x0[e]);
+    if (two) {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (i + step + e < b1) f(x1[e]);
+    }
+  }
 }
 
 // LDS histogram slots flushed into the array's global slots (non-zero bins only)
@@ -115,49 +141,79 @@ __device__ __forceinline__ void flush_hist(const unsigned* h, int n, unsigned* g
 }
 
 // pass p >= 1: histogram of digit p over the keys matching a target's prefix
+// On the last pass also the block's sums [all values, values whose key lies
+// above the boundary target's bucket, their count] (part2, fixed order)
 template <typename VT>
-__global__ void __launch_bounds__(kT) sel_hist_kernel(const VT* vals, int64_t N, int p, const SelState* sel,
-                                                      unsigned* hist) {
+__global__ void __launch_bounds__(kT) sel_hist_kernel(const VT* vals, int64_t N, int p, int last, const SelState* sel,
+                                                      unsigned* hist, double* part2) {
   typedef typename KeyT<VT>::K K;
   constexpr int bits = 8 * sizeof(VT);
   int shift, width;
   sel_digit(bits, p, shift, width);
   const int l = blockIdx.y;
   __shared__ unsigned h[4 * kSelBins];
-  for (int i = threadIdx.x; i < 4 * kSelBins; i += kT) h[i] = 0;
   K pre[4];
   bool on[4];
-  bool any = false;
+  const bool top_on = sel[l * 4].valid != 0;
+  const K pre0 = (K)sel[l * 4].prefix;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const SelState s = sel[l * 4 + q];
     on[q] = s.valid && s.src == q;
     pre[q] = (K)s.prefix;
-    any |= on[q];
+    if (on[q])
+      for (int i = threadIdx.x; i < kSelBins; i += kT) h[q * kSelBins + i] = 0;
   }
   __syncthreads();
-  if (!any) return;
   int64_t b0, b1;
   chunk_range(N, blockIdx.x, gridDim.x, b0, b1);
-  const VT* v = vals + (int64_t)l * N;
   const K mask = ((K)1 << width) - 1;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) {
-    const K key = okey(v[i]);
+  double sa = 0.0, sab = 0.0, cab = 0.0;
+  for_vals(vals + (int64_t)l * pad4(N), b0, b1, [&](VT x) {
+    const K key = okey(x);
     const unsigned d = (unsigned)((key >> shift) & mask);
     const K hi = key >> (shift + width);
 #pragma unroll
     for (int q = 0; q < 4; ++q)
       if (on[q] && hi == pre[q]) atomicAdd(&h[q * kSelBins + d], 1u);
-  }
+    if (last) {
+      sa += (double)x;
+      if (top_on && hi > pre0) {
+        sab += (double)x;
+        cab += 1.0;
+      }
+    }
+  });
   __syncthreads();
-  flush_hist(h, 4 * kSelBins, hist + (int64_t)l * 4 * kSelBins);
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (on[q]) flush_hist(h + q * kSelBins, kSelBins, hist + ((int64_t)l * 4 + q) * kSelBins);
+  if (!last) return;
+  __shared__ double red[3][kT];
+  red[0][threadIdx.x] = sa;
+  red[1][threadIdx.x] = sab;
+  red[2][threadIdx.x] = cab;
+  __syncthreads();
+  for (int hh = kT / 2; hh > 0; hh >>= 1) {
+    if ((int)threadIdx.x < hh)
+      for (int k = 0; k < 3; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + hh];
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < 3) part2[((int64_t)l * gridDim.x + blockIdx.x) * 3 + threadIdx.x] = red[threadIdx.x][0];
 }
 
 // per array (one workgroup, wave q = target q): the bin of digit p that holds
 // the target's rank; then the array's histogram slots are zeroed for the next
 // pass and equal prefixes are pointed at one histogram
-__global__ void __launch_bounds__(256) sel_scan_kernel(int bits, int p, int64_t N, int64_t top, SelState* sel,
-                                                       unsigned* hist) {
+// On the last pass wave 0 also forms the groups' means from the hist blocks'
+// sums and the boundary bucket's histogram (every bin of the last digit is one
+// value): means[l][0..4] = mean all, top, adjusted, and the boundary value's
+// copies in the top and the adjusted group.
+template <typename VT>
+__global__ void __launch_bounds__(256) sel_scan_kernel(int p, int last, int64_t N, int64_t top, SelState* sel,
+                                                       unsigned* hist, const double* part2, double* means) {
+  typedef typename KeyT<VT>::K K;
+  constexpr int bits = 8 * sizeof(VT);
   const int l = blockIdx.x, q = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int shift, width;
   sel_digit(bits, p, shift, width);
@@ -173,10 +229,15 @@ __global__ void __launch_bounds__(256) sel_scan_kernel(int bits, int p, int64_t 
     s.src = q;
   }
   unsigned* base = hist + (int64_t)l * 4 * kSelBins;
+  double gsum = 0.0, gcnt = 0.0, ceq = 0.0;  // last pass, wave 0: the boundary bucket above / at the boundary
   if (s.valid) {
     const unsigned* h = base + (p == 0 ? 0 : s.src) * kSelBins;
+    unsigned cb[kSelBins / 64];
+#pragma unroll
+    for (int j = 0; j < kSelBins / 64; ++j) cb[j] = j < per ? h[lane * per + j] : 0u;
     unsigned long long mine = 0;
-    for (int j = 0; j < per; ++j) mine += h[lane * per + j];
+#pragma unroll
+    for (int j = 0; j < kSelBins / 64; ++j) mine += cb[j];
     unsigned long long incl = mine;
     for (int o = 1; o < 64; o <<= 1) {
       const unsigned long long u = __shfl_up(incl, o, 64);
@@ -191,20 +252,60 @@ __global__ void __launch_bounds__(256) sel_scan_kernel(int bits, int p, int64_t 
       unsigned long long below = 0;
       if (lane == L) {
         unsigned long long cum = incl - mine;
-        for (int j = 0; j < per; ++j) {
-          const unsigned c = h[lane * per + j];
-          if (cum + c > (unsigned long long)s.rank) {
+        bool found = false;
+#pragma unroll
+        for (int j = 0; j < kSelBins / 64; ++j) {
+          const unsigned c = cb[j];
+          if (!found && j < per && cum + c > (unsigned long long)s.rank) {
             bin = lane * per + j;
             below = cum;
-            break;
+            found = true;
           }
           cum += c;
         }
       }
       bin = __shfl(bin, L, 64);
       below = __shfl(below, L, 64);
+      if (last && q == 0) {
+#pragma unroll
+        for (int j = 0; j < kSelBins / 64; ++j) {
+          const int bj = lane * per + j;
+          if (j < per && bj > bin) {
+            gsum += (double)cb[j] * (double)kval((K)((s.prefix << width) | (unsigned long long)bj));
+            gcnt += (double)cb[j];
+          }
+          if (j < per && bj == bin) ceq = (double)cb[j];
+        }
+      }
       s.prefix = (s.prefix << width) | (unsigned long long)bin;
       s.rank -= (long long)below;
+    }
+  }
+  if (last && q == 0) {
+    double sa = 0.0, sab = gsum, cab = gcnt;
+    for (int b = lane; b < kSelBlocks; b += 64) {
+      sa += part2[((int64_t)l * kSelBlocks + b) * 3];
+      sab += part2[((int64_t)l * kSelBlocks + b) * 3 + 1];
+      cab += part2[((int64_t)l * kSelBlocks + b) * 3 + 2];
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+      sa += __shfl_xor(sa, o, 64);
+      sab += __shfl_xor(sab, o, 64);
+      cab += __shfl_xor(cab, o, 64);
+      ceq += __shfl_xor(ceq, o, 64);
+    }
+    if (lane == 0) {
+      const bool has_top = s.valid != 0;
+      const double vk = has_top ? (double)kval((K)s.prefix) : 0.0;
+      const double nt = (double)top;
+      const double tie_top = has_top ? nt - cab : 0.0;
+      const double sum_top = has_top ? sab + tie_top * vk : 0.0;
+      double* m = means + l * 8;
+      m[0] = sa / (double)N;
+      m[1] = sum_top / nt;
+      m[2] = N > top ? (sa - sum_top) / (double)(N - top) : NAN;
+      m[3] = tie_top;
+      m[4] = has_top ? ceq - tie_top : 0.0;
     }
   }
   __shared__ SelState ss[4];
@@ -231,7 +332,7 @@ __global__ void __launch_bounds__(kT) sel_sums_kernel(const VT* vals, int64_t N,
                                                       const double* means, int pass, double* part) {
   typedef typename KeyT<VT>::K K;
   const int l = blockIdx.y, c = blockIdx.x;
-  const VT* s = vals + (int64_t)l * N;
+  const VT* s = vals + (int64_t)l * pad4(N);
   const bool has_top = sel[l * 4].valid != 0;
   const double vk = has_top ? (double)kval((K)sel[l * 4].prefix) : 0.0;
   int64_t b0, b1;
@@ -239,8 +340,8 @@ __global__ void __launch_bounds__(kT) sel_sums_kernel(const VT* vals, int64_t N,
   double acc[6] = {0, 0, 0, 0, 0, 0};
   const double ma = pass ? means[l * 8 + 0] : 0.0, mt = pass ? means[l * 8 + 1] : 0.0,
                md = pass ? means[l * 8 + 2] : 0.0;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) {
-    const double v = (double)s[i];
+  for_vals(s, b0, b1, [&](VT x) {
+    const double v = (double)x;
     const bool gt = has_top && v > vk, lt = !has_top || v < vk;
     if (!pass) {
       acc[0] += v;
@@ -264,7 +365,7 @@ __global__ void __launch_bounds__(kT) sel_sums_kernel(const VT* vals, int64_t N,
         acc[5] += d * d;
       }
     }
-  }
+  });
   __shared__ double red[6][kT];
   for (int q = 0; q < 6; ++q) red[q][threadIdx.x] = acc[q];
   __syncthreads();
@@ -285,11 +386,14 @@ __global__ void sel_fold_kernel(int64_t N, int64_t top, int n_arr, const SelStat
                                 double* means, const float* extra, int n_extra, float* data, int rows, int row0,
                                 int steps, int t) {
   typedef typename KeyT<VT>::K K;
-  const int l = blockIdx.x * blockDim.x + threadIdx.x;
-  if (l >= n_arr) return;
+  const int l = blockIdx.x;  // one wave per array: lane c folds chunks c, c + 64, ..., then a fixed butterfly
   double s[6] = {0, 0, 0, 0, 0, 0};
-  for (int c = 0; c < kChunks; ++c)
+  for (int c = threadIdx.x; c < kChunks; c += 64)
     for (int q = 0; q < 6; ++q) s[q] += part[((int64_t)l * kChunks + c) * 6 + q];
+#pragma unroll
+  for (int q = 0; q < 6; ++q)
+    for (int o = 32; o > 0; o >>= 1) s[q] += __shfl_xor(s[q], o, 64);
+  if (threadIdx.x != 0) return;
   const double na = (double)N, nt = (double)top, nd = (double)(N - top);
   const bool has_top = sel[l * 4].valid != 0;
   const double vk = has_top ? (double)kval((K)sel[l * 4].prefix) : 0.0;
@@ -331,11 +435,13 @@ struct SelWork {
   unsigned* hist;  // [n_arr][4][kSelBins], zero between passes
   SelState* sel;   // [n_arr][4]
   double* part;    // [n_arr][kChunks][6]
+  double* part2;   // [n_arr][kSelBlocks][3]
   double* means;   // [n_arr][8]
 };
 
 size_t sel_work_bytes(int64_t n_arr) {
-  return (size_t)n_arr * (4 * kSelBins * 4 + 4 * sizeof(SelState) + kChunks * 6 * 8 + 8 * 8) + 1024;
+  return (size_t)n_arr * (4 * kSelBins * 4 + 4 * sizeof(SelState) + kChunks * 6 * 8 + kSelBlocks * 3 * 8 + 8 * 8) +
+         1024;
 }
 
 SelWork sel_work(unsigned char* p, int64_t n_arr) {
@@ -343,7 +449,8 @@ SelWork sel_work(unsigned char* p, int64_t n_arr) {
   w.hist = reinterpret_cast<unsigned*>(p);
   w.sel = reinterpret_cast<SelState*>(p + n_arr * 4 * kSelBins * 4);
   w.part = reinterpret_cast<double*>(w.sel + n_arr * 4);
-  w.means = w.part + n_arr * kChunks * 6;
+  w.part2 = w.part + n_arr * kChunks * 6;
+  w.means = w.part2 + n_arr * kSelBlocks * 3;
   return w;
 }
 
@@ -354,24 +461,24 @@ int sel_stats(const VT* vals, int64_t N, int64_t top, int n_arr, const SelWork& 
               int n_extra, float* data, int rows, int row0, int steps, int t, hipStream_t st) {
   constexpr int bits = 8 * sizeof(VT);
   const int P = sel_passes(bits);
+  RLMD_CHECK(hist0_done, "select: first digit histogram missing");
   for (int p = 0; p < P; ++p) {
+    const int last = p == P - 1 ? 1 : 0;
     if (p > 0) {
-      hipLaunchKernelGGL(sel_hist_kernel<VT>, dim3(kSelBlocks, n_arr), dim3(kT), 0, st, vals, N, p, w.sel, w.hist);
+      hipLaunchKernelGGL(sel_hist_kernel<VT>, dim3(kSelBlocks, n_arr), dim3(kT), 0, st, vals, N, p, last, w.sel,
+                         w.hist, w.part2);
       RLMD_LAUNCH_CHECK();
-    } else {
-      RLMD_CHECK(hist0_done, "select: first digit histogram missing");
     }
-    hipLaunchKernelGGL(sel_scan_kernel, dim3(n_arr), dim3(256), 0, st, bits, p, N, top, w.sel, w.hist);
+    hipLaunchKernelGGL(sel_scan_kernel<VT>, dim3(n_arr), dim3(256), 0, st, p, last, N, top, w.sel, w.hist, w.part2,
+                       w.means);
     RLMD_LAUNCH_CHECK();
   }
-  for (int pass = 0; pass < 2; ++pass) {
-    hipLaunchKernelGGL(sel_sums_kernel<VT>, dim3(kChunks, n_arr), dim3(kT), 0, st, vals, N, w.sel, w.means, pass,
-                       w.part);
-    RLMD_LAUNCH_CHECK();
-    hipLaunchKernelGGL(sel_fold_kernel<VT>, dim3((n_arr + 63) / 64), dim3(64), 0, st, N, top, n_arr, w.sel, w.part,
-                       pass, w.means, extra, n_extra, data, rows, row0, steps, t);
-    RLMD_LAUNCH_CHECK();
-  }
+  // the deviations from the means, then the column
+  hipLaunchKernelGGL(sel_sums_kernel<VT>, dim3(kChunks, n_arr), dim3(kT), 0, st, vals, N, w.sel, w.means, 1, w.part);
+  RLMD_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sel_fold_kernel<VT>, dim3(n_arr), dim3(64), 0, st, N, top, n_arr, w.sel, w.part, 1, w.means,
+                     extra, n_extra, data, rows, row0, steps, t);
+  RLMD_LAUNCH_CHECK();
   return 0;
 }
 
@@ -390,7 +497,7 @@ __global__ void __launch_bounds__(256) lev_window_kernel(const T* src, int64_t i
   __syncthreads();
   for (int e = threadIdx.x; e < 64 * kW; e += 256) {
     const int c = e / 64, r = e - c * 64;
-    if (i0 + r < inv && c < ns) win[(int64_t)c * inv + i0 + r] = tile[r][c];
+    if (i0 + r < inv && c < ns) win[(int64_t)c * pad4(inv) + i0 + r] = tile[r][c];
   }
 }
 
@@ -406,14 +513,6 @@ struct SortedArgs {
   float* val;          // [n_lev][investors]
 };
 
-__device__ __forceinline__ float factor(const SortedArgs& a, int l, int64_t i, int s) {
-  if (a.kind == 0) {
-    const int o = a.wcat[(int64_t)s * a.investors + i];
-    return a.table[l * 3 + (o > 2 ? 2 : o)];
-  }
-  return expf(a.levs[l] * a.wgbm[(int64_t)s * a.investors + i]);
-}
-
 // t == 0: val = value_0 * factor(t = 0); else val *= factor(t); with hist, the
 // new values' first select digit histogrammed on the way (key bits [21, 32))
 __global__ void __launch_bounds__(kT) lev_advance_kernel(SortedArgs a, int t, int s, float value_0, int hist,
@@ -425,12 +524,34 @@ __global__ void __launch_bounds__(kT) lev_advance_kernel(SortedArgs a, int t, in
   __syncthreads();
   int64_t b0, b1;
   chunk_range(a.investors, blockIdx.x, gridDim.x, b0, b1);
-  float* v = a.val + (int64_t)l * a.investors;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) {
-    const float g = factor(a, l, i, s);
-    const float x = t == 0 ? value_0 * g : v[i] * g;
-    v[i] = x;
-    if (hist) atomicAdd(&h[okey(x) >> (32 - kSelB)], 1u);
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const int64_t P4 = pad4(a.investors);
+  float* v = a.val + (int64_t)l * P4;
+  const float lv = a.levs[l];
+  float tab[3] = {0.f, 0.f, 0.f};
+  if (a.kind == 0)
+    for (int q = 0; q < 3; ++q) tab[q] = a.table[l * 3 + q];
+  // 4 investors per thread: 16-B value loads / stores, 4-B (codes) or 16-B
+  // (GBM) outcome loads; lanes past N sit in the row padding
+  for (int64_t i = b0 + 4 * threadIdx.x; i < b1; i += 4 * kT) {
+    f32x4 x = t == 0 ? f32x4{0.f, 0.f, 0.f, 0.f} : *reinterpret_cast<const f32x4*>(v + i);
+    float g[4];
+    if (a.kind == 0) {
+      const uchar4 o = *reinterpret_cast<const uchar4*>(a.wcat + (int64_t)s * P4 + i);
+      const int oc[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) g[e] = oc[e] == 0 ? tab[0] : (oc[e] == 1 ? tab[1] : tab[2]);
+    } else {
+      const f32x4 o = *reinterpret_cast<const f32x4*>(a.wgbm + (int64_t)s * P4 + i);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) g[e] = expf(lv * o[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      x[e] = t == 0 ? value_0 * g[e] : x[e] * g[e];
+      if (hist && i + e < b1) atomicAdd(&h[okey(x[e]) >> (32 - kSelB)], 1u);
+    }
+    *reinterpret_cast<f32x4*>(v + i) = x;
   }
   if (!hist) return;
   __syncthreads();
@@ -478,9 +599,9 @@ __global__ void __launch_bounds__(kT) lev_brain_advance_kernel(BrainArgs a, int 
   const int c = blockIdx.y;
   if (i >= a.investors) return;
   const float* k = a.cfg + 5 * c;
-  const int o = a.wcat[(int64_t)s * a.investors + i];
+  const int o = a.wcat[(int64_t)s * pad4(a.investors) + i];
   const VT r = (VT)a.ret[o > 2 ? 2 : o];
-  const int64_t j = (int64_t)c * a.investors + i;
+  const int64_t j = (int64_t)c * pad4(a.investors) + i;
   VT* val = static_cast<VT*>(a.val);
   VT* lev = static_cast<VT*>(a.lev);
   const VT v = t == 0 ? (VT)a.value_0 * ((VT)1 + (VT)k[2] * r) : val[j] * ((VT)1 + lev[j] * r);
@@ -498,8 +619,8 @@ __global__ void __launch_bounds__(kT) sel_hist0_kernel(const VT* vals, int64_t N
   __syncthreads();
   int64_t b0, b1;
   chunk_range(N, blockIdx.x, gridDim.x, b0, b1);
-  const VT* v = vals + (int64_t)l * N;
-  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) atomicAdd(&h[(unsigned)(okey(v[i]) >> (bits - kSelB))], 1u);
+  for_vals(vals + (int64_t)l * pad4(N), b0, b1,
+           [&](VT x) { atomicAdd(&h[(unsigned)(okey(x) >> (bits - kSelB))], 1u); });
   __syncthreads();
   flush_hist(h, kSelBins, hist + (int64_t)l * 4 * kSelBins);
 }
@@ -510,8 +631,8 @@ extern "C" {
 
 int64_t rlmd_lev_sorted_workspace_bytes(int64_t investors, int32_t n_lev) {
   if (investors <= 0 || investors > INT32_MAX || n_lev <= 0) return -1;
-  const int64_t vals = (int64_t)n_lev * investors * 4;
-  const int64_t win = (int64_t)kW * investors * 4;  // f32 or u8 outcome window
+  const int64_t vals = (int64_t)n_lev * pad4(investors) * 4;
+  const int64_t win = (int64_t)kW * pad4(investors) * 4;  // f32 or u8 outcome window
   const int64_t small = (int64_t)n_lev * 16 * 4;
   return ((vals + 255) & ~255ll) + ((win + 255) & ~255ll) + (int64_t)sel_work_bytes(n_lev) + small + 256;
 }
@@ -531,8 +652,8 @@ static int sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investor
   const int64_t tp = top < investors ? (top > 0 ? top : 0) : investors;
   hipStream_t st = (hipStream_t)stream;
   unsigned char* w = static_cast<unsigned char*>(workspace);
-  const int64_t vals = (int64_t)n_lev * investors * 4;
-  const int64_t winb = (int64_t)kW * investors * 4;
+  const int64_t vals = (int64_t)n_lev * pad4(investors) * 4;
+  const int64_t winb = (int64_t)kW * pad4(investors) * 4;
   float* val = reinterpret_cast<float*>(w);
   void* win = w + ((vals + 255) & ~255ll);
   unsigned char* ws = static_cast<unsigned char*>(win) + ((winb + 255) & ~255ll);
@@ -574,7 +695,8 @@ static int sweep_sorted(int32_t kind, const void* outcomes_dev, int64_t investor
                                   final_only ? 0 : t - 1, st));
   }
   if (data_T_dev)
-    RLMD_HIP(hipMemcpyAsync(data_T_dev, val, sizeof(float) * n_lev * investors, hipMemcpyDeviceToDevice, st));
+    RLMD_HIP(hipMemcpy2DAsync(data_T_dev, sizeof(float) * investors, val, sizeof(float) * pad4(investors),
+                              sizeof(float) * investors, n_lev, hipMemcpyDeviceToDevice, st));
   return 0;
 }
 
@@ -596,8 +718,8 @@ int rlmd_lev_final_sorted(int32_t kind, const void* outcomes_dev, int64_t invest
 
 int64_t rlmd_lev_brain_workspace_bytes(int64_t investors, int32_t n_cfg) {
   if (investors <= 0 || investors > INT32_MAX || n_cfg <= 0) return -1;
-  const int64_t vals = 2 * (int64_t)n_cfg * investors * 8;  // values, leverages (f64 at most)
-  const int64_t win = (int64_t)kW * investors;
+  const int64_t vals = 2 * (int64_t)n_cfg * pad4(investors) * 8;  // values, leverages (f64 at most)
+  const int64_t win = (int64_t)kW * pad4(investors);
   const int64_t small = (int64_t)n_cfg * 8 * 4;
   return ((vals + 255) & ~255ll) + ((win + 255) & ~255ll) + (int64_t)sel_work_bytes(n_cfg) + small + 256;
 }
@@ -610,11 +732,11 @@ static int lev_brain(const uint8_t* outcomes_dev, int64_t investors, int32_t hor
                      void* workspace, float* data_dev, hipStream_t st) {
   const int64_t tp = top < investors ? (top > 0 ? top : 0) : investors;
   unsigned char* w = static_cast<unsigned char*>(workspace);
-  const int64_t NC = (int64_t)n_cfg * investors;
+  const int64_t NC = (int64_t)n_cfg * pad4(investors);
   VT* val = reinterpret_cast<VT*>(w);
   VT* lev = val + NC;
   uint8_t* win = w + ((2 * NC * 8 + 255) & ~255ll);
-  unsigned char* ws = win + (((int64_t)kW * investors + 255) & ~255ll);
+  unsigned char* ws = win + (((int64_t)kW * pad4(investors) + 255) & ~255ll);
   const SelWork sw = sel_work(ws, n_cfg);
   float* cfg = reinterpret_cast<float*>(ws + sel_work_bytes(n_cfg));  // [n_cfg][5] | extra [n_cfg][2]
   float* extra = cfg + 5 * n_cfg;
