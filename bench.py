@@ -271,11 +271,20 @@ def main():
         raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # more ranks than GPUs (a rehearsal of the N-rank path on a smaller box): the
+    # ranks share the GPUs round-robin and exchange over gloo on the host; the
+    # line says so ("rehearsal"), it is never a scaling measurement
+    ndev = torch.cuda.device_count()
+    shared = world > 1 and ndev < world
+    local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from rlmd_amd import _abi
     from rlmd_amd.trainer import VecTrainer
@@ -328,8 +337,8 @@ def main():
     eval_s = time.perf_counter() - te
     if args.eval_every > 0:
         elapsed += eval_s * args.steps / args.eval_every
-    t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(N * args.steps), world, dev,
-                                   extra=(float(ms_n),))
+    t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(N * args.steps), world,
+                                   torch.device("cpu") if shared else dev, extra=(float(ms_n),))
     total_steps = float(slab_all[:, 4].sum().item())
     value = total_steps / t_max
     ms_per_rank = [int(v) for v in slab_all[:, 5].tolist()]
@@ -433,7 +442,8 @@ def main():
                        "eval_ms_per_event": 1e3 * eval_s, "eval_every_vector_steps": args.eval_every,
                        "lanes_per_gpu": N, "global_lanes": N * world, "k_updates_per_vector_step": K,
                        "mini_batch": tr.batch, "topk": tr.topk, "utd_updates_per_env_step": K / N,
-                       "parallelism": f"independent seeds x{world} (no data-path collective)",
+                       "parallelism": f"independent seeds x{world} (no data-path collective)"
+                                      + (f"; REHEARSAL: {world} ranks sharing {ndev} GPU(s) over gloo" if shared else ""),
                        "fused_act_env": fused,
                        "phase_ms_per_step": {"act": act_ms, "env_kernel": env_ms, "learn_k": learn_ms}},
             "updates_per_s": K * args.steps * world / t_max,
