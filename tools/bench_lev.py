@@ -23,8 +23,10 @@ def main():
     ap.add_argument("--horizon", type=int, default=3000)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--kind", default="coin", choices=["coin", "dice", "dice_sh", "gbm"])
+    ap.add_argument("--kind", default="coin", choices=["coin", "dice", "dice_sh", "gbm", "coin_flip"])
     a = ap.parse_args()
+    if a.kind == "coin_flip":
+        return coin_flip_main(a)
     if a.kind != "coin":
         return sorted_main(a)
     dev = torch.device("cuda:0")
@@ -112,6 +114,52 @@ def sorted_main(a):
         dt = time.perf_counter() - t0
         out["cpu_baseline"] = {"value": 20000 * 100 * 10 / dt, "unit": "1/s", "cores": 1, "kind": "port",
                                "sample": "20000 investors x 100 steps x 10 leverages, sort per step (NumPy)"}
+    print(json.dumps(out))
+
+
+def coin_flip_main(a):
+    """The whole of lev/coin_flip.py's experiment (:154-235) on the device at its
+    own size (1e6 investors x 3e3 steps, Bernoulli(0.5), seed-independent
+    synthetic outcomes): coin_fixed_final_lev over 20 leverages, coin_smart_lev
+    over 10, coin_big_brain_lev for investor 2 (1 configuration) and investor 3
+    (19 stop-losses x 6 retention ratios = 114 configurations; the reference's
+    own coin_optimal_lev raises TypeError there, see rlmd_amd/lev.py).  Each
+    call timed with events; one JSON line."""
+    dev = torch.device("cuda:0")
+    inv, hor = a.investors, a.horizon
+    g = torch.Generator(device=dev).manual_seed(420)
+    o = torch.empty((inv, hor), dtype=torch.uint8, device=dev)
+    step = 1 << 17
+    for i in range(0, inv, step):
+        n = min(step, inv - i)
+        o[i:i + n] = (torch.rand((n, hor), generator=g, device=dev) < 0.5).to(torch.uint8)
+    top = int(inv * 1e-4)
+    calls = {
+        "coin_fixed_final_lev (20 levs)": lambda: lev.coin_fixed_final_lev(dev, o, top, 100.0, 0.5, -0.4, 0.05, 1.0,
+                                                                           0.05),
+        "coin_smart_lev (10 levs)": lambda: lev.coin_smart_lev(dev, o, inv, hor, top, 100.0, 0.5, -0.4, 0.1, 1.0, 0.1),
+        "coin_big_brain_lev inv2 (1 cfg)": lambda: lev.coin_big_brain_lev(dev, o, inv, hor, top, 100.0, 0.5, -0.4,
+                                                                           2.5, 0.1, 0.1, 0.1, 0.0, 0.0, 0.1),
+        "coin_big_brain_lev inv3 (114 cfg)": lambda: lev.coin_big_brain_lev(dev, o, inv, hor, top, 100.0, 0.5, -0.4,
+                                                                             2.5, 0.05, 0.95, 0.05, 0.7, 0.95, 0.05),
+    }
+    out = {"metric": "lev/coin_flip.py experiment wall time on one MI355X", "unit": "s",
+           "config": {"investors": inv, "horizon": hor, "top": top}, "calls_ms": {}}
+    total = 0.0
+    for name, fn in calls.items():
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        out["calls_ms"][name] = ms
+        total += ms
+        first = r[0] if isinstance(r, tuple) else r
+        out.setdefault("finite_frac", {})[name] = float(torch.isfinite(first).float().mean().item())
+        del r, first
+    out["value"] = total / 1e3
     print(json.dumps(out))
 
 
