@@ -592,37 +592,42 @@ __device__ __forceinline__ VT optimal_lev(VT v, float v0, float vmin, float roll
   return (VT)(lf * (1.f - loss / vf));
 }
 
-// t == 0: v = value_0 (1 + lev0 r[0]); else v = v (1 + lev r[t]); then lev = optimal(v)
+// t == 0: v = value_0 (1 + lev0 r[0]); else v = v (1 + lev r[t]); then lev =
+// optimal(v); the first select digit of the new leverages (hist_lev) and, when
+// hist_val, of the new values histogrammed on the way
 template <typename VT>
-__global__ void __launch_bounds__(kT) lev_brain_advance_kernel(BrainArgs a, int t, int s) {
-  const int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x;
-  const int c = blockIdx.y;
-  if (i >= a.investors) return;
-  const float* k = a.cfg + 5 * c;
-  const int o = a.wcat[(int64_t)s * pad4(a.investors) + i];
-  const VT r = (VT)a.ret[o > 2 ? 2 : o];
-  const int64_t j = (int64_t)c * pad4(a.investors) + i;
-  VT* val = static_cast<VT*>(a.val);
-  VT* lev = static_cast<VT*>(a.lev);
-  const VT v = t == 0 ? (VT)a.value_0 * ((VT)1 + (VT)k[2] * r) : val[j] * ((VT)1 + lev[j] * r);
-  val[j] = v;
-  lev[j] = optimal_lev<VT>(v, a.value_0, k[0], k[1], k[3] != 0.f, a.lev_factor);
-}
-
-// the first select digit of an existing array (the brain's arrays)
-template <typename VT>
-__global__ void __launch_bounds__(kT) sel_hist0_kernel(const VT* vals, int64_t N, unsigned* hist) {
+__global__ void __launch_bounds__(kT) lev_brain_advance_kernel(BrainArgs a, int t, int s, unsigned* hist_lev,
+                                                               unsigned* hist_val) {
   constexpr int bits = 8 * sizeof(VT);
-  const int l = blockIdx.y;
-  __shared__ unsigned h[kSelBins];
-  for (int i = threadIdx.x; i < kSelBins; i += kT) h[i] = 0;
+  const int c = blockIdx.y;
+  __shared__ unsigned hl[kSelBins], hv[kSelBins];
+  for (int i = threadIdx.x; i < kSelBins; i += kT) {
+    hl[i] = 0;
+    hv[i] = 0;
+  }
   __syncthreads();
+  const float* k = a.cfg + 5 * c;
+  const float vmin = k[0], roll = k[1], lev0 = k[2];
+  const bool rolling = k[3] != 0.f;
+  const int64_t P4 = pad4(a.investors);
+  VT* val = static_cast<VT*>(a.val) + (int64_t)c * P4;
+  VT* lev = static_cast<VT*>(a.lev) + (int64_t)c * P4;
+  const uint8_t* wc = a.wcat + (int64_t)s * P4;
   int64_t b0, b1;
-  chunk_range(N, blockIdx.x, gridDim.x, b0, b1);
-  for_vals(vals + (int64_t)l * pad4(N), b0, b1,
-           [&](VT x) { atomicAdd(&h[(unsigned)(okey(x) >> (bits - kSelB))], 1u); });
+  chunk_range(a.investors, blockIdx.x, gridDim.x, b0, b1);
+  for (int64_t i = b0 + threadIdx.x; i < b1; i += kT) {
+    const int o = wc[i];
+    const VT r = (VT)a.ret[o > 2 ? 2 : o];
+    const VT v = t == 0 ? (VT)a.value_0 * ((VT)1 + (VT)lev0 * r) : val[i] * ((VT)1 + lev[i] * r);
+    const VT l = optimal_lev<VT>(v, a.value_0, vmin, roll, rolling, a.lev_factor);
+    val[i] = v;
+    lev[i] = l;
+    atomicAdd(&hl[(unsigned)(okey(l) >> (bits - kSelB))], 1u);
+    if (hist_val) atomicAdd(&hv[(unsigned)(okey(v) >> (bits - kSelB))], 1u);
+  }
   __syncthreads();
-  flush_hist(h, kSelBins, hist + (int64_t)l * 4 * kSelBins);
+  flush_hist(hl, kSelBins, hist_lev + (int64_t)c * 4 * kSelBins);
+  if (hist_val) flush_hist(hv, kSelBins, hist_val + (int64_t)c * 4 * kSelBins);
 }
 
 }  // namespace
@@ -721,7 +726,7 @@ int64_t rlmd_lev_brain_workspace_bytes(int64_t investors, int32_t n_cfg) {
   const int64_t vals = 2 * (int64_t)n_cfg * pad4(investors) * 8;  // values, leverages (f64 at most)
   const int64_t win = (int64_t)kW * pad4(investors);
   const int64_t small = (int64_t)n_cfg * 8 * 4;
-  return ((vals + 255) & ~255ll) + ((win + 255) & ~255ll) + (int64_t)sel_work_bytes(n_cfg) + small + 256;
+  return ((vals + 255) & ~255ll) + ((win + 255) & ~255ll) + 2 * (int64_t)sel_work_bytes(n_cfg) + small + 256;
 }
 
 }  // extern "C"
@@ -737,15 +742,16 @@ static int lev_brain(const uint8_t* outcomes_dev, int64_t investors, int32_t hor
   VT* lev = val + NC;
   uint8_t* win = w + ((2 * NC * 8 + 255) & ~255ll);
   unsigned char* ws = win + (((int64_t)kW * pad4(investors) + 255) & ~255ll);
-  const SelWork sw = sel_work(ws, n_cfg);
-  float* cfg = reinterpret_cast<float*>(ws + sel_work_bytes(n_cfg));  // [n_cfg][5] | extra [n_cfg][2]
+  const SelWork wl = sel_work(ws, n_cfg), wv = sel_work(ws + sel_work_bytes(n_cfg), n_cfg);  // leverages, values
+  float* cfg = reinterpret_cast<float*>(ws + 2 * sel_work_bytes(n_cfg));  // [n_cfg][5] | extra [n_cfg][2]
   float* extra = cfg + 5 * n_cfg;
   std::vector<float> ex(2 * (size_t)n_cfg);
   for (int c = 0; c < n_cfg; ++c) {  // rows 24 / 25: stop level and roll
     ex[2 * c] = cfg_host[5 * c + 4];
     ex[2 * c + 1] = cfg_host[5 * c + 1];
   }
-  RLMD_HIP(hipMemsetAsync(sw.hist, 0, (size_t)n_cfg * 4 * kSelBins * 4, st));
+  RLMD_HIP(hipMemsetAsync(wl.hist, 0, (size_t)n_cfg * 4 * kSelBins * 4, st));
+  RLMD_HIP(hipMemsetAsync(wv.hist, 0, (size_t)n_cfg * 4 * kSelBins * 4, st));
   RLMD_HIP(hipMemcpyAsync(cfg, cfg_host, sizeof(float) * 5 * n_cfg, hipMemcpyHostToDevice, st));
   RLMD_HIP(hipMemcpyAsync(extra, ex.data(), sizeof(float) * 2 * n_cfg, hipMemcpyHostToDevice, st));
   BrainArgs a{};
@@ -757,12 +763,11 @@ static int lev_brain(const uint8_t* outcomes_dev, int64_t investors, int32_t hor
   a.cfg = cfg;
   a.val = val;
   a.lev = lev;
-  const dim3 grid_adv((unsigned)((investors + kT - 1) / kT), (unsigned)n_cfg);
+  const dim3 grid_adv(kSelBlocks, (unsigned)n_cfg);
   const dim3 grid_win((unsigned)((investors + 63) / 64));
   const int steps = horizon - 1;
-  auto stats = [&](const VT* src, int row0, const float* ext, int n_ext, int t) -> int {
-    hipLaunchKernelGGL(sel_hist0_kernel<VT>, dim3(kSelBlocks, n_cfg), dim3(kT), 0, st, src, investors, sw.hist);
-    RLMD_LAUNCH_CHECK();
+  // the advance histograms both arrays' first digit (the values' from step 1 on)
+  auto stats = [&](const VT* src, const SelWork& sw, int row0, const float* ext, int n_ext, int t) -> int {
     return sel_stats<VT>(src, investors, tp, n_cfg, sw, true, ext, n_ext, data_dev, 26, row0, steps, t, st);
   };
   auto advance = [&](int t) -> int {
@@ -771,15 +776,16 @@ static int lev_brain(const uint8_t* outcomes_dev, int64_t investors, int32_t hor
                          std::min(kW, (int)horizon - t), win);
       RLMD_LAUNCH_CHECK();
     }
-    hipLaunchKernelGGL(lev_brain_advance_kernel<VT>, grid_adv, dim3(kT), 0, st, a, t, t % kW);
+    hipLaunchKernelGGL(lev_brain_advance_kernel<VT>, grid_adv, dim3(kT), 0, st, a, t, t % kW, wl.hist,
+                       t > 0 ? wv.hist : nullptr);
     RLMD_LAUNCH_CHECK();
     return 0;
   };
   RLMD_TRY_INT(advance(0));
   for (int t = 0; t < steps; ++t) {
-    RLMD_TRY_INT(stats(lev, 12, extra, 2, t));
+    RLMD_TRY_INT(stats(lev, wl, 12, extra, 2, t));
     RLMD_TRY_INT(advance(t + 1));
-    RLMD_TRY_INT(stats(val, 0, nullptr, 0, t));
+    RLMD_TRY_INT(stats(val, wv, 0, nullptr, 0, t));
   }
   return 0;
 }
