@@ -101,17 +101,20 @@ constexpr int kMaxRounds = 64;
 constexpr int kSortPopulation = 8192;  // M at or below: sort-based subset
 
 __global__ void __launch_bounds__(kSampleThreads)
-    replay_sample_kernel(rlmd::ReplayView rb, int64_t M, int B, uint64_t seed, uint32_t ctr_lo,
+    replay_sample_kernel(rlmd::ReplayView rb, int64_t M, int B, int G, uint64_t seed, uint32_t ctr_lo,
                          uint32_t ctr_hi, int64_t* idx_out, float* s, float* a,
                          float* r, float* s2, uint8_t* done, float* xsa, int32_t* eff) {
   __shared__ uint64_t keys[kSortPopulation];
   __shared__ int64_t cand[kSampleThreads];
   __shared__ int any_dup;
   const int i = threadIdx.x;
-  // workgroup k of a K-batch launch draws mini-batch k with counter ctr + k and
-  // writes it at offset k (one independent sample per workgroup)
+  // workgroups [G k, G k + G) of a K-batch launch all draw mini-batch k with
+  // counter ctr + k (the same distinct set: the draw is a function of the
+  // counter) and each gathers 1 / G of its rows — the gather's scattered
+  // row reads spread over G CUs — into offset k
+  const int part = blockIdx.x % G;
   {
-    const int k = blockIdx.x;
+    const int k = blockIdx.x / G;
     const uint64_t ctr = ((uint64_t)ctr_hi << 32 | ctr_lo) + (uint64_t)k;
     ctr_lo = (uint32_t)ctr;
     ctr_hi = (uint32_t)(ctr >> 32);
@@ -192,7 +195,8 @@ __global__ void __launch_bounds__(kSampleThreads)
     }
   }
   __syncthreads();
-  if (i >= B) return;
+  const int per = (B + G - 1) / G;
+  if (i >= B || i < part * per || i >= (part + 1) * per) return;
   const int64_t row = cand[i];
   if (idx_out) idx_out[i] = row;
   gather_row(rb, row, i, s, a, r, s2, done, xsa, eff);
@@ -250,7 +254,8 @@ int replay_sample_launch(const ReplayView& rb, int64_t M, int B, int K, uint64_t
   RLMD_CHECK(K >= 1, "need at least one mini-batch");
   RLMD_CHECK(M >= B, "replay holds fewer transitions than the mini-batch");
   RLMD_CHECK(M <= (int64_t)1 << 52, "replay too large");
-  hipLaunchKernelGGL(replay_sample_kernel, dim3(K), dim3(kSampleThreads), 0, stream, rb, M, B, seed,
+  const int G = B >= 256 ? 8 : 1;  // gather parts per mini-batch
+  hipLaunchKernelGGL(replay_sample_kernel, dim3(K * G), dim3(kSampleThreads), 0, stream, rb, M, B, G, seed,
                      (uint32_t)ctr, (uint32_t)(ctr >> 32), idx, s, a, r, s2, done, xsa, eff);
   RLMD_LAUNCH_CHECK();
   return 0;
