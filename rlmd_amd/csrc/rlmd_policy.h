@@ -25,7 +25,11 @@ constexpr float kHalfLog2Pi = 0.91893853320467274178f;  // log(sqrt(2 pi))
 constexpr double kF32Eps = 1.1920928955078125e-07;        // torch.finfo(float32).eps
 
 // Philox noise of component j of row b: a standard normal (N, MVN) or the
-// Laplace sampler's uniform in (eps - 1, 1).
+// Laplace sampler's uniform in (eps - 1, 1).  The normal is an f32 Box-Muller
+// pair from 24-bit uniforms with the hardware log / sin / cos (the reference
+// draws this exploration noise in f32 with torch; an f64 pair here was a
+// ~5k-cycle chain on the target pass's critical path).  The env's own draws
+// (env.hip) keep NumPy's f64 construction.
 __device__ __forceinline__ float policy_draw(int dist, uint64_t seed, uint32_t b, uint32_t ctr, uint32_t tag,
                                              int j) {
   const rlmd_u32x4 v = rlmd_philox(seed, b, ctr, tag, (uint32_t)(j >> 1));
@@ -34,9 +38,12 @@ __device__ __forceinline__ float policy_draw(int dist, uint64_t seed, uint32_t b
     const float w = (float)((kF32Eps - 1.0) + (2.0 - kF32Eps) * u01);
     return fminf(w, 0x1.fffffep-1f);  // strictly below 1: log1p(-|w|) finite
   }
-  double z0, z1;
-  rlmd_normal2(v, z0, z1);
-  return (float)((j & 1) ? z1 : z0);
+  const float u1 = (float)(v.x >> 8) * 0x1p-24f;  // [0, 1): 1 - u1 in (0, 1]
+  const float u2 = (float)(v.z >> 8) * 0x1p-24f;
+  const float r = __fsqrt_rn(-2.f * __logf(1.f - u1));
+  float sn, cs;
+  __sincosf(6.28318530717958647692f * u2, &sn, &cs);
+  return (j & 1) ? r * sn : r * cs;
 }
 
 // One component of the sampler.  In: mu and the log-scale head with biases,
