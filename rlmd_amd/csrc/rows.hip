@@ -266,8 +266,19 @@ __device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, cons
   const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(p, o.size * 4);
   // j < in and h < nh are uniform: skipped loads are not issued (a wave holds at
   // most 63 loads in flight, and the first load round is at that limit)
+  // the fc1 row (in <= 8 contiguous floats) as one or two 16-B loads: a wave's
+  // 64 consecutive units are one 1.5 KB span, and per-float loads touched its
+  // cache lines once per input (the load round is bound by line accesses)
+  {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const int off = (int)((o.w1 + (int64_t)m.c * in) * 4);
+    const u32x4 lo = __builtin_amdgcn_raw_buffer_load_b128(rp, own ? off : 0x7fffffff, 0, 0);
+    u32x4 hi = u32x4{0u, 0u, 0u, 0u};
+    if (in > 4) hi = __builtin_amdgcn_raw_buffer_load_b128(rp, own ? off + 16 : 0x7fffffff, 0, 0);
 #pragma unroll
-  for (int j = 0; j < W1P; ++j) k.w1[j] = j < in ? rlmd_ldf(rp, o.w1 + (int64_t)m.c * in + j, own) : 0.f;
+    for (int j = 0; j < W1P; ++j)
+      k.w1[j] = j < in ? __builtin_bit_cast(float, j < 4 ? lo[j & 3] : hi[j & 3]) : 0.f;
+  }
   k.b1 = rlmd_ldf(rp, o.b1 + m.c, own);
   const int64_t oa = wa - p, ob = (wb ? wb : wa) - p;  // head rows relative to p
 #pragma unroll
@@ -701,14 +712,18 @@ __device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const uint8_t* m1, con
   // m2: this thread's kMR consecutive rows of column m.c from kMR / 4 aligned
   // words (+ one when its first row is not word aligned: fewer than 4 rows per
   // thread, H2p < 128)
+  // the column's 16-row record is one aligned 16-B load (one access per line
+  // instead of one per word)
   constexpr int NWD = kMR<NBW> / 4;
   const int sh = m.r0 & 3, rbase = m.r0 & ~3;
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 rec =
+      __builtin_amdgcn_raw_buffer_load_b128(r2, m.r0 < R ? (int)m2_index(rb, H2p, 0, m.c) : 0x7fffffff, 0, 0);
   uint32_t wd[NWD + 1];
 #pragma unroll
   for (int w = 0; w <= NWD; ++w) {
-    const int64_t e = m2_index(rb, H2p, rbase + 4 * w, m.c);
-    const bool need = m.r0 < R && (w < NWD || sh != 0);
-    wd[w] = __builtin_amdgcn_raw_buffer_load_b32(r2, need ? (int)e : 0x7fffffff, 0, 0);
+    const int qi = (rbase >> 2) + w;  // <= 3 wherever the word is read (rows of one 16-row record)
+    wd[w] = qi == 0 ? rec.x : (qi == 1 ? rec.y : (qi == 2 ? rec.z : rec.w));
   }
 #pragma unroll
   for (int rr = 0; rr < kMR<NBW>; ++rr) {
