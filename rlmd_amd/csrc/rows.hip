@@ -712,18 +712,14 @@ __device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const uint8_t* m1, con
   // m2: this thread's kMR consecutive rows of column m.c from kMR / 4 aligned
   // words (+ one when its first row is not word aligned: fewer than 4 rows per
   // thread, H2p < 128)
-  // the column's 16-row record is one aligned 16-B load (one access per line
-  // instead of one per word)
   constexpr int NWD = kMR<NBW> / 4;
   const int sh = m.r0 & 3, rbase = m.r0 & ~3;
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x4 rec =
-      __builtin_amdgcn_raw_buffer_load_b128(r2, m.r0 < R ? (int)m2_index(rb, H2p, 0, m.c) : 0x7fffffff, 0, 0);
   uint32_t wd[NWD + 1];
 #pragma unroll
   for (int w = 0; w <= NWD; ++w) {
-    const int qi = (rbase >> 2) + w;  // <= 3 wherever the word is read (rows of one 16-row record)
-    wd[w] = qi == 0 ? rec.x : (qi == 1 ? rec.y : (qi == 2 ? rec.z : rec.w));
+    const int64_t e = m2_index(rb, H2p, rbase + 4 * w, m.c);
+    const bool need = m.r0 < R && (w < NWD || sh != 0);
+    wd[w] = __builtin_amdgcn_raw_buffer_load_b32(r2, need ? (int)e : 0x7fffffff, 0, 0);
   }
 #pragma unroll
   for (int rr = 0; rr < kMR<NBW>; ++rr) {
