@@ -133,7 +133,8 @@ def run_env():
     lib.rlmd_train_set_fused(0)
     from rlmd_amd.trainer import VecTrainer
 
-    tr = VecTrainer("gbm", "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
+    fam = sys.argv[2] if len(sys.argv) > 2 else "gbm"
+    tr = VecTrainer(fam, "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
                     replay_capacity=1 << 20, k_updates=1, device="cuda:0")
     nb = 256
     buf = (C.c_ulonglong * (8 * nb))()
