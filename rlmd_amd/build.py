@@ -19,7 +19,9 @@ SOURCES = ["abi.hip", "env.hip", "replay.hip", "gemm.hip", "learn.hip", "act.hip
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable"]
 # env math must round where NumPy rounds (no FMA contraction); GEMM/learner may fuse
-PER_FILE = {"env.hip": ["-ffp-contract=off"], "eval.hip": ["-ffp-contract=off"], "shadow.hip": ["-ffp-contract=off"],
+# act.hip as env.hip: the two acting kernels (act.hip, env.hip act_env_kernel) share
+# rlmd_act_rows.h and must round alike (fused and two-launch steps are bit-equal)
+PER_FILE = {"env.hip": ["-ffp-contract=off"], "act.hip": ["-ffp-contract=off"], "eval.hip": ["-ffp-contract=off"], "shadow.hip": ["-ffp-contract=off"],
             "lev_sort.hip": ["-ffp-contract=off"]}
 DEFAULT_EXTRA = ["-ffp-contract=fast"]
 

@@ -14,6 +14,10 @@
 // padded to 32, kept current by the optimiser; learn.hip refresh_copies), so
 // the same kernel serves SAC 256/256 (H1p 256, NB 4) and TD3 400/300 (H1p 416,
 // NB 5: 320 columns); other nets use the generic GEMM path (learn.hip: agent_act).
+// FP contraction is off, as in env.hip, whose act_env_kernel runs the same
+// acting body: the two-launch and the fused steady state are bit-equal
+// (tests/test_fused_env_gpu.py).
+#pragma clang fp contract(off)
 #include <math.h>
 #include <hip/hip_ext.h>
 

@@ -695,8 +695,8 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
 // step of env_train_kernel with the action still in registers and the
 // observation still in LDS — one launch per vector step instead of two, and the
 // actions never round-trip through HBM.  This file compiles with FP contraction
-// off (the env's NumPy rounding), so the acting body here rounds the sampler's
-// few multiply-adds separately where act.hip fuses them (<= 1 ulp of an action).
+// off (the env's NumPy rounding), and so does act.hip: the fused and two-launch
+// steps produce bit-equal actions, rings and wealth.
 // ---------------------------------------------------------------------------
 template <int FAM, int NG, int H1P, int NB, int SP>
 __global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,

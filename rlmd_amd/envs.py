@@ -42,6 +42,8 @@ class VecEnv:
         pp = None
         if prices is not None:
             self._prices = np.ascontiguousarray(prices, dtype=np.float64)
+            if self._prices.ndim != 2 or self._prices.shape[1] != n_gambles:
+                raise ValueError(f"prices must be [days, n_assets = {n_gambles}], got {self._prices.shape}")
             n_days = self._prices.shape[0]
             pp = self._prices.ctypes.data_as(C.c_void_p)
         h = C.c_void_p()

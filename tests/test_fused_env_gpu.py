@@ -1,0 +1,130 @@
+"""The steady-state kernel (env.hip act_env_kernel: policy acting + env step +
+replay insert + auto-reset + episode rows in one launch) for every env family
+and investor, at both acting widths (SAC 256/256, TD3 400/300) — GPU only.
+
+Post-window policy steps (warm-up 0, smoothing 0, bf16 nets): every step's
+ring rows (s, a, r, s', learn_done) are replayed through the oracle env
+(oracle/envs.py, pinned to the reference's own traces) with the recorded f32
+policy actions and the same Philox draws: f32-exact rows, f64 wealth within
+1e-12 (Box-Muller libm ulps), done flags exact, and the per-episode rows the
+kernel appends (ballot-compacted per wave) equal to the oracle's episode ends.
+Reference steps covered: envs/coin_flip_envs.py:150-521,
+envs/dice_roll_envs.py:153-524, envs/dice_roll_sh_envs.py:160-645,
+envs/gbm_envs.py:147-515, envs/market_envs.py:133-202 / :283-358 / :440-528
+(D1), dones tools/env_resources.py:26-200.
+
+Shapes the fused kernel does not instantiate (action_dim > 2: the C investors
+and Dice_SH B/C) run the two-launch path (acting kernel + env_train_kernel);
+the test asserts which path ran (rlmd_train_last_fused) and checks both.
+
+Fused vs unfused: the same seeded loop with rlmd_train_set_fused(1) and (0),
+learning on (K = 1), must produce bit-identical rings, wealth and parameters
+(act.hip and the fused kernel share rlmd_act_rows.h and both compile with FP
+contraction off).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import envs as oe
+from tests.test_train_gpu import _market_kw, read_ring
+
+pytestmark = pytest.mark.gpu
+
+FAMS = {"coin": oe.COIN, "dice": oe.DICE, "gbm": oe.GBM, "dice_sh": oe.DICE_SH, "market": oe.MARKET}
+INVS = {"A": oe.INV_A, "B": oe.INV_B, "C": oe.INV_C, "INSURED": oe.INV_INSURED}
+CASES = ([(f, i) for f in ("coin", "dice", "gbm") for i in "ABC"]
+         + [("dice_sh", i) for i in ("INSURED", "A", "B", "C")] + [("market", i) for i in "ABC"])
+
+
+def _lib():
+    from rlmd_amd import _abi
+
+    return _abi.lib()
+
+
+def _trainer(dev, golden, env, inv, algo, N, T, k=0, seed=11):
+    from rlmd_amd.trainer import VecTrainer
+
+    kw = {}
+    if env == "market":  # one asset: stooq_usei's first column
+        kw = _market_kw(golden, 1)
+        kw["prices"] = np.ascontiguousarray(kw["prices"][:, :1])
+    return VecTrainer(env=env, investor=inv, n_lanes=N, algo=algo, k_updates=k, seed=seed, init_seed=seed,
+                      warmup_steps=0, smoothing_window=0, replay_capacity=N * T, precision="bf16", device=dev,
+                      **kw), kw
+
+
+@pytest.mark.parametrize("algo", ["SAC", "TD3"])
+@pytest.mark.parametrize("env,inv", CASES)
+def test_policy_steps_match_oracle(golden, dev, env, inv, algo):
+    N, T, seed = 4000, 16, 11  # 4000 lanes: a ragged last 64-lane block
+    _lib().rlmd_train_set_fused(1)
+    tr, kw = _trainer(dev, golden, env, inv, algo, N, T, seed=seed)
+    ora = oe.OracleVecEnv(FAMS[env], INVS[inv], N, 1, seed=seed, **kw)
+    obs = ora.reset()
+    tr.episode_log(64)
+    at = 1e-45 if env == "market" else 1e-30
+    length = np.ones(N, dtype=np.int64)
+    expect_fused = ora.A <= 2 and ora.S <= 8
+    ended = 0
+    for t in range(T):
+        tr.step()
+        assert _lib().rlmd_train_last_fused() == int(expect_fused), "unexpected acting + env path"
+        s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
+        assert np.all(np.abs(a_r) <= 0.99) and np.all(np.isfinite(a_r))
+        ns, r, d, risk = ora.step(a_r.astype(np.float32))  # post-window policy actions: f32
+        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s")
+        np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6, err_msg=f"t={t} r")
+        np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s2")
+        np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
+        w_gpu, t_gpu = tr.env.lane_state()
+        live = ~d[:, 0]
+        np.testing.assert_allclose(w_gpu[live], ora.wealth[live], rtol=1e-12, atol=0, err_msg=f"t={t} wealth")
+        np.testing.assert_array_equal(t_gpu[live], ora.time[live])
+        m = d[:, 0]
+        rows, dropped = tr.drain_episodes()
+        assert dropped == 0
+        np.testing.assert_array_equal(rows[:, 1], np.nonzero(m)[0], err_msg=f"t={t} finished lanes")
+        np.testing.assert_array_equal(rows[:, 0], np.full(len(rows), t), err_msg=f"t={t} step column")
+        np.testing.assert_array_equal(rows[:, 2], r[m].astype(np.float32), err_msg=f"t={t} final rewards")
+        np.testing.assert_array_equal(rows[:, 3], length[m], err_msg=f"t={t} lengths")
+        np.testing.assert_allclose(rows[:, 4:], risk[m].astype(np.float32), rtol=1e-6, atol=0, err_msg=f"t={t} risk")
+        ended += int(m.sum())
+        length += 1
+        length[m] = 1
+        obs = ns.copy()
+        if m.any():
+            obs[m] = ora.reset(m)[m]
+    np.testing.assert_allclose(tr.obs.cpu().numpy(), obs.astype(np.float32), rtol=1e-6, atol=at)
+    assert np.unique(a_r[:, 0]).size > N // 4  # stochastic policy actions
+    if env == "market":
+        assert ended > 0  # 12-day episodes: lanes finish and restart inside the test
+
+
+@pytest.mark.parametrize("algo", ["SAC", "TD3"])
+@pytest.mark.parametrize("env,inv", [("coin", "B"), ("dice", "A"), ("gbm", "A"), ("dice_sh", "INSURED"),
+                                     ("dice_sh", "A"), ("market", "B")])
+def test_fused_equals_unfused(golden, dev, env, inv, algo):
+    N, T = 2048, 12
+    out = []
+    try:
+        for fused in (1, 0):
+            _lib().rlmd_train_set_fused(fused)
+            tr, _ = _trainer(dev, golden, env, inv, algo, N, T, k=1, seed=5)
+            for t in range(T):
+                tr.step()
+                assert _lib().rlmd_train_last_fused() == fused
+            ring = read_ring(tr, 0, N * T)
+            w, tt = tr.env.lane_state()
+            out.append((ring, w, tt, tr.obs.cpu().numpy(), tr.agent.params.cpu().numpy().copy()))
+            del tr
+    finally:
+        _lib().rlmd_train_set_fused(1)
+    (ra, wa, ta, oa, pa), (rb, wb, tb, ob, pb) = out
+    for name, x, y in zip(("s", "a", "r", "s2", "d"), ra, rb):
+        np.testing.assert_array_equal(x, y, err_msg=f"ring {name}")
+    np.testing.assert_array_equal(wa, wb)
+    np.testing.assert_array_equal(ta, tb)
+    np.testing.assert_array_equal(oa, ob)
+    np.testing.assert_array_equal(pa, pb)  # the K = 1 updates learned from identical rings
