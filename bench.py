@@ -24,6 +24,7 @@ import glob
 import json
 import math
 import os
+import re
 import sys
 import time
 
@@ -78,15 +79,15 @@ def td3_update_flops(S, A, H1, H2, B, actor_every=2):
     return 2.0 * B * (per + act / actor_every)
 
 
-def synthetic_prices(days=9167, n_assets=1, seed=7):
-    """Stand-in for tools/market_data/stooq_snp.npy (9167 x 1 daily closes; the
-    reference's data is not on the GPU box): a geometric random walk with an
-    equity-like daily drift 3e-4 and volatility 1.2 %."""
+def stooq_snp_prices():
+    """tools/market_data/stooq_snp.npy (9167 x 1 S&P 500 daily closes, the C4
+    workload of SURVEY §8d) from the committed data fixture
+    tests/golden/stooq_snp.npz (tests/golden/make_market_data.py copies it out
+    of the reference; the GPU box has no /root/reference)."""
     import numpy as np
 
-    rng = np.random.default_rng(seed)
-    r = rng.normal(3e-4, 0.012, (days - 1, n_assets))
-    return 100.0 * np.exp(np.vstack([np.zeros((1, n_assets)), np.cumsum(r, 0)]))
+    with np.load(os.path.join(ROOT, "tests", "golden", "stooq_snp.npz"), allow_pickle=False) as z:
+        return np.ascontiguousarray(z["prices"], dtype=np.float64)
 
 
 # BASELINE.json configs (SURVEY §8 C2-C5) as single-GPU workloads.  C2 is the
@@ -98,7 +99,7 @@ CONFIGS = {
     "c3": dict(env="dice_sh", investor="A", n=1, algo="TD3", lanes=65536, replay=1 << 20, multi_steps=1,
                workload="C3: Dice_SH_InvA (key 18, S=6,A=2), TD3 400/300, B=200/k=100, replay 1M/GPU"),
     "c4": dict(env="market", investor="A", n=1, algo="SAC", lanes=8192, replay=1 << 20, multi_steps=1,
-               workload="C4: Market_InvA_D1 on a synthetic 9167-day price table (stooq_snp shape), "
+               workload="C4: Market_InvA_D1 on stooq_snp (9167 S&P 500 daily closes), "
                         "train 1000 d, shuffle 5, SAC 256/256, 8192 lanes/GPU (one seed shard per GPU)"),
     "c5": dict(env="gbm", investor="A", n=1, algo="TD3", lanes=65536, replay=1 << 24, multi_steps=5,
                workload="C5: GBM_InvA, TD3 400/300, multi-step n=5 (A), replay 16,777,216 transitions/GPU"),
@@ -161,17 +162,33 @@ def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H
                       f"torch-CPU, {threads} thread(s)), {el:.1f} s"}
 
 
-def load_traffic():
-    """HBM bytes per env_train_kernel launch from the newest committed PMC summary
-    (profiles/<round>_pmc_env.json, written by tools/pmc_summary.py from separate
-    rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same bench command)."""
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_env.json")))
-    if not paths:
+def load_traffic(kernel, config, lanes):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    written for it (profiles/<round>_pmc_env.json, tools/pmc_summary.py, from
+    separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same bench command).
+    kernel: "act_env_marginal" (the fused kernel minus the acting kernel: the env
+    step's marginal traffic) or "env_train_kernel" (the separate env kernel).
+    Only a summary of the same kernel, config and lane count is used; the newest
+    round wins (r03 > r02b > r02a > r02)."""
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_env.json")):
+        try:
+            d = json.load(open(path))
+        except Exception:
+            continue
+        kid = d.get("kernel_id") or ("act_env_marginal" if d.get("kernel", "").startswith("act_env_kernel")
+                                     else "env_train_kernel")
+        if kid != kernel or d.get("config", "c2") != config or d.get("lanes") != lanes:
+            continue
+        tag = os.path.basename(path)[:-len("_pmc_env.json")]
+        m = re.match(r"r(\d+)([a-z]*)", tag)
+        key = (int(m.group(1)), len(m.group(2)) > 0, m.group(2)) if m else (0, False, tag)
+        if best is None or key > best[0]:
+            best = (key, d, tag)
+    if best is None:
         return None
-    try:
-        return json.load(open(paths[-1]))
-    except Exception:
-        return None
+    return {"hbm_bytes_per_launch": best[1]["hbm_bytes_per_launch"], "source": f"profiles/{best[2]}_pmc_env.json",
+            "kernel": best[1].get("kernel")}
 
 
 def reduce_ranks(elapsed, ep_stats, steps, world, device, extra=()):
@@ -239,6 +256,93 @@ def timed_steps(tr, steps, k=None):
     return 1e3 * (time.perf_counter() - t0) / steps
 
 
+def timed_region(tr, steps, warmup, world, sync, on_start=None):
+    """`warmup` untimed steps, then exactly `steps` timed steps bracketed by a
+    barrier + device synchronize on both sides (the harness contract); returns
+    this rank's wall seconds."""
+    import torch.distributed as dist
+
+    for _ in range(warmup):
+        tr.step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    if on_start is not None:
+        on_start()
+        sync()
+        if world > 1:
+            dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        tr.step()
+    sync()
+    if world > 1:
+        dist.barrier()
+    return time.perf_counter() - t0
+
+
+def whole_job(elapsed, tr, lanes, steps, world, device, ms_n):
+    """Whole-job value: the env steps every rank timed / the max-over-ranks
+    wall time (reduce_ranks, the run's one collective); plus each rank's
+    multi-step n as the ranks report it."""
+    t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(lanes * steps), world, device,
+                                   extra=(float(ms_n),))
+    total_steps = float(slab_all[:, 4].sum().item())
+    return t_max, total_steps / t_max, [int(v) for v in slab_all[:, 5].tolist()]
+
+
+class DryTrainer:
+    """--dry-run stand-in for VecTrainer (no HIP library, no GPU): a fixed host
+    sleep per vector step, longer on higher ranks, so the N-rank plumbing
+    (spawn_ranks, rendezvous, per-rank multi-step n, barrier-bracketed timing,
+    max-over-ranks, all_gather, the JSON line) runs on CPU over gloo
+    (tests/test_bench_cli_cpu.py)."""
+
+    def __init__(self, rank, step_s=0.002):
+        self.rank, self.step_s, self.t = rank, step_s, 0
+
+    def step(self, k=None):
+        time.sleep(self.step_s * (1 + self.rank))
+        self.t += 1
+
+    def flush_stats(self):
+        import torch
+
+        return torch.tensor([0.0, 0.0, 0.0, float(self.t)])
+
+
+def dry_run(args):
+    """The N-rank launch path of main() with DryTrainer: gloo on the host,
+    rank 0 prints the headline fields it would print for the real loop,
+    labelled DRY-RUN (never a measurement)."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    cfg = CONFIGS[args.config]
+    N = args.lanes or cfg["lanes"]
+    ms_n = parse_multi_steps(args.multi_steps, rank, cfg["multi_steps"])
+    tr = DryTrainer(rank)
+    elapsed = timed_region(tr, args.steps, args.warmup, world, lambda: None)
+    t_max, value, ms_per_rank = whole_job(elapsed, tr, N, args.steps, world, torch.device("cpu"), ms_n)
+    if rank == 0:
+        print(json.dumps({"metric": "DRY-RUN (host stand-in trainer; not a measurement)", "value": value,
+                          "unit": "env steps/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": 1e3 * t_max / args.steps, "t_max_s": t_max,
+                          "rank0_elapsed_s": elapsed, "scaling": "weak",
+                          "config": {"config": args.config, "lanes_per_gpu": N, "global_lanes": N * world,
+                                     "multi_steps_per_rank": ms_per_rank}}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -258,10 +362,14 @@ def main():
                     help="vector steps between evaluations (eval_freq 1e3, main.py); amortised into value")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="the N-rank launch path with a host stand-in trainer (gloo, no GPU): plumbing test only")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
+    if args.dry_run:
+        return dry_run(args)
 
     import torch
     import torch.distributed as dist
@@ -296,7 +404,7 @@ def main():
     ms_n = parse_multi_steps(args.multi_steps, rank, cfg["multi_steps"])
     kw = {}
     if cfg["env"] == "market":
-        kw = dict(prices=synthetic_prices(), obs_days=1, time_length=1000, shuffle_days=5,
+        kw = dict(prices=stooq_snp_prices(), obs_days=1, time_length=1000, shuffle_days=5,
                   sample_days=1000 + 250 + 1 + 20 - 1)
     if ms_n > 1:
         replay = (replay // N) * N  # per-lane rings: capacity a multiple of the lanes
@@ -304,22 +412,8 @@ def main():
                     loss=args.loss, k_updates=K, replay_capacity=replay, seed=420 + rank, warmup_steps=0,
                     smoothing_window=0, precision=args.precision, device=dev, init_seed=420 + rank,
                     multi_steps=ms_n, dynamics="A", **kw)
-    for _ in range(args.warmup):
-        tr.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    _abi.check(_abi.lib().rlmd_profile_enable(1))
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        tr.step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed_region(tr, args.steps, args.warmup, world, torch.cuda.synchronize,
+                           on_start=lambda: _abi.check(_abi.lib().rlmd_profile_enable(1)))
     ms = (C.c_double * 3)()
     cnt = (C.c_int64 * 3)()
     _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
@@ -337,11 +431,8 @@ def main():
     eval_s = time.perf_counter() - te
     if args.eval_every > 0:
         elapsed += eval_s * args.steps / args.eval_every
-    t_max, slab_all = reduce_ranks(elapsed, tr.flush_stats().double(), float(N * args.steps), world,
-                                   torch.device("cpu") if shared else dev, extra=(float(ms_n),))
-    total_steps = float(slab_all[:, 4].sum().item())
-    value = total_steps / t_max
-    ms_per_rank = [int(v) for v in slab_all[:, 5].tolist()]
+    t_max, value, ms_per_rank = whole_job(elapsed, tr, N, args.steps, world,
+                                          torch.device("cpu") if shared else dev, ms_n)
 
     # after the headline region (rank-local, no collective): K sweep at the same
     # lanes, and the fp32 companion (the reference's arithmetic) at the headline K
@@ -370,10 +461,8 @@ def main():
     learn_ms = ms[2] / max(cnt[2], 1)
     act_ms = ms[0] / max(cnt[0], 1)
     n_assets = cfg["n"] if cfg["env"] == "market" else 0
-    pmc = load_traffic()
-    traffic = None
-    if pmc and pmc.get("lanes") == N and pmc.get("config", "c2") == args.config:
-        traffic = pmc.get("hbm_bytes_per_launch")
+    pmc = load_traffic("act_env_marginal" if fused else "env_train_kernel", args.config, N)
+    traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     H1, H2 = tr.agent.h1, tr.agent.h2
     lib = _abi.lib()
     if fused:
@@ -402,8 +491,8 @@ def main():
         act_fl = act_flops_per_row(S, A, H1, H2, cfg["algo"]) * N
         roofline = {"kernel": "act_env_kernel: env step + replay insert + auto-reset in the acting kernel's epilogue",
                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "algorithmic_bytes_per_launch": env_bytes,
-                    "avg_launch_ms": marginal_ms,
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc and pmc["source"],
+                    "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": marginal_ms,
                     "timing": "marginal: act_env_kernel (kernel-attached HIP events, every timed step) minus the "
                               "standalone fused acting kernel on the same rows (kernel-attached events, 20 launches)",
                     "fused_kernel_ms": fused_ms, "act_only_kernel_ms": act_only_ms,
@@ -422,7 +511,7 @@ def main():
         achieved = env_bytes / (env_ms * 1e-3) / 1e9
         roofline = {"kernel": "env_train_kernel (fused env step + replay insert + reset)",
                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc and pmc["source"],
                     "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms,
                     "timing": "HIP events attached to every env_train_kernel dispatch of the timed region "
                               "(hipExtLaunchKernelGGL start/stop: the dispatch's own begin/end)"}
@@ -436,7 +525,8 @@ def main():
             "metric": "env steps/sec (whole node), 64k-parallel GBM+SAC at 1/2/4/8 MI355X",
             "value": value, "unit": "env steps/sec", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1e3 * t_max / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.precision,
+            "data": "real: stooq_snp daily closes" if cfg["env"] == "market" else "synthetic",
             "config": {"workload": cfg["workload"], "config": args.config, "critic_loss": args.loss,
                        "replay_per_gpu": replay, "multi_steps": ms_n, "multi_steps_per_rank": ms_per_rank,
                        "eval_ms_per_event": 1e3 * eval_s, "eval_every_vector_steps": args.eval_every,

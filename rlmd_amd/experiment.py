@@ -48,26 +48,32 @@ def _world():
 
 
 def gather_logs(lg, owner, world, device):
-    """One all_gather of every rank's four log arrays (flattened f64, lossless for
-    the f32 logs) plus per-trial row counts; trial t is taken from rank owner[t].
-    The trial arrays are first widened to the largest row count of any rank (one
-    all_reduce of that count)."""
+    """Two all_gathers: every rank's four log arrays as one flat f32 slab (the
+    logs' own dtype: no widening) and the per-trial row counts (int64); trial t
+    is taken from rank owner[t].  The trial arrays are first widened to the
+    largest row count of any rank (one all_reduce of that count).  The slab is
+    n_trials x (rows x (19 + risk) + evals x n_eval x (20 + risk)) x 4 B per
+    rank; ExperimentLog.max_rows bounds the rows before the run gets here."""
     import torch.distributed as dist
 
     width = torch.tensor([lg.trial.shape[1]], dtype=torch.int64, device=device)
     dist.all_reduce(width, op=dist.ReduceOp.MAX)
     lg.grow(int(width.item()))
-    parts = [lg.trial, lg.eval, lg.trial_risk, lg.eval_risk, lg.rows.astype(np.float64)]
-    flat = torch.from_numpy(np.concatenate([np.asarray(p, np.float64).ravel() for p in parts])).to(device)
+    parts = [lg.trial, lg.eval, lg.trial_risk, lg.eval_risk]
+    flat = torch.from_numpy(np.concatenate([np.asarray(p, np.float32).ravel() for p in parts])).to(device)
     out = [torch.empty_like(flat) for _ in range(world)]
     dist.all_gather(out, flat)
+    rows = torch.from_numpy(lg.rows.astype(np.int64)).to(device)
+    rows_out = [torch.empty_like(rows) for _ in range(world)]
+    dist.all_gather(rows_out, rows)
     got = [o.cpu().numpy() for o in out]
+    got_rows = [o.cpu().numpy() for o in rows_out]
     sizes = [p.size for p in parts]
     offs = np.concatenate([[0], np.cumsum(sizes)])
     for t, r in enumerate(owner):
         src = [got[r][offs[i]:offs[i + 1]].reshape(parts[i].shape) for i in range(len(parts))]
         lg.trial[t], lg.eval[t], lg.trial_risk[t], lg.eval_risk[t] = src[0][t], src[1][t], src[2][t], src[3][t]
-        lg.rows[t] = int(src[4][t])
+        lg.rows[t] = int(got_rows[r][t])
     return lg
 
 
@@ -105,17 +111,26 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
                    eval_freq=1000, n_eval=100, max_eval_steps=100, n_trials=1, k_updates=1, log_every=1,
                    warmup_steps=1000, smoothing_window=2000, buffer=1_000_000, multi_steps=1, precision="bf16",
                    seed=0, results_root=".", test_agent=True, device="cuda:0", test_days=250,
-                   trainer_factory=None, gather_device=None, episode_rows=True, episode_cap=256, trail=50,
-                   checkpoint=True, continue_trials=False, **trainer_kw):
+                   trainer_factory=None, gather_device=None, episode_rows=True, episode_cap=None, trail=50,
+                   checkpoint=True, continue_trials=False, max_episode_rows=1 << 22, **trainer_kw):
     """Train n_trials independent vectorised agents (sharded over the ranks of an
     initialised process group, trial t on rank t % world) and save the
     reference's four log arrays on rank 0; returns (file stem, ExperimentLog),
     the log complete on every rank.
 
-    episode_rows: one trial row per finished episode from the device episode log
-    (drained every `log_every` vector steps); False: one aggregate row per
-    interval.  checkpoint: trailing-`trail` checkpoints under the reference's
-    models/ path.  continue_trials: inputs["continue"] — trial t starts from
+    episode_rows: one trial row per finished episode from the device episode log;
+    False: one aggregate row per interval.  A lane finishes at most one episode
+    per vector step, so a wave's log slots (episode_cap rows per 64 lanes per
+    drain) never overflow when episode_cap >= 64 x the steps between drains:
+    the default drains every `log_every` steps with 64 x log_every slots per
+    wave up to log_every 64, and beyond that drains every step (64 slots) into a
+    host list folded into the row at the log step.  A drain that reports
+    dropped rows raises (a lossy log would bias the trial rows and the
+    trailing-score checkpoints towards low lanes).  max_episode_rows bounds the
+    per-episode trial rows of one trial (host memory and the logging gather:
+    (19 + risk) x 4 B per row); a run that exceeds it raises, pointing at
+    episode_rows=False (one aggregate row per logging interval).
+    checkpoint: trailing-`trail` checkpoints under the reference's models/ path.  continue_trials: inputs["continue"] — trial t starts from
     trial t-1's last checkpoint and final log temperature (run on one rank, as
     the chain is sequential).  trainer_factory(seed, init_logtemp) replaces the
     VecTrainer construction (tests)."""
@@ -129,7 +144,7 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
     n_rows = (n_cumsteps + log_every - 1) // log_every
     n_evals = n_cumsteps // eval_freq
     rdim = (logs.market_log_dim(eid, n_gambles) if market else logs.multi_log_dim(eid, n_gambles))
-    lg = logs.ExperimentLog(n_trials, n_rows, n_evals, n_eval, rdim, market=market)
+    lg = logs.ExperimentLog(n_trials, n_rows, n_evals, n_eval, rdim, market=market, max_rows=max_episode_rows)
     if trainer_factory is None:
         from .trainer import VecTrainer
 
@@ -155,19 +170,33 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
             st = logs.save_directory(dict(inputs, trial=trial + 1), results=False)
             prefix = os.path.join(results_root, st[2:] if st.startswith("./") else st)
         ck = _Checkpoint(trail, prefix, floor)
+        drain_every = log_every
         if episode_rows:
-            tr.episode_log(episode_cap)
+            cap = episode_cap
+            if cap is None:
+                drain_every = log_every if log_every <= 64 else 1
+                cap = 64 * drain_every
+            tr.episode_log(cap)
+        pending = []
         prev = np.zeros(3)
         t_row, steps_in_row = time.perf_counter(), 0
         eval_run = 0
         for step in range(1, n_cumsteps + 1):
             tr.step()
             steps_in_row += 1
-            if step % log_every == 0 or step == n_cumsteps:
+            log_now = step % log_every == 0 or step == n_cumsteps
+            if episode_rows and (log_now or step % drain_every == 0):
+                got, dropped = tr.drain_episodes()
+                if dropped:
+                    raise RuntimeError(f"episode log dropped {dropped} rows at step {step}: episode_cap "
+                                       f"{episode_cap} < 64 x steps between drains")
+                pending.append(got)
+            if log_now:
                 now = time.perf_counter()
                 stats = tr.last_stats(shadow=True)
                 if episode_rows:
-                    rows, _ = tr.drain_episodes()
+                    rows = np.concatenate(pending) if len(pending) > 1 else pending[0]
+                    pending = []
                     per_step = (now - t_row) / steps_in_row
                     lg.log_episodes(trial, rows[:, 3] * per_step, rows[:, 2], rows[:, 3], stats, rows[:, 4:])
                     ck.update(tr, rows[:, 2])

@@ -63,7 +63,7 @@ def market_log_dim(env_id, n_assets):
 class ExperimentLog:
     """The four arrays of one experiment, filled trial by trial."""
 
-    def __init__(self, n_trials, n_rows, n_evals, n_eval, risk_dim, market=False):
+    def __init__(self, n_trials, n_rows, n_evals, n_eval, risk_dim, market=False, max_rows=1 << 22):
         self.trial = np.zeros((n_trials, n_rows, 19), dtype=np.float32)
         self.eval = np.zeros((n_trials, n_evals, n_eval, 20), dtype=np.float32)
         self.trial_risk = np.zeros((n_trials, n_rows, risk_dim), dtype=np.float32)
@@ -71,12 +71,20 @@ class ExperimentLog:
         self.eval_risk = np.zeros((n_trials, n_evals, n_eval, risk_dim + (1 if market else 0)), dtype=np.float32)
         self.market = market
         self.rows = np.zeros(n_trials, dtype=np.int64)
+        # per-episode rows grow with lanes x steps / episode length (the reference's
+        # single stream never sees this): bounded, (19 + risk) x 4 B per row per trial
+        self.max_rows = int(max_rows)
 
     def grow(self, n_rows):
-        """Widen the trial arrays to at least n_rows rows per trial (zero rows)."""
+        """Widen the trial arrays to at least n_rows rows per trial (zero rows),
+        doubling up to max_rows."""
         cur = self.trial.shape[1]
         if n_rows <= cur:
             return
+        if n_rows > self.max_rows:
+            raise RuntimeError(f"trial log needs {n_rows} rows per trial > max_rows {self.max_rows} "
+                               f"({self.trial.shape[0]} trials x {19 + self.trial_risk.shape[2]} x 4 B per row): "
+                               "log one aggregate row per interval (episode_rows=False) or raise the bound")
         t = np.zeros((self.trial.shape[0], n_rows, 19), dtype=np.float32)
         r = np.zeros((self.trial.shape[0], n_rows, self.trial_risk.shape[2]), dtype=np.float32)
         t[:, :cur], r[:, :cur] = self.trial, self.trial_risk
@@ -92,7 +100,7 @@ class ExperimentLog:
             return
         i = int(self.rows[trial])
         if i + n > self.trial.shape[1]:
-            self.grow(max(2 * self.trial.shape[1], i + n))
+            self.grow(max(min(2 * self.trial.shape[1], self.max_rows), i + n))
         st = np.asarray(stats16, dtype=np.float64)
         t = self.trial[trial, i:i + n]
         t[:, 0], t[:, 1], t[:, 2] = seconds, score, steps

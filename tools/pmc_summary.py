@@ -1,12 +1,16 @@
-"""Turn one round's rocprofv3 outputs (tools/profile_round.sh) into profiles/.
-
-  python tools/pmc_summary.py r01
+"""Turn one round's rocprofv3 outputs (tools/profile_round.sh) into profiles/:
 
 writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats, per kernel),
 profiles/<tag>_kernel_summary.txt (top kernels, per-dispatch averages) and
-profiles/<tag>_pmc_env.json: HBM bytes per env_train_kernel launch from the
-separate FETCH_SIZE and WRITE_SIZE passes.  Units and gfx950 corrections
-(MI355X_MICROARCH.md, HBM section): both counters are KiB; FETCH_SIZE counts
+profiles/<tag>_pmc_env.json: HBM bytes per launch of the env step from the
+separate FETCH_SIZE and WRITE_SIZE passes (the fused act_env_kernel minus the
+acting kernel when the trace has both, else env_train_kernel), tagged with
+"kernel_id", "round" and "config" so that bench.py attaches it only to the
+roofline of the same kernel and workload.
+
+  python tools/pmc_summary.py r03 [c2]
+
+Units and gfx950 corrections (MI355X_MICROARCH.md, HBM section): both counters are KiB; FETCH_SIZE counts
 half the bytes of wide coalesced reads on gfx950, so it is doubled.
 """
 import csv
@@ -55,7 +59,7 @@ def mfma_summary(path, stat_rows, dst):
     print(json.dumps(out, indent=1))
 
 
-def main(tag):
+def main(tag, config="c2"):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -84,14 +88,16 @@ def main(tag):
     if "act_env_kernel" in per and "fused_act_kernel" in per:
         a, b = per["act_env_kernel"], per["fused_act_kernel"]
         out = {"kernel": "act_env_kernel - fused_act_kernel (the env step's marginal traffic)",
+               "kernel_id": "act_env_marginal",
                "lanes": a["grid"] // 4, "hbm_bytes_per_launch": a["hbm_bytes"] - b["hbm_bytes"],
                "fetch_bytes_per_launch": a["fetch_bytes"] - b["fetch_bytes"],
                "write_bytes_per_launch": a["write_bytes"] - b["write_bytes"], "per_kernel": per}
     else:
         e = per["env_train_kernel"]
-        out = {"kernel": "env_train_kernel", "lanes": e["grid"], "launches": e["launches"],
+        out = {"kernel": "env_train_kernel", "kernel_id": "env_train_kernel", "lanes": e["grid"], "launches": e["launches"],
                "fetch_bytes_per_launch": e["fetch_bytes"], "write_bytes_per_launch": e["write_bytes"],
                "hbm_bytes_per_launch": e["hbm_bytes"], "per_kernel": per}
+    out["round"], out["config"] = tag, config
     out["method"] = ("median over launches of separate --pmc FETCH_SIZE / --pmc WRITE_SIZE passes; KiB x 1024; "
                      "FETCH_SIZE doubled (gfx950 half-count of wide coalesced reads)")
     json.dump(out, open(os.path.join(dst, f"{tag}_pmc_env.json"), "w"), indent=1)
@@ -103,4 +109,4 @@ def main(tag):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01")
+    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else "c2")
