@@ -187,6 +187,13 @@ int rlmd_env_lane_state(rlmd_env_t env, double* wealth_host, int32_t* time_host)
 /* Market lanes' episode start rows (i32 [N]) read back (eval_market's
  * eval_start_idx = start_idx + step, rl_market.py:283-284). */
 int rlmd_env_lane_start(rlmd_env_t env, int32_t* start_host);
+/* Market envs: overwrite rows [row0, row0 + n_rows) of the env's device price
+ * table (f64 [n_rows, n_assets], host memory), ordered on `stream`.  The
+ * reference-API single env (Market_Inv?_D1/Dx(n_assets, time_length, obs_days):
+ * reset(assets) / step(action, next_assets), envs/market_envs.py:133-223,
+ * :611-703) hands each step's observation to the device this way: the step
+ * kernel then reads the rows it gathers for that observation. */
+int rlmd_env_write_prices(rlmd_env_t env, const double* rows_host, int64_t row0, int64_t n_rows, void* stream);
 
 /* ------------------------------------------------------------------ replay */
 typedef struct rlmd_replay_s* rlmd_replay_t;

@@ -43,14 +43,15 @@ def rollout(family, investor, n, action_f32, cum, warmup, smoothing, n_eval, max
 
 
 def market_rollout(algo, actor, prices, investor, obs_days, test_days, starts, cum, warmup, smoothing,
-                   shuffle_days=1, seed=0, max_action=0.99):
+                   shuffle_days=1, seed=0, max_action=0.99, policy=None):
     """eval_market (tools/eval_episodes.py:402-611): episode i runs a Market_Inv?_D1/Dx
     env of time_length test_days + obs_days - 1 over the extract starting at price
     row starts[i] (gap + eval_start_idx), shuffled in blocks of shuffle_days (the
     Philox block permutations of oracle.envs); every step the deterministic policy
     (tanh(mu) * max_action, algo_sac.py:220-236 / algo_td3.py:225-238) acts on the
     f32 cast of the state (:507), action_window'd when cum <= smoothing (:509-517).
-    actor: {param name: tensor} of the actor net.  Returns (last reward, steps,
+    actor: {param name: tensor} of the actor net (policy: a callable state f32 ->
+    mu replacing its forward, e.g. a restatement of the bf16 kernel).  Returns (last reward, steps,
     last risk) per episode, as eval_log[..., 1], eval_log[..., 2], eval_risk_log[..., 1:]."""
     import torch
 
@@ -69,7 +70,8 @@ def market_rollout(algo, actor, prices, investor, obs_days, test_days, starts, c
     n_steps = tl if obs_days == 1 else tl - obs_days + 1
     with np.errstate(all="ignore"), torch.no_grad():
         for k in range(n_steps):
-            _, mu = mlp(actor, torch.from_numpy(state.astype(np.float32)), head)
+            x = torch.from_numpy(state.astype(np.float32))
+            mu = policy(x) if policy is not None else mlp(actor, x, head)[1]
             a = (torch.tanh(mu) * max_action).numpy()
             a = window_action(a, cum, warmup, smoothing)
             state, r, d, rk = env.step(a)

@@ -97,6 +97,7 @@ SIGNATURES = {
     "rlmd_train_last_fused": (C.c_int, []),
     "rlmd_train_episode_drain": (C.c_int, [P, P, C.c_int64, P, P, P]),
     "rlmd_env_lane_start": (C.c_int, [P, P]),
+    "rlmd_env_write_prices": (C.c_int, [P, P, I64, I64, P]),
     "rlmd_shadow_means": (C.c_int, [P, I32, I32, C.c_float, C.c_float, P, I32, P]),
     "rlmd_shadow_equiv": (C.c_int, [P, P, P, P, C.c_double, I64, P, P]),
     "rlmd_lev_workspace_bytes": (I64, [I64, I32]),

@@ -1641,6 +1641,17 @@ int rlmd_env_lane_start(rlmd_env_t env, int32_t* start_host) {
   return 0;
 }
 
+int rlmd_env_write_prices(rlmd_env_t env, const double* rows_host, int64_t row0, int64_t n_rows, void* stream) {
+  RLMD_CHECK(env && (rows_host || n_rows == 0), "null argument");
+  const EnvParams& P = env->P;
+  RLMD_CHECK(P.fam == RLMD_MARKET && env->d_prices, "price rows: market envs only");
+  RLMD_CHECK(row0 >= 0 && n_rows >= 0 && row0 + n_rows <= P.n_days, "price rows outside the table");
+  if (n_rows == 0) return 0;
+  RLMD_HIP(hipMemcpyAsync(env->d_prices + row0 * P.n, rows_host, sizeof(double) * n_rows * P.n,
+                          hipMemcpyHostToDevice, (hipStream_t)stream));
+  return 0;
+}
+
 int rlmd_train_flush_stats(rlmd_env_t env, void* stream) {
   RLMD_CHECK(env, "null env");
   return rlmd::flush_stats(env, (hipStream_t)stream);

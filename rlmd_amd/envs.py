@@ -160,13 +160,55 @@ globals().update(_CLASSES)
 
 
 class _MarketEnv(_SingleEnv):
-    """Market_Inv{A,B,C}_{D1,Dx}(n_assets, time_length, obs_days): the price
-    window is supplied at construction (the driver's shuffled extract)."""
+    """Market_Inv{A,B,C}_{D1,Dx}(n_assets, time_length, obs_days) of
+    envs/market_envs.py with its interface: ``reset(assets)`` takes the
+    episode's first observation and ``step(action, next_assets)`` the next one
+    (scripts/rl_market.py:202-245 hands them over from its shuffled extract).
+    The step is the device kernel of the vectorised loop; it reads the
+    observation from a price table of time_length * action_days + 1 rows that
+    this class fills one observation at a time (rlmd_env_write_prices): D1's
+    observation is row t * action_days, Dx's the rows [t * action_days,
+    t * action_days + obs_days) flattened and reversed
+    (tools/env_resources.py:203-226), written back in row order.
 
-    def __init__(self, n_assets, time_length, obs_days, prices, device="cuda:0", seed=None):
-        ext = np.ascontiguousarray(prices, dtype=np.float64)
-        _SingleEnv.__init__(self, n_assets, device=device, seed=seed, prices=ext,
-                            obs_days=obs_days, time_length=time_length, sample_days=ext.shape[0] - 1)
+    ``prices=`` instead supplies the whole extract at construction (the device
+    then needs no observations; ``step(action)``)."""
+
+    def __init__(self, n_assets, time_length, obs_days, prices=None, action_days=1, device="cuda:0", seed=None):
+        self.obs_days, self.action_days, self._t = int(obs_days), int(action_days), 0
+        self._feed = prices is None
+        ext = (np.zeros((int(time_length) * self.action_days + 1, n_assets)) if self._feed
+               else np.ascontiguousarray(prices, dtype=np.float64))
+        _SingleEnv.__init__(self, n_assets, device=device, seed=seed, prices=ext, obs_days=obs_days,
+                            time_length=time_length, action_days=action_days, sample_days=ext.shape[0] - 1)
+        self.time_length = int(time_length) if self.obs_days == 1 else int(time_length) - self.obs_days + 1
+
+    def _write_obs(self, t, obs):
+        """The rows observation t was read from (observed_market_state inverted)."""
+        n, d = self.n_gambles, self.obs_days
+        obs = np.asarray(obs, dtype=np.float64).reshape(-1)
+        rows = obs.reshape(1, n) if d == 1 else obs[::-1].reshape(-1, n)
+        if rows.shape[0] != d:
+            raise ValueError(f"observation of {obs.size} prices, expected obs_days x n_assets = {d * n}")
+        rows = np.ascontiguousarray(rows)
+        check(_abi.lib().rlmd_env_write_prices(self._v.h, rows.ctypes.data_as(C.c_void_p), t * self.action_days,
+                                               rows.shape[0], stream_ptr()))
+
+    def reset(self, assets=None):
+        if self._feed:
+            if assets is None:
+                raise ValueError("reset(assets): the episode's first observation")
+            self._write_obs(0, assets)
+        self._t = 1
+        return _SingleEnv.reset(self)
+
+    def step(self, action, next_assets=None):
+        if self._feed:
+            if next_assets is None:
+                raise ValueError("step(action, next_assets): the next observation")
+            self._write_obs(self._t, next_assets)
+        self._t += 1
+        return _SingleEnv.step(self, action)
 
 
 for _i in "ABC":

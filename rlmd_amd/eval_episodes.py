@@ -9,6 +9,19 @@ last risk row (:263-273).  All episodes run as lanes of one rlmd_eval_rollout
 launch; the event's wall time is split evenly over them.  The reference's
 printed summary statistics come from rlmd_eval_stats (NumPy-exact).
 
+``eval_market`` keeps tools/eval_episodes.py:402-611's signature and log
+layout for the single-stream market driver (rlmd_amd.scripts.rl_market): the
+gaps are drawn on the host as the reference draws them (one
+``np.random.randint(gap_min, gap_max + 1, n_eval)``, offset by
+eval_start_idx), then every episode runs as one lane of rlmd_eval_market
+(trainer.market_evaluate: test slice of test_days + obs_days - 1 steps from
+row gap_i, shuffled in blocks of test_shuffle_days, the deterministic policy
+acting every day, the action window as at cum_steps), logging
+[time, reward, steps, loss[11], logtemp, loss_params[4], cum_steps] and
+[gap, risk...] per episode (:528-543).  The evaluation env is created once per
+(price table, shape) and reused; each event's resets advance its Philox
+episode counters, so every event draws fresh shuffles.
+
 ``agent_shadow_mean`` is tools/utils.py:441-471 on the device
 (rlmd_shadow_means on the 16-entry statistics row).
 """
@@ -79,3 +92,60 @@ def eval_multiplicative(n_gambles, agent, inputs, eval_log, eval_risk_log, multi
     e[:, 19] = cum_steps
     eval_risk_log[round, eval_run] = rk
     return {"reward": r, "steps": st, "risk": rk}
+
+
+_MARKET_EVAL_ENVS = {}
+
+
+def _market_eval_env(market_data, investor, obs_days, test_length, n_eval, shuffle, action_days, device):
+    from .envs import VecEnv
+
+    key = (id(market_data), investor, obs_days, test_length, n_eval, shuffle, action_days, str(device))
+    hit = _MARKET_EVAL_ENVS.get(key)
+    if hit is not None and hit[0] is market_data:
+        return hit[1]
+    seed = int(np.random.randint(0, 2**31 - 1))
+    env = VecEnv("market", investor, n_eval, market_data.shape[1], seed=seed, prices=market_data,
+                 obs_days=obs_days, time_length=test_length, action_days=action_days, shuffle_days=shuffle,
+                 sample_days=test_length * action_days + 1, device=device)
+    _MARKET_EVAL_ENVS[key] = (market_data, env)
+    return env
+
+
+def market_investor(env_id):
+    """'A' / 'B' / 'C' of a market env_id such as SNP_InvB_D1_T1 (the
+    reference's inputs["env_id"][-10:-6] is 'InvB')."""
+    return str(env_id).split("_Inv")[1][0]
+
+
+def eval_market(market_data, obs_days, eval_start_idx, agent, inputs, eval_log, eval_risk_log, multi_step, cum_steps,
+                round, eval_run, loss, logtemp, loss_params, device=None):
+    from .trainer import market_evaluate
+
+    market_data = np.asarray(market_data, dtype=np.float64)
+    n_eval = int(inputs["n_eval"])
+    action_days = int(inputs["action_days"])
+    test_length = int(inputs["test_days"] + obs_days - 1)
+    gap = np.random.randint(int(inputs["gap_days_min"]), int(inputs["gap_days_max"]) + 1, size=n_eval)
+    gap += eval_start_idx
+    dev = torch.device(device or agent.dev.device)
+    inv = market_investor(inputs["env_id"])
+    env = _market_eval_env(market_data, inv, obs_days, test_length, n_eval, int(inputs["test_shuffle_days"]),
+                           action_days, dev)
+    t0 = time.perf_counter()
+    res = market_evaluate(agent.dev, market_data, inv, obs_days, int(inputs["test_days"]), gap, int(cum_steps),
+                          int(inputs["random"]), int(inputs["smoothing_window"]),
+                          shuffle_days=int(inputs["test_shuffle_days"]), action_days=action_days, device=dev, env=env)
+    dt = time.perf_counter() - t0
+    e = eval_log[round, eval_run]
+    e[:, 0] = dt / n_eval
+    e[:, 1] = res["reward"]
+    e[:, 2] = res["steps"]
+    e[:, 3:14] = np.asarray(loss, dtype=np.float64)
+    e[:, 14] = logtemp
+    e[:, 15:19] = np.asarray(loss_params, dtype=np.float64)
+    e[:, 19] = cum_steps
+    eval_risk_log[round, eval_run, :, 0] = gap
+    eval_risk_log[round, eval_run, :, 1:] = res["risk"]
+    return dict(res, gap=gap)
+

@@ -589,7 +589,22 @@ EVAL_MARKET_CASES = [
 ]
 
 
-def eval_market_fixtures(seed=31, n_eval=12, test_days=40):
+# the production widths (SAC 256/256, TD3 400/300): the shapes the one-launch
+# evaluation kernel (env.hip eval_market_loop_kernel) is instantiated for
+EVAL_MARKET_FULL_CASES = [
+    ("SAC", "A", 1, "stooq_snp", 5000, 1000, 2000, (256, 256)),
+    ("TD3", "B", 1, "stooq_snp", 1500, 1000, 2000, (400, 300)),
+    ("SAC", "C", 3, "stooq_usei", 3000, 1000, 2000, (256, 256)),
+    ("TD3", "A", 5, "stooq_snp", 6000, 1000, 2000, (400, 300)),
+]
+
+
+def eval_market_full_fixtures():
+    out = eval_market_fixtures(seed=37, n_eval=32, test_days=60, cases=EVAL_MARKET_FULL_CASES)
+    return {k: v for k, v in out.items() if "/init/" not in k or "/init/actor." in k}  # evaluation reads the actor
+
+
+def eval_market_fixtures(seed=31, n_eval=12, test_days=40, cases=None):
     import algos.algo_sac as asac
     import algos.algo_td3 as atd3
     import envs.market_envs as me
@@ -597,7 +612,8 @@ def eval_market_fixtures(seed=31, n_eval=12, test_days=40):
 
     out = {}
     rng = np.random.default_rng(seed)
-    for ci, (algo, inv, d, pfile, cum, warm, sw) in enumerate(EVAL_MARKET_CASES):
+    cases = cases or [c + ((32, 24),) for c in EVAL_MARKET_CASES]
+    for ci, (algo, inv, d, pfile, cum, warm, sw, hid) in enumerate(cases):
         prices = np.load(f"/root/reference/tools/market_data/{pfile}.npy")
         n = prices.shape[1]
         test_length = test_days + d - 1
@@ -605,7 +621,6 @@ def eval_market_fixtures(seed=31, n_eval=12, test_days=40):
         probe = cls(n, test_length, d)
         S, A = probe.observation_space.shape[0], probe.action_space.shape[0]
         T.manual_seed(seed + ci)
-        hid = (32, 24)
         agent = (asac.Agent_sac if algo == "SAC" else atd3.Agent_td3)(_inputs(algo, S, A, hid, "MSE", 16, 8))
         init = {}
         for nm in _net_names(algo):
@@ -1027,6 +1042,182 @@ def c1_trace(n_steps=2500, seed=0):
 
 
 # ----------------------------------------------------------------------------
+# F6-market: the reference's own market loop (scripts/rl_market.py), recorded
+# ----------------------------------------------------------------------------
+def market_trace(obs_days, n_steps=2500, seed=0, key=22, algo="TD3", loss_fn="HUB", train_days=200):
+    """scripts/rl_market.market_env as the reference runs it: main.py's tables
+    (key 22 = SNP_InvB on tools/market_data/stooq_snp.npy), TD3, HUB, one trial
+    of n_steps with eval every 1e3 steps (4 episodes), train_days 200 (so a
+    dozen episodes end inside the run), seeded np.random + torch.  n_steps =
+    2500 covers the warm-up (raw samples, < 1e3), the smoothing window (f64
+    clip, <= 2e3) and the policy phase.  Recorded for the TRAINING env
+    instance: each episode's start row and shuffled extract (time_slice /
+    shuffle_data outside eval_market), every step's action as the env received
+    it, the observation handed to step(), state / next_state / reward / done /
+    risk; every select_next_action output and learn() return; every
+    eval_market call's arguments; the steps of every save_models(); and the
+    saved trial / trial_risk logs."""
+    import importlib
+
+    import main as ref_main
+    import envs.market_envs as me
+    from algos import algo_sac, algo_td3
+    from tools import env_resources as er
+    from tools import eval_episodes as ev
+    from tools import utils
+
+    agent_cls = algo_td3.Agent_td3 if algo == "TD3" else algo_sac.Agent_sac
+    rec = {k: [] for k in ("action", "action_dtype", "obs", "state", "next_state", "reward", "done", "risk",
+                           "policy", "learn_loss", "learn_logtemp", "learn_params", "save_step", "start_idx",
+                           "extract", "reset_obs", "eval_start_idx", "eval_cum_steps", "eval_loss",
+                           "eval_logtemp", "eval_params")}
+    env_ids, ctx = [], {"eval": False, "steps": 0}
+    cls = getattr(me, "Market_" + ref_main.gym_envs[str(key)][0][-4:] + ("_D1" if obs_days == 1 else "_Dx"))
+    orig = dict(init=cls.__init__, step=cls.step, reset=cls.reset, ts=er.time_slice, sd=er.shuffle_data,
+                ev=ev.eval_market, sel=agent_cls.select_next_action, learn=agent_cls.learn, save=agent_cls.save_models)
+
+    def init(self, *a, **kw):
+        env_ids.append(id(self))  # before the constructor's own reset(assets=None)
+        orig["init"](self, *a, **kw)
+
+    def train(self):
+        return id(self) == env_ids[0] and not ctx["eval"]
+
+    def step(self, action, next_assets):
+        if train(self):
+            rec["state"].append(self._mt_last.copy())
+            rec["action"].append(np.asarray(action).astype(np.float64).copy())
+            rec["action_dtype"].append(np.asarray(action).dtype == np.float64)
+            rec["obs"].append(np.asarray(next_assets, np.float64).copy())
+        s2, r, d, risk = orig["step"](self, action, next_assets)
+        if train(self):
+            rec["next_state"].append(np.asarray(s2, np.float64).copy())
+            rec["reward"].append(float(r))
+            rec["done"].append(list(d))
+            rec["risk"].append(np.asarray(risk, np.float64).ravel().copy())
+            self._mt_last = np.asarray(s2, np.float64).copy()
+            ctx["steps"] += 1
+        return s2, r, d, risk
+
+    def reset(self, assets):
+        s = orig["reset"](self, assets)
+        if assets is not None and train(self):
+            rec["reset_obs"].append(np.asarray(assets, np.float64).copy())
+            self._mt_last = np.asarray(s, np.float64).copy()
+        return s
+
+    def time_slice(*a, **kw):
+        out, start = orig["ts"](*a, **kw)
+        if not ctx["eval"]:
+            rec["start_idx"].append(int(start))
+        return out, start
+
+    def shuffle_data(*a, **kw):
+        out = orig["sd"](*a, **kw)
+        if not ctx["eval"]:
+            rec["extract"].append(np.asarray(out, np.float64).copy())
+        return out
+
+    def eval_market(market_data, od, eval_start_idx, agent, inputs, eval_log, eval_risk_log, mstep, cum_steps, rnd,
+                    eval_run, loss, logtemp, loss_params):
+        rec["eval_start_idx"].append(int(eval_start_idx))
+        rec["eval_cum_steps"].append(int(cum_steps))
+        rec["eval_loss"].append(np.asarray([float(x) for x in loss], np.float64))
+        rec["eval_logtemp"].append(float(logtemp))
+        rec["eval_params"].append(np.asarray([float(x) for x in loss_params], np.float64))
+        ctx["eval"] = True
+        try:
+            return orig["ev"](market_data, od, eval_start_idx, agent, inputs, eval_log, eval_risk_log, mstep,
+                              cum_steps, rnd, eval_run, loss, logtemp, loss_params)
+        finally:
+            ctx["eval"] = False
+
+    def sel(self, state):
+        a = orig["sel"](self, state)
+        rec["policy"].append(np.asarray(a).astype(np.float64).copy())
+        return a
+
+    def learn(self):
+        loss, logtemp, params = orig["learn"](self)
+        rec["learn_loss"].append(np.asarray([float(x) for x in loss], np.float64))
+        rec["learn_logtemp"].append(float(logtemp))
+        rec["learn_params"].append(np.asarray([float(x) for x in params], np.float64))
+        return loss, logtemp, params
+
+    def save(self):
+        rec["save_step"].append(ctx["steps"])
+        orig["save"](self)
+
+    cls.__init__, cls.step, cls.reset = init, step, reset
+    er.time_slice, er.shuffle_data, ev.eval_market = time_slice, shuffle_data, eval_market
+    agent_cls.select_next_action, agent_cls.learn, agent_cls.save_models = sel, learn, save
+    rl = importlib.import_module("scripts.rl_market")
+    import contextlib
+    import glob
+    import io
+
+    try:
+        data = np.load("/root/reference/tools/market_data/stooq_snp.npy", allow_pickle=False)
+        inputs = dict(ref_main.inputs)
+        inputs.update({"n_trials_mkt": 1, "n_cumsteps_mkt": float(n_steps), "eval_freq_mkt": 1e3, "n_eval_mkt": 4,
+                       "train_days": float(train_days), "gpu": "cpu", "buffer_gpu": False})
+        inputs = utils.input_initialisation(inputs, [key], [algo], [loss_fn], [1])
+        inputs["test_agent"] = True
+        inputs["ENV_KEY"] = key
+        np.random.seed(seed)
+        T.manual_seed(seed)
+        for f in glob.glob("results/test_market/**/*.npy", recursive=True):
+            os.remove(f)
+        with contextlib.redirect_stdout(io.StringIO()):
+            rl.market_env(ref_main.gym_envs, inputs, market_data=data, obs_days=obs_days)
+        stem = glob.glob(f"results/test_market/**/*_D{obs_days}_T1*_trial.npy", recursive=True)[0][:-len("_trial.npy")]
+        logs_out = {nm: np.load(stem + f"_{nm}.npy") for nm in ("trial", "eval", "trial_risk", "eval_risk")}
+    finally:
+        cls.__init__, cls.step, cls.reset = orig["init"], orig["step"], orig["reset"]
+        er.time_slice, er.shuffle_data, ev.eval_market = orig["ts"], orig["sd"], orig["ev"]
+        agent_cls.select_next_action, agent_cls.learn, agent_cls.save_models = orig["sel"], orig["learn"], orig["save"]
+    out = {k: np.asarray(v) for k, v in rec.items() if k != "extract"}
+    out["extract"] = np.stack(rec["extract"])  # every slice has train_length + 1 rows
+    for nm, v in logs_out.items():
+        out[nm] = v
+    out["params"] = np.array([n_steps, seed, key, obs_days, train_days], dtype=np.int64)
+    out["spec"] = np.array([algo, loss_fn])
+    return out
+
+
+def env_resources_kat(seed=123):
+    """tools/env_resources.py's time_slice / shuffle_data / observed_market_state
+    on stooq_usei rows with np.random seeded: the outputs and the generator
+    state after each call (pins the draw order of the host restatement,
+    rlmd_amd/env_resources.py)."""
+    from tools import env_resources as er
+
+    prices = np.load("/root/reference/tools/market_data/stooq_usei.npy")[:400]
+    out = {"prices": prices}
+    np.random.seed(seed)
+    for i, (ext_days, sample_days, interval) in enumerate([(20, 60, 5), (33, 40, 3), (7, 390, 1), (12, 100, 4)]):
+        sl, st = er.time_slice(prices, ext_days, 1, sample_days)
+        sh = er.shuffle_data(sl, interval)
+        out[f"case{i}/params"] = np.array([ext_days, sample_days, interval])
+        out[f"case{i}/start"] = np.int64(st)
+        out[f"case{i}/shuffled"] = sh
+        out[f"case{i}/next_u"] = np.float64(np.random.random_sample())
+        for d in (1, 3):
+            for t in (0, 2):
+                out[f"case{i}/obs_d{d}_t{t}"] = np.asarray(er.observed_market_state(sh, t, 1, d))
+    return out
+
+
+def market_traces():
+    T.set_num_threads(2)  # the reference's small-batch learn() is slower on more threads beside other jobs
+    out = {}
+    for d in (1, 5):
+        for k, v in market_trace(d).items():
+            out[f"d{d}/{k}"] = v
+    return out
+
+
+# ----------------------------------------------------------------------------
 # F10: *_fixed_final_lev (statistics captured at the reference's torch calls)
 #      and coin_galaxy_brain_lev
 # ----------------------------------------------------------------------------
@@ -1182,10 +1373,13 @@ def main():
         "multistep.npz": multistep_fixtures,
         "eval.npz": eval_fixtures,
         "eval_market.npz": eval_market_fixtures,
+        "eval_market_full.npz": eval_market_full_fixtures,
         "logs.npz": log_fixtures,
         "learn.npz": learn_fixtures,
         "lev.npz": lev_fixtures,
         "c1_trace.npz": c1_trace,
+        "market_trace.npz": market_traces,
+        "env_resources_kat.npz": env_resources_kat,
         "aggregate.npz": aggregate_fixtures,
         "lev_final.npz": lev_final_fixtures,
     }

@@ -229,3 +229,54 @@ def test_eval_market_one_launch_time(dev):
         lib.rlmd_train_set_fused(1)
     print(f"C4 eval event: one launch {ms[1]:.3f} ms, per-day loop {ms[0]:.3f} ms")
     assert ms[1] < ms[0]
+
+
+def _bf16_actor(actor):
+    """The one-launch kernel's policy numerics restated in torch (as
+    test_train_gpu._bf16_act_reference): layer 1 f32, h1 and fc2.weight rounded
+    to bf16, f32 accumulation and heads."""
+    import torch.nn.functional as F
+
+    def policy(state, head):
+        h1 = F.relu(F.linear(state, actor["fc1.weight"], actor["fc1.bias"])).bfloat16().float()
+        h2 = F.relu(F.linear(h1, actor["fc2.weight"].bfloat16().float(), actor["fc2.bias"]))
+        return None, F.linear(h2, actor[head + ".weight"], actor[head + ".bias"])
+
+    return policy
+
+
+@pytest.mark.parametrize("c", range(4))
+def test_eval_market_one_launch_matches_reference(golden, dev, c):
+    """The one-launch bf16 evaluation (eval_market_loop_kernel) at the production
+    widths (SAC 256/256, TD3 400/300; tests/golden/eval_market_full.npz: the
+    reference's own eval_market with those agents, 32 episodes x 60 test days,
+    D1 and Dx, inside / outside the action window) — the C4 evaluation path:
+      * against the oracle rollout with the kernel's bf16 policy numerics
+        restated (layer 1 f32, bf16 h1 / fc2.weight, f32 heads): steps exact,
+        rewards within 1e-5 (layer 1's f32 summation order now and then moves
+        one h1 element to its bf16 neighbour);
+      * against the reference's fp32 run: steps exact, rewards within the bf16
+        policy tolerance 2e-3 (the actions differ by bf16 rounding of layer 2)."""
+    from rlmd_amd import _abi
+    from rlmd_amd.agent import DeviceAgent, layer_names, reference_init
+    from rlmd_amd.trainer import market_evaluate
+    from tests.test_oracle_golden import _eval_market_case, _golden_actor
+
+    g = golden("eval_market_full.npz")
+    algo, inv, d, n, test_days, cum, warm, sw, n_eval, h1, h2 = _eval_market_case(g, c)
+    S, A = 4 + d * n, n + inv
+    init = reference_init(algo, S, A, h1, h2, seed=1)
+    init["actor"] = [torch.from_numpy(g[f"case{c}/init/actor.{pn}"]) for pn in layer_names(algo, "actor")]
+    ag = DeviceAgent(algo, S, A, h1, h2, 16, 8, precision="bf16", init=init, device=dev)
+    _abi.lib().rlmd_train_set_fused(1)
+    out = market_evaluate(ag, g[f"case{c}/prices"], inv, d, test_days, g[f"case{c}/gaps"], cum, warm, sw,
+                          shuffle_days=1, device=dev)
+    head = "pi" if algo == "SAC" else "mu"
+    pol = _bf16_actor(_golden_actor(g, c))
+    rew, steps, risk = oev.market_rollout(algo, None, g[f"case{c}/prices"], inv, d, test_days, g[f"case{c}/gaps"],
+                                          cum, warm, sw, policy=lambda s: pol(s, head)[1])
+    np.testing.assert_array_equal(out["steps"], steps)
+    np.testing.assert_allclose(out["reward"], rew, rtol=1e-5, atol=0)
+    np.testing.assert_array_equal(out["steps"], g[f"case{c}/steps"])
+    np.testing.assert_allclose(out["reward"], g[f"case{c}/reward"], rtol=2e-3, atol=0)
+    assert out["steps"].max() == test_days

@@ -107,3 +107,79 @@ def test_c5_full_ring_multistep_gathers(dev):
     assert np.all(np.isfinite(st.cpu().numpy()[:, [0, 1, 2, 3, 4, 5]]))
     f, _ = tr.agent.status()
     assert f == 0
+
+
+def _replay_steps(tr, ora, T, cap, atol=1e-30):
+    """Step the trainer T times, replaying every step's ring rows through the
+    oracle env (f32 policy actions, the same Philox draws)."""
+    N = tr.n_lanes
+    obs = ora.reset()
+    for t in range(T):
+        tr.step()
+        s_r, a_r, r_r, s2_r, d_r = read_ring(tr, (t * N) % cap, N)
+        ns, r, d, _ = ora.step(a_r.astype(np.float32))
+        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=atol, err_msg=f"t={t} s")
+        np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6, err_msg=f"t={t} r")
+        np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=atol, err_msg=f"t={t} s2")
+        np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
+        w_gpu, _ = tr.env.lane_state()
+        live = ~d[:, 0]
+        np.testing.assert_allclose(w_gpu[live], ora.wealth[live], rtol=1e-12, atol=0, err_msg=f"t={t} wealth")
+        obs = ns.copy()
+        m = d[:, 0]
+        if m.any():
+            obs[m] = ora.reset(m)[m]
+    return a_r
+
+
+@pytest.mark.parametrize("loss", ["MSE", "HUB", "MAE", "HSC"])
+def test_c3_full_size_dice_sh_td3(dev, loss):
+    """C3 at its size: 65,536 Dice_SH_InvA lanes (key 18: S = 6, A = 2), TD3
+    400/300 bf16 (the fused act_env_kernel<DICE_SH, 416>), K = 8 updates of
+    B = 200 / top-k 100 per vector step, one critic loss of the sweep; every
+    step's ring rows replayed through the oracle env (envs/dice_roll_sh_envs.py:
+    290-365), then the learner's counters and statistics."""
+    from rlmd_amd import _abi
+    from rlmd_amd.trainer import VecTrainer
+
+    N, T, K, cap, seed = 65536, 4, 8, 1 << 20, 18
+    _abi.lib().rlmd_train_set_fused(1)
+    tr = VecTrainer("dice_sh", "A", N, algo="TD3", loss=loss, k_updates=K, replay_capacity=cap, seed=seed,
+                    warmup_steps=0, smoothing_window=0, precision="bf16", device=dev, init_seed=seed)
+    ora = oe.OracleVecEnv(oe.DICE_SH, oe.INV_A, N, 1, seed=seed)
+    a_r = _replay_steps(tr, ora, T, cap)
+    assert _abi.lib().rlmd_train_last_fused() == 1
+    assert tr.batch == 200 and tr.topk == 100 and a_r.shape == (N, 2)
+    assert np.abs(a_r).max() <= 0.99 and np.unique(a_r[:, 0]).size > N // 4
+    sc = tr.agent.scalars()
+    assert sc["learn_step_cntr"] == T * K and sc["nan_flag"] == 0
+    st = tr.last_stats()
+    assert np.all(np.isfinite(st[[0, 1, 2, 3, 4, 5, 10]])), st
+
+
+def test_c4_full_size_market_on_stooq_snp(golden, dev):
+    """C4's per-GPU shard at its size: 8,192 Market_InvA_D1 lanes on the
+    S&P 500 closes (stooq_snp, committed data fixture), train slices of 1,000
+    days shuffled in blocks of 5, SAC 256/256 bf16, K = 8 updates of B = 512;
+    every step's ring rows replayed through the oracle env
+    (envs/market_envs.py:133-202, env_resources.py:203-291 with the Philox
+    starts / permutations), then one evaluation event (100 episodes x 250
+    test days, blocks of 3, gaps 5..20) on the device."""
+    from rlmd_amd import _abi
+    from rlmd_amd.trainer import VecTrainer
+
+    N, T, K, cap, seed = 8192, 12, 8, 1 << 20, 0
+    prices = golden("stooq_snp.npz")["prices"]
+    kw = dict(prices=prices, obs_days=1, time_length=1000, shuffle_days=5, sample_days=1000 + 250 + 1 + 20 - 1)
+    _abi.lib().rlmd_train_set_fused(1)
+    tr = VecTrainer("market", "A", N, algo="SAC", k_updates=K, replay_capacity=cap, seed=seed, warmup_steps=0,
+                    smoothing_window=0, precision="bf16", device=dev, init_seed=seed, **kw)
+    ora = oe.OracleVecEnv(oe.MARKET, oe.INV_A, N, 1, seed=seed, **kw)
+    _replay_steps(tr, ora, T, cap, atol=1e-45)
+    assert _abi.lib().rlmd_train_last_fused() == 1
+    np.testing.assert_array_equal(tr.env.lane_start(), ora.start)
+    sc = tr.agent.scalars()
+    assert sc["learn_step_cntr"] == T * K and sc["nan_flag"] == 0
+    ev = tr.evaluate_market(n_eval=100, test_days=250)
+    assert ev["steps"].min() >= 1 and ev["steps"].max() <= 250 and np.isfinite(ev["reward"]).all()
+    assert ev["stats"].shape == (14,) and np.isfinite(ev["stats"]).all()

@@ -208,22 +208,29 @@ def _golden_actor(g, c):
     return {k[len(pre):]: torch.from_numpy(g[k]) for k in g.files if k.startswith(pre)}
 
 
-@pytest.mark.parametrize("c", range(4))
-def test_eval_market_matches_reference(golden, c):
+@pytest.mark.parametrize("fixture,c", [("eval_market.npz", c) for c in range(4)]
+                         + [("eval_market_full.npz", c) for c in range(4)])
+def test_eval_market_matches_reference(golden, fixture, c):
     """oracle.eval.market_rollout vs the reference's eval_market (real agent,
     deterministic policy on every state, injected gaps, unshuffled test slice):
     steps exact; last reward / risk within fp32-policy noise (the actor runs in
     float32 in both, on the same f32 states — rtol 1e-6 covers ulp-level matmul
-    summation-order differences propagated through tanh and three env steps)."""
+    summation-order differences propagated through tanh and three env steps).
+    eval_market_full.npz: the production widths (SAC 256/256, TD3 400/300),
+    32 episodes x 60 days."""
     from oracle import eval as oev
 
-    g = golden("eval_market.npz")
+    g = golden(fixture)
     algo, inv, d, n, test_days, cum, warm, sw, n_eval, _, _ = _eval_market_case(g, c)
     rew, steps, risk = oev.market_rollout(algo, _golden_actor(g, c), g[f"case{c}/prices"], inv, d, test_days,
                                           g[f"case{c}/gaps"], cum, warm, sw)
     np.testing.assert_array_equal(steps, g[f"case{c}/steps"])
     np.testing.assert_allclose(rew, g[f"case{c}/reward"], rtol=1e-6, atol=0)
-    np.testing.assert_allclose(risk, g[f"case{c}/risk_log"][:, 1:], rtol=1e-6, atol=1e-12, equal_nan=True)
+    # risk holds the float32 leverages 3 a: at 256 / 400 hidden units the fp32
+    # summation order (the oracle's F.linear vs the reference module's addmm) moves a
+    # by a few float32 ulps
+    rr = 1e-6 if fixture == "eval_market.npz" else 1e-5
+    np.testing.assert_allclose(risk, g[f"case{c}/risk_log"][:, 1:], rtol=rr, atol=1e-12, equal_nan=True)
     st = oev.market_summary(rew, steps, np.concatenate([g[f"case{c}/risk_log"][:, :1], risk], 1))
     ref = oev.market_summary(g[f"case{c}/reward"], g[f"case{c}/steps"], g[f"case{c}/risk_log"])
     np.testing.assert_allclose(st, ref, rtol=1e-5, atol=1e-9)
