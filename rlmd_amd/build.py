@@ -15,7 +15,7 @@ BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "librlmd_amd.so")
 ARCH = os.environ.get("RLMD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["abi.hip", "env.hip", "replay.hip", "gemm.hip", "learn.hip", "act.hip", "rows.hip", "eval.hip", "shadow.hip", "lev.hip", "lev_sort.hip"]
+SOURCES = ["abi.hip", "env.hip", "replay.hip", "gemm.hip", "learn.hip", "act.hip", "rows.hip", "eval.hip", "shadow.hip", "lev.hip", "lev_sort.hip", "update.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
          "-Wno-unused-variable"]
 # env math must round where NumPy rounds (no FMA contraction); GEMM/learner may fuse

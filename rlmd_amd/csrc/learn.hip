@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "learn_kernels.h"
+#include "rlmd_update.h"
 #include "rlmd_act_rows.h"
 #include "rlmd_block.h"
 #include "rlmd_loss.h"
@@ -240,6 +241,10 @@ struct Scratch {
   // ReLU masks (bytes, rows.hip m1_index / m2_index layouts) of c1/c2, e1/e2, h1/h2
   uint8_t *cm1[2], *cm2[2], *em1[2], *em2[2], *am1, *am2;
   float* stats;  // [16] when the caller passes none
+  // fused critic update (update.hip): row-packed h1 / h2 (compute type), the
+  // backward basis U1 (f32) and the q_value.weight snapshot per critic
+  unsigned char *hp1[2], *hp2[2];
+  float *u1[2], *w3s[2];
 };
 
 }  // namespace
@@ -278,6 +283,9 @@ struct rlmd_agent_s {
   // rlmd_agent_params_written (host writes through the parameter tensors);
   // the optimiser keeps them current otherwise
   bool copies_dirty = true;
+  // critic step as one launch (update.hip) for B <= 512; RLMD_NO_FUSED_UPDATE=1:
+  // row backward + weight-gradient GEMM + Adam launches
+  bool fused_update = false;
 };
 
 namespace rlmd {
@@ -544,6 +552,15 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     f.xsan = S_.xsan;
     f.logp = S_.logp;
     f.save = S_.save;
+    if (ag->fused_update) {
+      for (int g = 0; g < 2; ++g) {
+        f.u1[g] = S_.u1[g];
+        f.hp1[g] = S_.hp1[g];
+        f.hp2[g] = S_.hp2[g];
+        f.w3s[g] = S_.w3s[g];
+      }
+      f.bsnap = S_.qbias;
+    }
     RLMD_TRY(fwd_rows_launch(f, st));
   }
   // ---- critic loss (algo_sac.py:413-465)
@@ -592,8 +609,49 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       }
     }
   }
-  // ---- critic backward: data gradients per row, then all weight gradients
-  {
+  // ---- critic step in one launch: loss gradient of every row, weight-gradient
+  //      tiles, Adam + Polyak + compute copies of the owned parameters (update.hip)
+  if (ag->fused_update) {
+    CritUpdArgs cu{};
+    cu.d = d;
+    cu.co = co;
+    cu.loss = loss_fused;
+    for (int g = 0; g < 2; ++g) {
+      cu.loss.qb[g] = S_.qbias + g;  // loss-time biases: the forward's snapshot
+      cu.loss.tb[g] = S_.qbias + 2 + g;
+      cu.m2[g] = S_.cm2[g];
+      cu.hp1[g] = S_.hp1[g];
+      cu.hp2[g] = S_.hp2[g];
+      cu.u1[g] = S_.u1[g];
+      cu.w3s[g] = S_.w3s[g];
+    }
+    cu.x = mb.xsa;
+    AdamArgs ad{};
+    ad.p = Pc[0];
+    ad.g = Gc[0];
+    ad.m = ag->m + ag->off_c[0];
+    ad.v = ag->v + ag->off_c[0];
+    ad.target = Tc[0];
+    ad.n = 2 * co.size;
+    ad.lr = c.lr_critic;
+    ad.tau = c.tau;
+    ad.cnt = (int32_t)cntr;
+    ad.interval = 1;
+    ad.polyak_interval = c.target_critic_update;
+    ad.st = ag->st;
+    adam_copies(ag, ad, co, SLOT_C0, 2, true);
+    adam_scalars(ad.lr, ad.cnt / ad.interval, ad.step_size, ad.bc2_sqrt);
+    cu.adam = ad;
+    cu.tj = d.H1p / 32;
+    cu.ti = d.H2p / 32;
+    cu.n_w2 = cu.ti * cu.tj;
+    cu.n_w1 = d.H1p / 32;
+    RLMD_TRY(critic_update_launch(cu, st));
+    if (loss_stats.B > 0 && !actor_step) {
+      hipLaunchKernelGGL(critic_loss_kernel<512>, dim3(1), dim3(512), 0, st, loss_stats);
+      RLMD_LAUNCH_CHECK();
+    }
+  } else {
     CBwdArgs cb{};
     cb.d = d;
     cb.co = co;
@@ -905,6 +963,18 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_ALLOC(s.dh1, B * H1);
   RLMD_ALLOC(s.stats, 16);
   RLMD_ALLOC(s.qbias, 4);
+  {
+    const size_t nrb = (size_t)(B + 15) / 16, ts = c.precision == RLMD_BF16 ? 2 : 4;
+    const size_t e1 = nrb * rlmd::pad32(H1) * 16, e2 = nrb * rlmd::pad32(H2) * 16;
+    for (int g = 0; g < 2; ++g) {
+      RLMD_ALLOC(s.hp1[g], e1 * ts);
+      RLMD_ALLOC(s.hp2[g], e2 * ts);
+      RLMD_ALLOC(s.u1[g], e1);
+      RLMD_ALLOC(s.w3s[g], H2);
+    }
+    const char* nf = getenv("RLMD_NO_FUSED_UPDATE");
+    ag->fused_update = B <= 512 && X <= 8 && !(nf && atoi(nf) != 0);
+  }
   {  // weight-gradient tiles of the larger phase (critics: both nets; actor)
     using rlmd::bwd_w_tiles;
     const int tc = 2 * (bwd_w_tiles(1, H2) + bwd_w_tiles(H2, H1) + bwd_w_tiles(H1, X));

@@ -146,6 +146,16 @@ struct FwdRowsArgs {
   float* xsan;
   float* logp;
   float* save;  // [B, 5A]
+  // fused critic update (update.hip) when u1[0] is set: per critic g the
+  // row-packed operands of its weight-gradient tiles — h1 / h2 in the compute
+  // type (hp1 / hp2), the backward basis U1 = [h1 > 0] * (([h2 > 0] * w3) W2)
+  // in f32 (dh1 = dq * U1) — and snapshots of the head weights / biases the
+  // update reads while other workgroups step them
+  float* u1[2];
+  void* hp1[2];
+  void* hp2[2];
+  float* w3s[2];  // [H2]
+  float* bsnap;   // [4] online q bias 0 / 1, target q bias 0 / 1
 };
 
 // Critics evaluated on (s, a_new) after their update: y = g.

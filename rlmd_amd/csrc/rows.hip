@@ -90,8 +90,8 @@ struct CT<RLMD_FP32> {
 // LDS carve-up, identical on host (launch size) and device.
 // ---------------------------------------------------------------------------
 struct Lds {
-  int xs, a1, aT, h2s, part, hout, ghs, rowv, vkey, vval, runs, rank, red, total;  // byte offsets
-  int ldx, lda1, ldaT, ldh2;                          // row pitches (elements)
+  int xs, a1, aT, h2s, part, hout, ghs, rowv, vkey, vval, runs, rank, red, aU, m1s, total;  // byte offsets
+  int ldx, lda1, ldaT, ldh2;                                    // row pitches (elements)
 };
 __host__ __device__ inline Lds lds_layout(const RowDims& d) {
   const int ts = d.prec == RLMD_BF16 ? 2 : 4;
@@ -129,6 +129,10 @@ __host__ __device__ inline Lds lds_layout(const RowDims& d) {
   o = up(o + 3 * NT * 4);
   l.red = o;
   o = up(o + 16 * 9 * 4);
+  l.aU = o;  // A operand of the backward-basis pass (fwd U = (m2 w3) W2), pitch lda1
+  o = up(o + R * l.lda1 * ts);
+  l.m1s = o;  // layer-1 ReLU mask bytes [R][hmax] (f32 h1 > 0)
+  o = up(o + R * hmax);
   l.total = o;
   return l;
 }
@@ -306,11 +310,31 @@ __device__ __forceinline__ int64_t m2_index(int rb, int H2p, int row, int col) {
   return (((int64_t)rb * H2p + col) << 4) + (row & 15);
 }
 
+// Row-packed operands of the weight-gradient tiles (update.hip): element (b, c)
+// of a [B x Hp] matrix at ((b / 16) * Hp + c) * 16 + b % 16, so the 8 (bf16) or
+// 4 (f32) consecutive mini-batch rows an MFMA fragment lane holds along K are
+// one contiguous 16-byte run.
+__device__ __forceinline__ int64_t rp_index(int rb, int Hp, int row, int col) {
+  return (((int64_t)rb * Hp + col) << 4) + (row & 15);
+}
+
+// Extra outputs of one net's forward for the fused update kernels (nullable
+// members: not written): h1 / h2 row-packed in the compute type; the layer-1
+// mask bytes (LDS) and the A operand of the backward-basis pass (LDS).
+template <int PREC>
+struct FwdExtra {
+  typename CT<PREC>::T* hp1;
+  typename CT<PREC>::T* hp2;
+  uint8_t* m1s;
+  typename CT<PREC>::T* aU;
+  const float* whead;  // per-column weight of the basis pass (critic: w3, LDS-free: from FwdConst)
+};
+
 // h1 = relu(x W1^T + b1): A operand (T, zero-padded to H1p) + f32 to HBM (nullable)
 template <int PREC, int NBW>
 __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, const NetOff& o, const float* xs,
                                        int ldx, int in, typename CT<PREC>::T* a1, int lda1, float* h1_out,
-                                       uint8_t* m1_out, int row0, int B) {
+                                       uint8_t* m1_out, int row0, int B, const FwdExtra<PREC>* ex = nullptr) {
   const int H1 = o.h1;
   const ElemMap m = elem_map(pad32(H1));
   const float* w = p + o.w1 + (int64_t)m.c * in;
@@ -328,15 +352,20 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
     }
     if (m1_out) m1_out[m1_index(row0 / R, pad32(H1), r, m.c)] = v > 0.f ? 1 : 0;
     a1[r * lda1 + m.c] = CT<PREC>::cvt(v);
+    if (ex) {
+      if (ex->hp1) ex->hp1[rp_index(row0 / R, pad32(H1), r, m.c)] = CT<PREC>::cvt(row0 + r < B ? v : 0.f);
+      if (ex->m1s) ex->m1s[r * pad32(H1) + m.c] = v > 0.f ? 1 : 0;
+    }
   }
 }
 
 // relu(acc + b2) -> HBM (nullable), LDS rows (nullable) and the per-wave head
 // partials part[wave][row][h] (nh <= NHF).
-template <int NBW>
+template <int NBW, int PREC = RLMD_BF16>
 __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdConst<NBW>& k, const NetOff& o,
                                              int nh, float* h2_out, uint8_t* m2_out, float* h2s, int ldh2,
-                                             float* part, int row0, int B) {
+                                             float* part, int row0, int B, const FwdExtra<PREC>* ex = nullptr,
+                                             int lda1 = 0) {
   const int H2 = o.h2, nblk = pad32(H2) / 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float ph[4][NHF];
@@ -356,6 +385,11 @@ __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdC
         const float v = cin ? fmaxf(acc[i][rg] + k.b2[i], 0.f) : 0.f;
         if (h2_out && cin && row0 + r < B) h2_out[(int64_t)(row0 + r) * H2 + col] = v;
         if (h2s) h2s[r * ldh2 + col] = v;
+        if (ex) {
+          if (ex->hp2) ex->hp2[rp_index(row0 / R, pad32(H2), r, col)] = CT<PREC>::cvt(row0 + r < B ? v : 0.f);
+          // critic basis pass A operand: [h2 > 0] * w3 (the head weight of this column)
+          if (ex->aU) ex->aU[r * lda1 + col] = CT<PREC>::cvt(v > 0.f ? k.hw[i][0] : 0.f);
+        }
         mw |= (v > 0.f ? 1u : 0u) << (8 * rg);
 #pragma unroll
         for (int h = 0; h < NHF; ++h) ph[rg][h] = fmaf(v, k.hw[i][h], ph[rg][h]);
@@ -408,13 +442,13 @@ template <int PREC, int NBW, bool MULTI>
 __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>& k, Pre<PREC, NBW, MULTI>& pre,
                          const float* xs, int ldx, int in, int nh, const float* wa, const float* wb, int na,
                          unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B,
-                         uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr) {
+                         uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr, const FwdExtra<PREC>* ex = nullptr) {
   using T = typename CT<PREC>::T;
   T* a1 = reinterpret_cast<T*>(smem + L.a1);
   float* part = reinterpret_cast<float*>(smem + L.part);
   float* hout = reinterpret_cast<float*>(smem + L.hout);
   float* h2s = reinterpret_cast<float*>(smem + L.h2s);
-  layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, m1_out, row0, B);
+  layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, m1_out, row0, B, ex);
   if (blockIdx.y == 2) RLMD_TSR(63);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(64);
@@ -423,7 +457,7 @@ __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>
   mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, pad32(o.h2) / 16, acc);
   if (blockIdx.y == 2) RLMD_TSR(65);
   const bool fused = nh <= NHF;
-  fwd_epilogue<NBW>(acc, k, o, nh, h2_out, m2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B);
+  fwd_epilogue<NBW, PREC>(acc, k, o, nh, h2_out, m2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B, ex, L.lda1);
   if (blockIdx.y == 2) RLMD_TSR(66);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(67);
@@ -625,20 +659,54 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
                                nullptr, row0, B);
     RLMD_TSR(16 * job + 5);
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qt[job][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
+    if (a.bsnap && blockIdx.x == 0 && threadIdx.x == 0) a.bsnap[2 + job] = cn.p[a.co.b3];
   } else if (job <= 3) {  // online critics on (s, a) (algo_sac.py:413-417)
     if (job == 2) RLMD_TSR(60);
     const int g = job - 2;
     const RowNet& cn = a.crit[g];
+    const bool upd = a.u1[0] != nullptr;
     const StageReg sr = stage_issue(a.xsa, d.X, L.ldx, row0, B);
     FwdConst<NBW> kc;
     critic_const<NBW>(kc, cn, a.co, d);
-    Pre<PREC, NBW, MULTI> pc;
+    Pre<PREC, NBW, MULTI> pc, pw;
     pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    if (upd) pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
     stage_commit(sr, a.xsa, d.X, xs, L.ldx, row0, B);
     __syncthreads();
     if (job == 2) RLMD_TSR(61);
-    mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.c1[g],
-                               a.c2[g], row0, B, a.cm1[g], a.cm2[g]);
+    if (!upd) {
+      mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.c1[g],
+                                 a.c2[g], row0, B, a.cm1[g], a.cm2[g]);
+    } else {
+      using T = typename CT<PREC>::T;
+      T* aU = reinterpret_cast<T*>(smem + L.aU);
+      uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + L.m1s);
+      const FwdExtra<PREC> ex{static_cast<T*>(a.hp1[g]), static_cast<T*>(a.hp2[g]), m1s, aU, nullptr};
+      mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
+                                 nullptr, row0, B, nullptr, a.cm2[g], &ex);
+      // the backward basis of these rows: U1 = [h1 > 0] * (([h2 > 0] w3) W2), so
+      // that the critic update forms dh1 = dq * U1 once dq is known (update.hip)
+      f32x4 acc[NBW];
+      mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H2p, H2p, H1p / 16, acc);
+      const int wave = threadIdx.x >> 6;
+#pragma unroll
+      for (int i = 0; i < NBW; ++i) {
+        if (wave + NW * i < H1p / 16) {
+          const int col = acc_col(i);
+          f32x4 u;
+#pragma unroll
+          for (int rg = 0; rg < 4; ++rg) {
+            const int r = acc_row(rg);
+            u[rg] = (m1s[r * H1p + col] && row0 + r < B) ? acc[i][rg] : 0.f;
+          }
+          *reinterpret_cast<f32x4*>(a.u1[g] + rp_index(row0 / R, H1p, acc_row(0), col)) = u;
+        }
+      }
+      if (blockIdx.x == 0) {  // snapshots of what the update reads while stepping it
+        for (int c = threadIdx.x; c < d.H2; c += NT) a.w3s[g][c] = cn.p[a.co.w3 + c];
+        if (threadIdx.x == 0) a.bsnap[g] = cn.p[a.co.b3];
+      }
+    }
     if (job == 2) RLMD_TSR(62);
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)

@@ -124,7 +124,17 @@ def test_fused_optimiser_epilogue(dev, monkeypatch, algo, S, A, h1, h2, B, k, sp
     the accumulators); same numerics as adam_kernel up to the K-sum order."""
     monkeypatch.setenv("RLMD_FUSE_ADAM", "1")
     monkeypatch.setenv("RLMD_FUSE_SPLITS", splits)
+    monkeypatch.setenv("RLMD_NO_FUSED_UPDATE", "1")  # the critic step through the GEMM too
     test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, "MSE")
+
+
+@pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL[:2])
+@pytest.mark.parametrize("loss", ["MSE", "HUB"])
+def test_launch_chain_critic_step_matches_oracle(dev, monkeypatch, algo, S, A, h1, h2, B, k, loss):
+    """RLMD_NO_FUSED_UPDATE=1: the critic step as row backward + weight-gradient
+    GEMM + Adam launches (the path B > 512 takes) against the same oracle."""
+    monkeypatch.setenv("RLMD_NO_FUSED_UPDATE", "1")
+    test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss)
 
 
 @pytest.mark.parametrize("s_dist", ["L", "MVN"])
