@@ -245,6 +245,10 @@ struct Scratch {
   // backward basis U1 (f32) and the q_value.weight snapshot per critic
   unsigned char *hp1[2], *hp2[2];
   float *u1[2], *w3s[2];
+  // fused actor update: the policy's row-packed h1 / h2, its per-head backward
+  // bases, the head weights' snapshot, the critics' dq/da per row
+  unsigned char *hp1a, *hp2a;
+  float *ua, *wheads, *dqda[2];
 };
 
 }  // namespace
@@ -286,6 +290,7 @@ struct rlmd_agent_s {
   // critic step as one launch (update.hip) for B <= 512; RLMD_NO_FUSED_UPDATE=1:
   // row backward + weight-gradient GEMM + Adam launches
   bool fused_update = false;
+  bool fused_actor = false;  // the actor step too (actions <= 2)
 };
 
 namespace rlmd {
@@ -561,6 +566,10 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       }
       f.bsnap = S_.qbias;
     }
+    if (ag->fused_actor && actor_step) {
+      f.hp1a = S_.hp1a;
+      f.hp2a = S_.hp2a;
+    }
     RLMD_TRY(fwd_rows_launch(f, st));
   }
   // ---- critic loss (algo_sac.py:413-465)
@@ -706,8 +715,76 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       qe.em1[g] = S_.em1[g];
       qe.em2[g] = S_.em2[g];
       qe.qn[g] = S_.qnpart[g];
+      if (ag->fused_actor) qe.dqda[g] = S_.dqda[g];
+    }
+    qe.nq = nq;
+    if (ag->fused_actor) {  // + the policy's per-head backward bases
+      qe.nab = sac ? 2 * A : A;
+      qe.ao = ao;
+      qe.actor = row_net(ag, SLOT_ACTOR);
+      qe.am1 = S_.am1;
+      qe.am2 = S_.am2;
+      qe.ua = S_.ua;
+      qe.wheads = S_.wheads;
     }
     RLMD_TRY(qeval_rows_launch(qe, nq, st));
+    if (ag->fused_actor) {
+      // the actor (+ temperature) step in one launch (update.hip)
+      ActUpdArgs au{};
+      au.d = d;
+      au.ao = ao;
+      au.smp = smp;
+      au.nq = nq;
+      for (int g = 0; g < 2; ++g) {
+        au.qn[g] = S_.qnpart[g];
+        au.qb[g] = Pc[g] + co.b3;
+        au.dqda[g] = S_.dqda[g];
+      }
+      au.logp = S_.logp;
+      au.save = S_.save;
+      au.am2 = S_.am2;
+      au.hp1a = S_.hp1a;
+      au.hp2a = S_.hp2a;
+      au.ua = S_.ua;
+      au.wheads = S_.wheads;
+      au.s = mb.s;
+      au.st = ag->st;
+      au.stats = stats;
+      au.k = c.topk;
+      au.topk = c.actor_topk;
+      au.target_entropy = -(float)A;
+      AdamArgs ad{};
+      ad.p = P + ag->off_actor;
+      ad.g = Ga;
+      ad.m = ag->m + ag->off_actor;
+      ad.v = ag->v + ag->off_actor;
+      ad.target = sac ? nullptr : T + ag->off_actor;
+      ad.n = ao.size;
+      ad.lr = c.lr_actor;
+      ad.tau = c.tau;
+      ad.cnt = (int32_t)cntr;
+      ad.interval = c.actor_update_interval;
+      ad.polyak_interval = sac ? 0 : c.target_actor_update;
+      ad.st = ag->st;
+      ad.temp = sac ? 1 : 0;
+      ad.lr_temp = c.lr_temp;
+      ad.temp_interval = c.temp_update_interval;
+      ad.stats = stats;
+      adam_copies(ag, ad, ao, SLOT_ACTOR, 1, !sac);
+      adam_scalars(ad.lr, ad.cnt / ad.interval, ad.step_size, ad.bc2_sqrt);
+      if (ad.temp && ad.cnt % ad.temp_interval == 0)
+        adam_scalars(ad.lr_temp, ad.cnt / ad.temp_interval, ad.temp_step_size, ad.temp_bc2_sqrt);
+      au.adam = ad;
+      au.cstats = loss_stats;
+      au.cstats.keep_actor_slot = 1;   // stats[10]: the actor loss
+      au.cstats.keep_logtemp_slot = 1; // stats[11]: the temperature step
+      au.tj = d.H1p / 32;
+      au.ti = d.H2p / 32;
+      au.n_w2 = au.ti * au.tj;
+      au.n_w1 = d.H1p / 32;
+      RLMD_TRY(actor_update_launch(au, st));
+      return 0;
+    }
     // B <= 512: the actor loss is fused into abwd_rows (row ranks + a loss
     // workgroup); larger mini-batches use the one-workgroup loss kernel
     const bool fused_loss = B <= 512;
@@ -974,6 +1051,14 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
     }
     const char* nf = getenv("RLMD_NO_FUSED_UPDATE");
     ag->fused_update = B <= 512 && X <= 8 && !(nf && atoi(nf) != 0);
+    const char* na = getenv("RLMD_NO_FUSED_ACTOR");
+    ag->fused_actor = ag->fused_update && A <= 2 && !(na && atoi(na) != 0);
+    const int nh = c.algo == RLMD_SAC ? 2 * A : A;
+    RLMD_ALLOC(s.hp1a, e1 * ts);
+    RLMD_ALLOC(s.hp2a, e2 * ts);
+    RLMD_ALLOC(s.ua, e1 * nh);
+    RLMD_ALLOC(s.wheads, nh * H2);
+    for (int g = 0; g < 2; ++g) RLMD_ALLOC(s.dqda[g], B * A);
   }
   {  // weight-gradient tiles of the larger phase (critics: both nets; actor)
     using rlmd::bwd_w_tiles;

@@ -21,6 +21,7 @@ struct LearnState {
   int32_t nan_flag;    // tests/test_live_learning.py guards -> flag, no exit()
   float pad_temp_grad;  // temperature gradient handed from actor_loss to adam
   int32_t nan_update;   // learn_cntr when nan_flag was first set
+  uint32_t arrive;      // fused actor update: workgroups done reading log_alpha (update.hip)
 };
 
 // Per-net parameter offsets (floats) inside a flat buffer, torch nn.Linear
@@ -156,6 +157,10 @@ struct FwdRowsArgs {
   void* hp2[2];
   float* w3s[2];  // [H2]
   float* bsnap;   // [4] online q bias 0 / 1, target q bias 0 / 1
+  // fused actor update when hp1a is set: the policy's h1 / h2 row-packed in the
+  // compute type (its masks go to am1 / am2; the bases are qeval_rows' head jobs)
+  void* hp1a;
+  void* hp2a;
 };
 
 // Critics evaluated on (s, a_new) after their update: y = g.
@@ -169,6 +174,19 @@ struct QEvalArgs {
   uint8_t* em1[2];
   uint8_t* em2[2];
   float* qn[2];
+  // fused actor update: dq/da per row of each critic, [B][A] (nullable), and
+  // y = nq + h (h < nab): the policy's backward basis of head h (mu rows, then
+  // log-scale rows for SAC) U_h = [h1 > 0] * (([h2 > 0] W_head[h]) W2) from the
+  // forward's masks am1 / am2, f32 row-packed [nh][nrb][H1p][16], and the head
+  // weights' snapshot [nh][H2] the actor update reads while stepping them
+  float* dqda[2];
+  int32_t nq, nab;
+  NetOff ao;
+  RowNet actor;
+  const uint8_t* am1;
+  const uint8_t* am2;
+  float* ua;
+  float* wheads;
 };
 
 // Critic data-gradients: y = g.  dh2 = dq w3 * [h2 > 0], dh1 = (dh2 W2) * [h1 > 0].
@@ -195,6 +213,7 @@ struct LossArgs {
   int32_t B, k, loss_type, algo;
   float log_noise, grad_scale;
   int32_t keep_actor_slot;  // 1: leave stats[10] (actor loss) alone
+  int32_t keep_logtemp_slot;  // 1: leave stats[11] (log temperature) to the temperature step
 };
 
 struct CBwdArgs {

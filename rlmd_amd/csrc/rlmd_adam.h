@@ -84,8 +84,19 @@ __device__ __forceinline__ AdamIn adam_load(const AdamArgs& a, int i, bool polya
   return o;
 }
 
+// Compute-copy destinations of one net (wc / wt and the Polyak target's).
+struct CopyDst {
+  void *wc, *wt, *twc, *twt;
+};
+// For a workgroup-uniform net: read the kernel-argument pointers once, up front.
+__device__ __forceinline__ CopyDst copy_dst(const AdamArgs& a, int net) {
+  return net == 0 ? CopyDst{a.wc[0], a.wt[0], a.twc[0], a.twt[0]} : CopyDst{a.wc[1], a.wt[1], a.twc[1], a.twt[1]};
+}
+
 // One parameter: Adam with gradient g, then Polyak and the compute copies.
-__device__ __forceinline__ void adam_apply(const AdamArgs& a, int i, float g, const AdamIn& in, bool polyak) {
+// jw2: the element's index inside its net's fc2.weight (-1: not fc2.weight).
+__device__ __forceinline__ void adam_apply_dst(const AdamArgs& a, int i, float g, const AdamIn& in, bool polyak,
+                                               int jw2, const CopyDst& cd) {
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
   float m = in.m, v = in.v;
   m = m + (1.f - b1) * (g - m);
@@ -100,21 +111,28 @@ __device__ __forceinline__ void adam_apply(const AdamArgs& a, int i, float g, co
     tv = a.tau * p + (1.f - a.tau) * in.t;
     a.target[i] = tv;
   }
-  if (a.ncopy) {
-    const int ns = (int)a.net_size;
-    const int net = i / ns;
-    const int j = i - net * ns - (int)a.w2_off;
-    if (net < a.ncopy && j >= 0 && j < a.H1 * a.H2) {
-      const int n = j / a.H1, k = j - n * a.H1;
-      const int64_t ic = frag_index(n, k, a.H1p, a.bf16), it = frag_index(k, n, a.H2p, a.bf16);
-      store_copy(a.wc[net], ic, p, a.bf16);
-      store_copy(a.wt[net], it, p, a.bf16);
-      if (polyak && a.twc[net]) {
-        store_copy(a.twc[net], ic, tv, a.bf16);
-        store_copy(a.twt[net], it, tv, a.bf16);
-      }
+  if (jw2 >= 0) {
+    const int n = jw2 / a.H1, k = jw2 - n * a.H1;
+    const int64_t ic = frag_index(n, k, a.H1p, a.bf16), it = frag_index(k, n, a.H2p, a.bf16);
+    store_copy(cd.wc, ic, p, a.bf16);
+    store_copy(cd.wt, it, p, a.bf16);
+    if (polyak && cd.twc) {
+      store_copy(cd.twc, ic, tv, a.bf16);
+      store_copy(cd.twt, it, tv, a.bf16);
     }
   }
+}
+
+// The same for any element of the stepped nets (net = i / net_size per lane).
+__device__ __forceinline__ void adam_apply(const AdamArgs& a, int i, float g, const AdamIn& in, bool polyak) {
+  int jw2 = -1, net = 0;
+  if (a.ncopy) {
+    const int ns = (int)a.net_size;
+    net = i / ns;
+    const int j = i - net * ns - (int)a.w2_off;
+    if (net < a.ncopy && j >= 0 && j < a.H1 * a.H2) jw2 = j;
+  }
+  adam_apply_dst(a, i, g, in, polyak, jw2, copy_dst(a, net));
 }
 
 // Once per step (one thread): the learner counter and the temperature Adam.

@@ -66,6 +66,7 @@ struct CriticRow {
 struct CriticLoads {
   float qt[2], q[2], rw, lpn;
   int eff;
+  bool has_eff;
   uint8_t dn;
   // uniform scalars issued with the row loads: head biases, log alpha, Cauchy scales
   float tb[2], qb[2], log_alpha, cauchy[2];
@@ -80,11 +81,13 @@ __device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
     L.q[g] = rlmd_ldf(rlmd_rsrc(a.qpart[g], nB), b, in);
   }
   L.rw = rlmd_ldf(rlmd_rsrc(a.r, nB), b, in);
-  L.lpn = a.logp_next ? rlmd_ldf(rlmd_rsrc(a.logp_next, nB), b, in) : 0.f;
+  // optional operands through zero-sized resources when absent (the load then
+  // reads 0): no branch around a load, whose use would wait right there
+  L.lpn = rlmd_ldf(rlmd_rsrc(a.logp_next, a.logp_next ? nB : 0), b, in);
   L.dn = __builtin_amdgcn_raw_buffer_load_b8(rlmd_rsrc(a.done, B), in ? b : 0x7fffffff, 0, 0);
-  L.eff = a.eff ? (int)__builtin_bit_cast(
-                      int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, nB), in ? b * 4 : 0x7fffffff, 0, 0))
-                : 1;
+  L.eff = (int)__builtin_bit_cast(
+      int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, a.eff ? nB : 0), in ? b * 4 : 0x7fffffff, 0, 0));
+  L.has_eff = a.eff != nullptr;
   for (int g = 0; g < 2; ++g) {
     L.tb[g] = a.tb[g][0];
     L.qb[g] = a.qb[g][0];
@@ -101,7 +104,7 @@ __device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, C
   float qt[2] = {L.qt[0], L.qt[1]}, q[2] = {L.q[0], L.q[1]};
   const float rw = L.rw, lpn = L.lpn;
   const uint8_t dn = L.dn;
-  const int eff = L.eff;
+  const int eff = L.has_eff ? L.eff : 1;
   float y = 0.f;
   for (int g = 0; g < 2; ++g) {
     qt[g] += L.tb[g];
@@ -236,7 +239,7 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
     if (fl && !st->nan_flag) st->nan_update = st->learn_cntr;
     st->nan_flag = fl;
     if (!a.keep_actor_slot) a.stats[10] = NAN;
-    a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
+    if (!a.keep_logtemp_slot) a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
     a.stats[12] = newc[0];
     a.stats[13] = newc[1];
     a.stats[14] = o.kern[0];

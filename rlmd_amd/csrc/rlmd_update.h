@@ -22,7 +22,36 @@ struct CritUpdArgs {
   int32_t ti, tj, n_w2, n_w1;
 };
 
+// The actor (+ temperature) step of one update in one launch
+// (update.hip actor_update_kernel).  Grid: n_w2 fc2.weight tiles + n_w1 fc1
+// blocks of the policy, then one critic-statistics workgroup when cstats.B > 0.
+struct ActUpdArgs {
+  RowDims d;
+  NetOff ao;
+  SampleCfg smp;
+  int32_t nq;              // critics in the actor loss: SAC 2 (min), TD3 1
+  const float* qn[2];      // updated critics on (s, a_new), no head bias [B]
+  const float* qb[2];      // their q_value.bias (not stepped in this launch)
+  const float* dqda[2];    // dq/da per row [B][A] (qeval_rows)
+  const float* logp;       // [B] (SAC)
+  const float* save;       // sampling save [B][5A] (fwd_rows job 4)
+  const uint8_t* am2;      // the policy's [h2 > 0], row-packed bytes
+  const void* hp1a;        // the policy's h1 / h2 row-packed, compute type
+  const void* hp2a;
+  const float* ua;         // backward bases per head [nh][nrb * H1p * 16], f32
+  const float* wheads;     // head weights' snapshot [nh][H2]
+  const float* s;          // states [B][S]
+  LearnState* st;
+  float* stats;
+  int32_t k, topk;
+  float target_entropy;
+  AdamArgs adam;           // the actor (+ temperature when adam.temp)
+  LossArgs cstats;         // critic statistics workgroup (B == 0: none)
+  int32_t ti, tj, n_w2, n_w1;
+};
+
 size_t critic_update_lds();
+int actor_update_launch(const ActUpdArgs& a, hipStream_t st);
 int critic_update_launch(const CritUpdArgs& a, hipStream_t st);
 
 }  // namespace rlmd

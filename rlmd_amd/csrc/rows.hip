@@ -45,7 +45,15 @@ __device__ unsigned long long g_ts_rows[128];
   do {                                                                                   \
     if (threadIdx.x == 0 && blockIdx.x == 0) g_ts_rows[i] = __builtin_amdgcn_s_memtime(); \
   } while (0)
+// job windows (constant-rate clock, comparable across workgroups): block x = 0
+#define RLMD_TSJ(i)                                                                          \
+  do {                                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x == 0) g_ts_rows[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
+#define RLMD_TSJ(i) \
+  do {              \
+  } while (0)
 #define RLMD_TSR(i) \
   do {              \
   } while (0)
@@ -245,6 +253,10 @@ __device__ __forceinline__ ElemMap elem_map(int Hp) {
   return m;
 }
 
+// rows per thread of a [16 x Hp] elementwise map, Hp <= 128 NBW: 16 / (512 / Hp) <= 4 NBW
+template <int NBW>
+constexpr int kMR = 4 * NBW < R ? 4 * NBW : R;
+
 // MFMA accumulator element (i, rg) of this lane: column and row
 __device__ __forceinline__ int acc_col(int i, int nb0 = 0) {
   return (nb0 + (threadIdx.x >> 6) + NW * i) * 16 + (threadIdx.x & 15);
@@ -326,18 +338,55 @@ struct FwdExtra {
   typename CT<PREC>::T* hp1;
   typename CT<PREC>::T* hp2;
   uint8_t* m1s;
-  typename CT<PREC>::T* aU;
-  const float* whead;  // per-column weight of the basis pass (critic: w3, LDS-free: from FwdConst)
+  typename CT<PREC>::T* aU;  // critic basis pass A operand ([h2 > 0] w3), written in the epilogue
 };
+
+// A thread's nr consecutive rows [r0, r0 + nr) of one column, contiguous in the
+// row-packed layout (element idx = rp_index(rb, Hp, r0, c); r0 a multiple of nr,
+// nr in {1, 2, 4, 8, 16}): stored with the widest buffer stores that cover them.
+template <int PREC, int MR>
+__device__ __forceinline__ void store_rp_rows(typename CT<PREC>::T* base, int64_t idx, const typename CT<PREC>::T (&v)[MR],
+                                              int nr) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  constexpr int TS = sizeof(typename CT<PREC>::T);
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  const int off = (int)(idx * TS);
+  uint32_t w[(MR * TS + 3) / 4];
+  if constexpr (PREC == RLMD_BF16) {
+#pragma unroll
+    for (int k = 0; k < (MR + 1) / 2; ++k) w[k] = (uint32_t)v[2 * k] | (2 * k + 1 < MR ? (uint32_t)v[2 * k + 1] << 16 : 0u);
+  } else {
+#pragma unroll
+    for (int k = 0; k < MR; ++k) w[k] = __float_as_uint(v[k]);
+  }
+  const int nw = nr * TS / 4;  // whole words (0: one bf16 row)
+  if (nw >= 4) {
+#pragma unroll
+    for (int q = 0; q < (MR * TS) / 16; ++q)
+      if (4 * q < nw)
+        __builtin_amdgcn_raw_buffer_store_b128(u32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]}, rs, off + 16 * q,
+                                               0, 0);
+  } else if (nw == 2) {
+    if constexpr ((MR * TS) / 4 >= 2) __builtin_amdgcn_raw_buffer_store_b64(u32x2{w[0], w[1]}, rs, off, 0, 0);
+  } else if (nw == 1) {
+    __builtin_amdgcn_raw_buffer_store_b32(w[0], rs, off, 0, 0);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w[0], rs, off, 0, 0);
+  }
+}
 
 // h1 = relu(x W1^T + b1): A operand (T, zero-padded to H1p) + f32 to HBM (nullable)
 template <int PREC, int NBW>
 __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, const NetOff& o, const float* xs,
                                        int ldx, int in, typename CT<PREC>::T* a1, int lda1, float* h1_out,
                                        uint8_t* m1_out, int row0, int B, const FwdExtra<PREC>* ex = nullptr) {
-  const int H1 = o.h1;
-  const ElemMap m = elem_map(pad32(H1));
+  constexpr int MR = kMR<NBW>;
+  const int H1 = o.h1, H1p = pad32(H1);
+  const ElemMap m = elem_map(H1p);
+  const int nr = m.r1 - m.r0;
   const float* w = p + o.w1 + (int64_t)m.c * in;
+  uint64_t mk[(MR + 7) / 8] = {};  // the thread's mask bytes, row r0 + rr at byte rr
   for (int r = m.r0; r < m.r1; ++r) {
     float v = 0.f;
     if (m.c < H1) {
@@ -350,11 +399,40 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
       v = fmaxf(acc + k.b1, 0.f);
       if (h1_out && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + m.c] = v;
     }
-    if (m1_out) m1_out[m1_index(row0 / R, pad32(H1), r, m.c)] = v > 0.f ? 1 : 0;
     a1[r * lda1 + m.c] = CT<PREC>::cvt(v);
-    if (ex) {
-      if (ex->hp1) ex->hp1[rp_index(row0 / R, pad32(H1), r, m.c)] = CT<PREC>::cvt(row0 + r < B ? v : 0.f);
-      if (ex->m1s) ex->m1s[r * pad32(H1) + m.c] = v > 0.f ? 1 : 0;
+    if (ex && ex->m1s) ex->m1s[r * H1p + m.c] = v > 0.f ? 1 : 0;
+    const int rr = r - m.r0;
+    const uint64_t bit = (uint64_t)(v > 0.f ? 1u : 0u) << (8 * (rr & 7));
+    if constexpr (MR > 8) {
+      if (rr < 8) mk[0] |= bit;
+      else mk[1] |= bit;
+    } else {
+      mk[0] |= bit;
+    }
+  }
+  if (m.r0 < R) {
+    // the mask bytes: one word per 4 rows (m1_index keeps rows 4q..4q+3 of a column together)
+    if (m1_out) {
+      if (nr >= 4) {
+#pragma unroll
+        for (int q = 0; q < MR / 4; ++q)
+          if (4 * q < nr)
+            *reinterpret_cast<uint32_t*>(m1_out + m1_index(row0 / R, H1p, m.r0 + 4 * q, m.c)) =
+                (uint32_t)(mk[q / 2] >> (32 * (q & 1)));
+      } else {
+#pragma unroll
+        for (int rr = 0; rr < (MR < 2 ? MR : 2); ++rr)
+          if (rr < nr) m1_out[m1_index(row0 / R, H1p, m.r0 + rr, m.c)] = (uint8_t)(mk[0] >> (8 * rr));
+      }
+    }
+    if (ex && ex->hp1) {
+      // h1 in the compute type as the A operand holds it (this thread's own LDS
+      // writes), rows past B zero, packed into the row-packed layout
+      typename CT<PREC>::T hz[MR];
+#pragma unroll
+      for (int rr = 0; rr < MR; ++rr)
+        hz[rr] = (rr < nr && row0 + m.r0 + rr < B) ? a1[(m.r0 + rr) * lda1 + m.c] : typename CT<PREC>::T(0);
+      store_rp_rows<PREC, MR>(ex->hp1, rp_index(row0 / R, H1p, m.r0, m.c), hz, nr);
     }
   }
 }
@@ -379,22 +457,23 @@ __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdC
       const int col = acc_col(i);
       const bool cin = col < H2;
       uint32_t mw = 0;
+      typename CT<PREC>::T hz[4];
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         const int r = acc_row(rg);
         const float v = cin ? fmaxf(acc[i][rg] + k.b2[i], 0.f) : 0.f;
         if (h2_out && cin && row0 + r < B) h2_out[(int64_t)(row0 + r) * H2 + col] = v;
         if (h2s) h2s[r * ldh2 + col] = v;
-        if (ex) {
-          if (ex->hp2) ex->hp2[rp_index(row0 / R, pad32(H2), r, col)] = CT<PREC>::cvt(row0 + r < B ? v : 0.f);
-          // critic basis pass A operand: [h2 > 0] * w3 (the head weight of this column)
-          if (ex->aU) ex->aU[r * lda1 + col] = CT<PREC>::cvt(v > 0.f ? k.hw[i][0] : 0.f);
-        }
+        // critic basis pass A operand: [h2 > 0] * w3 (the head weight of this column)
+        if (ex && ex->aU) ex->aU[r * lda1 + col] = CT<PREC>::cvt(v > 0.f ? k.hw[i][0] : 0.f);
+        hz[rg] = CT<PREC>::cvt(row0 + r < B ? v : 0.f);
         mw |= (v > 0.f ? 1u : 0u) << (8 * rg);
 #pragma unroll
         for (int h = 0; h < NHF; ++h) ph[rg][h] = fmaf(v, k.hw[i][h], ph[rg][h]);
       }
       if (m2_out) *reinterpret_cast<uint32_t*>(m2_out + m2_index(row0 / R, pad32(H2), acc_row(0), col)) = mw;
+      // the lane's 4 rows of h2, contiguous in the row-packed layout
+      if (ex && ex->hp2) store_rp_rows<PREC, 4>(ex->hp2, rp_index(row0 / R, pad32(H2), acc_row(0), col), hz, 4);
     }
   }
   if (nh <= NHF) {
@@ -439,7 +518,7 @@ __device__ void row_dots(const float* src, int lds, int ncols, int nh, const flo
 // One 2-hidden-layer MLP forward over the block's rows (x in LDS), heads left in
 // hout[r][h] (no head bias).  pre: this net's fc2 fragments, already issued.
 template <int PREC, int NBW, bool MULTI>
-__device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>& k, Pre<PREC, NBW, MULTI>& pre,
+__device__ __forceinline__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>& k, Pre<PREC, NBW, MULTI>& pre,
                          const float* xs, int ldx, int in, int nh, const float* wa, const float* wb, int na,
                          unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B,
                          uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr, const FwdExtra<PREC>* ex = nullptr) {
@@ -450,17 +529,22 @@ __device__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>
   float* h2s = reinterpret_cast<float*>(smem + L.h2s);
   layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, m1_out, row0, B, ex);
   if (blockIdx.y == 2) RLMD_TSR(63);
+  if (blockIdx.y == 4) RLMD_TSR(87);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(64);
+  if (blockIdx.y == 4) RLMD_TSR(88);
   f32x4 acc[NBW];
   const int H1p = pad32(o.h1);
   mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, pad32(o.h2) / 16, acc);
   if (blockIdx.y == 2) RLMD_TSR(65);
+  if (blockIdx.y == 4) RLMD_TSR(89);
   const bool fused = nh <= NHF;
   fwd_epilogue<NBW, PREC>(acc, k, o, nh, h2_out, m2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B, ex, L.lda1);
   if (blockIdx.y == 2) RLMD_TSR(66);
+  if (blockIdx.y == 4) RLMD_TSR(90);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(67);
+  if (blockIdx.y == 4) RLMD_TSR(91);
   if (fused) {
     if ((int)threadIdx.x < R * nh) {
       const int r = threadIdx.x % R, h = threadIdx.x / R;
@@ -514,7 +598,7 @@ __device__ __forceinline__ Noise2 noise_pre(const SampleCfg& smp, const RowDims&
 // action into xs[:, S:S+A] and xa_out (nullable).  Same arithmetic as
 // learn.hip's actor_head_kernel.  mode 0 stochastic, 1 deterministic.  hb: the
 // head biases preloaded (A <= 2) when has_hb, else read here.
-__device__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, const SampleCfg& smp, float* xs,
+__device__ __forceinline__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, const SampleCfg& smp, float* xs,
                             int ldx, const float* hout, int mode, int tag, const float* eps_in, float noise_std,
                             float noise_clip, int clamp_noise, float* logp_out, float* save, float* xa_out, int row0,
                             int B, HeadBias hbv = HeadBias{{0.f, 0.f}, {0.f, 0.f}}, bool has_hb = false,
@@ -616,6 +700,31 @@ __device__ __forceinline__ void critic_const(FwdConst<NBW>& k, const RowNet& n, 
   fwd_const<NBW>(k, n.p, co, d.X, 1, n.p + co.w3, n.p + co.w3, 1);
 }
 
+// The backward-basis pass of one net over the block's rows: acc = aU (LDS,
+// [R][H2p]) times fc2.weight through the transposed compute copy, masked by
+// [h1 > 0] (m1s) and stored row-packed in f32 (u, [nrb][H1p][16]).
+template <int PREC, int NBW, bool MULTI>
+__device__ __forceinline__ void basis_pass(Pre<PREC, NBW, MULTI>& pw, const typename CT<PREC>::T* aU, int lda,
+                                           const void* wt, int H1p, int H2p, const uint8_t* m1s, float* u, int row0,
+                                           int B) {
+  f32x4 acc[NBW];
+  mfma_rows<PREC, NBW, MULTI>(pw, aU, lda, wt, H2p, H2p, H1p / 16, acc);
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NBW; ++i) {
+    if (wave + NW * i < H1p / 16) {
+      const int col = acc_col(i);
+      f32x4 v;
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int r = acc_row(rg);
+        v[rg] = (m1s[r * H1p + col] && row0 + r < B) ? acc[i][rg] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(u + rp_index(row0 / R, H1p, acc_row(0), col)) = v;
+    }
+  }
+}
+
 // y = 0, 1: target path with target critic y (the policy sample is recomputed
 // per critic: same Philox draws, the logp written once); y = 2, 3: online
 // critic y - 2 on (s, a); y = 4: policy on s for the actor step.
@@ -630,6 +739,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
   const bool sac = d.algo == RLMD_SAC;
   const int H1p = pad32(d.H1), H2p = pad32(d.H2);
   const int na = sac ? 2 * d.A : d.A;
+  RLMD_TSJ(40 + job);
   if (job <= 1) {  // target path (algo_sac.py:300-367 / algo_td3.py:302-361)
     RLMD_TSR(16 * job + 0);
     const RowNet& an = a.tactor;
@@ -681,27 +791,12 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
       using T = typename CT<PREC>::T;
       T* aU = reinterpret_cast<T*>(smem + L.aU);
       uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + L.m1s);
-      const FwdExtra<PREC> ex{static_cast<T*>(a.hp1[g]), static_cast<T*>(a.hp2[g]), m1s, aU, nullptr};
+      const FwdExtra<PREC> ex{static_cast<T*>(a.hp1[g]), static_cast<T*>(a.hp2[g]), m1s, aU};
       mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
                                  nullptr, row0, B, nullptr, a.cm2[g], &ex);
       // the backward basis of these rows: U1 = [h1 > 0] * (([h2 > 0] w3) W2), so
       // that the critic update forms dh1 = dq * U1 once dq is known (update.hip)
-      f32x4 acc[NBW];
-      mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H2p, H2p, H1p / 16, acc);
-      const int wave = threadIdx.x >> 6;
-#pragma unroll
-      for (int i = 0; i < NBW; ++i) {
-        if (wave + NW * i < H1p / 16) {
-          const int col = acc_col(i);
-          f32x4 u;
-#pragma unroll
-          for (int rg = 0; rg < 4; ++rg) {
-            const int r = acc_row(rg);
-            u[rg] = (m1s[r * H1p + col] && row0 + r < B) ? acc[i][rg] : 0.f;
-          }
-          *reinterpret_cast<f32x4*>(a.u1[g] + rp_index(row0 / R, H1p, acc_row(0), col)) = u;
-        }
-      }
+      basis_pass<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H1p, H2p, m1s, a.u1[g], row0, B);
       if (blockIdx.x == 0) {  // snapshots of what the update reads while stepping it
         for (int c = threadIdx.x; c < d.H2; c += NT) a.w3s[g][c] = cn.p[a.co.w3 + c];
         if (threadIdx.x == 0) a.bsnap[g] = cn.p[a.co.b3];
@@ -710,6 +805,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     if (job == 2) RLMD_TSR(62);
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)
+    RLMD_TSR(80);
     const RowNet& an = a.actor;
     const StageReg sr = stage_issue(a.s, d.S, L.ldx, row0, B);
     const HeadBias hb = head_bias(an.p, a.ao, d);
@@ -721,45 +817,28 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     const Noise2 nz = pre_nz ? noise_pre(a.smp, d, a.a_tag, row0) : Noise2{{0.f, 0.f}};
     stage_commit(sr, a.s, d.S, xs, L.ldx, row0, B);
     __syncthreads();
+    RLMD_TSR(81);
     for (int e = threadIdx.x; e < R * d.S; e += NT) {
       const int r = e / d.S, k = e % d.S;
       if (row0 + r < B) a.xsan[(int64_t)(row0 + r) * d.X + k] = xs[r * L.ldx + k];
     }
+    // fused actor update (hp1a set): h1 / h2 row-packed for its weight-gradient
+    // tiles instead of the launch chain's f32 rows
+    using T = typename CT<PREC>::T;
+    const bool fa = a.hp1a != nullptr;
+    const FwdExtra<PREC> ex{static_cast<T*>(a.hp1a), static_cast<T*>(a.hp2a), nullptr, nullptr};  // null: not written
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
-                               d.A, smem, L, a.h1a, a.h2a, row0, B, a.am1, a.am2);
+                               d.A, smem, L, fa ? nullptr : a.h1a, fa ? nullptr : a.h2a, row0, B, a.am1, a.am2, &ex);
+    RLMD_TSR(82);
     sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, a.a_mode, a.a_tag, a.eps_cur, 0.f, 0.f, 0, a.logp, a.save,
                 a.xsan, row0, B, hb, true, nz, pre_nz);
+    RLMD_TSR(83);
   }
+  RLMD_TSJ(45 + job);
 }
 
-template <int PREC, int NBW, bool MULTI>
-__global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const RowDims& d = a.d;
-  const Lds L = lds_layout(d);
-  float* xs = reinterpret_cast<float*>(smem + L.xs);
-  const float* hout = reinterpret_cast<const float*>(smem + L.hout);
-  const int row0 = blockIdx.x * R, g = blockIdx.y, B = d.B;
-  const RowNet& cn = a.crit[g];
-  Pre<PREC, NBW, MULTI> pc;
-  pre_issue<PREC, NBW, MULTI>(pc, cn.wc, pad32(d.H1), pad32(d.H1), pad32(d.H2) / 16);
-  FwdConst<NBW> kc;
-  critic_const<NBW>(kc, cn, a.co, d);
-  stage_rows(a.x, d.X, xs, L.ldx, row0, B);
-  __syncthreads();
-  mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.e1[g], a.e2[g],
-                             row0, B, a.em1[g], a.em2[g]);
-  if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qn[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
-}
-
-// ---------------------------------------------------------------------------
-// backward pieces
-// ---------------------------------------------------------------------------
 // per-thread ReLU masks of one net's rows: m2 in the elementwise map over H2p
 // (for dh2), m1 in the MFMA accumulator layout over H1p (for dh1)
-// rows per thread of the [16 x H2p] elementwise map: 16 / (512 / H2p) <= 4 NBW
-template <int NBW>
-constexpr int kMR = 4 * NBW < R ? 4 * NBW : R;
 
 template <int NBW>
 struct BwdMask {
@@ -807,6 +886,128 @@ __device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const uint8_t* m1, con
   }
 }
 
+template <int PREC, int NBW, bool MULTI>
+__global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const RowDims& d = a.d;
+  const Lds L = lds_layout(d);
+  float* xs = reinterpret_cast<float*>(smem + L.xs);
+  const float* hout = reinterpret_cast<const float*>(smem + L.hout);
+  const int row0 = blockIdx.x * R, g = blockIdx.y, B = d.B;
+  const int H1p = pad32(d.H1), H2p = pad32(d.H2);
+  if (g >= a.nq) {
+    // the policy's backward basis of head h over the block's rows (fused actor
+    // update): aU = [h2 > 0] * W_head[h] from the forward's masks, times fc2.weight
+    // through the transposed copy, masked by [h1 > 0], stored row-packed f32
+    using T = typename CT<PREC>::T;
+    const int h = g - a.nq, nrb = (B + R - 1) / R;
+    const RowNet& an = a.actor;
+    Pre<PREC, NBW, MULTI> pw;
+    pre_issue<PREC, NBW, MULTI>(pw, an.wt, H2p, H2p, H1p / 16);
+    BwdMask<NBW> k;
+    bwd_mask<NBW>(k, a.am1, a.am2, nullptr, a.ao, row0, B);
+    const ElemMap m = elem_map(H2p);
+    const int64_t wrow = h < d.A ? a.ao.w3 + (int64_t)h * d.H2 : a.ao.w4 + (int64_t)(h - d.A) * d.H2;
+    const float wk = rlmd_ldf(rlmd_rsrc(an.p, a.ao.size * 4), wrow + m.c, m.c < d.H2);
+    if (blockIdx.x == 0 && m.r0 == 0 && m.c < d.H2) a.wheads[(int64_t)h * d.H2 + m.c] = wk;
+    T* aU = reinterpret_cast<T*>(smem + L.aU);
+#pragma unroll
+    for (int rr = 0; rr < kMR<NBW>; ++rr) {
+      const int r = m.r0 + rr;
+      if (r < m.r1) aU[r * L.lda1 + m.c] = CT<PREC>::cvt(k.m2[rr] > 0.f ? wk : 0.f);
+    }
+    __syncthreads();
+    f32x4 acc[NBW];
+    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, an.wt, H2p, H2p, H1p / 16, acc);
+    float* u = a.ua + (int64_t)h * nrb * H1p * R;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      if (wave + NW * i < H1p / 16) {
+        const int col = acc_col(i);
+        f32x4 v;
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) v[rg] = (k.m1[i][rg] > 0.f && row0 + acc_row(rg) < B) ? acc[i][rg] : 0.f;
+        *reinterpret_cast<f32x4*>(u + rp_index(row0 / R, H1p, acc_row(0), col)) = v;
+      }
+    }
+    return;
+  }
+  const RowNet& cn = a.crit[g];
+  const bool upd = a.dqda[0] != nullptr;
+  Pre<PREC, NBW, MULTI> pc, pw;
+  pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+  FwdConst<NBW> kc;
+  critic_const<NBW>(kc, cn, a.co, d);
+  float w1a[NBW][NHF];  // W1[c][S + j] of this lane's accumulator columns (fused actor update)
+  if (upd) {
+    pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
+    const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(cn.p, a.co.size * 4);
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      const int col = acc_col(i);
+#pragma unroll
+      for (int j = 0; j < NHF; ++j)
+        w1a[i][j] = j < d.A ? rlmd_ldf(rp, a.co.w1 + (int64_t)col * d.X + d.S + j, col < d.H1) : 0.f;
+    }
+  }
+  stage_rows(a.x, d.X, xs, L.ldx, row0, B);
+  __syncthreads();
+  if (!upd) {
+    mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.e1[g],
+                               a.e2[g], row0, B, a.em1[g], a.em2[g]);
+  } else {
+    // the critic on (s, a_new) and its input gradient dq/da per row: the basis
+    // pass [h1 > 0] * (([h2 > 0] w3) W2) contracted with W1[:, S:S+A] (the
+    // launch-chain path's abwd_rows dh1 with dq = 1; the actor update scales it)
+    using T = typename CT<PREC>::T;
+    T* aU = reinterpret_cast<T*>(smem + L.aU);
+    const uint8_t* m1s = reinterpret_cast<const uint8_t*>(smem + L.m1s);
+    float* part = reinterpret_cast<float*>(smem + L.part);
+    const FwdExtra<PREC> ex{nullptr, nullptr, reinterpret_cast<uint8_t*>(smem + L.m1s), aU};
+    mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
+                               nullptr, row0, B, nullptr, nullptr, &ex);
+    f32x4 acc[NBW];
+    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H2p, H2p, H1p / 16, acc);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float pd[4][NHF];
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+      for (int j = 0; j < NHF; ++j) pd[rg][j] = 0.f;
+#pragma unroll
+    for (int i = 0; i < NBW; ++i) {
+      if (wave + NW * i < H1p / 16) {
+        const int col = acc_col(i);
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const float v = m1s[acc_row(rg) * H1p + col] ? acc[i][rg] : 0.f;
+#pragma unroll
+          for (int j = 0; j < NHF; ++j) pd[rg][j] = fmaf(v, w1a[i][j], pd[rg][j]);
+        }
+      }
+    }
+#pragma unroll
+    for (int rg = 0; rg < 4; ++rg)
+#pragma unroll
+      for (int j = 0; j < NHF; ++j) {
+        if (j < d.A) {
+          const float c = rlmd_row16_sum(pd[rg][j]);
+          if ((lane & 15) == 0) part[(wave * R + acc_row(rg)) * NHF + j] = c;
+        }
+      }
+    __syncthreads();
+    if ((int)threadIdx.x < R * d.A) {
+      const int r = threadIdx.x % R, j = threadIdx.x / R;
+      if (row0 + r < B) a.dqda[g][(int64_t)(row0 + r) * d.A + j] = head_sum(part, r, j);
+    }
+  }
+  if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qn[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
+}
+
+// ---------------------------------------------------------------------------
+// backward pieces
+// ---------------------------------------------------------------------------
 // dh2 = dq[r] * w3 * [h2 > 0] -> A operand (T) and HBM (nullable)
 template <int PREC, int NBW>
 __device__ __forceinline__ void dh2_from_q(const BwdMask<NBW>& k, const float* dqr, const NetOff& o,
@@ -1321,7 +1522,10 @@ namespace rlmd {
 int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st) {
   return launch_rows(a.d, 0, &a, a.with_actor ? 5 : 4, st);
 }
-int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st) { return launch_rows(a.d, 1, &a, nq, st); }
+int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st) {
+  RLMD_CHECK(a.nq == nq && (a.nab == 0 || (a.ua && a.wheads && a.am1 && a.am2)), "qeval_rows: head jobs need their buffers");
+  return launch_rows(a.d, 1, &a, nq + a.nab, st);
+}
 // cbwd: dh1 columns in halves when each half is a whole number of column blocks
 // per wave (the per-workgroup W2^T stream is the kernel's cost)
 int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st) {

@@ -28,6 +28,7 @@
 #include "rlmd_adam.h"
 #include "rlmd_block.h"
 #include "rlmd_loss.h"
+#include "rlmd_policy.h"
 #include "rlmd_update.h"
 
 namespace rlmd {
@@ -38,11 +39,24 @@ typedef short bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int NT = 512;
 constexpr int TW = 32;  // tile edge (fc2.weight tiles TW x TW, fc1 blocks of TW rows)
 
+#ifdef RLMD_TIMING
+// experiment builds only (tools/ts_probe.py upd): thread-0 s_memtime stamps of
+// three workgroups (slot 0: tile (0, 0), 1: tile (0, 1), 2: the first fc1 block)
+__device__ unsigned long long g_ts_upd[64];
+#define RLMD_TSU(i)                                                                       \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && ts_slot >= 0) g_ts_upd[ts_slot * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define RLMD_TSU(i) \
+  do {              \
+  } while (0)
+#endif
+
+// f32 -> bf16, round to nearest even: the plain cast lowers to v_cvt_pk_bf16_f32
+// (NaN stays NaN; no per-element branch)
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
-  unsigned u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (unsigned short)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (unsigned short)(u >> 16);
+  return __builtin_bit_cast(unsigned short, (__bf16)f);
 }
 
 // Operand fragments of one K-step over rows: bf16 16x16x32 (8 rows per lane) or
@@ -138,8 +152,20 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   const bool first_col = w2tile && (t % a.tj) == 0;
   const int64_t pbase = (int64_t)g * co.size;  // this critic's parameters in the Adam base
   const bool polyak = adam_polyak(a.adam);
+  const CopyDst cd = copy_dst(a.adam, g);
+  // Adam on an element of this critic (fc2.weight elements also refresh the copies)
+  auto step = [&](int pi, float gv, const AdamIn& in) {
+    const int j = pi - (int)pbase - (int)co.w2;
+    adam_apply_dst(a.adam, pi, gv, in, polyak, (j >= 0 && j < H1 * H2) ? j : -1, cd);
+  };
+  const int ts_slot = blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : (int)blockIdx.x == a.n_w2 ? 2 : -1;
+  (void)ts_slot;
+  RLMD_TSU(0);
 
-  // ---- first load round: loss inputs, this workgroup's operands, Adam state
+  // ---- first load round: loss inputs, this workgroup's operands, Adam state.
+  //      Branch-free: every load is issued by every workgroup, predicated through
+  //      the range check on its role (a load inside `if (role)` is copied out of
+  //      its registers at the merge, which waits for it on the spot)
   const CriticLoads cl = critic_row_load(a.loss);
   // (a) dW2 tile: per wave rows [64 w, 64 w + 64), per K-step the A masks (two i
   //     sub-blocks) and B fragments (two j sub-blocks)
@@ -148,54 +174,85 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   typename K::Frag bf[NKS][2];
   const __amdgpu_buffer_rsrc_t rm2 = rlmd_rsrc(a.m2[g], (int64_t)nrb * H2p * 16),
                                rh1 = rlmd_rsrc(a.hp1[g], (int64_t)nrb * H1p * 16 * sizeof(typename K::T));
-  float w3l[2] = {0.f, 0.f};
-  if (w2tile) {
+  float w3l[2];
 #pragma unroll
-    for (int s = 0; s < NKS; ++s) {
-      const int row = 64 * wave + s * K::KS + K::RPL * (lane >> 4);
-      const bool rok = row < nrb * 16;
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int i = i0 + 16 * h + (lane & 15), j = j0 + 16 * h + (lane & 15);
-        K::load_mask(rm2, rp_idx(row, H2p, i), rok && i < H2p, mw[s][h]);
-        bf[s][h] = K::load_b(rh1, rp_idx(row, H1p, j), rok && j < H1p);
-      }
-    }
+  for (int s = 0; s < NKS; ++s) {
+    const int row = 64 * wave + s * K::KS + K::RPL * (lane >> 4);
+    const bool rok = w2tile && row < nrb * 16;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int i = i0 + 16 * h + (lane & 15);
-      w3l[h] = rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), i, i < H2);
+      const int i = i0 + 16 * h + (lane & 15), j = j0 + 16 * h + (lane & 15);
+      K::load_mask(rm2, rp_idx(row, H2p, i), rok && i < H2p, mw[s][h]);
+      bf[s][h] = K::load_b(rh1, rp_idx(row, H1p, j), rok && j < H1p);
     }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = i0 + 16 * h + (lane & 15);
+    w3l[h] = rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), i, w2tile && i < H2);
   }
   // (b) Adam state of the owned parameters: a dW2 tile's 1024 elements, 2 per thread
   int pidx[2];
   AdamIn ain[2];
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    pidx[e] = -1;
-    if (w2tile) {
-      const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
-      const int i = i0 + 16 * (blk >> 1) + 4 * (ln >> 4) + rg, j = j0 + 16 * (blk & 1) + (ln & 15);
-      if (i < H2 && j < H1) pidx[e] = (int)(pbase + co.w2 + (int64_t)i * H1 + j);
-    }
+    const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
+    const int i = i0 + 16 * (blk >> 1) + 4 * (ln >> 4) + rg, j = j0 + 16 * (blk & 1) + (ln & 15);
+    pidx[e] = (w2tile && i < H2 && j < H1) ? (int)(pbase + co.w2 + (int64_t)i * H1 + j) : -1;
     ain[e] = adam_load(a.adam, pidx[e], polyak);
   }
-  // (c) fc1 block: the critic inputs of every row into LDS
+  // (c) first-column tiles: this thread's column of h2 and [h2 > 0] over its 32 rows
+  //     (thread: column i0 + tid % 32, rows [32 p, 32 p + 32) of part p = tid / 32)
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int NV = 16 * sizeof(typename K::T) / 16;  // 16-byte loads per 16 rows of h2
+  u32x4 fmb[2], fhv[2][NV];
+  {
+    const int ci = tid & 31, p = tid >> 5, i = i0 + ci;
+    const __amdgpu_buffer_rsrc_t rh2 = rlmd_rsrc(a.hp2[g], (int64_t)nrb * H2p * 16 * sizeof(typename K::T));
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb) {
+      const int r0 = 32 * p + 16 * hb;
+      const bool ok = first_col && r0 < nrb * 16;
+      const int64_t ix = rp_idx(r0, H2p, i);
+      fmb[hb] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rm2, ok ? (int)ix : 0x7fffffff, 0, 0));
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        fhv[hb][v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                   rh2, ok ? (int)(ix * sizeof(typename K::T) + 16 * v) : 0x7fffffff,
+                                                   0, 0));
+    }
+  }
+  // (d) fc1 blocks: the critic inputs of this thread's 8 LDS slots and U1 of its
+  //     column over its 32 rows
   float* xs = reinterpret_cast<float*>(smem + ULds::xs);
-  if (!w2tile) {
+  float xv[8];
+  f32x4 u1v[8];
+  {
     const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.x, (int64_t)B * X * 4);
-    for (int e = tid; e < 512 * 8; e += NT) {
-      const int r = e >> 3, c = e & 7;
-      xs[e] = rlmd_ldf(rx, (int64_t)r * X + c, r < B && c < X);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + q * NT, r = e >> 3, c = e & 7;
+      xv[q] = rlmd_ldf(rx, (int64_t)r * X + c, !w2tile && r < B && c < X);
+    }
+    const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
+    const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.u1[g], (int64_t)nrb * H1p * 16 * 4);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = 32 * p + 4 * q;
+      u1v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             ru, (!w2tile && r < nrb * 16 && j < H1p) ? (int)(rp_idx(r, H1p, j) * 4)
+                                                                                        : 0x7fffffff, 0, 0));
     }
   }
 
+  RLMD_TSU(1);
   // ---- the loss gradient of every row (critic g): critic_row_loss, top-k by
   //      rank among all B keys (critic_loss.py:438-453)
   {
     float* red = reinterpret_cast<float*>(smem + ULds::red);
     CriticRow o;
     critic_row_loss(a.loss, red, o, cl);
+    RLMD_TSU(2);
     const int kk = B > a.loss.k ? a.loss.k : B;
     bool sel = o.in;
     if (B > a.loss.k) {
@@ -207,6 +264,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     if (blockIdx.x == 0 && tid == 0) adam_scalar_step(a.adam);  // learn_step_cntr (no temperature here)
   }
   __syncthreads();
+  RLMD_TSU(3);
 
   if (w2tile) {
     // ---- dW2[i0.., j0..] = sum_b dh2[b, i] h1[b, j] over this wave's rows
@@ -235,44 +293,35 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       for (int v = 0; v < 2; ++v)
         *reinterpret_cast<f32x4*>(part + ((wave * 4 + h * 2 + v) * 64 + lane) * 4) = acc[h][v];
     __syncthreads();
+    RLMD_TSU(4);
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int el = tid * 2 + e;
       float gs = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) gs += part[w * 1024 + el];
-      if (pidx[e] >= 0) adam_apply(a.adam, pidx[e], gs, ain[e], polyak);
+      if (pidx[e] >= 0) step(pidx[e], gs, ain[e]);
     }
+    RLMD_TSU(5);
     if (first_col) {
       // ---- db2[i] = w3[i] sum_b dq[b] [h2 > 0], dW3[i] = sum_b dq[b] h2[b, i]
       //      (thread: column i0 + tid % 32, rows [32 p, 32 p + 32) of part p = tid / 32)
       __syncthreads();  // part reused
-      const int ci = tid & 31, p = tid >> 5, i = i0 + ci;
-      const __amdgpu_buffer_rsrc_t rh2 = rlmd_rsrc(a.hp2[g], (int64_t)nrb * H2p * 16 * sizeof(typename K::T));
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const int ci = tid & 31, p = tid >> 5;
       float sm = 0.f, sh = 0.f;
 #pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {  // the part's two 16-row blocks of column i
+      for (int hb = 0; hb < 2; ++hb) {  // the part's two 16-row blocks of column i (prefetched)
         const int r0 = 32 * p + 16 * hb;
-        const bool ok = r0 < nrb * 16;
-        const int64_t ix = rp_idx(r0, H2p, i);
-        const u32x4 mb = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rm2, ok ? (int)ix : 0x7fffffff, 0, 0));
-        constexpr int NV = 16 * sizeof(typename K::T) / 16;  // 16-byte loads per 16 rows of h2
-        u32x4 hv[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v)
-          hv[v] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                rh2, ok ? (int)(ix * sizeof(typename K::T) + 16 * v) : 0x7fffffff, 0, 0));
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const float q = dqs[r0 + e];
-          const uint32_t byte = (mb[e >> 2] >> (8 * (e & 3))) & 0xffu;
+          const uint32_t byte = (fmb[hb][e >> 2] >> (8 * (e & 3))) & 0xffu;
           float h;
           if constexpr (PREC == RLMD_BF16) {
-            const uint32_t w = hv[e >> 3][(e >> 1) & 3];
+            const uint32_t w = fhv[hb][e >> 3][(e >> 1) & 3];
             h = __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
           } else {
-            h = __uint_as_float(hv[e >> 2][e & 3]);
+            h = __uint_as_float(fhv[hb][e >> 2][e & 3]);
           }
           sm += byte ? q : 0.f;
           sh = fmaf(q, h, sh);
@@ -288,7 +337,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
         if (c < H2) {
           const int pi = (int)(pbase + (tid < 32 ? co.b2 + c : co.w3 + c));
           const float gv = tid < 32 ? v * rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), c, true) : v;
-          adam_apply(a.adam, pi, gv, adam_load(a.adam, pi, polyak), polyak);
+          step(pi, gv, adam_load(a.adam, pi, polyak));
         }
       }
       if (t == 0) {  // db3 = sum_b dq[b]
@@ -297,23 +346,19 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
         block_allreduce<1, 0>(s3, mx, reinterpret_cast<float*>(smem + ULds::red));
         if (tid == 0) {
           const int pi = (int)(pbase + co.b3);
-          adam_apply(a.adam, pi, s3[0], adam_load(a.adam, pi, polyak), polyak);
+          step(pi, s3[0], adam_load(a.adam, pi, polyak));
         }
       }
+      RLMD_TSU(6);
     }
   } else {
     // ---- dW1[j, x] = sum_b dq[b] U1[b, j] x[b, x], db1[j] = sum_b dq[b] U1[b, j]
     //      (thread: fc1 row j0 + tid % 32, rows [32 p, 32 p + 32) of part p)
-    const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
-    const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.u1[g], (int64_t)nrb * H1p * 16 * 4);
-    f32x4 u[8];
+    const int cj = tid & 31, p = tid >> 5;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int r = 32 * p + 4 * q;
-      u[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                           ru, (r < nrb * 16 && j < H1p) ? (int)(rp_idx(r, H1p, j) * 4) : 0x7fffffff,
-                                           0, 0));
-    }
+    for (int q = 0; q < 8; ++q) xs[tid + q * NT] = xv[q];
+    __syncthreads();
+    const f32x4* u = u1v;
     float acc[9];
 #pragma unroll
     for (int c = 0; c < 9; ++c) acc[c] = 0.f;
@@ -327,6 +372,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc[c] = fmaf(du, xs[r * 8 + c], acc[c]);
       }
+    RLMD_TSU(4);
     __syncthreads();  // xs / part
 #pragma unroll
     for (int c = 0; c < 9; ++c) part[(p * 9 + c) * 32 + cj] = acc[c];
@@ -340,7 +386,437 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
         const int jr = j0 + jj;
         if (jr < H1) {
           const int pi = (int)(pbase + (c == 8 ? co.b1 + jr : co.w1 + (int64_t)jr * X + c));
-          adam_apply(a.adam, pi, v, adam_load(a.adam, pi, polyak), polyak);
+          step(pi, v, adam_load(a.adam, pi, polyak));
+        }
+      }
+    }
+    RLMD_TSU(5);
+  }
+  RLMD_TSU(7);
+}
+
+// ---------------------------------------------------------------------------
+// The actor (+ temperature) step in one launch (algos/algo_sac.py:524-595,
+// algo_td3.py:503-531).  Every workgroup ranks all B rows' actor objective
+// v = min(q1, q2) - alpha log pi (SAC, descending) / q1 (TD3, ascending) itself
+// (Q5), forms dL/da = sum_c dL/dq_c dq_c/da with the critics' input gradients
+// that qeval_rows produced, back-propagates through the policy's sampling and
+// heads per row (gh = dL/d[mu, log_scale] or dL/d pre-tanh), and then, like the
+// critic step: fc2.weight tiles with dh2 = [h2 > 0] * (gh . W_head), fc1 blocks
+// with dh1 = sum_h gh[., h] U_h (the forward's per-head backward bases), the
+// heads on the first tile column, Adam + Polyak + copies of what it owns.  One
+// extra workgroup computes this update's critic statistics.  The last workgroup
+// to finish reading log_alpha (an arrival counter) steps the temperature.
+// ---------------------------------------------------------------------------
+constexpr int kHM = 4;  // heads per row held in LDS (2 A; the fused actor step takes A <= 2)
+constexpr int kAM = 2;  // actions
+
+struct ALds {
+  static constexpr int gh = 0;                      // f32 [512][kHM] head gradients per row
+  static constexpr int runs = gh + 512 * kHM * 4;   // u64 [512]
+  static constexpr int rank = runs + 512 * 8;       // int [3 * 512] (critic statistics: 3 ranks)
+  static constexpr int red = rank + 3 * 512 * 4;    // 16 * 9 floats
+  static constexpr int part = red + 16 * 9 * 4;     // f32 [8][4][256]
+  static constexpr int xs = part + 8 * 4 * 256 * 4; // f32 [512][8] states
+  static constexpr int flag = xs + 512 * 8 * 4;     // int: this workgroup arrived last
+  static constexpr int total = flag + 16;
+};
+
+template <int PREC>
+__global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
+  using K = KT<PREC>;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* ghs = reinterpret_cast<float*>(smem + ALds::gh);
+  float* part = reinterpret_cast<float*>(smem + ALds::part);
+  float* red = reinterpret_cast<float*>(smem + ALds::red);
+  int* lastf = reinterpret_cast<int*>(smem + ALds::flag);
+  const RowDims& d = a.d;
+  const NetOff& ao = a.ao;
+  const int B = d.B, H1 = d.H1, H2 = d.H2, H1p = d.H1p, H2p = d.H2p, S = d.S, A = d.A;
+  const bool sac = d.algo == RLMD_SAC;
+  const int nh = sac ? 2 * A : A;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nrb = (B + 15) / 16;
+  const int t = blockIdx.x;
+  const int nwg = a.n_w2 + a.n_w1 + (a.cstats.B > 0 ? 1 : 0);
+  LearnState* st = a.st;
+  // this workgroup has read log_alpha; returns true on the last one to arrive
+  auto arrive = [&]() {
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      *lastf = old == (unsigned)(nwg - 1);
+    }
+    __syncthreads();
+    return *lastf != 0;
+  };
+  const bool stats_wg = a.cstats.B > 0 && t == nwg - 1;
+  const bool w2tile = !stats_wg && t < a.n_w2, w1blk = !stats_wg && !w2tile;
+  const int i0 = w2tile ? (t / a.tj) * TW : 0, j0 = w2tile ? (t % a.tj) * TW : (t - a.n_w2) * TW;
+  const bool first_col = w2tile && (t % a.tj) == 0;
+  const bool polyak = adam_polyak(a.adam);
+  const CopyDst cd = copy_dst(a.adam, 0);
+  auto step = [&](int pi, float gv, const AdamIn& in) {
+    const int j = pi - (int)ao.w2;
+    adam_apply_dst(a.adam, pi, gv, in, polyak, (j >= 0 && j < H1 * H2) ? j : -1, cd);
+  };
+  float v = 0.f, lpv = 0.f, alpha = 0.f;
+  bool sel = false;
+  int kk = B;
+  // every workgroup has read log_alpha: the last to arrive writes the actor-loss
+  // value and steps the temperature
+  auto temperature_step = [&]() {
+    if (arrive()) {
+      float sm[2] = {sel ? v : 0.f, (tid < B && sac) ? -(lpv + a.target_entropy) : 0.f};
+      float mx[1] = {-INFINITY};
+      block_allreduce<2, 0>(sm, mx, red);
+      if (tid == 0) {
+        if (sac) st->pad_temp_grad = sm[1] / B * alpha;
+        a.stats[10] = -sm[0] / kk;
+        adam_scalar_step(a.adam);  // learn_step_cntr, temperature Adam, stats[11]
+        st->arrive = 0u;           // every workgroup has arrived: reset for the next update
+      }
+    }
+  };
+  if (stats_wg) {
+    // this update's critic statistics (rlmd_loss.h), off the critical path
+    critic_loss_block(a.cstats, reinterpret_cast<uint64_t*>(smem + ALds::runs), reinterpret_cast<int*>(smem + ALds::rank),
+                      red);
+    // the actor loss of every row, should this workgroup arrive last
+    const bool in = tid < B;
+    const int64_t nB = (int64_t)B * 4;
+    const float q1r = rlmd_ldf(rlmd_rsrc(a.qn[0], nB), tid, in);
+    const float q2r = rlmd_ldf(rlmd_rsrc(a.qn[1], a.nq > 1 ? nB : 0), tid, in);
+    lpv = rlmd_ldf(rlmd_rsrc(a.logp, sac ? nB : 0), tid, in);
+    const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
+    alpha = sac ? expf(st->log_alpha) : 0.f;
+    const float q1 = q1r + qb0, q2 = a.nq > 1 ? q2r + qb1 : q1;
+    v = sac ? fminf(q1, q2) - alpha * lpv : q1;
+    kk = a.topk ? (B < a.k ? B : a.k) : B;
+    sel = in;
+    if (a.topk) {
+      int* rank_of = reinterpret_cast<int*>(smem + ALds::rank);
+      block_rank(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
+                 reinterpret_cast<uint64_t*>(smem + ALds::runs), rank_of);
+      sel = in && rank_of[tid] < kk;
+    }
+    temperature_step();
+    return;
+  }
+  float* xs = reinterpret_cast<float*>(smem + ALds::xs);
+  // ---- first load round, branch-free (predicated on the workgroup's role through
+  //      the range checks, as in critic_update_kernel): the row's loss inputs, the
+  //      tile operands, Adam state, the fc1 block's states and first two bases
+  const bool in = tid < B;
+  const int64_t nB = (int64_t)B * 4;
+  const float q1r = rlmd_ldf(rlmd_rsrc(a.qn[0], nB), tid, in);
+  const float q2r = rlmd_ldf(rlmd_rsrc(a.qn[1], a.nq > 1 ? nB : 0), tid, in);
+  lpv = rlmd_ldf(rlmd_rsrc(a.logp, sac ? nB : 0), tid, in);
+  float dqda[2][kAM], sv[5][kAM];
+  {
+    const bool rin = in && !stats_wg;
+    const __amdgpu_buffer_rsrc_t r0 = rlmd_rsrc(a.dqda[0], nB * A), r1 = rlmd_rsrc(a.dqda[1], a.nq > 1 ? nB * A : 0),
+                                 rs = rlmd_rsrc(a.save, nB * 5 * A);
+#pragma unroll
+    for (int j = 0; j < kAM; ++j) {
+      dqda[0][j] = rlmd_ldf(r0, (int64_t)tid * A + j, rin && j < A);
+      dqda[1][j] = rlmd_ldf(r1, (int64_t)tid * A + j, rin && j < A);
+#pragma unroll
+      for (int q = 0; q < 5; ++q) sv[q][j] = rlmd_ldf(rs, (int64_t)tid * 5 * A + q * A + j, rin && j < A);
+    }
+  }
+  constexpr int NKS = 64 / K::KS;
+  uint32_t mw[NKS][2][2];
+  typename K::Frag bf[NKS][2];
+  float wh[2][kHM];
+  int pidx[2];
+  AdamIn ain[2];
+  const __amdgpu_buffer_rsrc_t rm2 = rlmd_rsrc(a.am2, (int64_t)nrb * H2p * 16),
+                               rh1 = rlmd_rsrc(a.hp1a, (int64_t)nrb * H1p * 16 * sizeof(typename K::T));
+  const __amdgpu_buffer_rsrc_t rw = rlmd_rsrc(a.wheads, (int64_t)nh * H2 * 4);
+#pragma unroll
+  for (int s = 0; s < NKS; ++s) {
+    const int row = 64 * wave + s * K::KS + K::RPL * (lane >> 4);
+    const bool rok = w2tile && row < nrb * 16;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = i0 + 16 * h + (lane & 15), j = j0 + 16 * h + (lane & 15);
+      K::load_mask(rm2, rp_idx(row, H2p, i), rok && i < H2p, mw[s][h]);
+      bf[s][h] = K::load_b(rh1, rp_idx(row, H1p, j), rok && j < H1p);
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = i0 + 16 * h + (lane & 15);
+#pragma unroll
+    for (int q = 0; q < kHM; ++q) wh[h][q] = rlmd_ldf(rw, (int64_t)q * H2 + i, w2tile && q < nh && i < H2);
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
+    const int i = i0 + 16 * (blk >> 1) + 4 * (ln >> 4) + rg, j = j0 + 16 * (blk & 1) + (ln & 15);
+    pidx[e] = (w2tile && i < H2 && j < H1) ? (int)(ao.w2 + (int64_t)i * H1 + j) : -1;
+    ain[e] = adam_load(a.adam, pidx[e], polyak);
+  }
+  float xv[8];
+  constexpr int kUP = 2;  // bases prefetched per fc1-block thread (the rest load in the loop)
+  f32x4 uv[kUP][8];
+  const int64_t ustride = (int64_t)nrb * H1p * 16;
+  const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * 4);
+  {
+    const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
+    const float log_alpha = sac ? st->log_alpha : 0.f;
+
+    // ---- actor loss over all rows (algo_sac.py:546-562 / algo_td3.py:507-523)
+    alpha = sac ? expf(log_alpha) : 0.f;
+    const float q1 = q1r + qb0, q2 = a.nq > 1 ? q2r + qb1 : q1;
+    v = sac ? fminf(q1, q2) - alpha * lpv : q1;
+    kk = a.topk ? (B < a.k ? B : a.k) : B;
+    sel = in;
+    if (a.topk) {
+      int* rank_of = reinterpret_cast<int*>(smem + ALds::rank);
+      block_rank(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
+                 reinterpret_cast<uint64_t*>(smem + ALds::runs), rank_of);
+      sel = in && rank_of[tid] < kk;
+    }
+    // the fc1 block operands: issued here, after the ranking, to bound register use
+    {
+      const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.s, (int64_t)B * S * 4);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int e = tid + q * NT, r = e >> 3, c = e & 7;
+        xv[q] = rlmd_ldf(rx, (int64_t)r * S + c, w1blk && r < B && c < S);
+      }
+      const int j = j0 + (tid & 31), p = tid >> 5;
+#pragma unroll
+      for (int h = 0; h < kUP; ++h)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int r = 32 * p + 4 * q;
+          const bool ok = w1blk && h < nh && r < nrb * 16 && j < H1p;
+          uv[h][q] = __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
+                                                           0, 0));
+        }
+    }
+    // ---- dL/da per row, then through the sampling and the heads (rlmd_policy.h)
+    const float dv = sel ? -1.f / (float)kk : 0.f;
+    float dq0 = dv, dq1 = 0.f, dlp = 0.f;
+    if (sac) {
+      const float g1 = q1 < q2 ? 1.f : (q1 > q2 ? 0.f : 0.5f);  // torch.minimum backward splits ties
+      dq0 = dv * g1;
+      dq1 = dv * (1.f - g1);
+      dlp = -alpha * dv;
+    }
+    float gh[kHM];
+#pragma unroll
+    for (int q = 0; q < kHM; ++q) gh[q] = 0.f;
+#pragma unroll
+    for (int j = 0; j < kAM; ++j) {
+      if (j < A && in) {
+        const float da = dq0 * dqda[0][j] + dq1 * dqda[1][j];
+        if (sac) {
+          float dmu, dls;
+          policy_comp_bwd(a.smp.dist, sv[0][j], sv[1][j], sv[2][j], sv[3][j], sv[4][j], da, dlp, a.smp.max_action,
+                          a.smp.reparam_noise, a.smp.ls_min, a.smp.ls_max, dmu, dls);
+          gh[j] = dmu;
+          gh[A + j] = dls;
+        } else {
+          const float th = tanhf(sv[0][j]);
+          gh[j] = da * a.smp.max_action * (1.f - th * th);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < kHM; ++q) ghs[tid * kHM + q] = gh[q];
+  }
+  temperature_step();
+
+  if (w2tile) {
+    // ---- dW2 = sum_b dh2[b, i] h1[b, j], dh2 = [h2 > 0] (sum_h gh[b, h] W_head[h, i])
+    f32x4 acc[2][2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) acc[h][u] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < NKS; ++s) {
+      const int row = 64 * wave + s * K::KS + K::RPL * (lane >> 4);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float dh[K::RPL];
+#pragma unroll
+        for (int e = 0; e < K::RPL; ++e) {
+          const float* gr = ghs + ((row + e) & 511) * kHM;
+          float acc_h = 0.f;  // the launch-chain order: mu_j then log_scale_j per action j
+#pragma unroll
+          for (int j = 0; j < kAM; ++j) {
+            if (j < A) {
+              acc_h = fmaf(gr[j], wh[h][j], acc_h);
+              if (sac) acc_h = fmaf(gr[A + j], wh[h][A + j], acc_h);
+            }
+          }
+          dh[e] = acc_h;
+        }
+        const typename K::Frag af = K::form_a(mw[s][h], dh, 1.f);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) K::mfma(af, bf[s][u], acc[h][u]);
+      }
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        *reinterpret_cast<f32x4*>(part + ((wave * 4 + h * 2 + u) * 64 + lane) * 4) = acc[h][u];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int el = tid * 2 + e;
+      float gs = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) gs += part[w * 1024 + el];
+      if (pidx[e] >= 0) step(pidx[e], gs, ain[e]);
+    }
+    if (first_col) {
+      // ---- db2[i] = sum_b dh2[b, i]; the heads dW_head[h, i] = sum_b gh[b, h] h2[b, i]
+      __syncthreads();
+      const int ci = tid & 31, p = tid >> 5, i = i0 + ci;
+      const __amdgpu_buffer_rsrc_t rh2 = rlmd_rsrc(a.hp2a, (int64_t)nrb * H2p * 16 * sizeof(typename K::T));
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      float whc[kHM];
+#pragma unroll
+      for (int q = 0; q < kHM; ++q)
+        whc[q] = rlmd_ldf(rlmd_rsrc(a.wheads, (int64_t)nh * H2 * 4), (int64_t)q * H2 + i, q < nh && i < H2);
+      float sb = 0.f, sw[kHM];
+#pragma unroll
+      for (int q = 0; q < kHM; ++q) sw[q] = 0.f;
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        const int r0 = 32 * p + 16 * hb;
+        const bool ok = r0 < nrb * 16;
+        const int64_t ix = rp_idx(r0, H2p, i);
+        const u32x4 mb =
+            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rm2, ok ? (int)ix : 0x7fffffff, 0, 0));
+        constexpr int NV = 16 * sizeof(typename K::T) / 16;
+        u32x4 hv[NV];
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+          hv[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rh2, ok ? (int)(ix * sizeof(typename K::T) + 16 * q) : 0x7fffffff, 0, 0));
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          const float* gr = ghs + (r0 + e) * kHM;
+          const uint32_t byte = (mb[e >> 2] >> (8 * (e & 3))) & 0xffu;
+          float hval;
+          if constexpr (PREC == RLMD_BF16) {
+            const uint32_t w = hv[e >> 3][(e >> 1) & 3];
+            hval = __uint_as_float((e & 1) ? (w & 0xffff0000u) : (w << 16));
+          } else {
+            hval = __uint_as_float(hv[e >> 2][e & 3]);
+          }
+          float acc_h = 0.f;
+#pragma unroll
+          for (int j = 0; j < kAM; ++j) {
+            if (j < A) {
+              acc_h = fmaf(gr[j], whc[j], acc_h);
+              if (sac) acc_h = fmaf(gr[A + j], whc[A + j], acc_h);
+            }
+          }
+          sb += byte ? acc_h : 0.f;
+#pragma unroll
+          for (int q = 0; q < kHM; ++q) sw[q] = fmaf(gr[q], hval, sw[q]);
+        }
+      }
+      part[p * 9 * 32 + ci] = sb;
+#pragma unroll
+      for (int q = 0; q < kHM; ++q) part[(p * 9 + 1 + q) * 32 + ci] = sw[q];
+      __syncthreads();
+      for (int o = tid; o < 9 * 32; o += NT) {
+        const int c = o / 32, ii = i0 + (o & 31);
+        if (c <= nh && ii < H2) {
+          float vsum = 0.f;
+          for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + (o & 31)];
+          int pi;
+          if (c == 0) pi = (int)(ao.b2 + ii);
+          else if (c - 1 < A) pi = (int)(ao.w3 + (int64_t)(c - 1) * H2 + ii);
+          else pi = (int)(ao.w4 + (int64_t)(c - 1 - A) * H2 + ii);
+          step(pi, vsum, adam_load(a.adam, pi, polyak));
+        }
+      }
+      if (t == 0) {  // the heads' biases: sum_b gh[b, h]
+        __syncthreads();
+        float sg[kHM];
+#pragma unroll
+        for (int q = 0; q < kHM; ++q) sg[q] = ghs[tid * kHM + q];
+        float mx[1] = {-INFINITY};
+        block_allreduce<kHM, 0>(sg, mx, red);
+        if (tid < nh) {
+          float gvb = 0.f;
+#pragma unroll
+          for (int q = 0; q < kHM; ++q) gvb = tid == q ? sg[q] : gvb;
+          const int pi = (int)(tid < A ? ao.b3 + tid : ao.b4 + (tid - A));
+          step(pi, gvb, adam_load(a.adam, pi, polyak));
+        }
+      }
+    }
+  } else {
+    // ---- dW1[j, x] = sum_b dh1[b, j] s[b, x], db1[j]; dh1 = sum_h gh[b, h] U_h[b, j]
+    const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) xs[tid + q * NT] = xv[q];
+    __syncthreads();
+    // dh1 of the thread's 32 rows: heads in order, the first from registers
+    f32x4 du[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int r = 32 * p + 4 * q;
+      du[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int h = 0; h < kUP; ++h)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(r + e) * kHM + h], uv[h][q][e], du[q][e]);
+    }
+    for (int h = kUP; h < nh; ++h) {
+      f32x4 u[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = 32 * p + 4 * q;
+        const bool ok = r < nrb * 16 && j < H1p;
+        u[q] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
+                                                         0, 0));
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(32 * p + 4 * q + e) * kHM + h], u[q][e], du[q][e]);
+    }
+    float acc[9];
+#pragma unroll
+    for (int c = 0; c < 9; ++c) acc[c] = 0.f;
+#pragma unroll 2
+    for (int q = 0; q < 8; ++q) {
+      const int r = 32 * p + 4 * q;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[8] += du[q][e];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) acc[c] = fmaf(du[q][e], xs[(r + e) * 8 + c], acc[c]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 9; ++c) part[(p * 9 + c) * 32 + cj] = acc[c];
+    __syncthreads();
+    for (int o = tid; o < 32 * 9; o += NT) {
+      const int jj = o % 32, c = o / 32;
+      if (c < S || c == 8) {
+        float vsum = 0.f;
+        for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + jj];
+        const int jr = j0 + jj;
+        if (jr < H1) {
+          const int pi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
+          step(pi, vsum, adam_load(a.adam, pi, polyak));
         }
       }
     }
@@ -349,7 +825,29 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 
 }  // namespace
 
+#ifdef RLMD_TIMING
+extern "C" int rlmd_debug_ts_upd(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_upd), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : 2;
+}
+#endif
+
 size_t critic_update_lds() { return (size_t)ULds::total; }
+
+int actor_update_launch(const ActUpdArgs& a, hipStream_t st) {
+  const RowDims& d = a.d;
+  RLMD_CHECK(d.B <= NT && d.S <= 8 && d.A <= kAM, "actor update: B <= 512, state width <= 8, actions <= 2");
+  RLMD_CHECK(a.tj == d.H1p / TW && a.ti * TW >= d.H2p && a.n_w2 == a.ti * a.tj && a.n_w1 == d.H1p / TW,
+             "actor update: tile grid inconsistent with the widths");
+  RLMD_CHECK(a.cstats.B <= NT, "critic statistics workgroup: mini-batch up to 512 rows");
+  const dim3 grid(a.n_w2 + a.n_w1 + (a.cstats.B > 0 ? 1 : 0));
+  if (d.prec == RLMD_BF16)
+    hipLaunchKernelGGL(actor_update_kernel<RLMD_BF16>, grid, dim3(NT), ALds::total, st, a);
+  else
+    hipLaunchKernelGGL(actor_update_kernel<RLMD_FP32>, grid, dim3(NT), ALds::total, st, a);
+  RLMD_LAUNCH_CHECK();
+  return 0;
+}
 
 int critic_update_launch(const CritUpdArgs& a, hipStream_t st) {
   const RowDims& d = a.d;

@@ -21,7 +21,7 @@ def build():
 
     b.build()
     os.makedirs(OUT, exist_ok=True)
-    timed = ("learn.hip", "rows.hip", "act.hip", "env.hip")
+    timed = ("learn.hip", "rows.hip", "act.hip", "env.hip", "update.hip")
     tobjs = []
     for src in timed:
         obj = os.path.join(OUT, src.replace(".hip", "_ts.o"))
@@ -78,6 +78,12 @@ def run():
     seq("fwd_rows critic job 2", [60, 61, 63, 64, 65, 66, 67, 62])
     seq("abwd_rows", [96, 95, 97, 98, 99, 100, 101, 103, 104, 105, 108, 109, 106, 107, 110, 111])
     seq("cbwd_rows (0, 0, 0)", [112, 113, 114, 115, 116, 117, 118])
+    seq("fwd_rows actor job 4", [80, 81, 87, 88, 89, 90, 91, 82, 83])
+    t0 = r[:, 40:45].min(axis=1)
+    print("fwd_rows job windows, block x = 0 (us from the first job start):")
+    for y in range(5):
+        s0, s1 = np.median(r[:, 40 + y] - t0) / 100, np.median(r[:, 45 + y] - t0) / 100
+        print(f"  job {y}: {s0:7.2f} .. {s1:7.2f}  ({s1 - s0:6.2f} us)")
 
 
 def run_act():
@@ -190,5 +196,44 @@ def run_mkt():
     print("  ", np.median(ph, 0), "total", np.median(np.sum(ph, 1)))
 
 
+def run_upd():
+    """critic_update_kernel (C2, K = 1 per step): thread-0 stamps of tile (0, 0),
+    tile (0, 1) and the first fc1 block, median cycles between stamps over 30 steps."""
+    import numpy as np
+    import torch
+
+    from rlmd_amd import _abi
+
+    _abi._LIB = _abi.load(LIB)
+    lib = _abi._LIB
+    lib.rlmd_debug_ts_upd.restype = C.c_int
+    lib.rlmd_debug_ts_upd.argtypes = [C.POINTER(C.c_ulonglong)]
+    from rlmd_amd.trainer import VecTrainer
+
+    algo = sys.argv[2] if len(sys.argv) > 2 else "SAC"
+    env, inv = ("gbm", "A") if algo == "SAC" else ("dice_sh", "A")
+    tr = VecTrainer(env, inv, 65536, algo=algo, precision="bf16", warmup_steps=0, smoothing_window=0,
+                    replay_capacity=1 << 20, k_updates=1, device="cuda:0")
+    buf = (C.c_ulonglong * 64)()
+    rows = []
+    for it in range(40):
+        tr.step()
+        torch.cuda.synchronize()
+        lib.rlmd_debug_ts_upd(buf)
+        if it >= 10:
+            rows.append(np.array(buf[:], dtype=np.int64).reshape(4, 16))
+    r = np.stack(rows)
+    names = ["entry", "loads issued", "row loss", "rank + dq", "mfma / fc1 sums", "adam", "first-col extras", "end"]
+    for slot, label in enumerate(["tile (0,0)", "tile (0,1)", "fc1 block 0"]):
+        t = r[:, slot]
+        print(f"{label}: total {np.median(t[:, 7] - t[:, 0]):.0f} cycles")
+        prev = 0
+        for i in range(1, 8):
+            if np.all(t[:, i] == 0):
+                continue
+            print(f"  {names[prev]:>16s} -> {names[i]:<16s} {np.median(t[:, i] - t[:, prev]):8.0f}")
+            prev = i
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run, "act": run_act, "env": run_env, "mkt": run_mkt}[sys.argv[1]]()
+    {"build": build, "run": run, "act": run_act, "env": run_env, "mkt": run_mkt, "upd": run_upd}[sys.argv[1]]()
