@@ -127,7 +127,7 @@ __global__ void __launch_bounds__(NTH) critic_loss_kernel(LossArgs a) {
   __shared__ __attribute__((aligned(16))) uint64_t runs[NTH];
   __shared__ int rank_of[3][NTH];
   __shared__ float red[16 * 9];
-  critic_loss_block(a, runs, &rank_of[0][0], red);
+  critic_loss_block<NTH / 64>(a, runs, &rank_of[0][0], red);
 }
 
 // ---------------------------------------------------------------------------
@@ -167,7 +167,7 @@ __global__ void __launch_bounds__(NTH) actor_loss_kernel(ActorLossArgs a) {
   if (a.topk) {
     // SAC sorts descending, TD3 ascending
     const uint64_t key = in ? ((uint64_t)(a.algo == RLMD_SAC ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)b : ~0ull;
-    block_rank(key, runs, rank_of);
+    block_rank<NTH / 64>(key, runs, rank_of);
     sel = in && rank_of[b] < k;
   }
   float sm[2] = {sel ? v : 0.f, in ? -(lp + a.target_entropy) : 0.f};

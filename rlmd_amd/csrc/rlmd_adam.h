@@ -93,10 +93,10 @@ __device__ __forceinline__ CopyDst copy_dst(const AdamArgs& a, int net) {
   return net == 0 ? CopyDst{a.wc[0], a.wt[0], a.twc[0], a.twt[0]} : CopyDst{a.wc[1], a.wt[1], a.twc[1], a.twt[1]};
 }
 
-// One parameter: Adam with gradient g, then Polyak and the compute copies.
-// jw2: the element's index inside its net's fc2.weight (-1: not fc2.weight).
-__device__ __forceinline__ void adam_apply_dst(const AdamArgs& a, int i, float g, const AdamIn& in, bool polyak,
-                                               int jw2, const CopyDst& cd) {
+// One parameter: Adam with gradient g, then Polyak; the new value and target
+// value returned (the caller writes the compute copies).
+__device__ __forceinline__ void adam_core(const AdamArgs& a, int i, float g, const AdamIn& in, bool polyak, float& p,
+                                          float& tv) {
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
   float m = in.m, v = in.v;
   m = m + (1.f - b1) * (g - m);
@@ -104,13 +104,21 @@ __device__ __forceinline__ void adam_apply_dst(const AdamArgs& a, int i, float g
   a.m[i] = m;
   a.v[i] = v;
   const float denom = sqrtf(v) / a.bc2_sqrt + eps;
-  const float p = in.p - a.step_size * (m / denom);
+  p = in.p - a.step_size * (m / denom);
   a.p[i] = p;
-  float tv = 0.f;
+  tv = 0.f;
   if (polyak) {
     tv = a.tau * p + (1.f - a.tau) * in.t;
     a.target[i] = tv;
   }
+}
+
+// One parameter: Adam with gradient g, then Polyak and the compute copies.
+// jw2: the element's index inside its net's fc2.weight (-1: not fc2.weight).
+__device__ __forceinline__ void adam_apply_dst(const AdamArgs& a, int i, float g, const AdamIn& in, bool polyak,
+                                               int jw2, const CopyDst& cd) {
+  float p, tv;
+  adam_core(a, i, g, in, polyak, p, tv);
   if (jw2 >= 0) {
     const int n = jw2 / a.H1, k = jw2 - n * a.H1;
     const int64_t ic = frag_index(n, k, a.H1p, a.bf16), it = frag_index(k, n, a.H2p, a.bf16);

@@ -84,28 +84,35 @@ __device__ __forceinline__ uint64_t wave_sort64(uint64_t key) {
 // Ranks of distinct 64-bit keys across the block (ascending; key ~0 = absent):
 // each wave sorts its 64 keys in registers, parks the sorted run in LDS, and the
 // key at lane l of run w gets rank l + sum over the other runs of a binary
-// search (6 probes over the first 63 entries + the last entry).  The rank is scattered to out[key & 0xffffffff] (the caller's
-// index in the low word) and read back by the key's owner after the barrier.
-// runs: LDS [blockDim.x] uint64; out: LDS int [blockDim.x].
+// search (6 probes over the first 63 entries + the last entry).  The searches
+// over the other runs are independent: each probe step reads all of them at
+// once, so the dependent LDS chain is 6 probes long, not 6 per run.  The rank is
+// scattered to out[key & 0xffffffff] (the caller's index in the low word) and
+// read back by the key's owner after the barrier.
+// runs: LDS [blockDim.x] uint64; out: LDS int [blockDim.x].  NW: the block's
+// waves (blockDim.x == 64 NW), a compile-time constant so that every probe is
+// an unconditional LDS read (one wait per probe step for all runs).
+template <int NW>
 __device__ __forceinline__ void block_rank(uint64_t key, uint64_t* runs, int* out) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const uint64_t sk = wave_sort64(key);
   runs[threadIdx.x] = sk;
   __syncthreads();
-  if (sk != ~0ull) {
-    int rank = l;
-    for (int v = 0; v < nw; ++v) {
-      if (v == w) continue;
-      const uint64_t* run = runs + 64 * v;
-      // 6 probes count the smaller keys among run[0..62]; run[63] separately
-      int pos = 0;
+  int pos[NW];
 #pragma unroll
-      for (int st = 32; st > 0; st >>= 1)
-        if (run[pos + st - 1] < sk) pos += st;
-      rank += pos + (run[63] < sk ? 1 : 0);
-    }
-    out[(int)(sk & 0xffffffffu)] = rank;
+  for (int v = 0; v < NW; ++v) pos[v] = 0;
+#pragma unroll
+  for (int st = 32; st > 0; st >>= 1) {
+    uint64_t probe[NW];
+#pragma unroll
+    for (int v = 0; v < NW; ++v) probe[v] = runs[64 * v + pos[v] + st - 1];
+#pragma unroll
+    for (int v = 0; v < NW; ++v) pos[v] += probe[v] < sk ? st : 0;
   }
+  int rank = l;
+#pragma unroll
+  for (int v = 0; v < NW; ++v) rank += v == w ? 0 : pos[v] + (runs[64 * v + 63] < sk ? 1 : 0);
+  if (sk != ~0ull) out[(int)(sk & 0xffffffffu)] = rank;
   __syncthreads();
 }
 

@@ -171,6 +171,8 @@ __device__ __forceinline__ uint64_t critic_sel_key(const CriticRow& o) {
 // The whole critic loss in one workgroup.  runs: LDS uint64 [blockDim.x];
 // rank_of: LDS int [3 * blockDim.x]; red: LDS float [16 * 9].  dq written when
 // a.dq[0] is set.
+// MAXW: the block's waves at most (block_rank)
+template <int MAXW = 16>
 __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* runs, int* rank_of, float* red) {
   const int b = threadIdx.x, B = a.B, nth = blockDim.x;
   CriticRow o;
@@ -182,7 +184,7 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
   bool sel = in;
   int rank = b;
   if (B > a.k) {
-    block_rank(critic_sel_key(o), runs, rank_of);
+    block_rank<MAXW>(critic_sel_key(o), runs, rank_of);
     rank = in ? rank_of[b] : B;
     sel = in && rank < k;
   }
@@ -194,8 +196,8 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
   // Zipf-plot tail index of the selected losses' order statistics
   // (critic_loss.py:238-266): each critic's selected losses ranked among
   // themselves, descending, ties by selection rank; that rank is the slot
-  block_rank(sel ? ((uint64_t)(~f2key(l[0])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + nth);
-  block_rank(sel ? ((uint64_t)(~f2key(l[1])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + 2 * nth);
+  block_rank<MAXW>(sel ? ((uint64_t)(~f2key(l[0])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + nth);
+  block_rank<MAXW>(sel ? ((uint64_t)(~f2key(l[1])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + 2 * nth);
   const int rz0 = sel ? rank_of[nth + rank] : 0, rz1 = sel ? rank_of[2 * nth + rank] : 0;
   const float lg0 = sel ? logf(l[0] + a.log_noise) : 0.f;
   const float lg1 = sel ? logf(l[1] + a.log_noise) : 0.f;

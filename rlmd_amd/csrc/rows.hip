@@ -73,8 +73,8 @@ struct CT<RLMD_BF16> {
   using T = unsigned short;
   using Frag = bf16x8;
   static constexpr int KS = 32;  // k covered by one 16-byte fragment per lane
-  __device__ static T cvt(float f) { return to_bf16(f); }
-  __device__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
+  __device__ __forceinline__ static T cvt(float f) { return to_bf16(f); }
+  __device__ __forceinline__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
 };
@@ -83,10 +83,10 @@ struct CT<RLMD_FP32> {
   using T = float;
   using Frag = f32x4;
   static constexpr int KS = 16;
-  __device__ static T cvt(float f) { return f; }
+  __device__ __forceinline__ static T cvt(float f) { return f; }
   // lane group q = lane >> 4 holds k = k0 + 4q + j in element j: four 16x16x4
   // MFMAs cover k0 .. k0 + 15 (a permutation of the k order, same products)
-  __device__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
+  __device__ __forceinline__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
@@ -1170,7 +1170,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const bool fused_da = A <= NHF;
   if (a.cstats.B > 0 && blockIdx.x == gridDim.x - 1) {
     // this update's critic statistics (rlmd_loss.h), off the critical path
-    critic_loss_block(a.cstats, reinterpret_cast<uint64_t*>(smem + L.runs), reinterpret_cast<int*>(smem + L.rank),
+    critic_loss_block<NT / 64>(a.cstats, reinterpret_cast<uint64_t*>(smem + L.runs), reinterpret_cast<int*>(smem + L.rank),
                       reinterpret_cast<float*>(smem + L.red));
     return;
   }
@@ -1236,7 +1236,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
     const int t = threadIdx.x;
     bool sel = t < B;
     if (a.topk) {
-      block_rank(t < B ? vkey[t] : ~0ull, runs, rank_of);
+      block_rank<NT / 64>(t < B ? vkey[t] : ~0ull, runs, rank_of);
       sel = t < B && rank_of[t] < kk;
     }
     float sm[2] = {sel ? vval[t] : 0.f, (t < B && sac) ? -(ld_lp + a.target_entropy) : 0.f};

@@ -43,12 +43,23 @@ constexpr int TW = 32;  // tile edge (fc2.weight tiles TW x TW, fc1 blocks of TW
 // experiment builds only (tools/ts_probe.py upd): thread-0 s_memtime stamps of
 // three workgroups (slot 0: tile (0, 0), 1: tile (0, 1), 2: the first fc1 block)
 __device__ unsigned long long g_ts_upd[64];
+__device__ unsigned long long g_ts_aupd[64];
 #define RLMD_TSU(i)                                                                       \
   do {                                                                                    \
-    if (threadIdx.x == 0 && ts_slot >= 0) g_ts_upd[ts_slot * 16 + (i)] = __builtin_amdgcn_s_memtime(); \
+    if (threadIdx.x == 0 && ts_slot >= 0)                                                 \
+      g_ts_upd[ts_slot * 16 + (i)] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
+  } while (0)
+// actor step: cycles (i < 14) and the constant-rate clock (i = 14, 15: entry / exit)
+#define RLMD_TSA(i)                                                                        \
+  do {                                                                                     \
+    if (threadIdx.x == 0 && ts_slot >= 0)                                                  \
+      g_ts_aupd[ts_slot * 16 + (i)] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
 #define RLMD_TSU(i) \
+  do {              \
+  } while (0)
+#define RLMD_TSA(i) \
   do {              \
   } while (0)
 #endif
@@ -57,6 +68,43 @@ __device__ unsigned long long g_ts_upd[64];
 // (NaN stays NaN; no per-element branch)
 __device__ __forceinline__ unsigned short bf16_rne(float f) {
   return __builtin_bit_cast(unsigned short, (__bf16)f);
+}
+
+// The compute copies of one stepped 32 x 32 fc2.weight tile (rows i0.., columns
+// j0..; new values in LDS, pcl[(i - i0) * 33 + (j - j0)], the Polyak targets'
+// at pcl + 32 * 33): the tile is 2 KB contiguous in each fragment-major copy
+// (frag_index: 16-row bands x KS-column steps of 64 lanes x EPF elements), so
+// the workgroup writes it as 16-byte chunks, one (copy, block, lane) per job,
+// instead of one 2- or 4-byte store per element per copy.
+template <int PREC>
+__device__ __forceinline__ void tile_copies(const float* pcl, const CopyDst& cd, bool targets, int i0, int j0, int H1p,
+                                            int H2p) {
+  constexpr bool BF = PREC == RLMD_BF16;
+  constexpr int KS = BF ? 32 : 16, EPF = KS / 4, NBLK = 2 * (32 / KS);  // blocks per tile
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const int njobs = (targets ? 4 : 2) * NBLK * 64;
+  for (int jb = threadIdx.x; jb < njobs; jb += NT) {
+    const int lane = jb & 63, blk = (jb >> 6) % NBLK, c = (jb >> 6) / NBLK;  // c: wc, wt, twc, twt
+    const bool tr = c & 1;
+    const float* src = pcl + (c >= 2 ? 32 * 33 : 0);
+    const int rb = blk % 2, st = blk / 2;                 // 16-row band, KS-column step inside the tile
+    const int row = 16 * rb + (lane & 15), col0 = st * KS + (lane >> 4) * EPF;  // tile-relative
+    float v[EPF];
+#pragma unroll
+    for (int e = 0; e < EPF; ++e) v[e] = tr ? src[(col0 + e) * 33 + row] : src[row * 33 + col0 + e];
+    // global chunk: wc (n = i0 + row, k = j0 + col), wt (k = j0 + row, n = i0 + col)
+    const int64_t at = tr ? frag_index(j0 + row, i0 + col0, H2p, BF) : frag_index(i0 + row, j0 + col0, H1p, BF);
+    void* dst = c == 0 ? cd.wc : c == 1 ? cd.wt : c == 2 ? cd.twc : cd.twt;
+    u32x4 w;
+    if constexpr (BF) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = (uint32_t)bf16_rne(v[2 * q]) | ((uint32_t)bf16_rne(v[2 * q + 1]) << 16);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) w[q] = __float_as_uint(v[q]);
+    }
+    *reinterpret_cast<u32x4*>(static_cast<unsigned char*>(dst) + at * (BF ? 2 : 4)) = w;
+  }
 }
 
 // Operand fragments of one K-step over rows: bf16 16x16x32 (8 rows per lane) or
@@ -69,20 +117,20 @@ struct KT<RLMD_BF16> {
   static constexpr int KS = 32;   // rows per K-step
   using T = unsigned short;
   using Frag = bf16x8;
-  __device__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
+  __device__ __forceinline__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
-  __device__ static Frag load_b(__amdgpu_buffer_rsrc_t r, int64_t elem, bool ok) {
+  __device__ __forceinline__ static Frag load_b(__amdgpu_buffer_rsrc_t r, int64_t elem, bool ok) {
     return __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (int)(elem * 2) : 0x7fffffff, 0, 0));
   }
   // 8 mask bytes of this lane's rows
-  __device__ static void load_mask(__amdgpu_buffer_rsrc_t r, int64_t byte, bool ok, uint32_t (&w)[2]) {
+  __device__ __forceinline__ static void load_mask(__amdgpu_buffer_rsrc_t r, int64_t byte, bool ok, uint32_t (&w)[2]) {
     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
     const u32x2 v = __builtin_bit_cast(u32x2, __builtin_amdgcn_raw_buffer_load_b64(r, ok ? (int)byte : 0x7fffffff, 0, 0));
     w[0] = v[0];
     w[1] = v[1];
   }
-  __device__ static Frag form_a(const uint32_t (&w)[2], const float* dq, float w3) {
+  __device__ __forceinline__ static Frag form_a(const uint32_t (&w)[2], const float* dq, float w3) {
     Frag f;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -98,20 +146,20 @@ struct KT<RLMD_FP32> {
   static constexpr int KS = 16;
   using T = float;
   using Frag = f32x4;
-  __device__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
+  __device__ __forceinline__ static void mfma(const Frag& a, const Frag& b, f32x4& c) {
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[0], b[0], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[1], b[1], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[2], b[2], c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[3], b[3], c, 0, 0, 0);
   }
-  __device__ static Frag load_b(__amdgpu_buffer_rsrc_t r, int64_t elem, bool ok) {
+  __device__ __forceinline__ static Frag load_b(__amdgpu_buffer_rsrc_t r, int64_t elem, bool ok) {
     return __builtin_bit_cast(Frag, __builtin_amdgcn_raw_buffer_load_b128(r, ok ? (int)(elem * 4) : 0x7fffffff, 0, 0));
   }
-  __device__ static void load_mask(__amdgpu_buffer_rsrc_t r, int64_t byte, bool ok, uint32_t (&w)[2]) {
+  __device__ __forceinline__ static void load_mask(__amdgpu_buffer_rsrc_t r, int64_t byte, bool ok, uint32_t (&w)[2]) {
     w[0] = __builtin_amdgcn_raw_buffer_load_b32(r, ok ? (int)byte : 0x7fffffff, 0, 0);
     w[1] = 0;
   }
-  __device__ static Frag form_a(const uint32_t (&w)[2], const float* dq, float w3) {
+  __device__ __forceinline__ static Frag form_a(const uint32_t (&w)[2], const float* dq, float w3) {
     Frag f;
 #pragma unroll
     for (int e = 0; e < 4; ++e) f[e] = ((w[0] >> (8 * e)) & 0xffu) ? dq[e] * w3 : 0.f;
@@ -131,7 +179,8 @@ struct ULds {
   static constexpr int red = rank + 512 * 4;    // block reductions (16 * 9 floats)
   static constexpr int part = red + 16 * 9 * 4; // f32 [8 waves][4 blocks][256] partial tiles / row partials
   static constexpr int xs = part + 8 * 4 * 256 * 4;  // f32 [512][8] critic inputs (fc1 blocks)
-  static constexpr int total = xs + 512 * 8 * 4;
+  static constexpr int pcl = xs + 512 * 8 * 4;       // f32 [2][32][33] stepped tile + targets (copies)
+  static constexpr int total = pcl + 2 * 32 * 33 * 4;
 };
 
 template <int PREC>
@@ -160,6 +209,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   };
   const int ts_slot = blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : (int)blockIdx.x == a.n_w2 ? 2 : -1;
   (void)ts_slot;
+  RLMD_TSU(14);
   RLMD_TSU(0);
 
   // ---- first load round: loss inputs, this workgroup's operands, Adam state.
@@ -222,6 +272,20 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
                                                    0, 0));
     }
   }
+  // (e) Adam state of the parameters stepped after the tile: on the first tile
+  //     column b2 / w3 (threads 0..63) and b3 (thread 64 of tile 0), on an fc1
+  //     block W1 / b1 (thread c * 32 + jj: input c < X, or c = 8 for the bias)
+  int xpi = -1;
+  {
+    const int c = i0 + (tid & 31);
+    if (first_col && tid < 64 && c < H2) xpi = (int)(pbase + (tid < 32 ? co.b2 + c : co.w3 + c));
+    if (first_col && tid == 64 && t == 0) xpi = (int)(pbase + co.b3);
+    const int jj = tid & 31, ci = tid >> 5, jr = j0 + jj;
+    if (!w2tile && tid < 32 * 9 && (ci < X || ci == 8) && jr < H1)
+      xpi = (int)(pbase + (ci == 8 ? co.b1 + jr : co.w1 + (int64_t)jr * X + ci));
+  }
+  const AdamIn xin = adam_load(a.adam, xpi, polyak);
+  const float w3c = rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), i0 + (tid & 31), first_col && tid < 32);
   // (d) fc1 blocks: the critic inputs of this thread's 8 LDS slots and U1 of its
   //     column over its 32 rows
   float* xs = reinterpret_cast<float*>(smem + ULds::xs);
@@ -257,7 +321,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     bool sel = o.in;
     if (B > a.loss.k) {
       int* rank_of = reinterpret_cast<int*>(smem + ULds::rank);
-      block_rank(critic_sel_key(o), reinterpret_cast<uint64_t*>(smem + ULds::runs), rank_of);
+      block_rank<NT / 64>(critic_sel_key(o), reinterpret_cast<uint64_t*>(smem + ULds::runs), rank_of);
       sel = o.in && rank_of[tid] < kk;
     }
     dqs[tid] = sel ? a.loss.grad_scale * (g == 0 ? o.dl[0] : o.dl[1]) / (float)kk : 0.f;
@@ -294,14 +358,21 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
         *reinterpret_cast<f32x4*>(part + ((wave * 4 + h * 2 + v) * 64 + lane) * 4) = acc[h][v];
     __syncthreads();
     RLMD_TSU(4);
+    float* pcl = reinterpret_cast<float*>(smem + ULds::pcl);
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int el = tid * 2 + e;
+      const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
+      const int ii = 16 * (blk >> 1) + 4 * (ln >> 4) + rg, jj = 16 * (blk & 1) + (ln & 15);
       float gs = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) gs += part[w * 1024 + el];
-      if (pidx[e] >= 0) step(pidx[e], gs, ain[e]);
+      float pn = 0.f, tn = 0.f;  // padding elements: zero in the copies
+      if (pidx[e] >= 0) adam_core(a.adam, pidx[e], gs, ain[e], polyak, pn, tn);
+      pcl[ii * 33 + jj] = pn;
+      pcl[32 * 33 + ii * 33 + jj] = tn;
     }
+    __syncthreads();
+    tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
     RLMD_TSU(5);
     if (first_col) {
       // ---- db2[i] = w3[i] sum_b dq[b] [h2 > 0], dW3[i] = sum_b dq[b] h2[b, i]
@@ -330,24 +401,16 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       part[p * 64 + ci] = sm;
       part[p * 64 + 32 + ci] = sh;
       __syncthreads();
-      if (tid < 64) {
+      if (tid < 64 && xpi >= 0) {
         float v = 0.f;
         for (int q = 0; q < 16; ++q) v += part[q * 64 + tid];
-        const int c = i0 + (tid & 31);
-        if (c < H2) {
-          const int pi = (int)(pbase + (tid < 32 ? co.b2 + c : co.w3 + c));
-          const float gv = tid < 32 ? v * rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), c, true) : v;
-          step(pi, gv, adam_load(a.adam, pi, polyak));
-        }
+        step(xpi, tid < 32 ? v * w3c : v, xin);
       }
-      if (t == 0) {  // db3 = sum_b dq[b]
+      if (t == 0) {  // db3 = sum_b dq[b] (thread 64)
         float s3[1] = {dqs[tid]};
         float mx[1] = {-INFINITY};
         block_allreduce<1, 0>(s3, mx, reinterpret_cast<float*>(smem + ULds::red));
-        if (tid == 0) {
-          const int pi = (int)(pbase + co.b3);
-          step(pi, s3[0], adam_load(a.adam, pi, polyak));
-        }
+        if (tid == 64) step(xpi, s3[0], xin);
       }
       RLMD_TSU(6);
     }
@@ -377,22 +440,17 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 #pragma unroll
     for (int c = 0; c < 9; ++c) part[(p * 9 + c) * 32 + cj] = acc[c];
     __syncthreads();
-    // 32 rows x (X + 1) outputs
-    for (int o = tid; o < 32 * 9; o += NT) {
-      const int jj = o % 32, c = o / 32;
-      if (c < X || c == 8) {
-        float v = 0.f;
-        for (int q = 0; q < 16; ++q) v += part[(q * 9 + c) * 32 + jj];
-        const int jr = j0 + jj;
-        if (jr < H1) {
-          const int pi = (int)(pbase + (c == 8 ? co.b1 + jr : co.w1 + (int64_t)jr * X + c));
-          step(pi, v, adam_load(a.adam, pi, polyak));
-        }
-      }
+    // 32 rows x (X + 1) outputs, thread c * 32 + jj (Adam state prefetched)
+    if (xpi >= 0) {
+      const int jj = tid & 31, c = tid >> 5;
+      float v = 0.f;
+      for (int q = 0; q < 16; ++q) v += part[(q * 9 + c) * 32 + jj];
+      step(xpi, v, xin);
     }
     RLMD_TSU(5);
   }
   RLMD_TSU(7);
+  RLMD_TSU(15);
 }
 
 // ---------------------------------------------------------------------------
@@ -419,7 +477,8 @@ struct ALds {
   static constexpr int part = red + 16 * 9 * 4;     // f32 [8][4][256]
   static constexpr int xs = part + 8 * 4 * 256 * 4; // f32 [512][8] states
   static constexpr int flag = xs + 512 * 8 * 4;     // int: this workgroup arrived last
-  static constexpr int total = flag + 16;
+  static constexpr int pcl = flag + 16;             // f32 [2][32][33] stepped tile + targets (copies)
+  static constexpr int total = pcl + 2 * 32 * 33 * 4;
 };
 
 template <int PREC>
@@ -439,6 +498,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const int nrb = (B + 15) / 16;
   const int t = blockIdx.x;
   const int nwg = a.n_w2 + a.n_w1 + (a.cstats.B > 0 ? 1 : 0);
+  const int ts_slot = t == 0 ? 0 : t == 1 ? 1 : t == a.n_w2 ? 2 : t == nwg - 1 ? 3 : -1;
+  (void)ts_slot;
+  RLMD_TSA(14);
+  RLMD_TSA(0);
   LearnState* st = a.st;
   // this workgroup has read log_alpha; returns true on the last one to arrive
   auto arrive = [&]() {
@@ -480,7 +543,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   };
   if (stats_wg) {
     // this update's critic statistics (rlmd_loss.h), off the critical path
-    critic_loss_block(a.cstats, reinterpret_cast<uint64_t*>(smem + ALds::runs), reinterpret_cast<int*>(smem + ALds::rank),
+    critic_loss_block<NT / 64>(a.cstats, reinterpret_cast<uint64_t*>(smem + ALds::runs), reinterpret_cast<int*>(smem + ALds::rank),
                       red);
     // the actor loss of every row, should this workgroup arrive last
     const bool in = tid < B;
@@ -496,14 +559,18 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     sel = in;
     if (a.topk) {
       int* rank_of = reinterpret_cast<int*>(smem + ALds::rank);
-      block_rank(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
+      block_rank<NT / 64>(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
                  reinterpret_cast<uint64_t*>(smem + ALds::runs), rank_of);
       sel = in && rank_of[tid] < kk;
     }
+    RLMD_TSA(3);
     temperature_step();
+    RLMD_TSA(4);
+    RLMD_TSA(15);
     return;
   }
   float* xs = reinterpret_cast<float*>(smem + ALds::xs);
+  RLMD_TSA(1);
   // ---- first load round, branch-free (predicated on the workgroup's role through
   //      the range checks, as in critic_update_kernel): the row's loss inputs, the
   //      tile operands, Adam state, the fc1 block's states and first two bases
@@ -558,6 +625,12 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     pidx[e] = (w2tile && i < H2 && j < H1) ? (int)(ao.w2 + (int64_t)i * H1 + j) : -1;
     ain[e] = adam_load(a.adam, pidx[e], polyak);
   }
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  constexpr int NV = 16 * sizeof(typename K::T) / 16;  // 16-byte loads per 16 rows of h2
+  u32x4 fmb[2], fhv[2][NV];
+  float whc[kHM];
+  int xpi = -1;
+  AdamIn xin;
   float xv[8];
   constexpr int kUP = 2;  // bases prefetched per fc1-block thread (the rest load in the loop)
   f32x4 uv[kUP][8];
@@ -575,10 +648,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     sel = in;
     if (a.topk) {
       int* rank_of = reinterpret_cast<int*>(smem + ALds::rank);
-      block_rank(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
+      block_rank<NT / 64>(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
                  reinterpret_cast<uint64_t*>(smem + ALds::runs), rank_of);
       sel = in && rank_of[tid] < kk;
     }
+    RLMD_TSA(2);
     // the fc1 block operands: issued here, after the ranking, to bound register use
     {
       const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.s, (int64_t)B * S * 4);
@@ -598,6 +672,37 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
               f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
                                                            0, 0));
         }
+    }
+    // the first tile column's operands: h2 / [h2 > 0] of its column over the
+    // thread's 32 rows, the heads' weights, and the Adam state of b2 / the heads'
+    // rows (thread c * 32 + ci: c = 0 b2, 1..nh head c - 1) and biases (thread
+    // 288 + h); on an fc1 block the Adam state of W1 / b1 (thread c * 32 + jj)
+    {
+      const int ci = tid & 31, p = tid >> 5, i = i0 + ci;
+      const __amdgpu_buffer_rsrc_t rh2 = rlmd_rsrc(a.hp2a, (int64_t)nrb * H2p * 16 * sizeof(typename K::T));
+#pragma unroll
+      for (int hb = 0; hb < 2; ++hb) {
+        const int r0 = 32 * p + 16 * hb;
+        const bool ok = first_col && r0 < nrb * 16;
+        const int64_t ix = rp_idx(r0, H2p, i);
+        fmb[hb] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rm2, ok ? (int)ix : 0x7fffffff, 0, 0));
+#pragma unroll
+        for (int q = 0; q < NV; ++q)
+          fhv[hb][q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                     rh2, ok ? (int)(ix * sizeof(typename K::T) + 16 * q) : 0x7fffffff,
+                                                     0, 0));
+      }
+#pragma unroll
+      for (int q = 0; q < kHM; ++q) whc[q] = rlmd_ldf(rw, (int64_t)q * H2 + i, first_col && q < nh && i < H2);
+      const int c = tid >> 5, ii = i0 + (tid & 31), jr = j0 + (tid & 31);
+      if (first_col && tid < 32 * 9 && c <= nh && ii < H2)
+        xpi = (int)(c == 0 ? ao.b2 + ii : c - 1 < A ? ao.w3 + (int64_t)(c - 1) * H2 + ii
+                                                   : ao.w4 + (int64_t)(c - 1 - A) * H2 + ii);
+      if (first_col && t == 0 && tid >= 288 && tid < 288 + nh)
+        xpi = (int)(tid - 288 < A ? ao.b3 + (tid - 288) : ao.b4 + (tid - 288 - A));
+      if (w1blk && tid < 32 * 9 && (c < S || c == 8) && jr < H1)
+        xpi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
+      xin = adam_load(a.adam, xpi, polyak);
     }
     // ---- dL/da per row, then through the sampling and the heads (rlmd_policy.h)
     const float dv = sel ? -1.f / (float)kk : 0.f;
@@ -630,7 +735,9 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
 #pragma unroll
     for (int q = 0; q < kHM; ++q) ghs[tid * kHM + q] = gh[q];
   }
+  RLMD_TSA(3);
   temperature_step();
+  RLMD_TSA(4);
 
   if (w2tile) {
     // ---- dW2 = sum_b dh2[b, i] h1[b, j], dh2 = [h2 > 0] (sum_h gh[b, h] W_head[h, i])
@@ -669,40 +776,35 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
       for (int u = 0; u < 2; ++u)
         *reinterpret_cast<f32x4*>(part + ((wave * 4 + h * 2 + u) * 64 + lane) * 4) = acc[h][u];
     __syncthreads();
+    RLMD_TSA(5);
+    float* pcl = reinterpret_cast<float*>(smem + ALds::pcl);
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
-      const int el = tid * 2 + e;
+      const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
+      const int ii = 16 * (blk >> 1) + 4 * (ln >> 4) + rg, jj = 16 * (blk & 1) + (ln & 15);
       float gs = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; ++w) gs += part[w * 1024 + el];
-      if (pidx[e] >= 0) step(pidx[e], gs, ain[e]);
+      float pn = 0.f, tn = 0.f;
+      if (pidx[e] >= 0) adam_core(a.adam, pidx[e], gs, ain[e], polyak, pn, tn);
+      pcl[ii * 33 + jj] = pn;
+      pcl[32 * 33 + ii * 33 + jj] = tn;
     }
+    __syncthreads();
+    tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
+    RLMD_TSA(6);
     if (first_col) {
       // ---- db2[i] = sum_b dh2[b, i]; the heads dW_head[h, i] = sum_b gh[b, h] h2[b, i]
       __syncthreads();
-      const int ci = tid & 31, p = tid >> 5, i = i0 + ci;
-      const __amdgpu_buffer_rsrc_t rh2 = rlmd_rsrc(a.hp2a, (int64_t)nrb * H2p * 16 * sizeof(typename K::T));
-      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-      float whc[kHM];
-#pragma unroll
-      for (int q = 0; q < kHM; ++q)
-        whc[q] = rlmd_ldf(rlmd_rsrc(a.wheads, (int64_t)nh * H2 * 4), (int64_t)q * H2 + i, q < nh && i < H2);
+      const int ci = tid & 31, p = tid >> 5;
       float sb = 0.f, sw[kHM];
 #pragma unroll
       for (int q = 0; q < kHM; ++q) sw[q] = 0.f;
 #pragma unroll
-      for (int hb = 0; hb < 2; ++hb) {
+      for (int hb = 0; hb < 2; ++hb) {  // the part's two 16-row blocks of column i (prefetched)
         const int r0 = 32 * p + 16 * hb;
-        const bool ok = r0 < nrb * 16;
-        const int64_t ix = rp_idx(r0, H2p, i);
-        const u32x4 mb =
-            __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rm2, ok ? (int)ix : 0x7fffffff, 0, 0));
-        constexpr int NV = 16 * sizeof(typename K::T) / 16;
-        u32x4 hv[NV];
-#pragma unroll
-        for (int q = 0; q < NV; ++q)
-          hv[q] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                                rh2, ok ? (int)(ix * sizeof(typename K::T) + 16 * q) : 0x7fffffff, 0, 0));
+        const u32x4& mb = fmb[hb];
+        const u32x4(&hv)[NV] = fhv[hb];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
           const float* gr = ghs + (r0 + e) * kHM;
@@ -731,17 +833,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
 #pragma unroll
       for (int q = 0; q < kHM; ++q) part[(p * 9 + 1 + q) * 32 + ci] = sw[q];
       __syncthreads();
-      for (int o = tid; o < 9 * 32; o += NT) {
-        const int c = o / 32, ii = i0 + (o & 31);
-        if (c <= nh && ii < H2) {
-          float vsum = 0.f;
-          for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + (o & 31)];
-          int pi;
-          if (c == 0) pi = (int)(ao.b2 + ii);
-          else if (c - 1 < A) pi = (int)(ao.w3 + (int64_t)(c - 1) * H2 + ii);
-          else pi = (int)(ao.w4 + (int64_t)(c - 1 - A) * H2 + ii);
-          step(pi, vsum, adam_load(a.adam, pi, polyak));
-        }
+      if (tid < 9 * 32 && xpi >= 0) {
+        const int c = tid >> 5;
+        float vsum = 0.f;
+        for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + (tid & 31)];
+        step(xpi, vsum, xin);
       }
       if (t == 0) {  // the heads' biases: sum_b gh[b, h]
         __syncthreads();
@@ -750,12 +846,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         for (int q = 0; q < kHM; ++q) sg[q] = ghs[tid * kHM + q];
         float mx[1] = {-INFINITY};
         block_allreduce<kHM, 0>(sg, mx, red);
-        if (tid < nh) {
+        if (tid >= 288 && tid < 288 + nh) {
           float gvb = 0.f;
 #pragma unroll
-          for (int q = 0; q < kHM; ++q) gvb = tid == q ? sg[q] : gvb;
-          const int pi = (int)(tid < A ? ao.b3 + tid : ao.b4 + (tid - A));
-          step(pi, gvb, adam_load(a.adam, pi, polyak));
+          for (int q = 0; q < kHM; ++q) gvb = tid - 288 == q ? sg[q] : gvb;
+          step(xpi, gvb, xin);
         }
       }
     }
@@ -804,23 +899,20 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         for (int c = 0; c < 8; ++c) acc[c] = fmaf(du[q][e], xs[(r + e) * 8 + c], acc[c]);
       }
     }
+    RLMD_TSA(5);
     __syncthreads();
 #pragma unroll
     for (int c = 0; c < 9; ++c) part[(p * 9 + c) * 32 + cj] = acc[c];
     __syncthreads();
-    for (int o = tid; o < 32 * 9; o += NT) {
-      const int jj = o % 32, c = o / 32;
-      if (c < S || c == 8) {
-        float vsum = 0.f;
-        for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + jj];
-        const int jr = j0 + jj;
-        if (jr < H1) {
-          const int pi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
-          step(pi, vsum, adam_load(a.adam, pi, polyak));
-        }
-      }
+    if (xpi >= 0) {  // 32 rows x (S + 1) outputs, thread c * 32 + jj (Adam state prefetched)
+      const int jj = tid & 31, c = tid >> 5;
+      float vsum = 0.f;
+      for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + jj];
+      step(xpi, vsum, xin);
     }
   }
+  RLMD_TSA(7);
+  RLMD_TSA(15);
 }
 
 }  // namespace
@@ -829,6 +921,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
 extern "C" int rlmd_debug_ts_upd(unsigned long long* out) {
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_upd), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : 2;
+}
+extern "C" int rlmd_debug_ts_aupd(unsigned long long* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_aupd), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : 2;
 }
 #endif
 

@@ -15,3 +15,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o trace
 echo PROF_RC=$?
 RLMD_NO_FUSED_ACTOR=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_noact -o trace -- python3 bench.py --no-cpu-baseline --no-companion --k-sweep= --steps 20 --warmup 5 > $OUT/trace_noact.log 2>&1
 echo PROF2_RC=$?
+timeout -k 10 200 python tools/ts_probe.py aupd > gpurun_out/ts_aupd.log 2>&1 && timeout -k 10 200 python tools/ts_probe.py upd > gpurun_out/ts_upd.log 2>&1
+echo PROBE_RC=$?

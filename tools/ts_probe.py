@@ -224,9 +224,11 @@ def run_upd():
             rows.append(np.array(buf[:], dtype=np.int64).reshape(4, 16))
     r = np.stack(rows)
     names = ["entry", "loads issued", "row loss", "rank + dq", "mfma / fc1 sums", "adam", "first-col extras", "end"]
+    t0 = r[:, :3, 14].min(axis=1)
     for slot, label in enumerate(["tile (0,0)", "tile (0,1)", "fc1 block 0"]):
         t = r[:, slot]
-        print(f"{label}: total {np.median(t[:, 7] - t[:, 0]):.0f} cycles")
+        w0, w1 = np.median(t[:, 14] - t0) / 100, np.median(t[:, 15] - t0) / 100
+        print(f"{label}: total {np.median(t[:, 7] - t[:, 0]):.0f} cycles, window {w0:6.2f} .. {w1:6.2f} us")
         prev = 0
         for i in range(1, 8):
             if np.all(t[:, i] == 0):
@@ -235,5 +237,47 @@ def run_upd():
             prev = i
 
 
+def run_aupd():
+    """actor_update_kernel (C2, K = 1 per step): thread-0 cycle stamps of tiles (0, 0)
+    and (0, 1), fc1 block 0 and the statistics workgroup, and their windows on the
+    constant-rate clock (us from the earliest entry)."""
+    import numpy as np
+    import torch
+
+    from rlmd_amd import _abi
+
+    _abi._LIB = _abi.load(LIB)
+    lib = _abi._LIB
+    lib.rlmd_debug_ts_aupd.restype = C.c_int
+    lib.rlmd_debug_ts_aupd.argtypes = [C.POINTER(C.c_ulonglong)]
+    from rlmd_amd.trainer import VecTrainer
+
+    tr = VecTrainer("gbm", "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
+                    replay_capacity=1 << 20, k_updates=1, device="cuda:0")
+    buf = (C.c_ulonglong * 64)()
+    rows = []
+    for it in range(40):
+        tr.step()
+        torch.cuda.synchronize()
+        lib.rlmd_debug_ts_aupd(buf)
+        if it >= 10:
+            rows.append(np.array(buf[:], dtype=np.int64).reshape(4, 16))
+    r = np.stack(rows)
+    names = {0: "entry", 1: "stats branch passed", 2: "loads + rank", 3: "policy bwd / pre-arrive", 4: "arrived",
+             5: "mfma / fc1 sums", 6: "adam", 7: "end"}
+    t0 = r[:, :, 14].min(axis=1)
+    for slot, label in enumerate(["tile (0,0)", "tile (0,1)", "fc1 block 0", "stats wg"]):
+        t = r[:, slot]
+        w0, w1 = np.median(t[:, 14] - t0) / 100, np.median(t[:, 15] - t0) / 100
+        print(f"{label}: window {w0:6.2f} .. {w1:6.2f} us")
+        prev = 0
+        for i in range(1, 8):
+            if np.all(t[:, i] == 0):
+                continue
+            print(f"  {names[prev]:>24s} -> {names[i]:<24s} {np.median(t[:, i] - t[:, prev]):8.0f}")
+            prev = i
+
+
 if __name__ == "__main__":
-    {"build": build, "run": run, "act": run_act, "env": run_env, "mkt": run_mkt, "upd": run_upd}[sys.argv[1]]()
+    {"build": build, "run": run, "act": run_act, "env": run_env, "mkt": run_mkt, "upd": run_upd,
+     "aupd": run_aupd}[sys.argv[1]]()
