@@ -171,15 +171,18 @@ __device__ __forceinline__ uint64_t critic_sel_key(const CriticRow& o) {
 // The whole critic loss in one workgroup.  runs: LDS uint64 [blockDim.x];
 // rank_of: LDS int [3 * blockDim.x]; red: LDS float [16 * 9].  dq written when
 // a.dq[0] is set.
-// MAXW: the block's waves at most (block_rank)
+// MAXW: the block's waves (block_rank).  part: -1 the whole loss; 0 / 1 split
+// over two workgroups: part 0 everything but critic 1's tail index, part 1 only
+// that (stats[9]) — the two Zipf ranks run in parallel.
 template <int MAXW = 16>
-__device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* runs, int* rank_of, float* red) {
+__device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* runs, int* rank_of, float* red,
+                                                  int part = -1) {
   const int b = threadIdx.x, B = a.B, nth = blockDim.x;
   CriticRow o;
   critic_row_loss(a, red, o);
   const bool in = o.in;
   const float* l = o.l;
-  if (in && a.y_out) a.y_out[b] = o.y;
+  if (in && a.y_out && part <= 0) a.y_out[b] = o.y;
   const int k = B > a.k ? a.k : B;
   bool sel = in;
   int rank = b;
@@ -196,9 +199,11 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
   // Zipf-plot tail index of the selected losses' order statistics
   // (critic_loss.py:238-266): each critic's selected losses ranked among
   // themselves, descending, ties by selection rank; that rank is the slot
-  block_rank<MAXW>(sel ? ((uint64_t)(~f2key(l[0])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + nth);
-  block_rank<MAXW>(sel ? ((uint64_t)(~f2key(l[1])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + 2 * nth);
-  const int rz0 = sel ? rank_of[nth + rank] : 0, rz1 = sel ? rank_of[2 * nth + rank] : 0;
+  if (part != 1)
+    block_rank<MAXW>(sel ? ((uint64_t)(~f2key(l[0])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + nth);
+  if (part != 0)
+    block_rank<MAXW>(sel ? ((uint64_t)(~f2key(l[1])) << 32) | (uint32_t)rank : ~0ull, runs, rank_of + 2 * nth);
+  const int rz0 = sel && part != 1 ? rank_of[nth + rank] : 0, rz1 = sel && part != 0 ? rank_of[2 * nth + rank] : 0;
   const float lg0 = sel ? logf(l[0] + a.log_noise) : 0.f;
   const float lg1 = sel ? logf(l[1] + a.log_noise) : 0.f;
   float s4[2] = {lg0, lg1};
@@ -211,7 +216,12 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
     a.dq[0][b] = sel ? a.grad_scale * o.dl[0] / (float)k : 0.f;
     a.dq[1][b] = sel ? a.grad_scale * o.dl[1] / (float)k : 0.f;
   }
-  if (b == 0) {
+  if (b == 0 && part == 1) {  // critic 1's tail index only
+    LearnState* st = a.st;
+    a.stats[9] = 1.f / (s5[1] / a.zipf_x2);
+    if (isnan(a.stats[9]) && atomicOr(&st->nan_flag, RLMD_STATUS_NAN_STATS) == 0) st->nan_update = st->learn_cntr;
+  }
+  if (b == 0 && part != 1) {
     LearnState* st = a.st;
     float newc[2];
     for (int g = 0; g < 2; ++g) {  // Nagy Cauchy-scale update (critic_loss.py:74-101)
@@ -221,7 +231,7 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
       a.stats[2 + g] = -m3[2 + g];
       a.stats[4 + g] = m3[g];
       a.stats[6 + g] = NAN;
-      a.stats[8 + g] = 1.f / (s5[g] / a.zipf_x2);
+      if (g == 0 || part < 0) a.stats[8 + g] = 1.f / (s5[g] / a.zipf_x2);
     }
     st->cauchy[0] = newc[0];
     st->cauchy[1] = newc[1];
@@ -231,15 +241,15 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
     // q1 / q2 / target (sac_ / td3_critic_stability :29-116), bit 1 = NaN in the
     // critic statistics loss[0:6] + loss[8:10] (critic_learning :119-255, whose
     // exit() becomes this sticky flag); nan_update = learn counter at first set
-    int32_t fl = st->nan_flag;
+    int32_t fl = 0;
     if (o.nan > 0.f) fl |= RLMD_STATUS_NAN_BATCH;
     bool sn = false;
 #pragma unroll
     for (int v = 0; v < 10; ++v)
-      if (v < 6 || v >= 8) sn |= isnan(a.stats[v]);
+      if (v < 6 || v == 8 || (v == 9 && part < 0)) sn |= isnan(a.stats[v]);
     if (sn) fl |= RLMD_STATUS_NAN_STATS;
-    if (fl && !st->nan_flag) st->nan_update = st->learn_cntr;
-    st->nan_flag = fl;
+    // sticky; atomic: with part 1 running alongside, the first to set it stamps nan_update
+    if (fl && atomicOr(&st->nan_flag, fl) == 0) st->nan_update = st->learn_cntr;
     if (!a.keep_actor_slot) a.stats[10] = NAN;
     if (!a.keep_logtemp_slot) a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
     a.stats[12] = newc[0];

@@ -43,7 +43,7 @@ constexpr int TW = 32;  // tile edge (fc2.weight tiles TW x TW, fc1 blocks of TW
 // experiment builds only (tools/ts_probe.py upd): thread-0 s_memtime stamps of
 // three workgroups (slot 0: tile (0, 0), 1: tile (0, 1), 2: the first fc1 block)
 __device__ unsigned long long g_ts_upd[64];
-__device__ unsigned long long g_ts_aupd[64];
+__device__ unsigned long long g_ts_aupd[128];
 #define RLMD_TSU(i)                                                                       \
   do {                                                                                    \
     if (threadIdx.x == 0 && ts_slot >= 0)                                                 \
@@ -497,8 +497,12 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nrb = (B + 15) / 16;
   const int t = blockIdx.x;
-  const int nwg = a.n_w2 + a.n_w1 + (a.cstats.B > 0 ? 1 : 0);
-  const int ts_slot = t == 0 ? 0 : t == 1 ? 1 : t == a.n_w2 ? 2 : t == nwg - 1 ? 3 : -1;
+  // workgroups: fc2.weight tiles, fc1 blocks, head workgroups (b2 and the heads
+  // of 32 fc2 rows each), and two critic-statistics workgroups
+  const int n_hd = a.ti, nst = a.cstats.B > 0 ? 2 : 0;
+  const int nwg = a.n_w2 + a.n_w1 + n_hd + nst;
+  const int sidx = t - (a.n_w2 + a.n_w1 + n_hd);  // >= 0: statistics part
+  const int ts_slot = t == 0 ? 0 : t == 1 ? 1 : t == a.n_w2 ? 2 : sidx == 0 ? 3 : t == a.n_w2 + a.n_w1 ? 4 : sidx == 1 ? 5 : -1;
   (void)ts_slot;
   RLMD_TSA(14);
   RLMD_TSA(0);
@@ -513,10 +517,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     __syncthreads();
     return *lastf != 0;
   };
-  const bool stats_wg = a.cstats.B > 0 && t == nwg - 1;
-  const bool w2tile = !stats_wg && t < a.n_w2, w1blk = !stats_wg && !w2tile;
-  const int i0 = w2tile ? (t / a.tj) * TW : 0, j0 = w2tile ? (t % a.tj) * TW : (t - a.n_w2) * TW;
-  const bool first_col = w2tile && (t % a.tj) == 0;
+  const bool stats_wg = sidx >= 0;
+  const bool w2tile = t < a.n_w2, first_col = !stats_wg && t >= a.n_w2 + a.n_w1;  // first_col: a head workgroup
+  const bool w1blk = !stats_wg && !w2tile && !first_col;
+  const int i0 = w2tile ? (t / a.tj) * TW : first_col ? (t - a.n_w2 - a.n_w1) * TW : 0;
+  const int j0 = w2tile ? (t % a.tj) * TW : w1blk ? (t - a.n_w2) * TW : 0;
   const bool polyak = adam_polyak(a.adam);
   const CopyDst cd = copy_dst(a.adam, 0);
   auto step = [&](int pi, float gv, const AdamIn& in) {
@@ -543,8 +548,8 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   };
   if (stats_wg) {
     // this update's critic statistics (rlmd_loss.h), off the critical path
-    critic_loss_block<NT / 64>(a.cstats, reinterpret_cast<uint64_t*>(smem + ALds::runs), reinterpret_cast<int*>(smem + ALds::rank),
-                      red);
+    critic_loss_block<NT / 64>(a.cstats, reinterpret_cast<uint64_t*>(smem + ALds::runs),
+                               reinterpret_cast<int*>(smem + ALds::rank), red, sidx);
     // the actor loss of every row, should this workgroup arrive last
     const bool in = tid < B;
     const int64_t nB = (int64_t)B * 4;
@@ -698,7 +703,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
       if (first_col && tid < 32 * 9 && c <= nh && ii < H2)
         xpi = (int)(c == 0 ? ao.b2 + ii : c - 1 < A ? ao.w3 + (int64_t)(c - 1) * H2 + ii
                                                    : ao.w4 + (int64_t)(c - 1 - A) * H2 + ii);
-      if (first_col && t == 0 && tid >= 288 && tid < 288 + nh)
+      if (first_col && i0 == 0 && tid >= 288 && tid < 288 + nh)
         xpi = (int)(tid - 288 < A ? ao.b3 + (tid - 288) : ao.b4 + (tid - 288 - A));
       if (w1blk && tid < 32 * 9 && (c < S || c == 8) && jr < H1)
         xpi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
@@ -793,9 +798,9 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     __syncthreads();
     tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
     RLMD_TSA(6);
-    if (first_col) {
+  } else if (first_col) {
+    {
       // ---- db2[i] = sum_b dh2[b, i]; the heads dW_head[h, i] = sum_b gh[b, h] h2[b, i]
-      __syncthreads();
       const int ci = tid & 31, p = tid >> 5;
       float sb = 0.f, sw[kHM];
 #pragma unroll
@@ -839,7 +844,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + (tid & 31)];
         step(xpi, vsum, xin);
       }
-      if (t == 0) {  // the heads' biases: sum_b gh[b, h]
+      if (i0 == 0) {  // the heads' biases: sum_b gh[b, h]
         __syncthreads();
         float sg[kHM];
 #pragma unroll
@@ -924,7 +929,7 @@ extern "C" int rlmd_debug_ts_upd(unsigned long long* out) {
 }
 extern "C" int rlmd_debug_ts_aupd(unsigned long long* out) {
   if (hipDeviceSynchronize() != hipSuccess) return 2;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_aupd), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_aupd), sizeof(unsigned long long) * 128) == hipSuccess ? 0 : 2;
 }
 #endif
 
@@ -936,7 +941,7 @@ int actor_update_launch(const ActUpdArgs& a, hipStream_t st) {
   RLMD_CHECK(a.tj == d.H1p / TW && a.ti * TW >= d.H2p && a.n_w2 == a.ti * a.tj && a.n_w1 == d.H1p / TW,
              "actor update: tile grid inconsistent with the widths");
   RLMD_CHECK(a.cstats.B <= NT, "critic statistics workgroup: mini-batch up to 512 rows");
-  const dim3 grid(a.n_w2 + a.n_w1 + (a.cstats.B > 0 ? 1 : 0));
+  const dim3 grid(a.n_w2 + a.n_w1 + a.ti + (a.cstats.B > 0 ? 2 : 0));
   if (d.prec == RLMD_BF16)
     hipLaunchKernelGGL(actor_update_kernel<RLMD_BF16>, grid, dim3(NT), ALds::total, st, a);
   else

@@ -254,19 +254,20 @@ def run_aupd():
 
     tr = VecTrainer("gbm", "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
                     replay_capacity=1 << 20, k_updates=1, device="cuda:0")
-    buf = (C.c_ulonglong * 64)()
+    buf = (C.c_ulonglong * 128)()
     rows = []
     for it in range(40):
         tr.step()
         torch.cuda.synchronize()
         lib.rlmd_debug_ts_aupd(buf)
         if it >= 10:
-            rows.append(np.array(buf[:], dtype=np.int64).reshape(4, 16))
+            rows.append(np.array(buf[:], dtype=np.int64).reshape(8, 16))
     r = np.stack(rows)
     names = {0: "entry", 1: "stats branch passed", 2: "loads + rank", 3: "policy bwd / pre-arrive", 4: "arrived",
              5: "mfma / fc1 sums", 6: "adam", 7: "end"}
-    t0 = r[:, :, 14].min(axis=1)
-    for slot, label in enumerate(["tile (0,0)", "tile (0,1)", "fc1 block 0", "stats wg"]):
+    t0 = r[:, :6, 14].min(axis=1)
+    for slot, label in enumerate(["tile (0,0)", "tile (0,1)", "fc1 block 0", "stats part 0", "head wg 0",
+                                  "stats part 1"]):
         t = r[:, slot]
         w0, w1 = np.median(t[:, 14] - t0) / 100, np.median(t[:, 15] - t0) / 100
         print(f"{label}: window {w0:6.2f} .. {w1:6.2f} us")
