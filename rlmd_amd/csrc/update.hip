@@ -469,9 +469,19 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 constexpr int kHM = 4;  // heads per row held in LDS (2 A; the fused actor step takes A <= 2)
 constexpr int kAM = 2;  // actions
 
+// dh2 = sum over the heads of gh[h] W_head[h] in the launch chain's order: mu_j
+// then log_scale_j per action j (SAC), mu_j (TD3).  Position q of that order
+// holds head head_at(q) (-1 past the nh heads), so that the sum runs over a
+// fixed kHM positions with no runtime-indexed register arrays.
+__device__ __forceinline__ int head_at(int q, int A, bool sac) {
+  const int nh = sac ? 2 * A : A;
+  return q >= nh ? -1 : !sac ? q : (q & 1) ? A + (q >> 1) : (q >> 1);
+}
+
 struct ALds {
-  static constexpr int gh = 0;                      // f32 [512][kHM] head gradients per row
-  static constexpr int runs = gh + 512 * kHM * 4;   // u64 [512]
+  static constexpr int gh = 0;                      // f32 [512][kHM] head gradients per row (head order)
+  static constexpr int ghp = gh + 512 * kHM * 4;    // the same in summation order (head_at), zero padded
+  static constexpr int runs = ghp + 512 * kHM * 4;  // u64 [512]
   static constexpr int rank = runs + 512 * 8;       // int [3 * 512] (critic statistics: 3 ranks)
   static constexpr int red = rank + 3 * 512 * 4;    // 16 * 9 floats
   static constexpr int part = red + 16 * 9 * 4;     // f32 [8][4][256]
@@ -486,6 +496,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   using K = KT<PREC>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* ghs = reinterpret_cast<float*>(smem + ALds::gh);
+  float* ghp = reinterpret_cast<float*>(smem + ALds::ghp);
   float* part = reinterpret_cast<float*>(smem + ALds::part);
   float* red = reinterpret_cast<float*>(smem + ALds::red);
   int* lastf = reinterpret_cast<int*>(smem + ALds::flag);
@@ -621,7 +632,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   for (int h = 0; h < 2; ++h) {
     const int i = i0 + 16 * h + (lane & 15);
 #pragma unroll
-    for (int q = 0; q < kHM; ++q) wh[h][q] = rlmd_ldf(rw, (int64_t)q * H2 + i, w2tile && q < nh && i < H2);
+    for (int q = 0; q < kHM; ++q) {  // summation order
+      const int hq = head_at(q, A, sac);
+      wh[h][q] = rlmd_ldf(rw, (int64_t)(hq < 0 ? 0 : hq) * H2 + i, w2tile && hq >= 0 && i < H2);
+    }
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
@@ -698,7 +712,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
                                                      0, 0));
       }
 #pragma unroll
-      for (int q = 0; q < kHM; ++q) whc[q] = rlmd_ldf(rw, (int64_t)q * H2 + i, first_col && q < nh && i < H2);
+      for (int q = 0; q < kHM; ++q) {  // summation order
+        const int hq = head_at(q, A, sac);
+        whc[q] = rlmd_ldf(rw, (int64_t)(hq < 0 ? 0 : hq) * H2 + i, first_col && hq >= 0 && i < H2);
+      }
       const int c = tid >> 5, ii = i0 + (tid & 31), jr = j0 + (tid & 31);
       if (first_col && tid < 32 * 9 && c <= nh && ii < H2)
         xpi = (int)(c == 0 ? ao.b2 + ii : c - 1 < A ? ao.w3 + (int64_t)(c - 1) * H2 + ii
@@ -739,6 +756,14 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     }
 #pragma unroll
     for (int q = 0; q < kHM; ++q) ghs[tid * kHM + q] = gh[q];
+#pragma unroll
+    for (int q = 0; q < kHM; ++q) {
+      const int hq = head_at(q, A, sac);
+      float v = 0.f;
+#pragma unroll
+      for (int h = 0; h < kHM; ++h) v = h == hq ? gh[h] : v;
+      ghp[tid * kHM + q] = v;
+    }
   }
   RLMD_TSA(3);
   temperature_step();
@@ -759,15 +784,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         float dh[K::RPL];
 #pragma unroll
         for (int e = 0; e < K::RPL; ++e) {
-          const float* gr = ghs + ((row + e) & 511) * kHM;
-          float acc_h = 0.f;  // the launch-chain order: mu_j then log_scale_j per action j
+          const float* gr = ghp + ((row + e) & 511) * kHM;
+          float acc_h = 0.f;  // the launch-chain order (head_at); padded positions add 0 * 0
 #pragma unroll
-          for (int j = 0; j < kAM; ++j) {
-            if (j < A) {
-              acc_h = fmaf(gr[j], wh[h][j], acc_h);
-              if (sac) acc_h = fmaf(gr[A + j], wh[h][A + j], acc_h);
-            }
-          }
+          for (int q = 0; q < kHM; ++q) acc_h = fmaf(gr[q], wh[h][q], acc_h);
           dh[e] = acc_h;
         }
         const typename K::Frag af = K::form_a(mw[s][h], dh, 1.f);
@@ -821,14 +841,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
           } else {
             hval = __uint_as_float(hv[e >> 2][e & 3]);
           }
+          const float* grp = ghp + (r0 + e) * kHM;
           float acc_h = 0.f;
 #pragma unroll
-          for (int j = 0; j < kAM; ++j) {
-            if (j < A) {
-              acc_h = fmaf(gr[j], whc[j], acc_h);
-              if (sac) acc_h = fmaf(gr[A + j], whc[A + j], acc_h);
-            }
-          }
+          for (int q = 0; q < kHM; ++q) acc_h = fmaf(grp[q], whc[q], acc_h);
           sb += byte ? acc_h : 0.f;
 #pragma unroll
           for (int q = 0; q < kHM; ++q) sw[q] = fmaf(gr[q], hval, sw[q]);
