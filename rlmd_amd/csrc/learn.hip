@@ -249,6 +249,7 @@ struct Scratch {
   // bases, the head weights' snapshot, the critics' dq/da per row
   unsigned char *hp1a, *hp2a;
   float *ua, *wheads, *dqda[2];
+  int32_t* rank1;  // the rows' top-k selection ranks of this update (critic update -> statistics)
 };
 
 }  // namespace
@@ -655,6 +656,8 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     cu.ti = d.H2p / 32;
     cu.n_w2 = cu.ti * cu.tj;
     cu.n_w1 = d.H1p / 32;
+    // the statistics workgroups of the fused actor step reuse the selection ranks
+    if (ag->fused_actor && actor_step && loss_stats.B > 0) cu.rank_out = S_.rank1;
     RLMD_TRY(critic_update_launch(cu, st));
     if (loss_stats.B > 0 && !actor_step) {
       hipLaunchKernelGGL(critic_loss_kernel<512>, dim3(1), dim3(512), 0, st, loss_stats);
@@ -776,6 +779,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
         adam_scalars(ad.lr_temp, ad.cnt / ad.temp_interval, ad.temp_step_size, ad.temp_bc2_sqrt);
       au.adam = ad;
       au.cstats = loss_stats;
+      au.cstats.rank_in = S_.rank1;  // critic_update_kernel wrote them (cu.rank_out)
       au.cstats.keep_actor_slot = 1;   // stats[10]: the actor loss
       au.cstats.keep_logtemp_slot = 1; // stats[11]: the temperature step
       au.tj = d.H1p / 32;
@@ -1059,6 +1063,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
     RLMD_ALLOC(s.ua, e1 * nh);
     RLMD_ALLOC(s.wheads, nh * H2);
     for (int g = 0; g < 2; ++g) RLMD_ALLOC(s.dqda[g], B * A);
+    RLMD_ALLOC(s.rank1, B);
   }
   {  // weight-gradient tiles of the larger phase (critics: both nets; actor)
     using rlmd::bwd_w_tiles;

@@ -206,6 +206,7 @@ struct LossArgs {
   float gamma, reward_scale;
   float* dq[2];
   float* y_out;  // nullable
+  const int32_t* rank_in;  // nullable: the rows' top-k selection ranks, already computed (critic update)
   const float* zipf_x;
   float zipf_x2;
   LearnState* st;

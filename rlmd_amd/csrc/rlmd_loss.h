@@ -187,8 +187,12 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
   bool sel = in;
   int rank = b;
   if (B > a.k) {
-    block_rank<MAXW>(critic_sel_key(o), runs, rank_of);
-    rank = in ? rank_of[b] : B;
+    if (a.rank_in) {
+      rank = in ? a.rank_in[b] : B;
+    } else {
+      block_rank<MAXW>(critic_sel_key(o), runs, rank_of);
+      rank = in ? rank_of[b] : B;
+    }
     sel = in && rank < k;
   }
   // R3: mean / min / max of the selected losses per critic

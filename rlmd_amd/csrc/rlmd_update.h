@@ -20,11 +20,13 @@ struct CritUpdArgs {
   const float* x;         // critic inputs [B, X]
   AdamArgs adam;          // both critics (p = critic 0's parameters, n = 2 x net size)
   int32_t ti, tj, n_w2, n_w1;
+  int32_t* rank_out;      // nullable: every row's top-k selection rank [B] (workgroup 0 writes it)
 };
 
 // The actor (+ temperature) step of one update in one launch
 // (update.hip actor_update_kernel).  Grid: n_w2 fc2.weight tiles + n_w1 fc1
-// blocks of the policy, then one critic-statistics workgroup when cstats.B > 0.
+// blocks of the policy, head workgroups (b2 and the heads of 32 fc2 rows each),
+// then two critic-statistics workgroups when cstats.B > 0.
 struct ActUpdArgs {
   RowDims d;
   NetOff ao;

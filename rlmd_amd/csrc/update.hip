@@ -323,6 +323,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       int* rank_of = reinterpret_cast<int*>(smem + ULds::rank);
       block_rank<NT / 64>(critic_sel_key(o), reinterpret_cast<uint64_t*>(smem + ULds::runs), rank_of);
       sel = o.in && rank_of[tid] < kk;
+      if (blockIdx.x == 0 && a.rank_out && o.in) a.rank_out[tid] = rank_of[tid];  // for the statistics
     }
     dqs[tid] = sel ? a.loss.grad_scale * (g == 0 ? o.dl[0] : o.dl[1]) / (float)kk : 0.f;
     if (blockIdx.x == 0 && tid == 0) adam_scalar_step(a.adam);  // learn_step_cntr (no temperature here)
