@@ -16,7 +16,7 @@ BENCH="bench.py --no-cpu-baseline --no-companion --k-sweep= --steps 25 --warmup 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o trace -- python3 $BENCH > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "act_env_kernel|fused_act_kernel|env_train_kernel" -f csv -d $OUT/fetch -o fetch -- python3 $BENCH > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "act_env_kernel|fused_act_kernel|env_train_kernel" -f csv -d $OUT/write -o write -- python3 $BENCH > $OUT/write.log 2>&1
-LEARN="act_env_kernel|fused_act_kernel|fwd_rows|cbwd_rows|qeval_rows|abwd_rows|gemm_kernel|adam_kernel|replay_sample"
+LEARN="act_env_kernel|fused_act_kernel|fwd_rows|cbwd_rows|qeval_rows|abwd_rows|gemm_kernel|adam_kernel|replay_sample|critic_update_kernel|actor_update_kernel"
 timeout -k 10 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-include-regex "$LEARN" -f csv -d $OUT/mfma -o mfma -- python3 $BENCH > $OUT/mfma.log 2>&1
 timeout -k 10 120 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 echo done
