@@ -556,31 +556,30 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
     int64_t ep_slot = -1;
     // action i: warm-up Philox draw (|.| unless GBM/market) or the policy's, then the
     // smoothing-window clip
+    // the policy's action i: a predicated buffer load (no branch around it, so it
+    // is not waited on at a merge)
+    const __amdgpu_buffer_rsrc_t ra = rlmd_rsrc(actions, actions ? (int64_t)P.n_lanes * A * 4 : 0);
     auto act_of = [&](int i) -> AT {
-      double v;
+      const double pv = (double)rlmd_ldf(ra, (int64_t)lane * A + i, !random_actions && i < A);
+      double v = pv;
       if (random_actions) {  // Box(-0.99, 0.99, float64).sample() = low + (high - low) * random_sample()
         const rlmd_u32x4 w = rlmd_philox(P.seed, lane, step, RLMD_TAG_WARMUP_ACTION, (uint32_t)(i >> 1));
         const double u = (i & 1) ? rlmd_u01(w.z, w.w) : rlmd_u01(w.x, w.y);
         v = -kMaxAbsAction + 2.0 * kMaxAbsAction * u;
         if (abs_actions) v = fabs(v);
-      } else {
-        v = (double)actions[(int64_t)lane * A + i];
       }
       if (sizeof(AT) == 4) return (AT)v;  // policy action outside the window: exact f32
       return (AT)fmin(fmax(v, clip_lo), clip_hi);
     };
+    // the actions in named registers when their count is known at compile time (an
+    // array here was promoted to LDS, each element's load waited on at its store)
     constexpr int AR = kActRegs<FAM, NG>;
-    AT areg[AR > 0 ? AR : 1];
-    if constexpr (AR > 0) {
-#pragma unroll
-      for (int i = 0; i < AR; ++i) areg[i] = i < A ? act_of(i) : (AT)0;
-    }
-    auto act = [&](int i) -> AT {  // select chain: a runtime index into areg would spill it to scratch
+    static_assert(AR <= 4, "action registers");
+    const AT a0 = AR > 0 && 0 < A ? act_of(0) : (AT)0, a1 = AR > 1 && 1 < A ? act_of(1) : (AT)0;
+    const AT a2 = AR > 2 && 2 < A ? act_of(2) : (AT)0, a3 = AR > 3 && 3 < A ? act_of(3) : (AT)0;
+    auto act = [&](int i) -> AT {
       if constexpr (AR > 0) {
-        AT v = areg[0];
-#pragma unroll
-        for (int k = 1; k < AR; ++k) v = i == k ? areg[k] : v;
-        return v;
+        return i == 0 ? a0 : i == 1 ? a1 : i == 2 ? a2 : a3;
       } else {
         return act_of(i);
       }
