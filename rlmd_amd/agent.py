@@ -127,6 +127,21 @@ class DeviceAgent:
                                            ptr(self.adam_m), ptr(self.adam_v), C.byref(h)))
         self.h = h
         self.stats = torch.full((1, 16), float("nan"), dtype=torch.float32, device=dev)
+        self._seen = self._versions()
+
+    def _versions(self):
+        # torch bumps a tensor's version on every in-place write, through any view
+        # (state_dict() entries, slices); the device's own updates do not touch it
+        return (self.params._version, self.target._version)
+
+    def sync_written(self):
+        """Mark the compute copies stale if the parameters or targets were written on
+        the torch side since the last call (every act / learn / train step calls it,
+        so a write through state_dict() without params_written() is still seen)."""
+        v = self._versions()
+        if v != self._seen:
+            self._seen = v
+            check(_abi.lib().rlmd_agent_params_written(self.h))
 
     def __del__(self):
         h = getattr(self, "h", None)
@@ -154,12 +169,14 @@ class DeviceAgent:
         n = obs.shape[0]
         out = torch.empty(n, self.A, dtype=torch.float32, device=self.device) if out is None else out
         e = None if eps is None else eps.to(device=self.device, dtype=torch.float32).contiguous()
+        self.sync_written()
         check(_abi.lib().rlmd_agent_act(self.h, ptr(obs), n, ptr(out), mode, noise_ctr, ptr(e), stream_ptr()))
         return out
 
     def learn(self, replay, k=1):
         if self.stats.shape[0] < k:
             self.stats = torch.full((k, 16), float("nan"), dtype=torch.float32, device=self.device)
+        self.sync_written()
         check(_abi.lib().rlmd_agent_learn(self.h, replay.h, k, ptr(self.stats), stream_ptr()))
         return self.stats[:k]
 
@@ -170,6 +187,7 @@ class DeviceAgent:
         f = lambda x: None if x is None else x.to(self.device, torch.float32).contiguous()
         args = [f(s), f(a), f(r), f(s2), done.to(self.device, torch.uint8).contiguous(),
                 None if eff is None else eff.to(self.device, torch.int32).contiguous(), f(eps_a), f(eps_b)]
+        self.sync_written()
         check(_abi.lib().rlmd_agent_learn_batch(self.h, *[ptr(x) for x in args], ptr(self.stats), stream_ptr()))
         return self.stats[0]
 
@@ -196,7 +214,9 @@ class DeviceAgent:
 
     def params_written(self):
         """Call after writing parameters through state_dict() / the flat tensors:
-        the device re-derives its MFMA compute copies before the next act / learn."""
+        the device re-derives its MFMA compute copies before the next act / learn
+        (sync_written() also catches torch-side writes by their version counters)."""
+        self._seen = self._versions()
         check(_abi.lib().rlmd_agent_params_written(self.h))
 
     def scalars(self):

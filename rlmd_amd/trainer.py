@@ -67,6 +67,7 @@ class VecTrainer:
     def step(self, k_updates=None):
         if k_updates is not None:
             self.cfg.k_updates = k_updates
+        self.agent.sync_written()
         check(_abi.lib().rlmd_train_step(self.env.h, self.replay.h, self.agent.h, self.cfg, ptr(self.obs),
                                          ptr(self.actions), ptr(self.ep_stats), ptr(self.stats), stream_ptr()))
         self.cfg.cum_step += 1
@@ -210,6 +211,7 @@ def market_evaluate(agent, prices, investor, obs_days, test_days, starts, cum_st
     steps = torch.empty(n, dtype=torch.int32, device=dev)
     risk = torch.empty(n, env.risk_dim, dtype=torch.float64, device=dev)
     lib = _abi.lib()
+    agent.sync_written()
     check(lib.rlmd_eval_market(env.h, agent.h, ptr(st), int(cum_step), int(warmup_steps), int(smoothing_window),
                                ptr(obs), ptr(act), ptr(live), ptr(reward), ptr(steps), ptr(risk), stream_ptr()))
     risk_log = torch.cat([st.double()[:, None], risk], 1).contiguous()

@@ -280,3 +280,22 @@ def test_eval_market_one_launch_matches_reference(golden, dev, c):
     np.testing.assert_array_equal(out["steps"], g[f"case{c}/steps"])
     np.testing.assert_allclose(out["reward"], g[f"case{c}/reward"], rtol=2e-3, atol=0)
     assert out["steps"].max() == test_days
+
+
+@pytest.mark.parametrize("precision", ["bf16", "fp32"])
+def test_state_dict_write_reaches_the_compute_copies(dev, precision):
+    """A torch-side write through state_dict() without params_written() is still
+    seen (version counters, DeviceAgent.sync_written): the next act runs on the
+    new fc2.weight, bit-equal to acting after an explicit params_written()."""
+    from rlmd_amd.agent import DeviceAgent
+
+    ag = DeviceAgent("SAC", 5, 1, 256, 256, 16, 8, precision=precision, seed=3, device=dev)
+    obs = torch.randn(256, 5, device=dev, generator=torch.Generator(device=dev).manual_seed(0)) * 0.5
+    a0 = ag.act(obs, mode=1).clone()
+    w2 = ag.state_dict("actor")["fc2.weight"]
+    w2.mul_(-1.0)  # in place through the view; no params_written()
+    a1 = ag.act(obs, mode=1).clone()
+    ag.params_written()
+    a2 = ag.act(obs, mode=1).clone()
+    assert not torch.equal(a0, a1)
+    assert torch.equal(a1, a2)
