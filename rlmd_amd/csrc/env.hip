@@ -32,6 +32,19 @@
 
 #include "../../include/rlmd_abi.h"
 #include "learn_kernels.h"
+#ifdef RLMD_TIMING
+// experiment builds only (tools/ts_probe.py actenv): act_env_kernel's acting-body
+// stamps per workgroup — [0] / [6] realtime entry / exit, [1..5] cycles after each
+// phase, [7] realtime at the start of the per-row sampling + env epilogue
+__device__ unsigned long long g_ts_actenv[4096][8];
+#define RLMD_TSA(i, v)                                                                    \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {                                          \
+      g_ts_actenv[blockIdx.x][i] = (v);                                                   \
+      if ((i) == 5) g_ts_actenv[blockIdx.x][7] = __builtin_amdgcn_s_memrealtime();        \
+    }                                                                                     \
+  } while (0)
+#endif
 #include "rlmd_act_rows.h"
 #include "rlmd_common.h"
 #include "rlmd_internal.h"
@@ -439,9 +452,11 @@ struct StatFold {
   int rows;
 };
 
-// one 256-thread block: fixed-order strided sums, then a fixed tree
-__device__ inline void fold_stat_rows(const double* src, int rows, double* dst) {
-  __shared__ double fr[3][256];
+// one 256-thread block: fixed-order strided sums, then a fixed tree.  fr: LDS
+// [3][256] doubles — the caller's dynamic LDS where it has one (act_env_kernel
+// folds before its acting body uses it), so that the fold's 6 KB do not cost
+// the acting kernel a workgroup per CU
+__device__ inline void fold_stat_rows(const double* src, int rows, double* dst, double (*fr)[256]) {
   const int i = threadIdx.x;
   double a = 0.0, b = 0.0, c = 0.0;
   for (int r = i; r < rows; r += blockDim.x) {
@@ -466,7 +481,8 @@ __device__ inline void fold_stat_rows(const double* src, int rows, double* dst) 
 }
 
 __global__ void __launch_bounds__(256) stat_fold_kernel(const double* src, int rows, double* dst) {
-  fold_stat_rows(src, rows, dst);
+  __shared__ double fr[3][256];
+  fold_stat_rows(src, rows, dst, fr);
 }
 
 template <int FAM>
@@ -543,7 +559,10 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
   RLMD_TSE(1, __builtin_amdgcn_s_memtime());
   // block 0 folds the previous launch's per-block rows into the caller's
   // accumulator first (its rows are complete: that launch has ended)
-  if (blockIdx.x == 0 && sf.fold_src) fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst);
+  if (blockIdx.x == 0 && sf.fold_src) {
+    __shared__ double fr[3][256];
+    fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst, fr);
+  }
   double st_n = 0.0, st_r = 0.0, st_t = 0.0;  // finished-episode stats of this lane
   if (lane < P.n_lanes) {
     const int S = P.state_dim, A = P.action_dim;
@@ -702,7 +721,8 @@ __global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) act_env_kernel(rlmd::
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
                                                       StatFold sf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  if (blockIdx.x == 0 && sf.fold_src) fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst);
+  if (blockIdx.x == 0 && sf.fold_src)
+    fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst, reinterpret_cast<double(*)[256]>(smem));
   const int tid = threadIdx.x;
   const int lane = blockIdx.x * rlmd::actrows::kRows + tid;  // this thread's env lane (tid < 64)
   const bool mine = tid < rlmd::actrows::kRows && lane < P.n_lanes;
@@ -1659,6 +1679,9 @@ int rlmd_train_flush_stats(rlmd_env_t env, void* stream) {
 #ifdef RLMD_TIMING
 int rlmd_debug_ts_env(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_env), sizeof(unsigned long long) * 8 * n) != hipSuccess;
+}
+int rlmd_debug_ts_actenv(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_actenv), sizeof(unsigned long long) * 8 * n) != hipSuccess;
 }
 #endif
 

@@ -279,6 +279,46 @@ def run_aupd():
             prev = i
 
 
+def run_actenv():
+    """act_env_kernel per-workgroup timeline (C3 by default: 65,536 Dice_SH_InvA lanes,
+    TD3 400/300; 'gbm' for C2): block spans and the sampling + env epilogue's share."""
+    import numpy as np
+    import torch
+
+    from rlmd_amd import _abi
+
+    _abi._LIB = _abi.load(LIB)
+    lib = _abi._LIB
+    lib.rlmd_debug_ts_actenv.restype = C.c_int
+    lib.rlmd_debug_ts_actenv.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
+    lib.rlmd_train_set_fused(1)
+    from rlmd_amd.trainer import VecTrainer
+
+    fam = sys.argv[2] if len(sys.argv) > 2 else "dice_sh"
+    algo = "SAC" if fam == "gbm" else "TD3"
+    tr = VecTrainer(fam, "A", 65536, algo=algo, precision="bf16", warmup_steps=0, smoothing_window=0,
+                    replay_capacity=1 << 20, k_updates=0, device="cuda:0")
+    nb = 1024
+    buf = (C.c_ulonglong * (8 * nb))()
+    rows = []
+    for it in range(12):
+        tr.step()
+        torch.cuda.synchronize()
+        lib.rlmd_debug_ts_actenv(buf, nb)
+        if it >= 2:
+            rows.append(np.array(buf[:], dtype=np.int64).reshape(nb, 8))
+    r = np.stack(rows)
+    t0 = r[:, :, 0].min(axis=1)[:, None]
+    st, en, ep = (r[:, :, 0] - t0) / 100, (r[:, :, 6] - t0) / 100, (r[:, :, 7] - t0) / 100
+    print(f"act_env_kernel {fam} {algo}: {nb} workgroups (us from the first entry)")
+    print("  entry  pct 0/50/100:", np.percentile(st, [0, 50, 100]))
+    print("  exit   pct 0/50/100:", np.percentile(en, [0, 50, 100]))
+    print("  span   pct 0/50/100:", np.percentile(en - st, [0, 50, 100]))
+    print("  epilogue (sampling + env) pct 0/50/100:", np.percentile(en - ep, [0, 50, 100]))
+    ph = np.diff(r[:, :, 1:6], axis=2).reshape(-1, 4)
+    print("  acting phases (cycles) median:", np.median(ph, 0))
+
+
 if __name__ == "__main__":
     {"build": build, "run": run, "act": run_act, "env": run_env, "mkt": run_mkt, "upd": run_upd,
-     "aupd": run_aupd}[sys.argv[1]]()
+     "aupd": run_aupd, "actenv": run_actenv}[sys.argv[1]]()
