@@ -1350,8 +1350,11 @@ int g_fuse_env = -1;  // -1: from RLMD_NO_FUSED_ENV at first use; rlmd_train_set
 bool env_act_fusable(rlmd_env_t env) {
   const EnvParams& P = env->P;
   if (g_fuse_env < 0) g_fuse_env = getenv("RLMD_NO_FUSED_ENV") != nullptr ? 0 : 1;
-  return g_fuse_env == 1 && P.n == 1 && (P.fam != RLMD_MARKET || P.obs_days == 1) && P.action_dim <= actrows::kMaxA &&
-         P.state_dim <= 8;
+  // any n_gambles / assets / observation days whose action fits the acting body
+  // (<= 2 actions) and whose state fits a 16-float staging row; the multi-asset
+  // and Dx state widths above 8 take the 16-pitch market instantiation
+  if (g_fuse_env != 1 || P.action_dim > actrows::kMaxA || P.state_dim > 16) return false;
+  return P.state_dim <= 8 || P.fam == RLMD_MARKET;
 }
 
 int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step, const FusedActArgs& a,
@@ -1360,7 +1363,7 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
   *launched = false;
   ring_base %= rb.capacity;
   const EnvParams& P = env->P;
-  const bool shape = sp == 8 && ((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5));
+  const bool shape = (sp == 8 || sp == 16) && ((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5));
   if (!env_act_fusable(env) || !shape || a.n != P.n_lanes) return 0;
   const int N = P.n_lanes;
   const dim3 grid((N + actrows::kRows - 1) / actrows::kRows), block(256);
@@ -1374,20 +1377,41 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
     sf.fold_dst = env->pending_dst;
   }
   if (ep_stats) sf.part_out = env->d_part + (size_t)env->part_parity * env->part_rows * 4;
-#define FUSED(F, H, B)                                                                                         \
-  hipExtLaunchKernelGGL((act_env_kernel<F, 1, H, B, 8>), grid, block, actrows::act_lds_bytes(H, 8), stream,    \
+  // NG = 1: one gamble / asset, one observation day (the BASELINE configs); NG = 0:
+  // n and the observation window read at run time (n_gambles / assets <= 2 with
+  // A <= 2, market Dx at the 16-float staging pitch)
+  const bool ng1 = P.n == 1 && (P.fam != RLMD_MARKET || P.obs_days == 1);
+  RLMD_CHECK(ng1 || P.fam != RLMD_DICE_SH, "fused acting + env step: dice_sh has one die");
+  RLMD_CHECK(sp == 8 || P.fam == RLMD_MARKET, "fused acting + env step: state wider than 8 (market only)");
+#define FUSED(F, NG, H, B, SP)                                                                                     \
+  hipExtLaunchKernelGGL((act_env_kernel<F, NG, H, B, SP>), grid, block, actrows::act_lds_bytes(H, SP), stream,     \
                         ev_start, ev_stop, 0, a, env->P, step, obs, rb, ring_base, sf)
-#define FUSED_FAM(F)                          \
-  {                                           \
-    if (h1p == 256) FUSED(F, 256, 4);         \
-    else FUSED(F, 416, 5);                    \
+#define FUSED_FAM(F)                                 \
+  {                                                  \
+    if (ng1) {                                       \
+      if (h1p == 256) FUSED(F, 1, 256, 4, 8);        \
+      else FUSED(F, 1, 416, 5, 8);                   \
+    } else {                                         \
+      if (h1p == 256) FUSED(F, 0, 256, 4, 8);        \
+      else FUSED(F, 0, 416, 5, 8);                   \
+    }                                                \
   }
   switch (P.fam) {
     case RLMD_COIN: FUSED_FAM(RLMD_COIN); break;
     case RLMD_DICE: FUSED_FAM(RLMD_DICE); break;
     case RLMD_GBM: FUSED_FAM(RLMD_GBM); break;
-    case RLMD_DICE_SH: FUSED_FAM(RLMD_DICE_SH); break;
-    default: FUSED_FAM(RLMD_MARKET); break;
+    case RLMD_DICE_SH:
+      if (h1p == 256) FUSED(RLMD_DICE_SH, 1, 256, 4, 8);
+      else FUSED(RLMD_DICE_SH, 1, 416, 5, 8);
+      break;
+    default:
+      if (sp == 16) {
+        if (h1p == 256) FUSED(RLMD_MARKET, 0, 256, 4, 16);
+        else FUSED(RLMD_MARKET, 0, 416, 5, 16);
+      } else {
+        FUSED_FAM(RLMD_MARKET);
+      }
+      break;
   }
 #undef FUSED_FAM
 #undef FUSED

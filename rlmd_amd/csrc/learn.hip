@@ -1347,7 +1347,7 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   if (!random && !window && ag && rlmd::fused_act_supported(ag->cfg) && rlmd::env_act_fusable(env)) {
     rlmd::actrows::fused_shape(ag->cfg, h1p, nb);
     sp = ag->cfg.state_dim <= 8 ? 8 : 16;
-    fused = sp == 8 && ((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5));
+    fused = (sp == 8 || sp == 16) && ((h1p == 256 && nb == 4) || (h1p == 416 && nb == 5));
     if (fused)
       fa = rlmd::fused_act_args(ag->cfg, obs, N, actions, ag->params + ag->off_actor, ag->actor,
                                 (const unsigned short*)rlmd::copy_wc(ag, rlmd::SLOT_ACTOR), 0,

@@ -13,9 +13,11 @@ envs/dice_roll_envs.py:153-524, envs/dice_roll_sh_envs.py:160-645,
 envs/gbm_envs.py:147-515, envs/market_envs.py:133-202 / :283-358 / :440-528
 (D1), dones tools/env_resources.py:26-200.
 
-Shapes the fused kernel does not instantiate (action_dim > 2: the C investors
-and Dice_SH B/C) run the two-launch path (acting kernel + env_train_kernel);
-the test asserts which path ran (rlmd_train_last_fused) and checks both.
+Two gambles / assets and market Dx windows run the kernel's run-time-n
+instantiations (WIDE).  Shapes the fused kernel does not instantiate
+(action_dim > 2: the C investors and Dice_SH B/C) run the two-launch path
+(acting kernel + env_train_kernel); the test asserts which path ran
+(rlmd_train_last_fused) and checks both.
 
 Fused vs unfused: the same seeded loop with rlmd_train_set_fused(1) and (0),
 learning on (K = 1), must produce bit-identical rings, wealth and parameters
@@ -43,30 +45,47 @@ def _lib():
     return _abi.lib()
 
 
-def _trainer(dev, golden, env, inv, algo, N, T, k=0, seed=11):
+def _trainer(dev, golden, env, inv, algo, N, T, k=0, seed=11, n=1, obs_days=1):
     from rlmd_amd.trainer import VecTrainer
 
     kw = {}
-    if env == "market":  # one asset: stooq_usei's first column
-        kw = _market_kw(golden, 1)
-        kw["prices"] = np.ascontiguousarray(kw["prices"][:, :1])
-    return VecTrainer(env=env, investor=inv, n_lanes=N, algo=algo, k_updates=k, seed=seed, init_seed=seed,
-                      warmup_steps=0, smoothing_window=0, replay_capacity=N * T, precision="bf16", device=dev,
-                      **kw), kw
+    if env == "market":  # n assets: stooq_usei's first n columns
+        kw = _market_kw(golden, obs_days)
+        kw["prices"] = np.ascontiguousarray(kw["prices"][:, :n])
+    return VecTrainer(env=env, investor=inv, n_lanes=N, n_gambles=n, algo=algo, k_updates=k, seed=seed,
+                      init_seed=seed, warmup_steps=0, smoothing_window=0, replay_capacity=N * T, precision="bf16",
+                      device=dev, **kw), kw
+
+
+# the fused kernel's run-time-n instantiations (act_env_kernel<F, 0, ...>): two
+# gambles / assets, and market Dx observation windows at the 16-float staging
+# pitch (gbm_envs.py:147-212's n-gamble branches, market_envs.py:611-682)
+WIDE = [("gbm", "A", 2, 1), ("coin", "A", 2, 1), ("dice", "A", 2, 1), ("market", "A", 2, 1),
+        ("market", "A", 1, 5), ("market", "B", 1, 5), ("market", "A", 2, 3)]
 
 
 @pytest.mark.parametrize("algo", ["SAC", "TD3"])
 @pytest.mark.parametrize("env,inv", CASES)
 def test_policy_steps_match_oracle(golden, dev, env, inv, algo):
+    _replay_policy_steps(golden, dev, env, inv, algo, 1, 1)
+
+
+@pytest.mark.parametrize("algo", ["SAC", "TD3"])
+@pytest.mark.parametrize("env,inv,n,obs_days", WIDE)
+def test_wide_shapes_match_oracle(golden, dev, env, inv, n, obs_days, algo):
+    _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days)
+
+
+def _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days):
     N, T, seed = 4000, 16, 11  # 4000 lanes: a ragged last 64-lane block
     _lib().rlmd_train_set_fused(1)
-    tr, kw = _trainer(dev, golden, env, inv, algo, N, T, seed=seed)
-    ora = oe.OracleVecEnv(FAMS[env], INVS[inv], N, 1, seed=seed, **kw)
+    tr, kw = _trainer(dev, golden, env, inv, algo, N, T, seed=seed, n=n, obs_days=obs_days)
+    ora = oe.OracleVecEnv(FAMS[env], INVS[inv], N, n, seed=seed, **kw)
     obs = ora.reset()
     tr.episode_log(64)
     at = 1e-45 if env == "market" else 1e-30
     length = np.ones(N, dtype=np.int64)
-    expect_fused = ora.A <= 2 and ora.S <= 8
+    expect_fused = ora.A <= 2 and (ora.S <= 8 or (env == "market" and ora.S <= 16))
     ended = 0
     for t in range(T):
         tr.step()
@@ -103,15 +122,16 @@ def test_policy_steps_match_oracle(golden, dev, env, inv, algo):
 
 
 @pytest.mark.parametrize("algo", ["SAC", "TD3"])
-@pytest.mark.parametrize("env,inv", [("coin", "B"), ("dice", "A"), ("gbm", "A"), ("dice_sh", "INSURED"),
-                                     ("dice_sh", "A"), ("market", "B")])
-def test_fused_equals_unfused(golden, dev, env, inv, algo):
+@pytest.mark.parametrize("env,inv,n,obs_days", [("coin", "B", 1, 1), ("dice", "A", 1, 1), ("gbm", "A", 1, 1),
+                                                ("dice_sh", "INSURED", 1, 1), ("dice_sh", "A", 1, 1),
+                                                ("market", "B", 1, 1), ("gbm", "A", 2, 1), ("market", "A", 1, 5)])
+def test_fused_equals_unfused(golden, dev, env, inv, n, obs_days, algo):
     N, T = 2048, 12
     out = []
     try:
         for fused in (1, 0):
             _lib().rlmd_train_set_fused(fused)
-            tr, _ = _trainer(dev, golden, env, inv, algo, N, T, k=1, seed=5)
+            tr, _ = _trainer(dev, golden, env, inv, algo, N, T, k=1, seed=5, n=n, obs_days=obs_days)
             for t in range(T):
                 tr.step()
                 assert _lib().rlmd_train_last_fused() == fused
