@@ -106,7 +106,7 @@ CONFIGS = {
 }
 
 
-def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H=256, B=512, topk=256):
+def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H=256, B=512, topk=256, seed=420):
     """The same loop on the host: CPU oracle (oracle/envs.py + oracle/learn.py,
     the restatement pinned to the reference) — NumPy env over all lanes,
     torch-CPU policy forward, a replay ring of `replay` transitions (the C2
@@ -120,14 +120,14 @@ def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H
     from rlmd_amd.agent import reference_init
 
     torch.set_num_threads(threads)
-    env = oe.OracleVecEnv(oe.GBM, oe.INV_A, lanes, 1, seed=420)
-    init = reference_init("SAC", S, A, H, H, seed=420)
+    env = oe.OracleVecEnv(oe.GBM, oe.INV_A, lanes, 1, seed=seed)
+    init = reference_init("SAC", S, A, H, H, seed=seed)
     lay, n = ol.layout("SAC", S, A, H, H)
     names = {nm: [x[0] for x in lay[nm]] for nm in ("actor", "critic_1", "critic_2")}
     p = ol.flatten({nm: dict(zip(names[nm], [t.numpy() for t in init[nm]])) for nm in names}, lay, n)
     t = ol.flatten({nm: dict(zip(names[nm], [t.numpy() for t in init["target_" + nm]])) for nm in names}, lay, n)
     learner = ol.OracleLearner("SAC", S, A, H, H, B, topk, "MSE", p, t)
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     obs = env.reset()
     cap = max(replay, lanes)
     ring_s, ring_s2 = np.zeros((cap, S), np.float32), np.zeros((cap, S), np.float32)
@@ -156,10 +156,38 @@ def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H
         el = time.perf_counter() - t0
         if el >= seconds:
             break
-    return {"value": lanes * steps / el, "unit": "env steps/sec", "cores": threads, "kind": "port",
+    return {"value": lanes * steps / el, "steps": steps, "elapsed_s": el, "unit": "env steps/sec", "cores": threads,
+            "kind": "port",
             "sample": f"{steps} vector steps x {lanes} GBM lanes, SAC 256/256 fp32, K={k_updates} updates "
                       f"of B={B} per vector step from a {cap}-row ring (oracle/envs.py + oracle/learn.py on "
                       f"torch-CPU, {threads} thread(s)), {el:.1f} s"}
+
+
+def cpu_baseline_seeds(lanes, k_updates, seconds, procs, replay=1 << 20):
+    """one independent seed per host core — `procs` single-threaded
+    worker processes (bench.py --cpu-worker, started as children: they never touch
+    the GPU) each run the cpu_baseline loop on their own seed at the full lane count;
+    value = all workers' env steps / the longest worker's time."""
+    import subprocess
+
+    env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", "--cpu-seconds", str(seconds),
+           "--k-updates", str(k_updates), "--lanes", str(lanes), "--replay", str(replay)]
+    ps = [subprocess.Popen(cmd + ["--seed", str(420 + i)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                           env=env, text=True) for i in range(procs)]
+    res = []
+    for pr in ps:
+        out, _ = pr.communicate(timeout=seconds * 4 + 300)
+        if pr.returncode != 0:
+            raise RuntimeError("cpu baseline worker failed")
+        res.append(json.loads(out.strip().splitlines()[-1]))
+    steps = sum(r["steps"] for r in res)
+    el = max(r["elapsed_s"] for r in res)
+    return {"value": lanes * steps / el, "unit": "env steps/sec", "cores": procs, "kind": "port",
+            "sample": f"{procs} independent seeds, one single-threaded process per host core, each {lanes} GBM "
+                      f"lanes, SAC 256/256 fp32, K={k_updates} updates of B=512 per vector step from a "
+                      f"{max(replay, lanes)}-row ring (oracle/envs.py + oracle/learn.py on torch-CPU): "
+                      f"{steps} vector steps in total, longest worker {el:.1f} s"}
 
 
 def load_traffic(kernel, config, lanes):
@@ -364,7 +392,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
                     help="the N-rank launch path with a host stand-in trainer (gloo, no GPU): plumbing test only")
+    ap.add_argument("--cpu-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--seed", type=int, default=420, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.cpu_worker:  # one seed of the per-core CPU baseline (never imports the GPU library)
+        r = cpu_baseline(args.lanes or 65536, args.k_updates, args.cpu_seconds, 1, replay=args.replay or (1 << 20),
+                         seed=args.seed)
+        print(json.dumps(r), flush=True)
+        return 0
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
@@ -549,7 +584,7 @@ def main():
         if not args.no_cpu_baseline and world == 1 and args.config == "c2":
             # all host cores of this GPU's share (16 on the box), and one core
             allc = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline(N, K, args.cpu_seconds, allc, replay=replay)
+            out["cpu_baseline"] = cpu_baseline_seeds(N, K, args.cpu_seconds, allc, replay=replay)
             out["cpu_baseline_1core"] = cpu_baseline(N, K, args.cpu_seconds, 1, replay=replay)
         else:
             out["cpu_baseline"] = None
