@@ -405,6 +405,15 @@ def main():
         sys.exit(spawn_ranks(args.gpus))
     if args.dry_run:
         return dry_run(args)
+    # the CPU baseline runs first, before this process opens the GPU: its worker
+    # processes import torch, and the box counts every process holding the device
+    cpu_lines = None
+    if not args.no_cpu_baseline and int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.config == "c2":
+        cfg0 = CONFIGS[args.config]
+        n0, rep0 = args.lanes or cfg0["lanes"], args.replay or cfg0["replay"]
+        allc = min(16, os.cpu_count() or 1)  # this GPU's host-core share on the box
+        cpu_lines = (cpu_baseline_seeds(n0, args.k_updates, args.cpu_seconds, allc, replay=rep0),
+                     cpu_baseline(n0, args.k_updates, args.cpu_seconds, 1, replay=rep0))
 
     import torch
     import torch.distributed as dist
@@ -581,11 +590,9 @@ def main():
                               "unit": "TFLOP/s", "frac": (mfma_tf or 0) / (BF16_PEAK_TFLOPS if args.precision == "bf16" else 157.3),
                               "algorithmic_flops_per_step": flops, "avg_phase_ms": learn_ms},
         }
-        if not args.no_cpu_baseline and world == 1 and args.config == "c2":
-            # all host cores of this GPU's share (16 on the box), and one core
-            allc = min(16, os.cpu_count() or 1)
-            out["cpu_baseline"] = cpu_baseline_seeds(N, K, args.cpu_seconds, allc, replay=replay)
-            out["cpu_baseline_1core"] = cpu_baseline(N, K, args.cpu_seconds, 1, replay=replay)
+        if cpu_lines is not None:
+            # all host cores of this GPU's share (16 on the box), one seed each; and one core
+            out["cpu_baseline"], out["cpu_baseline_1core"] = cpu_lines
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
