@@ -389,7 +389,9 @@ int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
  * Phase 1 is the env kernel's own begin / end (the fused acting + env kernel
  * when the step fused); rlmd_agent_act's fused acting kernel adds its own
  * begin / end to phase 0.
- * enable(1) resets the counters; read() synchronises and returns the summed
+ * enable(1) resets the counters and records every phase; enable(2) records
+ * only phase 1 (events attached to the env kernel's dispatch, no markers on the
+ * stream); enable(0) stops.  read() synchronises and returns the summed
  * milliseconds and the number of timed launches per phase. */
 int rlmd_profile_enable(int32_t on);
 int rlmd_profile_read(double* ms_out3, int64_t* count_out3);
