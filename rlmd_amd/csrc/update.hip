@@ -44,15 +44,20 @@ constexpr int TW = 32;  // tile edge (fc2.weight tiles TW x TW, fc1 blocks of TW
 // three workgroups (slot 0: tile (0, 0), 1: tile (0, 1), 2: the first fc1 block)
 __device__ unsigned long long g_ts_upd[64];
 __device__ unsigned long long g_ts_aupd[128];
+#ifdef RLMD_TIMING_WINDOWS  // entry / exit windows only: the phase stamps perturb the register allocation
+#define RLMD_TS_ON(i) ((i) >= 14)
+#else
+#define RLMD_TS_ON(i) true
+#endif
 #define RLMD_TSU(i)                                                                       \
   do {                                                                                    \
-    if (threadIdx.x == 0 && ts_slot >= 0)                                                 \
+    if (RLMD_TS_ON(i) && threadIdx.x == 0 && ts_slot >= 0)                                \
       g_ts_upd[ts_slot * 16 + (i)] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
   } while (0)
 // actor step: cycles (i < 14) and the constant-rate clock (i = 14, 15: entry / exit)
 #define RLMD_TSA(i)                                                                        \
   do {                                                                                     \
-    if (threadIdx.x == 0 && ts_slot >= 0)                                                  \
+    if (RLMD_TS_ON(i) && threadIdx.x == 0 && ts_slot >= 0)                                 \
       g_ts_aupd[ts_slot * 16 + (i)] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
   } while (0)
 #else
@@ -191,14 +196,17 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   float* part = reinterpret_cast<float*>(smem + ULds::part);
   const RowDims& d = a.d;
   const NetOff& co = a.co;
-  const int per = a.n_w2 + a.n_w1;
+  // per critic: fc2.weight tiles, fc1 blocks, then head workgroups (b2 / w3 of 32
+  // fc2 rows each, b3 on the first)
+  const int per = a.n_w2 + a.n_w1 + a.ti;
   const int g = blockIdx.x / per, t = blockIdx.x - g * per;
   const int B = d.B, H1 = d.H1, H2 = d.H2, H1p = d.H1p, H2p = d.H2p, X = d.X;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nrb = (B + 15) / 16;
-  const bool w2tile = t < a.n_w2;
-  const int i0 = w2tile ? (t / a.tj) * TW : 0, j0 = w2tile ? (t % a.tj) * TW : (t - a.n_w2) * TW;
-  const bool first_col = w2tile && (t % a.tj) == 0;
+  const bool w2tile = t < a.n_w2, first_col = t >= a.n_w2 + a.n_w1;  // first_col: a head workgroup
+  const int i0 = w2tile ? (t / a.tj) * TW : first_col ? (t - a.n_w2 - a.n_w1) * TW : 0;
+  const int j0 = w2tile ? (t % a.tj) * TW : first_col ? 0 : (t - a.n_w2) * TW;
+  const bool w1blk = !w2tile && !first_col;
   const int64_t pbase = (int64_t)g * co.size;  // this critic's parameters in the Adam base
   const bool polyak = adam_polyak(a.adam);
   const CopyDst cd = copy_dst(a.adam, g);
@@ -279,9 +287,9 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   {
     const int c = i0 + (tid & 31);
     if (first_col && tid < 64 && c < H2) xpi = (int)(pbase + (tid < 32 ? co.b2 + c : co.w3 + c));
-    if (first_col && tid == 64 && t == 0) xpi = (int)(pbase + co.b3);
+    if (first_col && tid == 64 && i0 == 0) xpi = (int)(pbase + co.b3);
     const int jj = tid & 31, ci = tid >> 5, jr = j0 + jj;
-    if (!w2tile && tid < 32 * 9 && (ci < X || ci == 8) && jr < H1)
+    if (w1blk && tid < 32 * 9 && (ci < X || ci == 8) && jr < H1)
       xpi = (int)(pbase + (ci == 8 ? co.b1 + jr : co.w1 + (int64_t)jr * X + ci));
   }
   const AdamIn xin = adam_load(a.adam, xpi, polyak);
@@ -296,7 +304,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int e = tid + q * NT, r = e >> 3, c = e & 7;
-      xv[q] = rlmd_ldf(rx, (int64_t)r * X + c, !w2tile && r < B && c < X);
+      xv[q] = rlmd_ldf(rx, (int64_t)r * X + c, w1blk && r < B && c < X);
     }
     const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
     const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.u1[g], (int64_t)nrb * H1p * 16 * 4);
@@ -304,7 +312,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     for (int q = 0; q < 8; ++q) {
       const int r = 32 * p + 4 * q;
       u1v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             ru, (!w2tile && r < nrb * 16 && j < H1p) ? (int)(rp_idx(r, H1p, j) * 4)
+                                             ru, (w1blk && r < nrb * 16 && j < H1p) ? (int)(rp_idx(r, H1p, j) * 4)
                                                                                         : 0x7fffffff, 0, 0));
     }
   }
@@ -375,10 +383,10 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     __syncthreads();
     tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
     RLMD_TSU(5);
-    if (first_col) {
+  } else if (first_col) {
+    {
       // ---- db2[i] = w3[i] sum_b dq[b] [h2 > 0], dW3[i] = sum_b dq[b] h2[b, i]
       //      (thread: column i0 + tid % 32, rows [32 p, 32 p + 32) of part p = tid / 32)
-      __syncthreads();  // part reused
       const int ci = tid & 31, p = tid >> 5;
       float sm = 0.f, sh = 0.f;
 #pragma unroll
@@ -407,7 +415,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
         for (int q = 0; q < 16; ++q) v += part[q * 64 + tid];
         step(xpi, tid < 32 ? v * w3c : v, xin);
       }
-      if (t == 0) {  // db3 = sum_b dq[b] (thread 64)
+      if (i0 == 0) {  // db3 = sum_b dq[b] (thread 64)
         float s3[1] = {dqs[tid]};
         float mx[1] = {-INFINITY};
         block_allreduce<1, 0>(s3, mx, reinterpret_cast<float*>(smem + ULds::red));
@@ -973,7 +981,7 @@ int critic_update_launch(const CritUpdArgs& a, hipStream_t st) {
   RLMD_CHECK(d.X <= 8, "critic update: critic input width up to 8");
   RLMD_CHECK(a.tj == d.H1p / TW && a.ti * TW >= d.H2p && a.n_w2 == a.ti * a.tj && a.n_w1 == d.H1p / TW,
              "critic update: tile grid inconsistent with the widths");
-  const dim3 grid(2 * (a.n_w2 + a.n_w1));
+  const dim3 grid(2 * (a.n_w2 + a.n_w1 + a.ti));
   if (d.prec == RLMD_BF16)
     hipLaunchKernelGGL(critic_update_kernel<RLMD_BF16>, grid, dim3(NT), ULds::total, st, a);
   else

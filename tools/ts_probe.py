@@ -25,7 +25,8 @@ def build():
     tobjs = []
     for src in timed:
         obj = os.path.join(OUT, src.replace(".hip", "_ts.o"))
-        subprocess.check_call([b.HIPCC, *b.FLAGS, *b.PER_FILE.get(src, b.DEFAULT_EXTRA), "-DRLMD_TIMING", "-c",
+        extra = ["-DRLMD_TIMING_WINDOWS"] if "--windows" in sys.argv else []
+        subprocess.check_call([b.HIPCC, *b.FLAGS, *b.PER_FILE.get(src, b.DEFAULT_EXTRA), "-DRLMD_TIMING", *extra, "-c",
                                os.path.join(b.CSRC, src), "-o", obj])
         tobjs.append(obj)
     objs = [os.path.join(b.BUILD, os.path.splitext(s)[0] + ".o") for s in b.SOURCES if s not in timed]
