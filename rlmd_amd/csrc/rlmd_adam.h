@@ -14,6 +14,7 @@
 #include <stdint.h>
 
 #include "learn_kernels.h"
+#include "rlmd_common.h"
 
 namespace rlmd {
 
@@ -52,9 +53,9 @@ __device__ __forceinline__ void store_copy(void* base, int64_t i, float v, int b
   if (bf16) {
     unsigned u = __float_as_uint(v);
     u += 0x7fffu + ((u >> 16) & 1u);  // RNE (finite weights)
-    static_cast<unsigned short*>(base)[i] = (unsigned short)(u >> 16);
+    rlmd_st_wt(static_cast<unsigned short*>(base) + i, (unsigned short)(u >> 16));
   } else {
-    static_cast<float*>(base)[i] = v;
+    rlmd_st_wt(static_cast<float*>(base) + i, v);
   }
 }
 
@@ -101,15 +102,15 @@ __device__ __forceinline__ void adam_core(const AdamArgs& a, int i, float g, con
   float m = in.m, v = in.v;
   m = m + (1.f - b1) * (g - m);
   v = v * b2 + (1.f - b2) * g * g;
-  a.m[i] = m;
-  a.v[i] = v;
+  rlmd_st_wt(a.m + i, m);
+  rlmd_st_wt(a.v + i, v);
   const float denom = sqrtf(v) / a.bc2_sqrt + eps;
   p = in.p - a.step_size * (m / denom);
-  a.p[i] = p;
+  rlmd_st_wt(a.p + i, p);
   tv = 0.f;
   if (polyak) {
     tv = a.tau * p + (1.f - a.tau) * in.t;
-    a.target[i] = tv;
+    rlmd_st_wt(a.target + i, tv);
   }
 }
 

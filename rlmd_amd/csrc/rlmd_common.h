@@ -125,6 +125,35 @@ __device__ __forceinline__ float rlmd_ldf(__amdgpu_buffer_rsrc_t r, int64_t idx,
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? (int)(idx * 4) : 0x7fffffff, 0, 0));
 }
 
+// Write-through stores for data the next kernel reads (optimiser state, compute
+// copies, row-packed activations, bases): a device-scope store (sc1) sends each
+// line on to memory as it is written, instead of leaving it dirty in the XCD's
+// L2 for the release at the end of the kernel, which writes every dirty line
+// back after the last workgroup has finished (≈1 µs per MB at the update
+// kernels' sizes, on the critical path of every launch).
+#ifndef RLMD_WT_STORES
+#define RLMD_WT_STORES 1
+#endif
+#if RLMD_WT_STORES
+#define RLMD_WT_AUX 16  // buffer-store cache policy: sc1 (device scope)
+#else
+#define RLMD_WT_AUX 0
+#endif
+template <class T>
+__device__ __forceinline__ void rlmd_st_wt(T* p, T v) {
+#if RLMD_WT_STORES
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+// 16 bytes (16-byte aligned) as two 8-byte device-scope stores
+__device__ __forceinline__ void rlmd_st_wt16(void* p, float a, float b, float c, float d) {
+  uint64_t* q = static_cast<uint64_t*>(p);
+  rlmd_st_wt(q, (uint64_t)__float_as_uint(a) | ((uint64_t)__float_as_uint(b) << 32));
+  rlmd_st_wt(q + 1, (uint64_t)__float_as_uint(c) | ((uint64_t)__float_as_uint(d) << 32));
+}
+
 __device__ inline uint64_t rlmd_block_bitonic(uint64_t key, int n, uint64_t* lds) {
   const int i = threadIdx.x;
   for (int k = 2; k <= n; k <<= 1) {

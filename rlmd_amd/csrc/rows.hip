@@ -366,13 +366,13 @@ __device__ __forceinline__ void store_rp_rows(typename CT<PREC>::T* base, int64_
     for (int q = 0; q < (MR * TS) / 16; ++q)
       if (4 * q < nw)
         __builtin_amdgcn_raw_buffer_store_b128(u32x4{w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]}, rs, off + 16 * q,
-                                               0, 0);
+                                               0, RLMD_WT_AUX);
   } else if (nw == 2) {
-    if constexpr ((MR * TS) / 4 >= 2) __builtin_amdgcn_raw_buffer_store_b64(u32x2{w[0], w[1]}, rs, off, 0, 0);
+    if constexpr ((MR * TS) / 4 >= 2) __builtin_amdgcn_raw_buffer_store_b64(u32x2{w[0], w[1]}, rs, off, 0, RLMD_WT_AUX);
   } else if (nw == 1) {
-    __builtin_amdgcn_raw_buffer_store_b32(w[0], rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(w[0], rs, off, 0, RLMD_WT_AUX);
   } else {
-    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w[0], rs, off, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b16((unsigned short)w[0], rs, off, 0, RLMD_WT_AUX);
   }
 }
 
@@ -417,8 +417,8 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
 #pragma unroll
         for (int q = 0; q < MR / 4; ++q)
           if (4 * q < nr)
-            *reinterpret_cast<uint32_t*>(m1_out + m1_index(row0 / R, H1p, m.r0 + 4 * q, m.c)) =
-                (uint32_t)(mk[q / 2] >> (32 * (q & 1)));
+            rlmd_st_wt(reinterpret_cast<uint32_t*>(m1_out + m1_index(row0 / R, H1p, m.r0 + 4 * q, m.c)),
+                       (uint32_t)(mk[q / 2] >> (32 * (q & 1))));
       } else {
 #pragma unroll
         for (int rr = 0; rr < (MR < 2 ? MR : 2); ++rr)
@@ -471,7 +471,7 @@ __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdC
 #pragma unroll
         for (int h = 0; h < NHF; ++h) ph[rg][h] = fmaf(v, k.hw[i][h], ph[rg][h]);
       }
-      if (m2_out) *reinterpret_cast<uint32_t*>(m2_out + m2_index(row0 / R, pad32(H2), acc_row(0), col)) = mw;
+      if (m2_out) rlmd_st_wt(reinterpret_cast<uint32_t*>(m2_out + m2_index(row0 / R, pad32(H2), acc_row(0), col)), mw);
       // the lane's 4 rows of h2, contiguous in the row-packed layout
       if (ex && ex->hp2) store_rp_rows<PREC, 4>(ex->hp2, rp_index(row0 / R, pad32(H2), acc_row(0), col), hz, 4);
     }
@@ -720,7 +720,7 @@ __device__ __forceinline__ void basis_pass(Pre<PREC, NBW, MULTI>& pw, const type
         const int r = acc_row(rg);
         v[rg] = (m1s[r * H1p + col] && row0 + r < B) ? acc[i][rg] : 0.f;
       }
-      *reinterpret_cast<f32x4*>(u + rp_index(row0 / R, H1p, acc_row(0), col)) = v;
+      rlmd_st_wt16(u + rp_index(row0 / R, H1p, acc_row(0), col), v[0], v[1], v[2], v[3]);
     }
   }
 }
@@ -928,7 +928,7 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
         f32x4 v;
 #pragma unroll
         for (int rg = 0; rg < 4; ++rg) v[rg] = (k.m1[i][rg] > 0.f && row0 + acc_row(rg) < B) ? acc[i][rg] : 0.f;
-        *reinterpret_cast<f32x4*>(u + rp_index(row0 / R, H1p, acc_row(0), col)) = v;
+        rlmd_st_wt16(u + rp_index(row0 / R, H1p, acc_row(0), col), v[0], v[1], v[2], v[3]);
       }
     }
     return;

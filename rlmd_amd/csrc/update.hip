@@ -42,21 +42,33 @@ constexpr int TW = 32;  // tile edge (fc2.weight tiles TW x TW, fc1 blocks of TW
 #ifdef RLMD_TIMING
 // experiment builds only (tools/ts_probe.py upd): thread-0 s_memtime stamps of
 // three workgroups (slot 0: tile (0, 0), 1: tile (0, 1), 2: the first fc1 block)
-__device__ unsigned long long g_ts_upd[64];
+__device__ unsigned long long g_ts_upd[128];
 __device__ unsigned long long g_ts_aupd[128];
 #ifdef RLMD_TIMING_WINDOWS  // entry / exit windows only: the phase stamps perturb the register allocation
 #define RLMD_TS_ON(i) ((i) >= 14)
 #else
 #define RLMD_TS_ON(i) true
 #endif
+// RLMD_TIMING_DRAIN: the exit stamp waits until the workgroup's stores have completed
+#ifdef RLMD_TIMING_DRAIN
+#define RLMD_TS_DRAIN(i)                              \
+  if ((i) == 15) {                                    \
+    __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    __syncthreads();                                  \
+  }
+#else
+#define RLMD_TS_DRAIN(i)
+#endif
 #define RLMD_TSU(i)                                                                       \
   do {                                                                                    \
+    RLMD_TS_DRAIN(i)                                                                      \
     if (RLMD_TS_ON(i) && threadIdx.x == 0 && ts_slot >= 0)                                \
       g_ts_upd[ts_slot * 16 + (i)] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
   } while (0)
 // actor step: cycles (i < 14) and the constant-rate clock (i = 14, 15: entry / exit)
 #define RLMD_TSA(i)                                                                        \
   do {                                                                                     \
+    RLMD_TS_DRAIN(i)                                                                       \
     if (RLMD_TS_ON(i) && threadIdx.x == 0 && ts_slot >= 0)                                 \
       g_ts_aupd[ts_slot * 16 + (i)] = (i) >= 14 ? __builtin_amdgcn_s_memrealtime() : __builtin_amdgcn_s_memtime(); \
   } while (0)
@@ -108,7 +120,8 @@ __device__ __forceinline__ void tile_copies(const float* pcl, const CopyDst& cd,
 #pragma unroll
       for (int q = 0; q < 4; ++q) w[q] = __float_as_uint(v[q]);
     }
-    *reinterpret_cast<u32x4*>(static_cast<unsigned char*>(dst) + at * (BF ? 2 : 4)) = w;
+    __builtin_amdgcn_raw_buffer_store_b128(w, __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7fffffff, 0x00020000),
+                                           (int)(at * (BF ? 2 : 4)), 0, RLMD_WT_AUX);
   }
 }
 
@@ -215,7 +228,9 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     const int j = pi - (int)pbase - (int)co.w2;
     adam_apply_dst(a.adam, pi, gv, in, polyak, (j >= 0 && j < H1 * H2) ? j : -1, cd);
   };
-  const int ts_slot = blockIdx.x == 0 ? 0 : blockIdx.x == 1 ? 1 : (int)blockIdx.x == a.n_w2 ? 2 : -1;
+  const int bx = blockIdx.x, pb = a.n_w2 + a.n_w1 + a.ti;
+  const int ts_slot = bx == 0 ? 0 : bx == 1 ? 1 : bx == a.n_w2 ? 2 : bx == a.n_w2 + a.n_w1 ? 3 : bx == pb ? 4
+                    : bx == (int)gridDim.x - 1 ? 5 : -1;
   (void)ts_slot;
   RLMD_TSU(14);
   RLMD_TSU(0);
@@ -950,7 +965,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
 #ifdef RLMD_TIMING
 extern "C" int rlmd_debug_ts_upd(unsigned long long* out) {
   if (hipDeviceSynchronize() != hipSuccess) return 2;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_upd), sizeof(unsigned long long) * 64) == hipSuccess ? 0 : 2;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ts_upd), sizeof(unsigned long long) * 128) == hipSuccess ? 0 : 2;
 }
 extern "C" int rlmd_debug_ts_aupd(unsigned long long* out) {
   if (hipDeviceSynchronize() != hipSuccess) return 2;

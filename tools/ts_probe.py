@@ -26,6 +26,7 @@ def build():
     for src in timed:
         obj = os.path.join(OUT, src.replace(".hip", "_ts.o"))
         extra = ["-DRLMD_TIMING_WINDOWS"] if "--windows" in sys.argv else []
+        extra += ["-DRLMD_TIMING_DRAIN"] if "--drain" in sys.argv else []
         subprocess.check_call([b.HIPCC, *b.FLAGS, *b.PER_FILE.get(src, b.DEFAULT_EXTRA), "-DRLMD_TIMING", *extra, "-c",
                                os.path.join(b.CSRC, src), "-o", obj])
         tobjs.append(obj)
@@ -215,18 +216,19 @@ def run_upd():
     env, inv = ("gbm", "A") if algo == "SAC" else ("dice_sh", "A")
     tr = VecTrainer(env, inv, 65536, algo=algo, precision="bf16", warmup_steps=0, smoothing_window=0,
                     replay_capacity=1 << 20, k_updates=1, device="cuda:0")
-    buf = (C.c_ulonglong * 64)()
+    buf = (C.c_ulonglong * 128)()
     rows = []
     for it in range(40):
         tr.step()
         torch.cuda.synchronize()
         lib.rlmd_debug_ts_upd(buf)
         if it >= 10:
-            rows.append(np.array(buf[:], dtype=np.int64).reshape(4, 16))
+            rows.append(np.array(buf[:], dtype=np.int64).reshape(8, 16))
     r = np.stack(rows)
     names = ["entry", "loads issued", "row loss", "rank + dq", "mfma / fc1 sums", "adam", "first-col extras", "end"]
-    t0 = r[:, :3, 14].min(axis=1)
-    for slot, label in enumerate(["tile (0,0)", "tile (0,1)", "fc1 block 0"]):
+    t0 = r[:, :6, 14].min(axis=1)
+    for slot, label in enumerate(["tile (0,0)", "tile (0,1)", "fc1 block 0", "head wg 0", "critic 2 tile (0,0)",
+                                  "last workgroup"]):
         t = r[:, slot]
         w0, w1 = np.median(t[:, 14] - t0) / 100, np.median(t[:, 15] - t0) / 100
         print(f"{label}: total {np.median(t[:, 7] - t[:, 0]):.0f} cycles, window {w0:6.2f} .. {w1:6.2f} us")
