@@ -97,6 +97,68 @@ __device__ void gather_row(const rlmd::ReplayView& rb, int64_t row, int i, float
   if (done) done[i] = rb.done[row];
   if (eff) eff[i] = e;
 }
+// Single-step rows (the training loop's case): every load of the row issued
+// before its first store. In gather_row's element loops each store is counted
+// in vmcnt and the outputs may alias the ring as far as the compiler knows, so
+// every element waited on its own scattered-row round trip (S + S + A + 2 of
+// them per row). Clamped indices keep the loads branch-free; the stores are
+// write-through (the next kernel reads them).
+__device__ __forceinline__ void gather_row1(const rlmd::ReplayView& rb, int64_t row, int i, float* s, float* a,
+                                            float* r, float* s2, uint8_t* done, float* xsa, int32_t* eff) {
+  constexpr int C = 8;
+  const int S = rb.S, A = rb.A, X = S + A;
+  const float* st = rb.state + row * S;
+  const float* ns = rb.next_state + row * S;
+  const float* ac = rb.action + row * A;
+  float sv[C], nv[C], av[C];
+#pragma unroll
+  for (int q = 0; q < C; ++q) {
+    sv[q] = st[q < S ? q : S - 1];
+    nv[q] = ns[q < S ? q : S - 1];
+    av[q] = ac[q < A ? q : A - 1];
+  }
+  const float rew = rb.reward[row];
+  const uint8_t dn = rb.done[row];
+#pragma unroll
+  for (int q = 0; q < C; ++q) {
+    if (q < S) {
+      if (s) rlmd_st_wt(s + (int64_t)i * S + q, sv[q]);
+      if (xsa) rlmd_st_wt(xsa + (int64_t)i * X + q, sv[q]);
+      if (s2) rlmd_st_wt(s2 + (int64_t)i * S + q, nv[q]);
+    }
+    if (q < A) {
+      if (a) rlmd_st_wt(a + (int64_t)i * A + q, av[q]);
+      if (xsa) rlmd_st_wt(xsa + (int64_t)i * X + S + q, av[q]);
+    }
+  }
+  if (r) rlmd_st_wt(r + i, rew);
+  if (done) rlmd_st_wt(done + i, dn);
+  if (eff) rlmd_st_wt(eff + i, (int32_t)1);
+  // wider rows (market Dx observations, many-action investors): the rest per chunk
+  for (int k0 = C; k0 < S || k0 < A; k0 += C) {
+#pragma unroll
+    for (int q = 0; q < C; ++q) {
+      const int k = k0 + q;
+      sv[q] = st[k < S ? k : S - 1];
+      nv[q] = ns[k < S ? k : S - 1];
+      av[q] = ac[k < A ? k : A - 1];
+    }
+#pragma unroll
+    for (int q = 0; q < C; ++q) {
+      const int k = k0 + q;
+      if (k < S) {
+        if (s) rlmd_st_wt(s + (int64_t)i * S + k, sv[q]);
+        if (xsa) rlmd_st_wt(xsa + (int64_t)i * X + k, sv[q]);
+        if (s2) rlmd_st_wt(s2 + (int64_t)i * S + k, nv[q]);
+      }
+      if (k < A) {
+        if (a) rlmd_st_wt(a + (int64_t)i * A + k, av[q]);
+        if (xsa) rlmd_st_wt(xsa + (int64_t)i * X + S + k, av[q]);
+      }
+    }
+  }
+}
+
 constexpr int kMaxRounds = 64;
 constexpr int kSortPopulation = 8192;  // M at or below: sort-based subset
 
@@ -199,7 +261,10 @@ __global__ void __launch_bounds__(kSampleThreads)
   if (i >= B || i < part * per || i >= (part + 1) * per) return;
   const int64_t row = cand[i];
   if (idx_out) idx_out[i] = row;
-  gather_row(rb, row, i, s, a, r, s2, done, xsa, eff);
+  if (rb.n_steps > 1)
+    gather_row(rb, row, i, s, a, r, s2, done, xsa, eff);
+  else
+    gather_row1(rb, row, i, s, a, r, s2, done, xsa, eff);
 }
 
 __global__ void replay_gather_kernel(rlmd::ReplayView rb, int n, const int64_t* rows, float* s, float* a,
