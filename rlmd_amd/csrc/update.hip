@@ -534,8 +534,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const int t = blockIdx.x;
   // workgroups: fc2.weight tiles, fc1 blocks, head workgroups (b2 and the heads
   // of 32 fc2 rows each), and two critic-statistics workgroups
-  const int n_hd = a.ti, nst = a.cstats.B > 0 ? 2 : 0;
-  const int nwg = a.n_w2 + a.n_w1 + n_hd + nst;
+  // the statistics workgroups do not take part in the arrival count: they read
+  // neither log_alpha nor anything the temperature step writes (learn_cntr already
+  // holds this update's count: critic_update_kernel set it)
+  const int n_hd = a.ti;
+  const int nwg = a.n_w2 + a.n_w1 + n_hd;
   const int sidx = t - (a.n_w2 + a.n_w1 + n_hd);  // >= 0: statistics part
   const int ts_slot = t == 0 ? 0 : t == 1 ? 1 : t == a.n_w2 ? 2 : sidx == 0 ? 3 : t == a.n_w2 + a.n_w1 ? 4 : sidx == 1 ? 5 : -1;
   (void)ts_slot;
@@ -585,26 +588,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     // this update's critic statistics (rlmd_loss.h), off the critical path
     critic_loss_block<NT / 64>(a.cstats, reinterpret_cast<uint64_t*>(smem + ALds::runs),
                                reinterpret_cast<int*>(smem + ALds::rank), red, sidx);
-    // the actor loss of every row, should this workgroup arrive last
-    const bool in = tid < B;
-    const int64_t nB = (int64_t)B * 4;
-    const float q1r = rlmd_ldf(rlmd_rsrc(a.qn[0], nB), tid, in);
-    const float q2r = rlmd_ldf(rlmd_rsrc(a.qn[1], a.nq > 1 ? nB : 0), tid, in);
-    lpv = rlmd_ldf(rlmd_rsrc(a.logp, sac ? nB : 0), tid, in);
-    const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
-    alpha = sac ? expf(st->log_alpha) : 0.f;
-    const float q1 = q1r + qb0, q2 = a.nq > 1 ? q2r + qb1 : q1;
-    v = sac ? fminf(q1, q2) - alpha * lpv : q1;
-    kk = a.topk ? (B < a.k ? B : a.k) : B;
-    sel = in;
-    if (a.topk) {
-      int* rank_of = reinterpret_cast<int*>(smem + ALds::rank);
-      block_rank<NT / 64>(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
-                 reinterpret_cast<uint64_t*>(smem + ALds::runs), rank_of);
-      sel = in && rank_of[tid] < kk;
-    }
     RLMD_TSA(3);
-    temperature_step();
     RLMD_TSA(4);
     RLMD_TSA(15);
     return;
