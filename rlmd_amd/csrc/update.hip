@@ -545,11 +545,16 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   RLMD_TSA(14);
   RLMD_TSA(0);
   LearnState* st = a.st;
-  // this workgroup has read log_alpha; returns true on the last one to arrive
+  // this workgroup has read log_alpha; returns true on the last one to arrive.
+  // Relaxed: no data crosses workgroups through the counter (the last arriver
+  // steps the temperature from its own all-rows sums, and every arriver's
+  // log_alpha load has already been consumed). An agent-scope acquire / release
+  // would write back and invalidate the XCD's L2 in the middle of every tile's
+  // critical path.
   auto arrive = [&]() {
     __syncthreads();
     if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned old = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       *lastf = old == (unsigned)(nwg - 1);
     }
     __syncthreads();
