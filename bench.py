@@ -36,13 +36,16 @@ BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 
 
 def env_bytes_per_step(S, A, n_assets=0, fused=False):
-    """Algorithmic HBM bytes of one lane-step of the env step + replay insert:
-    action read 4A + obs read 4S + wealth/time read+write 24 + obs write 4S
-    + replay row (s 4S, a 4A, r 4, s' 4S, done 1)  = 8A + 16S + 29;
-    market adds the two f64 price gathers per asset (P_t, P_0): 16 n_assets.
-    Fused into the acting kernel the action never leaves registers (no 4A read):
-    16S + 4A + 29."""
-    return (4 if fused else 8) * A + 16 * S + 29 + 16 * n_assets
+    """Algorithmic HBM bytes of one lane-step of the env step + replay insert.
+
+    fused (the env step in the acting kernel's epilogue, its marginal cost):
+    SURVEY §8(d)'s count, 8A + 12S + 35 = 103 B at C2 — action 4A, f64 wealth
+    read + write 16, i32 time read + write 8, obs write 4S, reward 4, two flag
+    bytes, and the replay row (2S + A + 1) * 4 + 1.  The observation the row's
+    s comes from is read by the acting body, which the marginal excludes.
+    separate (env_train_kernel): the same plus the obs read 4S it does itself.
+    Market adds the two f64 price gathers per asset (P_t, P_0): 16 n_assets."""
+    return 8 * A + 12 * S + 35 + (0 if fused else 4 * S) + 16 * n_assets
 
 
 def act_flops_per_row(S, A, H1, H2, algo):
@@ -120,6 +123,8 @@ def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H
     from rlmd_amd.agent import reference_init
 
     torch.set_num_threads(threads)
+    # the clock starts once the ring holds more than B rows (learn() returns NaN
+    # placeholders before that, algo_sac.py:380-396): every timed step updates
     env = oe.OracleVecEnv(oe.GBM, oe.INV_A, lanes, 1, seed=seed)
     init = reference_init("SAC", S, A, H, H, seed=seed)
     lay, n = ol.layout("SAC", S, A, H, H)
@@ -133,7 +138,7 @@ def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H
     ring_s, ring_s2 = np.zeros((cap, S), np.float32), np.zeros((cap, S), np.float32)
     ring_a, ring_r, ring_d = np.zeros((cap, A), np.float32), np.zeros(cap, np.float32), np.zeros(cap, bool)
     mem = 0
-    steps, t0 = 0, time.perf_counter()
+    steps, t0 = 0, None
     while True:
         with torch.no_grad():
             Pn = learner.nets(learner.P)
@@ -148,6 +153,10 @@ def cpu_baseline(lanes, k_updates, seconds, threads, replay=1 << 20, S=5, A=1, H
         if d[:, 0].any():
             obs[d[:, 0]] = env.reset(d[:, 0])[d[:, 0]]
         filled = min(mem, cap)
+        if filled <= B:
+            continue
+        if t0 is None:
+            t0 = time.perf_counter()
         for _ in range(k_updates):
             idx = rng.choice(filled, B, replace=False)
             learner.learn(ring_s[idx], ring_a[idx], ring_r[idx], ring_s2[idx], ring_d[idx],
@@ -173,21 +182,32 @@ def cpu_baseline_seeds(lanes, k_updates, seconds, procs, replay=1 << 20):
     env = dict(os.environ, OMP_NUM_THREADS="1", MKL_NUM_THREADS="1", HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
     cmd = [sys.executable, os.path.abspath(__file__), "--cpu-worker", "--cpu-seconds", str(seconds),
            "--k-updates", str(k_updates), "--lanes", str(lanes), "--replay", str(replay)]
-    ps = [subprocess.Popen(cmd + ["--seed", str(420 + i)], stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+    ps = [subprocess.Popen(cmd + ["--seed", str(420 + i)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                            env=env, text=True) for i in range(procs)]
     res = []
-    for pr in ps:
-        out, _ = pr.communicate(timeout=seconds * 4 + 300)
-        if pr.returncode != 0:
-            raise RuntimeError("cpu baseline worker failed")
-        res.append(json.loads(out.strip().splitlines()[-1]))
+    try:
+        for i, pr in enumerate(ps):
+            try:
+                out, err = pr.communicate(timeout=seconds * 4 + 300)
+            except subprocess.TimeoutExpired:
+                raise RuntimeError(f"cpu baseline worker {i} timed out")
+            if pr.returncode != 0:
+                tail = "\n".join((err or "").strip().splitlines()[-12:])
+                raise RuntimeError(f"cpu baseline worker {i} failed (rc {pr.returncode}):\n{tail}")
+            res.append(json.loads(out.strip().splitlines()[-1]))
+    finally:  # on any failure, end the workers still running
+        for pr in ps:
+            if pr.poll() is None:
+                pr.kill()
+                pr.wait()
     steps = sum(r["steps"] for r in res)
     el = max(r["elapsed_s"] for r in res)
+    what = "the reference's loop semantics: 1 env, 1 update per env step" if lanes == 1 and k_updates == 1 else \
+        f"{lanes} GBM lanes, K={k_updates} updates of B=512 per vector step"
     return {"value": lanes * steps / el, "unit": "env steps/sec", "cores": procs, "kind": "port",
-            "sample": f"{procs} independent seeds, one single-threaded process per host core, each {lanes} GBM "
-                      f"lanes, SAC 256/256 fp32, K={k_updates} updates of B=512 per vector step from a "
-                      f"{max(replay, lanes)}-row ring (oracle/envs.py + oracle/learn.py on torch-CPU): "
-                      f"{steps} vector steps in total, longest worker {el:.1f} s"}
+            "sample": f"{procs} independent seeds, one single-threaded process per host core, each {what}, "
+                      f"SAC 256/256 fp32 from a {max(replay, lanes)}-row ring (oracle/envs.py + oracle/learn.py on "
+                      f"torch-CPU): {steps} vector steps in total, longest worker {el:.1f} s"}
 
 
 def load_traffic(kernel, config, lanes):
@@ -413,7 +433,11 @@ def main():
         n0, rep0 = args.lanes or cfg0["lanes"], args.replay or cfg0["replay"]
         allc = min(16, os.cpu_count() or 1)  # this GPU's host-core share on the box
         cpu_lines = (cpu_baseline_seeds(n0, args.k_updates, args.cpu_seconds, allc, replay=rep0),
-                     cpu_baseline(n0, args.k_updates, args.cpu_seconds, 1, replay=rep0))
+                     cpu_baseline(n0, args.k_updates, args.cpu_seconds, 1, replay=rep0),
+                     # BASELINE.md's plan: the reference's own loop semantics (one env,
+                     # UTD = 1, single stream), one seed per core and on one core
+                     cpu_baseline_seeds(1, 1, args.cpu_seconds, allc, replay=rep0),
+                     cpu_baseline(1, 1, args.cpu_seconds, 1, replay=rep0))
 
     import torch
     import torch.distributed as dist
@@ -600,7 +624,8 @@ def main():
         }
         if cpu_lines is not None:
             # all host cores of this GPU's share (16 on the box), one seed each; and one core
-            out["cpu_baseline"], out["cpu_baseline_1core"] = cpu_lines
+            out["cpu_baseline"], out["cpu_baseline_1core"] = cpu_lines[:2]
+            out["cpu_baseline_utd1"] = {"all_cores": cpu_lines[2], "1core": cpu_lines[3]}
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

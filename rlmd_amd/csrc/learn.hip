@@ -782,6 +782,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       au.cstats.rank_in = S_.rank1;  // critic_update_kernel wrote them (cu.rank_out)
       au.cstats.keep_actor_slot = 1;   // stats[10]: the actor loss
       au.cstats.keep_logtemp_slot = 1; // stats[11]: the temperature step
+      au.cstats.use_snap = 1;          // log_alpha / Cauchy scales as of the update's start
       au.tj = d.H1p / 32;
       au.ti = d.H2p / 32;
       au.n_w2 = au.ti * au.tj;

@@ -22,6 +22,12 @@ struct LearnState {
   float pad_temp_grad;  // temperature gradient handed from actor_loss to adam
   int32_t nan_update;   // learn_cntr when nan_flag was first set
   uint32_t arrive;      // fused actor update: workgroups done reading log_alpha (update.hip)
+  // pre-step snapshot of the loss scalars, written by critic_update_kernel's
+  // workgroup 0: the fused actor step's statistics workgroups read these while
+  // its last tile workgroup steps log_alpha and statistics part 0 writes the new
+  // Cauchy scales in the same launch (update.hip)
+  float snap_log_alpha;
+  float snap_cauchy[2];
 };
 
 // Per-net parameter offsets (floats) inside a flat buffer, torch nn.Linear
@@ -215,6 +221,7 @@ struct LossArgs {
   float log_noise, grad_scale;
   int32_t keep_actor_slot;  // 1: leave stats[10] (actor loss) alone
   int32_t keep_logtemp_slot;  // 1: leave stats[11] (log temperature) to the temperature step
+  int32_t use_snap;  // 1: log_alpha / Cauchy scales from LearnState's pre-step snapshot
 };
 
 struct CBwdArgs {

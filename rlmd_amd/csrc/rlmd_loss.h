@@ -88,12 +88,14 @@ __device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
   L.eff = (int)__builtin_bit_cast(
       int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, a.eff ? nB : 0), in ? b * 4 : 0x7fffffff, 0, 0));
   L.has_eff = a.eff != nullptr;
+  // the snapshot when another workgroup of the same launch may be writing the
+  // live values (the fused actor step's statistics workgroups, update.hip)
   for (int g = 0; g < 2; ++g) {
     L.tb[g] = a.tb[g][0];
     L.qb[g] = a.qb[g][0];
-    L.cauchy[g] = a.st->cauchy[g];
+    L.cauchy[g] = a.use_snap ? a.st->snap_cauchy[g] : a.st->cauchy[g];
   }
-  L.log_alpha = a.st->log_alpha;
+  L.log_alpha = a.use_snap ? a.st->snap_log_alpha : a.st->log_alpha;
   return L;
 }
 

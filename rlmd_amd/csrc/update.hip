@@ -349,7 +349,14 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       if (blockIdx.x == 0 && a.rank_out && o.in) a.rank_out[tid] = rank_of[tid];  // for the statistics
     }
     dqs[tid] = sel ? a.loss.grad_scale * (g == 0 ? o.dl[0] : o.dl[1]) / (float)kk : 0.f;
-    if (blockIdx.x == 0 && tid == 0) adam_scalar_step(a.adam);  // learn_step_cntr (no temperature here)
+    if (blockIdx.x == 0 && tid == 0) {
+      adam_scalar_step(a.adam);  // learn_step_cntr (no temperature here)
+      // the loss scalars this update started from, for the actor step's statistics
+      // workgroups (they run beside the writers of log_alpha and the Cauchy scales)
+      a.loss.st->snap_log_alpha = cl.log_alpha;
+      a.loss.st->snap_cauchy[0] = cl.cauchy[0];
+      a.loss.st->snap_cauchy[1] = cl.cauchy[1];
+    }
   }
   __syncthreads();
   RLMD_TSU(3);
@@ -533,10 +540,12 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const int nrb = (B + 15) / 16;
   const int t = blockIdx.x;
   // workgroups: fc2.weight tiles, fc1 blocks, head workgroups (b2 and the heads
-  // of 32 fc2 rows each), and two critic-statistics workgroups
-  // the statistics workgroups do not take part in the arrival count: they read
-  // neither log_alpha nor anything the temperature step writes (learn_cntr already
-  // holds this update's count: critic_update_kernel set it)
+  // of 32 fc2 rows each), and two critic-statistics workgroups.
+  // The statistics workgroups do not take part in the arrival count: they read
+  // log_alpha and the Cauchy scales from LearnState's pre-step snapshot
+  // (critic_update_kernel wrote it; LossArgs::use_snap), never the live values
+  // that the last tile workgroup (log_alpha) and statistics part 0 (the Cauchy
+  // scales) write in this launch; learn_cntr already holds this update's count
   const int n_hd = a.ti;
   const int nwg = a.n_w2 + a.n_w1 + n_hd;
   const int sidx = t - (a.n_w2 + a.n_w1 + n_hd);  // >= 0: statistics part
@@ -547,10 +556,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   LearnState* st = a.st;
   // this workgroup has read log_alpha; returns true on the last one to arrive.
   // Relaxed: no data crosses workgroups through the counter (the last arriver
-  // steps the temperature from its own all-rows sums, and every arriver's
-  // log_alpha load has already been consumed). An agent-scope acquire / release
-  // would write back and invalidate the XCD's L2 in the middle of every tile's
-  // critical path.
+  // steps the temperature from its own all-rows sums). Every arriver's log_alpha
+  // load (an atomic load below, so it cannot be moved past the fetch_add) has
+  // been consumed by the actor objective before arrive() is reached. An
+  // agent-scope acquire / release would write back and invalidate the XCD's L2
+  // in the middle of every tile's critical path.
   auto arrive = [&]() {
     __syncthreads();
     if (tid == 0) {
@@ -585,7 +595,9 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         if (sac) st->pad_temp_grad = sm[1] / B * alpha;
         a.stats[10] = -sm[0] / kk;
         adam_scalar_step(a.adam);  // learn_step_cntr, temperature Adam, stats[11]
-        st->arrive = 0u;           // every workgroup has arrived: reset for the next update
+        // every workgroup has arrived: reset for the next update (visible to it
+        // through the kernel boundary)
+        __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   };
@@ -670,7 +682,8 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * 4);
   {
     const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
-    const float log_alpha = sac ? st->log_alpha : 0.f;
+    // must complete before this workgroup's arrive(): the last arriver overwrites it
+    const float log_alpha = sac ? __hip_atomic_load(&st->log_alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
 
     // ---- actor loss over all rows (algo_sac.py:546-562 / algo_td3.py:507-523)
     alpha = sac ? expf(log_alpha) : 0.f;

@@ -23,6 +23,17 @@ MAX_VALUE = {_abi.COIN: 1e18, _abi.DICE: 1e18, _abi.GBM: 1e18, _abi.DICE_SH: 1e1
 MIN_REWARD = {_abi.COIN: 1e-3, _abi.DICE: 1e-3, _abi.GBM: 1e-3, _abi.DICE_SH: 1e-6, _abi.MARKET: 1e-3}
 MAX_ABS_ACTION = 0.99
 
+_SEED_CTR = [0]
+
+
+def private_seed():
+    """A Philox seed for a device env created without one.  Drawn from a private
+    counter, never from np.random: the reference's env constructors consume no
+    NumPy draws, so taking one here would shift the global stream the drivers
+    consume in the reference's order (time_slice, shuffle_data, eval gaps)."""
+    _SEED_CTR[0] += 1
+    return (0x6576616C * _SEED_CTR[0] + 0x2545F491) & 0x7FFFFFFF
+
 
 class VecEnv:
     """N lanes of one reference env class, stepped by one HIP kernel launch."""
@@ -121,7 +132,7 @@ class _SingleEnv:
     investor = None
 
     def __init__(self, n_gambles=1, device="cuda:0", seed=None, **kw):
-        seed = int(np.random.randint(0, 2**31)) if seed is None else seed
+        seed = private_seed() if seed is None else seed
         self._v = VecEnv(self.family, self.investor, 1, n_gambles, seed=seed, device=device, **kw)
         self.n_gambles = n_gambles
         self.reward_range = (MIN_REWARD[self._v.family], np.inf)

@@ -32,9 +32,27 @@ import torch
 
 from . import _abi
 from ._abi import check, ptr, stream_ptr
-from .envs import ENV_CLASSES, VecEnv
+from .envs import ENV_CLASSES, VecEnv, private_seed
 
+# Evaluation envs, reused across the events of one driver run (building one
+# allocates device lanes).  Bounded, and cleared by the drivers when they return
+# (clear_eval_envs), so a run over many env keys does not keep every key's envs
+# and device price tables alive.
 _EVAL_ENVS = {}
+_MARKET_EVAL_ENVS = {}
+_MAX_CACHED = 4
+
+
+def _cache_put(cache, key, value):
+    while len(cache) >= _MAX_CACHED:
+        cache.pop(next(iter(cache)))
+    cache[key] = value
+
+
+def clear_eval_envs():
+    """Drop the cached evaluation envs (the drivers call this when they return)."""
+    _EVAL_ENVS.clear()
+    _MARKET_EVAL_ENVS.clear()
 
 
 def env_class_name(env_id):
@@ -48,9 +66,9 @@ def _eval_env(inputs, n_gambles, n_eval, device):
     key = (cls.family, cls.investor, n_gambles, n_eval, str(device))
     env = _EVAL_ENVS.get(key)
     if env is None:
-        seed = int(inputs.get("eval_seed", np.random.randint(0, 2**31 - 1)))
+        seed = int(inputs.get("eval_seed", private_seed()))
         env = VecEnv(cls.family, cls.investor, n_eval, n_gambles, seed=seed, device=device)
-        _EVAL_ENVS[key] = env
+        _cache_put(_EVAL_ENVS, key, env)
     return env
 
 
@@ -94,9 +112,6 @@ def eval_multiplicative(n_gambles, agent, inputs, eval_log, eval_risk_log, multi
     return {"reward": r, "steps": st, "risk": rk}
 
 
-_MARKET_EVAL_ENVS = {}
-
-
 def _market_eval_env(market_data, investor, obs_days, test_length, n_eval, shuffle, action_days, device):
     from .envs import VecEnv
 
@@ -104,11 +119,11 @@ def _market_eval_env(market_data, investor, obs_days, test_length, n_eval, shuff
     hit = _MARKET_EVAL_ENVS.get(key)
     if hit is not None and hit[0] is market_data:
         return hit[1]
-    seed = int(np.random.randint(0, 2**31 - 1))
+    seed = private_seed()
     env = VecEnv("market", investor, n_eval, market_data.shape[1], seed=seed, prices=market_data,
                  obs_days=obs_days, time_length=test_length, action_days=action_days, shuffle_days=shuffle,
                  sample_days=test_length * action_days + 1, device=device)
-    _MARKET_EVAL_ENVS[key] = (market_data, env)
+    _cache_put(_MARKET_EVAL_ENVS, key, (market_data, env))
     return env
 
 

@@ -18,7 +18,7 @@ import time
 
 import numpy as np
 
-from .config import GYM_ENVS, INPUTS, env_dynamics, input_initialisation
+from .config import GYM_ENVS, INPUTS, env_dynamics, env_tests, input_initialisation, learning_tests
 
 MARKET_FILES = ["stooq_snp.npy", "stooq_usei.npy", "stooq_minor.npy", "stooq_medium.npy", "stooq_major.npy",
                 "stooq_dji.npy", "stooq_full.npy"]
@@ -45,6 +45,9 @@ def load_market_data(key, gym_envs, inputs):
 def run(envs, algo=("SAC",), critic=("MSE",), multi_steps=(1,), inputs=None, gym_envs=None, log=print):
     gym_envs = gym_envs or GYM_ENVS
     inputs = input_initialisation(dict(inputs or INPUTS), list(envs), list(algo), list(critic), list(multi_steps))
+    # main.py:277-280: the input checks before any run (AssertionError on bad inputs)
+    learning_tests(inputs)
+    env_tests(gym_envs, inputs)
     multi_key, sh_key, market_key = env_dynamics(gym_envs)
     from .scripts.rl_market import market_env
     from .scripts.rl_multiplicative import multiplicative_env

@@ -46,6 +46,13 @@ def make_env(gym_envs, key, n_assets, train_length, obs_days, device=None, seed=
 
 
 def market_env(gym_envs, inputs, market_data, obs_days, env=None, agent_factory=None, log=print, device=None):
+    try:
+        return _market_env(gym_envs, inputs, market_data, obs_days, env, agent_factory, log, device)
+    finally:
+        eval_episodes.clear_eval_envs()  # the evaluation envs live for one driver run
+
+
+def _market_env(gym_envs, inputs, market_data, obs_days, env, agent_factory, log, device):
     market_data = np.asarray(market_data, dtype=np.float64)
     n_assets = market_data.shape[1]
     action_days = int(inputs["action_days"])

@@ -35,7 +35,7 @@ from .. import logs
 from ..agent import Agent_sac, Agent_td3
 from ..config import env_dynamics
 from ..envs import ENV_CLASSES
-from ..eval_episodes import agent_shadow_mean, eval_multiplicative
+from ..eval_episodes import agent_shadow_mean, clear_eval_envs, eval_multiplicative
 
 
 def smoothing_func(ratio):
@@ -75,6 +75,13 @@ def make_env(gym_envs, key, n_gambles, device=None, seed=None):
 
 
 def multiplicative_env(gym_envs, inputs, n_gambles, env=None, agent_factory=None, log=print, device=None):
+    try:
+        return _multiplicative_env(gym_envs, inputs, n_gambles, env, agent_factory, log, device)
+    finally:
+        clear_eval_envs()  # the evaluation envs live for one driver run
+
+
+def _multiplicative_env(gym_envs, inputs, n_gambles, env, agent_factory, log, device):
     inputs = {"env_id": gym_envs[str(inputs["ENV_KEY"])][0] + "_n" + str(n_gambles), **inputs}
     _, sh_key, _ = env_dynamics(gym_envs)
     if env is None:

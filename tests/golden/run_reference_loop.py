@@ -8,13 +8,17 @@ _refshim.py; the reference never travels).  Calls
 scripts/rl_multiplicative.multiplicative_env (rl_multiplicative.py:41-457)
 with main.py's gym_envs table and inputs dict (main.py:41-259) widened by
 utils.input_initialisation (tools/utils.py:80-106), one trial, SAC, MSE,
-seeded np.random + torch.  From the saved logs it keeps, per evaluation
+seeded np.random + torch, with --algo (SAC | TD3) and --loss (any of
+main.py:137's critic losses).  From the saved logs it keeps, per evaluation
 (every eval_freq = 1e3 steps, 100 episodes of <= 100 steps at one constant
 deterministic action): the mean leverage (eval_risk_log[..., 3],
-eval_episodes.py:296-297) and the final rewards (eval_log[..., 1]).
+eval_episodes.py:296-297), the final rewards (eval_log[..., 1]) and the whole
+eval risk row (for Dice_SH_InvA column 6 is the safe-haven leverage,
+dice_roll_sh_envs.py:355-362).
 
     python tests/golden/run_reference_loop.py --key 8 --steps 50000 --seed 0
-writes tests/golden/converge_ref_<key>_s<seed>.npz
+writes tests/golden/converge_ref_<key>_s<seed>.npz (SAC / MSE) or
+tests/golden/converge_ref_<key>_<algo>_<loss>_s<seed>.npz otherwise.
 """
 import argparse
 import glob
@@ -36,6 +40,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--threads", type=int, default=1)
+    ap.add_argument("--algo", default="SAC", choices=["SAC", "TD3"])
+    ap.add_argument("--loss", default="MSE")
     a = ap.parse_args()
     _refshim.install()
     import torch
@@ -46,7 +52,7 @@ def main():
 
     inputs = dict(ref_main.inputs)
     inputs.update({"n_trials_mul": 1, "n_cumsteps_mul": float(a.steps), "gpu": "cpu", "buffer_gpu": False})
-    inputs = utils.input_initialisation(inputs, [a.key], ["SAC"], ["MSE"], [1])
+    inputs = utils.input_initialisation(inputs, [a.key], [a.algo], [a.loss], [1])
     inputs["test_agent"] = True
     inputs["ENV_KEY"] = a.key
     import envs.dice_roll_sh_envs as sh_mod
@@ -65,7 +71,8 @@ def main():
             return np.array(obj, *args, **kw)
 
     sh_mod.np = _ArrayFix()
-    out = os.path.join(HERE, f"converge_ref_{a.key}_s{a.seed}.npz")
+    tag = "" if (a.algo, a.loss) == ("SAC", "MSE") else f"_{a.algo}_{a.loss}"
+    out = os.path.join(HERE, f"converge_ref_{a.key}{tag}_s{a.seed}.npz")
     np.random.seed(a.seed)
     torch.manual_seed(a.seed)
     cwd = os.getcwd()
@@ -81,7 +88,7 @@ def main():
             os.chdir(cwd)
     np.savez_compressed(out, key=a.key, seed=a.seed, steps=a.steps, env=ref_main.gym_envs[str(a.key)][0],
                         cum_steps=ev[0, :, 0, 19], reward=ev[0, :, :, 1], eval_steps=ev[0, :, :, 2],
-                        lev=er[0, :, :, 3])
+                        lev=er[0, :, :, 3], risk=er[0].astype(np.float32), algo=a.algo, loss=a.loss)
     print("wrote", out, "final mean lev", er[0, -5:, :, 3].mean(), "final mean reward", ev[0, -5:, :, 1].mean())
 
 

@@ -213,3 +213,42 @@ def test_nan_guard_sets_status(dev, algo):
     ag.learn_batch(*batch())
     assert ag.status()[0] == flags  # sticky
     assert ag.scalars()["nan_flag"] == flags
+
+
+@pytest.mark.parametrize("loss", ["CAU", "TCAU"])
+def test_fused_actor_statistics_use_prestep_scalars(dev, monkeypatch, loss):
+    """The fused actor step runs its two critic-statistics workgroups beside the
+    workgroups that write log_alpha (temperature step) and the Nagy Cauchy scales
+    in the same launch.  They read the pre-step snapshot critic_update_kernel
+    takes (LearnState::snap_*), so their statistics, the Cauchy scales (the next
+    update's CAU / TCAU loss scale) and log alpha must match the launch chain
+    (RLMD_NO_FUSED_ACTOR=1: statistics in abwd_rows' own workgroup, temperature in
+    adam_kernel after it) over consecutive SAC updates with a temperature step."""
+    from rlmd_amd.agent import reference_init
+
+    S, A, h1, h2, B, k = 5, 1, 256, 256, 512, 256
+    init = reference_init("SAC", S, A, h1, h2, seed=21)
+    rng = np.random.default_rng(8)
+    batches = []
+    for _ in range(6):
+        s, a, r, s2, d = _random_batch(rng, B, S, A)
+        r = r * 3.0  # targets well away from q: the Nagy update moves the scale
+        batches.append((s, a, r, s2, d, torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32)),
+                        torch.from_numpy(rng.standard_normal((B, A)).astype(np.float32))))
+    out = {}
+    for mode in ("fused", "chain"):
+        if mode == "chain":
+            monkeypatch.setenv("RLMD_NO_FUSED_ACTOR", "1")
+        ag = device_agent("SAC", S, A, h1, h2, B, k, loss, init)
+        rows = []
+        for bt in batches:
+            st = ag.learn_batch(*bt).double().cpu().numpy().copy()
+            sc = ag.scalars()
+            rows.append((st, sc["cauchy"], sc["log_alpha"]))
+        out[mode] = rows
+    for i, ((sf, cf, af), (sc_, cc, ac)) in enumerate(zip(out["fused"], out["chain"])):
+        np.testing.assert_allclose(sf[:16], sc_[:16], rtol=1e-5, atol=1e-7, equal_nan=True, err_msg=f"update {i}")
+        np.testing.assert_allclose(cf, cc, rtol=1e-5, err_msg=f"update {i} Cauchy scales")
+        np.testing.assert_allclose(af, ac, rtol=1e-5, atol=1e-7, err_msg=f"update {i} log alpha")
+    # the scales moved: the Nagy update is exercised, not held at its initial 1.0
+    assert abs(out["fused"][-1][1][0] - 1.0) > 1e-3

@@ -230,7 +230,7 @@ def test_market_driver_live_td3_through_main(golden, dev, tmp_path, monkeypatch)
     np.save(mdir / "stooq_snp.npy", golden("stooq_snp.npz")["prices"])
     np.random.seed(5)
     inputs = dict(INPUTS, n_trials_mkt=1, n_cumsteps_mkt=2000, n_eval_mkt=16, train_days=150, past_days=[1, 3],
-                  market_dir=str(mdir), test_agent=True)
+                  market_dir="./market_data/", test_agent=True)  # relative, as learning_tests requires
     out = run([21], ["TD3"], ["MSE"], [1], inputs=inputs, log=None)
     assert len(out[21]) == 2
     for d, ((directory, trial, ev, trial_risk, ev_risk),) in zip((1, 3), out[21]):

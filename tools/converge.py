@@ -44,10 +44,26 @@ GAMBLES = {
 SH_I_LF = (-1 - 5) / (-0.5 - 5)
 SH = dict(p=[1 / 6, 1 / 6, 2 / 3], r=[0.5, -0.5, 0.05], r_sh=[-0.99, 5.0, -0.99], lev_factor=SH_I_LF,
           investor="INSURED")
+# envs of the metric's own workloads: GBM_InvA (key 14, lev = a * 5,
+# gbm_envs.py:147-212) and Dice_SH_InvA (key 18, lev = a0 * 2, lev_sh = (a1 + .99) / 2,
+# dice_roll_sh_envs.py:290-365); the eval risk row holds lev at column 3 and, for
+# Dice_SH_InvA, lev_sh at column 6 (the reference's eval_risk_log columns)
+FAMILY = {"coin": ("coin", "A"), "dice": ("dice", "A"), "dice_sh": ("dice_sh", "INSURED"), "gbm": ("gbm", "A"),
+          "dice_sh_a": ("dice_sh", "A")}
+# GBM log-return N(mu - sigma^2 / 2, sigma) (gbm_envs.py:43-63): expected log growth
+# lev * (mu - sigma^2 / 2) per step, monotone in lev (the optimum is the 4.95 corner,
+# tempered by the lev_max termination)
+GBM_MU, GBM_SIGMA = 0.0540025395205692, 0.1897916175617430
 
 
-def growth(env, lev):
+def growth(env, lev, lev_sh=None):
     """Expected log growth per step of a constant leverage (natural log)."""
+    if env == "gbm":
+        return float(lev * (GBM_MU - GBM_SIGMA ** 2 / 2))
+    if env == "dice_sh_a":
+        p, r, rs = np.array(SH["p"]), np.array(SH["r"]), np.array(SH["r_sh"])
+        R = np.maximum(lev * r + (lev_sh if lev_sh is not None else 0.0) * rs, -0.99)
+        return float(np.sum(p * np.log1p(R)))
     if env == "dice_sh":
         p, r, rs = np.array(SH["p"]), np.array(SH["r"]), np.array(SH["r_sh"])
         R = lev * r + (1.0 - lev) * rs
@@ -59,7 +75,14 @@ def growth(env, lev):
 
 
 def kelly(env):
-    """Growth-optimal leverage (golden-section search of g) and its growth %/step."""
+    """Growth-optimal leverage (golden-section search of g) and its growth %/step.
+    GBM: the max-leverage corner; Dice_SH_InvA: a grid over (lev, lev_sh)."""
+    if env == "gbm":
+        return 4.95, 100.0 * math.expm1(growth("gbm", 4.95))
+    if env == "dice_sh_a":
+        best = max((growth(env, l, h), l, h) for l in np.linspace(-1.98, 1.98, 397)
+                   for h in np.linspace(0.0, 0.99, 100))
+        return best[1], 100.0 * math.expm1(best[0])
     lf = SH["lev_factor"] if env == "dice_sh" else GAMBLES[env]["lev_factor"]
     lo, hi = 0.0, 0.99 * lf
     for _ in range(200):
@@ -73,15 +96,13 @@ def kelly(env):
 
 
 def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eval_every=500, n_eval=4096,
-        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0"):
+        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE"):
     import torch
 
     from rlmd_amd.trainer import VecTrainer
 
-    fam = "dice_sh" if env == "dice_sh" else env
-    inv = SH["investor"] if env == "dice_sh" else GAMBLES[env]["investor"]
-    lf = SH["lev_factor"] if env == "dice_sh" else GAMBLES[env]["lev_factor"]
-    tr = VecTrainer(env=fam, investor=inv, n_lanes=lanes, n_gambles=1, algo=algo, k_updates=k,
+    fam, inv = FAMILY[env]
+    tr = VecTrainer(env=fam, investor=inv, n_lanes=lanes, n_gambles=1, algo=algo, loss=loss, k_updates=k,
                     replay_capacity=replay, seed=seed, warmup_steps=warmup, smoothing_window=smoothing,
                     precision=precision, device=device, init_seed=seed)
     l_star, g_star = kelly(env)
@@ -92,13 +113,17 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
     for step in range(1, steps + 1):
         tr.step()
         if step % eval_every == 0 or step == steps:
-            a = float(tr.agent.act(reset_obs, mode=1)[0, 0].item())
+            a = tr.agent.act(reset_obs, mode=1)[0].cpu().numpy()
             ev = tr.evaluate(n_eval=n_eval, max_steps=100, with_stats=False)
             grow = 100.0 * float(np.mean(ev["reward"] - 1.0))
-            lev = a * lf
-            rec = {"env": env, "precision": precision, "lanes": lanes, "k": k, "step": step,
-                   "updates": step * k, "env_steps": step * lanes, "action": a, "lev": lev,
-                   "eval_growth_pct": grow, "analytic_growth_pct": 100.0 * math.expm1(growth(env, lev)),
+            # the reference's statistic: the eval risk rows' leverage column
+            # (eval_episodes.py:267-274 -> eval_risk_log[..., 3]; lev_sh at 6)
+            lev = float(np.mean(ev["risk"][:, 3]))
+            lev_sh = float(np.mean(ev["risk"][:, 6])) if env == "dice_sh_a" else None
+            rec = {"env": env, "algo": algo, "loss": loss, "precision": precision, "lanes": lanes, "k": k,
+                   "replay": replay, "step": step, "updates": step * k, "env_steps": step * lanes,
+                   "action": [float(x) for x in a], "lev": lev, "lev_sh": lev_sh,
+                   "eval_growth_pct": grow, "analytic_growth_pct": 100.0 * math.expm1(growth(env, lev, lev_sh)),
                    "kelly_lev": l_star, "kelly_growth_pct": g_star, "wall_s": time.perf_counter() - t0,
                    "nan_flag": tr.agent.scalars()["nan_flag"]}
             recs.append(rec)
@@ -111,7 +136,7 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--env", default="coin", choices=["coin", "dice", "dice_sh"])
+    ap.add_argument("--env", default="coin", choices=sorted(FAMILY))
     ap.add_argument("--lanes", type=int, default=65536)
     ap.add_argument("--k", type=int, default=8)
     ap.add_argument("--steps", type=int, default=20000)
@@ -123,11 +148,12 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--replay", type=int, default=1 << 20)
     ap.add_argument("--algo", default="SAC", choices=["SAC", "TD3"])
+    ap.add_argument("--loss", default="MSE")
     ap.add_argument("--out", default=None, help="append JSON lines here")
     a = ap.parse_args()
     out = open(a.out, "a") if a.out else None
     run(a.env, a.lanes, a.k, a.steps, a.precision, a.warmup, a.smoothing, a.eval_every, a.n_eval, a.seed,
-        a.replay, a.algo, out)
+        a.replay, a.algo, out, loss=a.loss)
 
 
 if __name__ == "__main__":
