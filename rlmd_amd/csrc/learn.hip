@@ -145,6 +145,7 @@ struct ActorLossArgs {
   float* stats;
   int32_t B, k, algo, topk;
   float target_entropy;
+  int32_t cnt;  // learn_step_cntr (LearnState slot of log alpha)
 };
 
 template <int NTH>
@@ -155,7 +156,7 @@ __global__ void __launch_bounds__(NTH) actor_loss_kernel(ActorLossArgs a) {
   const int b = threadIdx.x, B = a.B;
   const bool in = b < B;
   LearnState* st = a.st;
-  const float alpha = a.algo == RLMD_SAC ? expf(st->log_alpha) : 0.f;
+  const float alpha = a.algo == RLMD_SAC ? expf(st->log_alpha[slot_rd(a.cnt)]) : 0.f;
   const int64_t nB = (int64_t)B * 4;
   float q1 = rlmd_ldf(rlmd_rsrc(a.qpart[0], nB), b, in) + a.qb[0][0];
   float q2 = a.qpart[1] ? rlmd_ldf(rlmd_rsrc(a.qpart[1], nB), b, in) + a.qb[1][0] : q1;
@@ -602,6 +603,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     la.algo = c.algo;
     la.log_noise = c.log_noise;
     la.grad_scale = sac ? 0.5f : 1.0f;  // SAC: 0.5 (q1_loss + q2_loss)
+    la.cnt = (int32_t)cntr;
     if (B > 512) {
       hipLaunchKernelGGL(critic_loss_kernel<1024>, dim3(1), dim3(1024), 0, st, la);
       RLMD_LAUNCH_CHECK();
@@ -652,17 +654,15 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     adam_copies(ag, ad, co, SLOT_C0, 2, true);
     adam_scalars(ad.lr, ad.cnt / ad.interval, ad.step_size, ad.bc2_sqrt);
     cu.adam = ad;
-    cu.tj = d.H1p / 32;
+    cu.tj = critic_update_tj(d);
     cu.ti = d.H2p / 32;
     cu.n_w2 = cu.ti * cu.tj;
     cu.n_w1 = d.H1p / 32;
     // the statistics workgroups of the fused actor step reuse the selection ranks
     if (ag->fused_actor && actor_step && loss_stats.B > 0) cu.rank_out = S_.rank1;
+    // no actor step: the statistics run as two workgroups of the critic step's launch
+    if (loss_stats.B > 0 && !actor_step) cu.cstats = loss_stats;
     RLMD_TRY(critic_update_launch(cu, st));
-    if (loss_stats.B > 0 && !actor_step) {
-      hipLaunchKernelGGL(critic_loss_kernel<512>, dim3(1), dim3(512), 0, st, loss_stats);
-      RLMD_LAUNCH_CHECK();
-    }
   } else {
     CBwdArgs cb{};
     cb.d = d;
@@ -782,7 +782,6 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       au.cstats.rank_in = S_.rank1;  // critic_update_kernel wrote them (cu.rank_out)
       au.cstats.keep_actor_slot = 1;   // stats[10]: the actor loss
       au.cstats.keep_logtemp_slot = 1; // stats[11]: the temperature step
-      au.cstats.use_snap = 1;          // log_alpha / Cauchy scales as of the update's start
       au.tj = d.H1p / 32;
       au.ti = d.H2p / 32;
       au.n_w2 = au.ti * au.tj;
@@ -810,6 +809,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       al.algo = c.algo;
       al.topk = c.actor_topk;
       al.target_entropy = -(float)A;
+      al.cnt = (int32_t)cntr;
       hipLaunchKernelGGL(actor_loss_kernel<1024>, dim3(1), dim3(1024), 0, st, al);
       RLMD_LAUNCH_CHECK();
     }
@@ -1112,8 +1112,8 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   RLMD_HIP(hipMemcpy(ag->zipf_x, zx.data(), sizeof(float) * k, hipMemcpyHostToDevice));
   RLMD_ALLOC(ag->st, 1);
   rlmd::LearnState st{};
-  st.cauchy[0] = st.cauchy[1] = c.cauchy_scale;
-  st.log_alpha = c.initial_logtemp;
+  st.cauchy[0][0] = st.cauchy[0][1] = st.cauchy[1][0] = st.cauchy[1][1] = c.cauchy_scale;
+  st.log_alpha[0] = st.log_alpha[1] = c.initial_logtemp;
   RLMD_HIP(hipMemcpy(ag->st, &st, sizeof(st), hipMemcpyHostToDevice));
   RLMD_HIP(hipMemset(m, 0, sizeof(float) * ag->n_params));
   RLMD_HIP(hipMemset(v, 0, sizeof(float) * ag->n_params));
@@ -1232,9 +1232,10 @@ int rlmd_agent_scalars(rlmd_agent_t ag, double* out) {
   rlmd::LearnState st;
   RLMD_HIP(hipDeviceSynchronize());
   RLMD_HIP(hipMemcpy(&st, ag->st, sizeof(st), hipMemcpyDeviceToHost));
-  out[0] = st.cauchy[0];
-  out[1] = st.cauchy[1];
-  out[2] = st.log_alpha;
+  const int s = rlmd::slot_wr(st.learn_cntr);  // the last update's values (both slots start equal)
+  out[0] = st.cauchy[s][0];
+  out[1] = st.cauchy[s][1];
+  out[2] = st.log_alpha[s];
   out[3] = st.learn_cntr;
   out[4] = st.nan_flag;
   return 0;

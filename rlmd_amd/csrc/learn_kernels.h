@@ -12,23 +12,28 @@ namespace rlmd {
 
 // Device-resident learner scalars (graph-replay safe: every per-update value a
 // kernel needs is read from here, never baked into kernel arguments).
+//
+// The two scalars an update both reads and rewrites — the Cauchy scales (its
+// loss scale, then the Nagy update) and log alpha (the target / actor loss,
+// then the temperature step) — are kept in two slots by update parity: update n
+// (learn_step_cntr n >= 1) reads slot (n - 1) & 1 and writes slot n & 1
+// (slot_rd / slot_wr below).  Workgroups of one launch may then read the value
+// the update started from while another workgroup of the same launch writes the
+// new one, with no ordering between them (the fused update kernels, update.hip).
+// The value after update n is in slot n & 1; both slots start at the initial value.
 struct LearnState {
-  float cauchy[2];  // Cauchy scales (algo_sac.py:468-473, Nagy update)
+  float cauchy[2][2];  // [slot][critic] Cauchy scales (algo_sac.py:468-473, Nagy update)
   float kernel[2];  // CIM kernel sizes of the last update (algo_sac.py:419-420)
-  float log_alpha;  // SAC log temperature (algo_sac.py:166-169)
+  float log_alpha[2];  // [slot] SAC log temperature (algo_sac.py:166-169)
   float temp_m, temp_v;
   int32_t learn_cntr;  // learn_step_cntr (algo_sac.py:475)
   int32_t nan_flag;    // tests/test_live_learning.py guards -> flag, no exit()
   float pad_temp_grad;  // temperature gradient handed from actor_loss to adam
   int32_t nan_update;   // learn_cntr when nan_flag was first set
-  uint32_t arrive;      // fused actor update: workgroups done reading log_alpha (update.hip)
-  // pre-step snapshot of the loss scalars, written by critic_update_kernel's
-  // workgroup 0: the fused actor step's statistics workgroups read these while
-  // its last tile workgroup steps log_alpha and statistics part 0 writes the new
-  // Cauchy scales in the same launch (update.hip)
-  float snap_log_alpha;
-  float snap_cauchy[2];
 };
+
+__host__ __device__ inline int slot_rd(int cnt) { return (cnt - 1) & 1; }  // the value update cnt starts from
+__host__ __device__ inline int slot_wr(int cnt) { return cnt & 1; }        // the value update cnt leaves
 
 // Per-net parameter offsets (floats) inside a flat buffer, torch nn.Linear
 // order: fc1.weight, fc1.bias, fc2.weight, fc2.bias, head(s).
@@ -221,7 +226,7 @@ struct LossArgs {
   float log_noise, grad_scale;
   int32_t keep_actor_slot;  // 1: leave stats[10] (actor loss) alone
   int32_t keep_logtemp_slot;  // 1: leave stats[11] (log temperature) to the temperature step
-  int32_t use_snap;  // 1: log_alpha / Cauchy scales from LearnState's pre-step snapshot
+  int32_t cnt;  // learn_step_cntr of this update: LearnState slots slot_rd(cnt) / slot_wr(cnt)
 };
 
 struct CBwdArgs {

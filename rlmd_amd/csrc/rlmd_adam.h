@@ -145,10 +145,17 @@ __device__ __forceinline__ void adam_apply(const AdamArgs& a, int i, float g, co
 }
 
 // Once per step (one thread): the learner counter and the temperature Adam.
+// The critics' call (temp = 0; every update makes it, before any actor step)
+// carries log alpha into this update's slot; an actor call with a temperature
+// step then overwrites that slot from the update's starting value.
 __device__ __forceinline__ void adam_scalar_step(const AdamArgs& a) {
   LearnState* st = a.st;
+  const int rs = slot_rd(a.cnt), ws = slot_wr(a.cnt);
   st->learn_cntr = a.cnt;
-  if (!a.temp) return;
+  if (!a.temp) {
+    st->log_alpha[ws] = st->log_alpha[rs];
+    return;
+  }
   if (a.cnt % a.temp_interval == 0) {
     const float b1 = 0.9f, b2 = 0.999f, eps = 1e-8f;
     const float g = st->pad_temp_grad;
@@ -157,9 +164,9 @@ __device__ __forceinline__ void adam_scalar_step(const AdamArgs& a) {
     st->temp_m = m;
     st->temp_v = v;
     const float denom = sqrtf(v) / a.temp_bc2_sqrt + eps;
-    st->log_alpha = st->log_alpha - a.temp_step_size * (m / denom);
+    st->log_alpha[ws] = st->log_alpha[rs] - a.temp_step_size * (m / denom);
   }
-  if (a.stats) a.stats[11] = st->log_alpha;
+  if (a.stats) a.stats[11] = st->log_alpha[ws];
 }
 
 }  // namespace

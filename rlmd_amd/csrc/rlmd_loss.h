@@ -88,14 +88,15 @@ __device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
   L.eff = (int)__builtin_bit_cast(
       int32_t, __builtin_amdgcn_raw_buffer_load_b32(rlmd_rsrc(a.eff, a.eff ? nB : 0), in ? b * 4 : 0x7fffffff, 0, 0));
   L.has_eff = a.eff != nullptr;
-  // the snapshot when another workgroup of the same launch may be writing the
-  // live values (the fused actor step's statistics workgroups, update.hip)
+  // the values this update started from (LearnState slots: another workgroup of
+  // the same launch may be writing this update's new ones)
+  const int rs = slot_rd(a.cnt);
   for (int g = 0; g < 2; ++g) {
     L.tb[g] = a.tb[g][0];
     L.qb[g] = a.qb[g][0];
-    L.cauchy[g] = a.use_snap ? a.st->snap_cauchy[g] : a.st->cauchy[g];
+    L.cauchy[g] = a.st->cauchy[rs][g];
   }
-  L.log_alpha = a.use_snap ? a.st->snap_log_alpha : a.st->log_alpha;
+  L.log_alpha = a.st->log_alpha[rs];
   return L;
 }
 
@@ -239,8 +240,8 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
       a.stats[6 + g] = NAN;
       if (g == 0 || part < 0) a.stats[8 + g] = 1.f / (s5[g] / a.zipf_x2);
     }
-    st->cauchy[0] = newc[0];
-    st->cauchy[1] = newc[1];
+    st->cauchy[slot_wr(a.cnt)][0] = newc[0];
+    st->cauchy[slot_wr(a.cnt)][1] = newc[1];
     st->kernel[0] = o.kern[0];
     st->kernel[1] = o.kern[1];
     // NaN guards (tests/test_live_learning.py): bit 0 = NaN in the mini-batch's
@@ -257,7 +258,8 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
     // sticky; atomic: with part 1 running alongside, the first to set it stamps nan_update
     if (fl && atomicOr(&st->nan_flag, fl) == 0) st->nan_update = st->learn_cntr;
     if (!a.keep_actor_slot) a.stats[10] = NAN;
-    if (!a.keep_logtemp_slot) a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha : NAN;
+    // no temperature step in this update: log alpha is the value it started from
+    if (!a.keep_logtemp_slot) a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha[slot_rd(a.cnt)] : NAN;
     a.stats[12] = newc[0];
     a.stats[13] = newc[1];
     a.stats[14] = o.kern[0];

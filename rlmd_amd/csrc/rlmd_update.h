@@ -21,6 +21,9 @@ struct CritUpdArgs {
   AdamArgs adam;          // both critics (p = critic 0's parameters, n = 2 x net size)
   int32_t ti, tj, n_w2, n_w1;
   int32_t* rank_out;      // nullable: every row's top-k selection rank [B] (workgroup 0 writes it)
+  // updates without an actor step (TD3's delayed actor): this update's critic
+  // statistics as two extra workgroups of the same launch (B == 0: none)
+  LossArgs cstats;
 };
 
 // The actor (+ temperature) step of one update in one launch
@@ -53,6 +56,7 @@ struct ActUpdArgs {
 };
 
 size_t critic_update_lds();
+int critic_update_tj(const RowDims& d);  // fc2.weight tile columns of the critic step (32 x 64 tiles at B <= 256)
 int actor_update_launch(const ActUpdArgs& a, hipStream_t st);
 int critic_update_launch(const CritUpdArgs& a, hipStream_t st);
 

@@ -1183,7 +1183,7 @@ __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
   const int tq = threadIdx.x, bq = row0 + (int)threadIdx.x;
   const float ld_q1 = rlmd_ldf(rq0, tq, tq < B), ld_q2 = rlmd_ldf(rq1, tq, tq < B && nq > 1);
   const float ld_lp = rlmd_ldf(rlp, tq, tq < B && sac);
-  const float log_alpha = sac ? a.st->log_alpha : 0.f;  // scalar loads, issued with the first round
+  const float log_alpha = sac ? a.st->log_alpha[slot_rd((int)a.smp.ctr)] : 0.f;  // scalar loads, issued with the first round
   const float qb0 = a.crit[0].p[co.b3], qb1 = nq > 1 ? a.crit[1].p[co.b3] : 0.f;
   const float row_q1 = rlmd_ldf(rq0, bq, tq < R && bq < B), row_q2 = rlmd_ldf(rq1, bq, tq < R && bq < B && nq > 1);
   // first round: what the loss and critic 1 need (under the 63-load vmcnt cap);

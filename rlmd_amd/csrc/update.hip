@@ -197,11 +197,16 @@ struct ULds {
   static constexpr int red = rank + 512 * 4;    // block reductions (16 * 9 floats)
   static constexpr int part = red + 16 * 9 * 4; // f32 [8 waves][4 blocks][256] partial tiles / row partials
   static constexpr int xs = part + 8 * 4 * 256 * 4;  // f32 [512][8] critic inputs (fc1 blocks)
-  static constexpr int pcl = xs + 512 * 8 * 4;       // f32 [2][32][33] stepped tile + targets (copies)
-  static constexpr int total = pcl + 2 * 32 * 33 * 4;
+  static constexpr int pcl = xs + 512 * 8 * 4;       // f32 [2 halves][2][32][33] stepped tile + targets (copies)
+  static constexpr int total = pcl + 2 * 2 * 32 * 33 * 4;
 };
 
-template <int PREC>
+// WIDE (mini-batch B <= 256, e.g. TD3's 200): a tile workgroup owns 32 x 64 of
+// fc2.weight — waves 0-3 cover the batch's 256 rows for columns [j0, j0 + 32),
+// waves 4-7 for [j0 + 32, j0 + 64) — where the 32 x 32 form would leave waves
+// 4-7 on rows past B.  Half the tile workgroups: TD3 400/300's 2 x 153 of them
+// exceed the 256 CUs at one workgroup per CU (a second dispatch round); 2 x 88 do not.
+template <int PREC, bool WIDE>
 __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   using K = KT<PREC>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -212,14 +217,26 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   // per critic: fc2.weight tiles, fc1 blocks, then head workgroups (b2 / w3 of 32
   // fc2 rows each, b3 on the first)
   const int per = a.n_w2 + a.n_w1 + a.ti;
+  if ((int)blockIdx.x >= 2 * per) {
+    // the critic statistics of an update without an actor step (rlmd_loss.h), beside
+    // the step: they read the loss scalars' starting slot, part 0 writes the other
+    critic_loss_block<NT / 64>(a.cstats, reinterpret_cast<uint64_t*>(smem + ULds::runs),
+                               reinterpret_cast<int*>(smem + ULds::part), reinterpret_cast<float*>(smem + ULds::red),
+                               (int)blockIdx.x - 2 * per);
+    return;
+  }
   const int g = blockIdx.x / per, t = blockIdx.x - g * per;
   const int B = d.B, H1 = d.H1, H2 = d.H2, H1p = d.H1p, H2p = d.H2p, X = d.X;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nrb = (B + 15) / 16;
   const bool w2tile = t < a.n_w2, first_col = t >= a.n_w2 + a.n_w1;  // first_col: a head workgroup
+  constexpr int TJ = WIDE ? 2 * TW : TW;  // fc2.weight columns per tile
+  constexpr int NH = WIDE ? 2 : 1;        // 32-column halves per tile
   const int i0 = w2tile ? (t / a.tj) * TW : first_col ? (t - a.n_w2 - a.n_w1) * TW : 0;
-  const int j0 = w2tile ? (t % a.tj) * TW : first_col ? 0 : (t - a.n_w2) * TW;
+  const int j0 = w2tile ? (t % a.tj) * TJ : first_col ? 0 : (t - a.n_w2) * TW;
   const bool w1blk = !w2tile && !first_col;
+  const int wrow = WIDE ? (wave & 3) : wave;     // this wave's 64-row slice of the batch
+  const int jw = j0 + (WIDE ? 32 * (wave >> 2) : 0);  // and its 32-column half
   const int64_t pbase = (int64_t)g * co.size;  // this critic's parameters in the Adam base
   const bool polyak = adam_polyak(a.adam);
   const CopyDst cd = copy_dst(a.adam, g);
@@ -250,11 +267,11 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   float w3l[2];
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
-    const int row = 64 * wave + s * K::KS + K::RPL * (lane >> 4);
+    const int row = 64 * wrow + s * K::KS + K::RPL * (lane >> 4);
     const bool rok = w2tile && row < nrb * 16;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int i = i0 + 16 * h + (lane & 15), j = j0 + 16 * h + (lane & 15);
+      const int i = i0 + 16 * h + (lane & 15), j = jw + 16 * h + (lane & 15);
       K::load_mask(rm2, rp_idx(row, H2p, i), rok && i < H2p, mw[s][h]);
       bf[s][h] = K::load_b(rh1, rp_idx(row, H1p, j), rok && j < H1p);
     }
@@ -264,16 +281,19 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     const int i = i0 + 16 * h + (lane & 15);
     w3l[h] = rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), i, w2tile && i < H2);
   }
-  // (b) Adam state of the owned parameters: a dW2 tile's 1024 elements, 2 per thread
-  int pidx[2];
-  AdamIn ain[2];
+  // (b) Adam state of the owned parameters: 1024 elements per 32-column half, 2
+  //     per thread and half
+  int pidx[NH][2];
+  AdamIn ain[NH][2];
 #pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
-    const int i = i0 + 16 * (blk >> 1) + 4 * (ln >> 4) + rg, j = j0 + 16 * (blk & 1) + (ln & 15);
-    pidx[e] = (w2tile && i < H2 && j < H1) ? (int)(pbase + co.w2 + (int64_t)i * H1 + j) : -1;
-    ain[e] = adam_load(a.adam, pidx[e], polyak);
-  }
+  for (int hf = 0; hf < NH; ++hf)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
+      const int i = i0 + 16 * (blk >> 1) + 4 * (ln >> 4) + rg, j = j0 + 32 * hf + 16 * (blk & 1) + (ln & 15);
+      pidx[hf][e] = (w2tile && i < H2 && j < H1) ? (int)(pbase + co.w2 + (int64_t)i * H1 + j) : -1;
+      ain[hf][e] = adam_load(a.adam, pidx[hf][e], polyak);
+    }
   // (c) first-column tiles: this thread's column of h2 and [h2 > 0] over its 32 rows
   //     (thread: column i0 + tid % 32, rows [32 p, 32 p + 32) of part p = tid / 32)
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -349,14 +369,8 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       if (blockIdx.x == 0 && a.rank_out && o.in) a.rank_out[tid] = rank_of[tid];  // for the statistics
     }
     dqs[tid] = sel ? a.loss.grad_scale * (g == 0 ? o.dl[0] : o.dl[1]) / (float)kk : 0.f;
-    if (blockIdx.x == 0 && tid == 0) {
-      adam_scalar_step(a.adam);  // learn_step_cntr (no temperature here)
-      // the loss scalars this update started from, for the actor step's statistics
-      // workgroups (they run beside the writers of log_alpha and the Cauchy scales)
-      a.loss.st->snap_log_alpha = cl.log_alpha;
-      a.loss.st->snap_cauchy[0] = cl.cauchy[0];
-      a.loss.st->snap_cauchy[1] = cl.cauchy[1];
-    }
+    // learn_step_cntr; log alpha carried into this update's slot (no temperature here)
+    if (blockIdx.x == 0 && tid == 0) adam_scalar_step(a.adam);
   }
   __syncthreads();
   RLMD_TSU(3);
@@ -370,7 +384,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       for (int v = 0; v < 2; ++v) acc[h][v] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int s = 0; s < NKS; ++s) {
-      const int row = 64 * wave + s * K::KS + K::RPL * (lane >> 4);
+      const int row = 64 * wrow + s * K::KS + K::RPL * (lane >> 4);
       float dq[K::RPL];
 #pragma unroll
       for (int e = 0; e < K::RPL; ++e) dq[e] = dqs[(row + e) & 511];
@@ -391,19 +405,25 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     RLMD_TSU(4);
     float* pcl = reinterpret_cast<float*>(smem + ULds::pcl);
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
-      const int ii = 16 * (blk >> 1) + 4 * (ln >> 4) + rg, jj = 16 * (blk & 1) + (ln & 15);
-      float gs = 0.f;
+    for (int hf = 0; hf < NH; ++hf)
 #pragma unroll
-      for (int w = 0; w < 8; ++w) gs += part[w * 1024 + el];
-      float pn = 0.f, tn = 0.f;  // padding elements: zero in the copies
-      if (pidx[e] >= 0) adam_core(a.adam, pidx[e], gs, ain[e], polyak, pn, tn);
-      pcl[ii * 33 + jj] = pn;
-      pcl[32 * 33 + ii * 33 + jj] = tn;
-    }
+      for (int e = 0; e < 2; ++e) {
+        const int el = tid * 2 + e, blk = el >> 8, ln = (el >> 2) & 63, rg = el & 3;
+        const int ii = 16 * (blk >> 1) + 4 * (ln >> 4) + rg, jj = 16 * (blk & 1) + (ln & 15);
+        float gs = 0.f;  // the half's waves in order (WIDE: 4 of 64 rows, else 8)
+#pragma unroll
+        for (int w = 0; w < 8 / NH; ++w) gs += part[(hf * (8 / NH) + w) * 1024 + el];
+        float pn = 0.f, tn = 0.f;  // padding elements: zero in the copies
+        if (pidx[hf][e] >= 0) adam_core(a.adam, pidx[hf][e], gs, ain[hf][e], polyak, pn, tn);
+        float* ph = pcl + hf * 2 * 32 * 33;
+        ph[ii * 33 + jj] = pn;
+        ph[32 * 33 + ii * 33 + jj] = tn;
+      }
     __syncthreads();
-    tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
+#pragma unroll
+    for (int hf = 0; hf < NH; ++hf)
+      if (j0 + 32 * hf < H1p)  // WIDE: the last tile's second half may lie past the padded width
+        tile_copies<PREC>(pcl + hf * 2 * 32 * 33, cd, polyak && cd.twc, i0, j0 + 32 * hf, H1p, H2p);
     RLMD_TSU(5);
   } else if (first_col) {
     {
@@ -517,8 +537,7 @@ struct ALds {
   static constexpr int red = rank + 3 * 512 * 4;    // 16 * 9 floats
   static constexpr int part = red + 16 * 9 * 4;     // f32 [8][4][256]
   static constexpr int xs = part + 8 * 4 * 256 * 4; // f32 [512][8] states
-  static constexpr int flag = xs + 512 * 8 * 4;     // int: this workgroup arrived last
-  static constexpr int pcl = flag + 16;             // f32 [2][32][33] stepped tile + targets (copies)
+  static constexpr int pcl = xs + 512 * 8 * 4;      // f32 [2][32][33] stepped tile + targets (copies)
   static constexpr int total = pcl + 2 * 32 * 33 * 4;
 };
 
@@ -530,7 +549,6 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   float* ghp = reinterpret_cast<float*>(smem + ALds::ghp);
   float* part = reinterpret_cast<float*>(smem + ALds::part);
   float* red = reinterpret_cast<float*>(smem + ALds::red);
-  int* lastf = reinterpret_cast<int*>(smem + ALds::flag);
   const RowDims& d = a.d;
   const NetOff& ao = a.ao;
   const int B = d.B, H1 = d.H1, H2 = d.H2, H1p = d.H1p, H2p = d.H2p, S = d.S, A = d.A;
@@ -540,12 +558,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const int nrb = (B + 15) / 16;
   const int t = blockIdx.x;
   // workgroups: fc2.weight tiles, fc1 blocks, head workgroups (b2 and the heads
-  // of 32 fc2 rows each), and two critic-statistics workgroups.
-  // The statistics workgroups do not take part in the arrival count: they read
-  // log_alpha and the Cauchy scales from LearnState's pre-step snapshot
-  // (critic_update_kernel wrote it; LossArgs::use_snap), never the live values
-  // that the last tile workgroup (log_alpha) and statistics part 0 (the Cauchy
-  // scales) write in this launch; learn_cntr already holds this update's count
+  // of 32 fc2 rows each), and two critic-statistics workgroups.  Every reader of
+  // log alpha and the Cauchy scales takes the update's starting slot, the
+  // temperature step (the last head workgroup) and statistics part 0 write the
+  // other one (LearnState): no ordering between the workgroups is needed.
+  // learn_cntr already holds this update's count (critic_update_kernel set it).
   const int n_hd = a.ti;
   const int nwg = a.n_w2 + a.n_w1 + n_hd;
   const int sidx = t - (a.n_w2 + a.n_w1 + n_hd);  // >= 0: statistics part
@@ -554,22 +571,6 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   RLMD_TSA(14);
   RLMD_TSA(0);
   LearnState* st = a.st;
-  // this workgroup has read log_alpha; returns true on the last one to arrive.
-  // Relaxed: no data crosses workgroups through the counter (the last arriver
-  // steps the temperature from its own all-rows sums). Every arriver's log_alpha
-  // load (an atomic load below, so it cannot be moved past the fetch_add) has
-  // been consumed by the actor objective before arrive() is reached. An
-  // agent-scope acquire / release would write back and invalidate the XCD's L2
-  // in the middle of every tile's critical path.
-  auto arrive = [&]() {
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned old = __hip_atomic_fetch_add(&st->arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *lastf = old == (unsigned)(nwg - 1);
-    }
-    __syncthreads();
-    return *lastf != 0;
-  };
   const bool stats_wg = sidx >= 0;
   const bool w2tile = t < a.n_w2, first_col = !stats_wg && t >= a.n_w2 + a.n_w1;  // first_col: a head workgroup
   const bool w1blk = !stats_wg && !w2tile && !first_col;
@@ -584,10 +585,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   float v = 0.f, lpv = 0.f, alpha = 0.f;
   bool sel = false;
   int kk = B;
-  // every workgroup has read log_alpha: the last to arrive writes the actor-loss
-  // value and steps the temperature
+  // the last head workgroup writes the actor-loss value and steps the
+  // temperature into this update's slot (the others read the starting slot)
   auto temperature_step = [&]() {
-    if (arrive()) {
+    if (t == nwg - 1) {
       float sm[2] = {sel ? v : 0.f, (tid < B && sac) ? -(lpv + a.target_entropy) : 0.f};
       float mx[1] = {-INFINITY};
       block_allreduce<2, 0>(sm, mx, red);
@@ -595,9 +596,6 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         if (sac) st->pad_temp_grad = sm[1] / B * alpha;
         a.stats[10] = -sm[0] / kk;
         adam_scalar_step(a.adam);  // learn_step_cntr, temperature Adam, stats[11]
-        // every workgroup has arrived: reset for the next update (visible to it
-        // through the kernel boundary)
-        __hip_atomic_store(&st->arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
   };
@@ -682,8 +680,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * 4);
   {
     const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
-    // must complete before this workgroup's arrive(): the last arriver overwrites it
-    const float log_alpha = sac ? __hip_atomic_load(&st->log_alpha, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.f;
+    const float log_alpha = sac ? st->log_alpha[slot_rd(a.adam.cnt)] : 0.f;
 
     // ---- actor loss over all rows (algo_sac.py:546-562 / algo_td3.py:507-523)
     alpha = sac ? expf(log_alpha) : 0.f;
@@ -976,6 +973,7 @@ extern "C" int rlmd_debug_ts_aupd(unsigned long long* out) {
 #endif
 
 size_t critic_update_lds() { return (size_t)ULds::total; }
+int critic_update_tj(const RowDims& d) { return d.B <= 256 ? (d.H1p / TW + 1) / 2 : d.H1p / TW; }
 
 int actor_update_launch(const ActUpdArgs& a, hipStream_t st) {
   const RowDims& d = a.d;
@@ -996,13 +994,22 @@ int critic_update_launch(const CritUpdArgs& a, hipStream_t st) {
   const RowDims& d = a.d;
   RLMD_CHECK(d.B <= NT, "critic update: mini-batch up to 512 rows");
   RLMD_CHECK(d.X <= 8, "critic update: critic input width up to 8");
-  RLMD_CHECK(a.tj == d.H1p / TW && a.ti * TW >= d.H2p && a.n_w2 == a.ti * a.tj && a.n_w1 == d.H1p / TW,
+  const bool wide = d.B <= 256;
+  RLMD_CHECK(a.tj == critic_update_tj(d) && a.ti * TW >= d.H2p && a.n_w2 == a.ti * a.tj && a.n_w1 == d.H1p / TW,
              "critic update: tile grid inconsistent with the widths");
-  const dim3 grid(2 * (a.n_w2 + a.n_w1 + a.ti));
-  if (d.prec == RLMD_BF16)
-    hipLaunchKernelGGL(critic_update_kernel<RLMD_BF16>, grid, dim3(NT), ULds::total, st, a);
-  else
-    hipLaunchKernelGGL(critic_update_kernel<RLMD_FP32>, grid, dim3(NT), ULds::total, st, a);
+  RLMD_CHECK(a.cstats.B <= NT, "critic statistics workgroups: mini-batch up to 512 rows");
+  const dim3 grid(2 * (a.n_w2 + a.n_w1 + a.ti) + (a.cstats.B > 0 ? 2 : 0));
+  if (d.prec == RLMD_BF16) {
+    if (wide)
+      hipLaunchKernelGGL((critic_update_kernel<RLMD_BF16, true>), grid, dim3(NT), ULds::total, st, a);
+    else
+      hipLaunchKernelGGL((critic_update_kernel<RLMD_BF16, false>), grid, dim3(NT), ULds::total, st, a);
+  } else {
+    if (wide)
+      hipLaunchKernelGGL((critic_update_kernel<RLMD_FP32, true>), grid, dim3(NT), ULds::total, st, a);
+    else
+      hipLaunchKernelGGL((critic_update_kernel<RLMD_FP32, false>), grid, dim3(NT), ULds::total, st, a);
+  }
   RLMD_LAUNCH_CHECK();
   return 0;
 }

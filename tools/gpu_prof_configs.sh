@@ -1,0 +1,14 @@
+#!/bin/bash
+# Kernel traces (rocprofv3 --kernel-trace --stats) of the bench's other configs,
+# C3 / C5 (TD3) and C4 (market), one pass each with its own time limit.
+set -e
+TAG=${1:-r04}
+OUT=gpurun_out/prof_$TAG
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+for C in ${CONFIGS:-c3 c5 c4}; do
+  BENCH="bench.py --config $C --no-cpu-baseline --no-companion --k-sweep= --steps 25 --warmup 5"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$C -o trace -- python3 $BENCH > $OUT/trace_$C.log 2>&1
+  tail -n 1 $OUT/trace_$C.log | cut -c1-300
+done
+echo done
