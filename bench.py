@@ -406,6 +406,9 @@ def main():
     ap.add_argument("--k-sweep", default="1,8,32,64",
                     help="K values timed after the headline region (env steps/s and updates/s each); '' = off")
     ap.add_argument("--no-companion", action="store_true", help="skip the fp32 companion measurement")
+    ap.add_argument("--seeds-per-gpu", default=None,
+                    help="independent seeds per GPU timed after the headline (SeedGroup: one stream per seed); "
+                         "default '2,4' (C4: '2,4,8'); '' = off")
     ap.add_argument("--eval-every", type=int, default=1000,
                     help="vector steps between evaluations (eval_freq 1e3, main.py); amortised into value")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -484,20 +487,17 @@ def main():
     # dispatch are recorded (profile mode 2): the phase markers around acting and
     # learning cost the stream ~25 us per C2 step (5 %), so the phase times come
     # from a separate pass after the headline
-    elapsed = timed_region(tr, args.steps, args.warmup, world, torch.cuda.synchronize,
-                           on_start=lambda: _abi.check(_abi.lib().rlmd_profile_enable(2)))
-    ms = (C.c_double * 3)()
-    cnt = (C.c_int64 * 3)()
-    _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
+    elapsed = timed_region(tr, args.steps, args.warmup, world, torch.cuda.synchronize, on_start=lambda: tr.profile(2))
+    ms, cnt = tr.profile_read()
     env_ms = ms[1] / max(cnt[1], 1)
-    _abi.check(_abi.lib().rlmd_profile_enable(1))  # the phase pass (untimed)
+    tr.profile(1)  # the phase pass (untimed)
     for _ in range(10):
         tr.step()
-    _abi.check(_abi.lib().rlmd_profile_read(ms, cnt))
-    _abi.check(_abi.lib().rlmd_profile_enable(0))
+    ms, cnt = tr.profile_read()
+    tr.profile(0)
     learn_ms = ms[2] / max(cnt[2], 1)
     act_ms = ms[0] / max(cnt[0], 1)
-    fused = bool(_abi.lib().rlmd_train_last_fused())
+    fused = tr.last_fused()
     # evaluation (eval_multiplicative / eval_market, 100 episodes) every eval_every
     # vector steps, timed on its own and amortised into the timed region
     ev = (lambda: tr.evaluate_market(n_eval=100, test_days=250)) if cfg["env"] == "market" else \
@@ -521,6 +521,31 @@ def main():
         sweep[str(kk)] = {"ms_per_step": ms_k, "env_steps_per_s": N * 1e3 / ms_k,
                           "updates_per_s": kk * 1e3 / ms_k, "utd_updates_per_env_step": kk / N}
     tr.step(K)
+    # several independent seeds per GPU (§8e "GPU g runs seeds {g, g+G, ...}"):
+    # T whole trainers on T streams, the per-GPU throughput of a trial sweep
+    seeds_spec = args.seeds_per_gpu if args.seeds_per_gpu is not None else ("2,4,8" if args.config == "c4" else "2,4")
+    per_gpu = {}
+    if world == 1:
+        from rlmd_amd.trainer import SeedGroup
+
+        for T in [int(v) for v in seeds_spec.split(",") if v.strip()]:
+            grp = SeedGroup([420 + 1000 * i for i in range(T)], device=dev, env=cfg["env"], investor=cfg["investor"],
+                            n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"], loss=args.loss, k_updates=K,
+                            replay_capacity=replay, warmup_steps=0, smoothing_window=0, precision=args.precision,
+                            multi_steps=ms_n, dynamics="A", **kw)
+            for _ in range(5):
+                grp.step()
+            grp.synchronize()
+            n_t = max(10, min(args.steps, 30))
+            t0 = time.perf_counter()
+            for _ in range(n_t):
+                grp.step()
+            grp.synchronize()
+            dt = time.perf_counter() - t0
+            per_gpu[str(T)] = {"env_steps_per_s": T * N * n_t / dt, "updates_per_s": T * K * n_t / dt,
+                               "ms_per_group_step": 1e3 * dt / n_t,
+                               "vs_one_seed": (T * N * n_t / dt) / (N * 1e3 / (1e3 * t_max / args.steps))}
+            del grp
     companion = None
     if not args.no_companion and world == 1 and args.precision == "bf16":
         tr32 = VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"],
@@ -547,18 +572,18 @@ def main():
         # events attached to the kernels' own dispatches), and, for comparison, the
         # separate env kernel of unfused steps
         fused_ms = env_ms
-        _abi.check(lib.rlmd_profile_enable(1))
-        for i in range(20):
+        tr.profile(1)
+        for i in range(20):  # 65,536-row launches only (the acting kernel on the training lanes)
             tr.agent.act(tr.obs, mode=0, noise_ctr=1_000_000 + i, out=tr.actions)
-        _abi.check(lib.rlmd_profile_read(ms, cnt))
+        ms, cnt = tr.profile_read()
         act_only_ms = ms[0] / max(cnt[0], 1)
-        _abi.check(lib.rlmd_train_set_fused(0))
-        _abi.check(lib.rlmd_profile_enable(1))
+        tr.set_fused(0)
+        tr.profile(1)
         for _ in range(10):
             tr.step()
-        _abi.check(lib.rlmd_profile_read(ms, cnt))
-        _abi.check(lib.rlmd_profile_enable(0))
-        _abi.check(lib.rlmd_train_set_fused(1))
+        ms, cnt = tr.profile_read()
+        tr.profile(0)
+        tr.set_fused(1)
         sep_env_ms = ms[1] / max(cnt[1], 1)
         env_bytes = env_bytes_per_step(S, A, n_assets, fused=True) * N
         marginal_ms = max(fused_ms - act_only_ms, 1e-6)
@@ -613,6 +638,9 @@ def main():
                        "fused_act_env": fused,
                        "phase_ms_per_step": {"act": act_ms, "env_kernel": env_ms, "learn_k": learn_ms}},
             "updates_per_s": K * args.steps * world / t_max,
+            "seeds_per_gpu": {"note": "T independent seeds of this workload on one GPU (SeedGroup: own lanes, "
+                                      "replay and learner per seed, one HIP stream each), per-GPU totals; eval not "
+                                      "amortised", **per_gpu} if per_gpu else None,
             "k_sweep": sweep,
             "fp32_companion": companion,
             "roofline": roofline,

@@ -376,16 +376,19 @@ int rlmd_train_episode_drain(rlmd_env_t env, float* out_dev, int64_t out_cap, in
 
 /* Post-window policy steps of rlmd_train_step run acting + env step + replay
  * insert + reset as ONE kernel when the env / net shapes allow (one gamble,
- * S <= 8, A <= 2, the headline nets; RLMD_NO_FUSED_ENV=1 or on = 0 here selects
- * the separate launches).  rlmd_train_last_fused: 1 if the last step fused. */
-int rlmd_train_set_fused(int32_t on);
-int rlmd_train_last_fused(void);
+ * S <= 8, A <= 2, the headline nets; RLMD_NO_FUSED_ENV=1 at env creation or
+ * on = 0 here selects the separate launches).  Per env handle (one trainer per
+ * handle; several trainers may share a process, each on its own stream).
+ * rlmd_train_last_fused: 1 if this env's last step fused. */
+int rlmd_train_set_fused(rlmd_env_t env, int32_t on);
+int rlmd_train_last_fused(rlmd_env_t env);
 
 /* Initialise obs_dev f32 [N, S] with every lane reset (episode start). */
 int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
 
 /* Live phase timing of rlmd_train_step with HIP events recorded on the step's
- * stream around its three phases (0 acting, 1 fused env kernel, 2 learn).
+ * stream around its three phases (0 acting, 1 fused env kernel, 2 learn), per
+ * agent handle (its train steps and rlmd_agent_act calls).
  * Phase 1 is the env kernel's own begin / end (the fused acting + env kernel
  * when the step fused); rlmd_agent_act's fused acting kernel adds its own
  * begin / end to phase 0.
@@ -393,8 +396,8 @@ int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
  * only phase 1 (events attached to the env kernel's dispatch, no markers on the
  * stream); enable(0) stops.  read() synchronises and returns the summed
  * milliseconds and the number of timed launches per phase. */
-int rlmd_profile_enable(int32_t on);
-int rlmd_profile_read(double* ms_out3, int64_t* count_out3);
+int rlmd_profile_enable(rlmd_agent_t ag, int32_t on);
+int rlmd_profile_read(rlmd_agent_t ag, double* ms_out3, int64_t* count_out3);
 
 /* ------------------------------------------------------------- test hooks */
 /* Copy ring rows (start + i) % capacity, i < n, into caller buffers (nullable). */

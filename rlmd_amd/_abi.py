@@ -93,8 +93,8 @@ SIGNATURES = {
     "rlmd_train_reset": (C.c_int, [P, P, P]),
     "rlmd_train_flush_stats": (C.c_int, [P, P]),
     "rlmd_train_episode_log": (C.c_int, [P, C.c_int32]),
-    "rlmd_train_set_fused": (C.c_int, [C.c_int32]),
-    "rlmd_train_last_fused": (C.c_int, []),
+    "rlmd_train_set_fused": (C.c_int, [P, C.c_int32]),
+    "rlmd_train_last_fused": (C.c_int, [P]),
     "rlmd_train_episode_drain": (C.c_int, [P, P, C.c_int64, P, P, P]),
     "rlmd_env_lane_start": (C.c_int, [P, P]),
     "rlmd_env_write_prices": (C.c_int, [P, P, I64, I64, P]),
@@ -109,8 +109,8 @@ SIGNATURES = {
     "rlmd_lev_coin_sweep": (C.c_int, [P, I64, I32, I64, I64, C.c_float, C.c_float, C.c_float, P, I32, P, I64, P, P,
                                        P]),
     "rlmd_eval_market": (C.c_int, [P, P, P, C.c_int64, C.c_int32, C.c_int32, P, P, P, P, P, P, P]),
-    "rlmd_profile_enable": (C.c_int, [I32]),
-    "rlmd_profile_read": (C.c_int, [P, P]),
+    "rlmd_profile_enable": (C.c_int, [P, I32]),
+    "rlmd_profile_read": (C.c_int, [P, P, P]),
     "rlmd_gemm": (C.c_int, [I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, P, I32, P, I32, P, P]),
 }
 

@@ -1264,6 +1264,11 @@ struct rlmd_env_s {
   // per-episode log (EnvParams::ep_rows / ep_cnt) and the drain's scratch
   int64_t* ep_offs = nullptr;
   int64_t* ep_tot = nullptr;
+  // per-handle switches (one trainer per env handle; several may share a process):
+  // the acting + env fusion (RLMD_NO_FUSED_ENV=1 at creation turns it off,
+  // rlmd_train_set_fused after), and whether the last rlmd_train_step fused
+  int fuse = 1;
+  int last_fused = 0;
 };
 
 namespace rlmd {
@@ -1344,18 +1349,18 @@ int env_train(rlmd_env_t env, const rlmd::ReplayView& rb, int64_t ring_base, uin
 }
 
 // the fused instantiations: one gamble / asset (market: one observed day), S <= 8,
-// A <= 2; RLMD_NO_FUSED_ENV=1 turns the fusion off (separate acting and env launches)
-int g_fuse_env = -1;  // -1: from RLMD_NO_FUSED_ENV at first use; rlmd_train_set_fused sets it
-
+// A <= 2; the env handle's switch (rlmd_train_set_fused; RLMD_NO_FUSED_ENV=1 at
+// creation) turns the fusion off (separate acting and env launches)
 bool env_act_fusable(rlmd_env_t env) {
   const EnvParams& P = env->P;
-  if (g_fuse_env < 0) g_fuse_env = getenv("RLMD_NO_FUSED_ENV") != nullptr ? 0 : 1;
   // any n_gambles / assets / observation days whose action fits the acting body
   // (<= 2 actions) and whose state fits a 16-float staging row; the multi-asset
   // and Dx state widths above 8 take the 16-pitch market instantiation
-  if (g_fuse_env != 1 || P.action_dim > actrows::kMaxA || P.state_dim > 16) return false;
+  if (env->fuse != 1 || P.action_dim > actrows::kMaxA || P.state_dim > 16) return false;
   return P.state_dim <= 8 || P.fam == RLMD_MARKET;
 }
+
+void env_set_last_fused(rlmd_env_t env, bool fused) { env->last_fused = fused ? 1 : 0; }
 
 int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint32_t step, const FusedActArgs& a,
                   int h1p, int nb, int sp, float* obs, double* ep_stats, hipStream_t stream, hipEvent_t ev_start,
@@ -1456,14 +1461,13 @@ int env_market_eval_step(rlmd_env_t env, const float* actions, int window, doubl
 
 // the whole market evaluation in one launch (eval_market_loop_kernel) for the
 // acting shapes with an instantiation; *launched = false leaves it to the
-// caller's per-day loop.  Off with the acting + env fusion (RLMD_NO_FUSED_ENV=1,
-// rlmd_train_set_fused(0)).
+// caller's per-day loop.  Off with the env handle's acting + env fusion
+// (RLMD_NO_FUSED_ENV=1, rlmd_train_set_fused(env, 0)).
 int env_act_market_eval(rlmd_env_t env, const FusedActArgs& a, int h1p, int nb, int T, int window, double lo,
                         double hi, float* obs, double* reward, int32_t* steps, double* risk, uint8_t* live,
                         hipStream_t stream, bool* launched) {
   *launched = false;
-  if (g_fuse_env < 0) g_fuse_env = getenv("RLMD_NO_FUSED_ENV") != nullptr ? 0 : 1;
-  const bool off = g_fuse_env == 0;
+  const bool off = env->fuse == 0;
   const EnvParams& P = env->P;
   const int sp = a.S <= 8 ? 8 : 16;
   if (off || P.fam != RLMD_MARKET || a.n != P.n_lanes || a.S > 16 || a.A > actrows::kMaxA || P.risk_dim > 8 ||
@@ -1522,6 +1526,7 @@ int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t 
   rlmd::env_dims_for(*cfg, S, A, R, D);
   RLMD_CHECK(A <= RLMD_MAX_ACTION, "action dim too large");
   auto* e = new rlmd_env_s();
+  e->fuse = getenv("RLMD_NO_FUSED_ENV") != nullptr ? 0 : 1;
   EnvParams& P = e->P;
   memset(&P, 0, sizeof(P));
   P.fam = cfg->family;
@@ -1709,10 +1714,13 @@ int rlmd_debug_ts_actenv(unsigned long long* out, int n) {
 }
 #endif
 
-int rlmd_train_set_fused(int32_t on) {
-  rlmd::g_fuse_env = on ? 1 : 0;
+int rlmd_train_set_fused(rlmd_env_t env, int32_t on) {
+  RLMD_CHECK(env, "null env");
+  env->fuse = on ? 1 : 0;
   return 0;
 }
+
+int rlmd_train_last_fused(rlmd_env_t env) { return env ? env->last_fused : 0; }
 
 int rlmd_train_episode_log(rlmd_env_t env, int32_t cap_per_wave) {
   RLMD_CHECK(env, "null env");

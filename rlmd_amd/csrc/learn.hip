@@ -253,6 +253,50 @@ struct Scratch {
   int32_t* rank1;  // the rows' top-k selection ranks of this update (critic update -> statistics)
 };
 
+// In-library event profiler of one agent handle (bench.py: live per-phase kernel
+// durations of its train steps and acting calls).
+struct PhaseProfiler {
+  ~PhaseProfiler() {
+    for (auto& ph : ev)
+      for (auto& v : ph)
+        for (hipEvent_t e : v) (void)hipEventDestroy(e);
+  }
+  bool enabled = false;
+  int mask = 7;  // phases recorded: bit p = phase p (rlmd_profile_enable: 1 all, 2 the env kernel's only)
+  std::vector<hipEvent_t> ev[3][2];  // phase x {start, stop}: 0 act, 1 env, 2 learn
+  size_t used[3] = {0, 0, 0};
+  int record(int phase, int which, hipStream_t s) {
+    if (!enabled || !(mask >> phase & 1)) return 0;
+    auto& v = ev[phase][which];
+    const size_t i = which == 0 ? used[phase] : used[phase] - 1;
+    if (i >= v.size()) {
+      hipEvent_t e;
+      RLMD_HIP(hipEventCreate(&e));
+      v.push_back(e);
+    }
+    RLMD_HIP(hipEventRecord(v[i], s));
+    if (which == 0) used[phase]++;
+    return 0;
+  }
+  // a {start, stop} pair for one kernel launch (hipExtLaunchKernelGGL stamps
+  // them at the dispatch's own begin / end, like rocprofv3's kernel trace);
+  // {null, null} when disabled
+  int pair(int phase, hipEvent_t* start, hipEvent_t* stop) {
+    *start = *stop = nullptr;
+    if (!enabled || !(mask >> phase & 1)) return 0;
+    const size_t i = used[phase];
+    for (int w = 0; w < 2; ++w)
+      if (i >= ev[phase][w].size()) {
+        hipEvent_t e;
+        RLMD_HIP(hipEventCreate(&e));
+        ev[phase][w].push_back(e);
+      }
+    *start = ev[phase][0][i];
+    *stop = ev[phase][1][i];
+    used[phase]++;
+    return 0;
+  }
+};
 }  // namespace
 }  // namespace rlmd
 
@@ -293,6 +337,7 @@ struct rlmd_agent_s {
   // row backward + weight-gradient GEMM + Adam launches
   bool fused_update = false;
   bool fused_actor = false;  // the actor step too (actions <= 2)
+  rlmd::PhaseProfiler prof;  // rlmd_profile_enable / _read
 };
 
 namespace rlmd {
@@ -1175,15 +1220,13 @@ int rlmd_eval_market(rlmd_env_t env, rlmd_agent_t ag, const int32_t* start_dev, 
   return 0;
 }
 
-static int prof_pair(int phase, hipEvent_t* start, hipEvent_t* stop);
-
 int rlmd_agent_act(rlmd_agent_t ag, const float* obs, int64_t n, float* actions, int32_t mode,
                    uint64_t noise_ctr, const float* eps, void* stream) {
   RLMD_CHECK(ag && obs && actions, "null argument");
   RLMD_CHECK(mode == 0 || mode == 1, "mode must be 0 (stochastic) or 1 (deterministic)");
   // with rlmd_profile_enable, the fused acting kernel's own begin / end land in phase 0
   hipEvent_t e0, e1;
-  RLMD_TRY(prof_pair(0, &e0, &e1));
+  RLMD_TRY(ag->prof.pair(0, &e0, &e1));
   return rlmd::agent_act(ag, obs, n, actions, mode, noise_ctr, eps, (hipStream_t)stream, false, e0, e1);
 }
 
@@ -1255,81 +1298,35 @@ int rlmd_status_poll(rlmd_agent_t ag, int32_t* flags_host, int32_t* nan_update_h
   return 0;
 }
 
-// ---- in-library event profiler (bench.py: live per-phase kernel durations) ----
-namespace {
-struct PhaseProfiler {
-  bool enabled = false;
-  int mask = 7;  // phases recorded: bit p = phase p (rlmd_profile_enable: 1 all, 2 the env kernel's only)
-  std::vector<hipEvent_t> ev[3][2];  // phase x {start, stop}: 0 act, 1 env, 2 learn
-  size_t used[3] = {0, 0, 0};
-  int record(int phase, int which, hipStream_t s) {
-    if (!enabled || !(mask >> phase & 1)) return 0;
-    auto& v = ev[phase][which];
-    const size_t i = which == 0 ? used[phase] : used[phase] - 1;
-    if (i >= v.size()) {
-      hipEvent_t e;
-      RLMD_HIP(hipEventCreate(&e));
-      v.push_back(e);
-    }
-    RLMD_HIP(hipEventRecord(v[i], s));
-    if (which == 0) used[phase]++;
-    return 0;
-  }
-  // a {start, stop} pair for one kernel launch (hipExtLaunchKernelGGL stamps
-  // them at the dispatch's own begin / end, like rocprofv3's kernel trace);
-  // {null, null} when disabled
-  int pair(int phase, hipEvent_t* start, hipEvent_t* stop) {
-    *start = *stop = nullptr;
-    if (!enabled || !(mask >> phase & 1)) return 0;
-    const size_t i = used[phase];
-    for (int w = 0; w < 2; ++w)
-      if (i >= ev[phase][w].size()) {
-        hipEvent_t e;
-        RLMD_HIP(hipEventCreate(&e));
-        ev[phase][w].push_back(e);
-      }
-    *start = ev[phase][0][i];
-    *stop = ev[phase][1][i];
-    used[phase]++;
-    return 0;
-  }
-};
-PhaseProfiler g_prof;
-}  // namespace
 
-static int prof_pair(int phase, hipEvent_t* start, hipEvent_t* stop) { return g_prof.pair(phase, start, stop); }
-
-int rlmd_profile_enable(int32_t on) {
+int rlmd_profile_enable(rlmd_agent_t ag, int32_t on) {
+  RLMD_CHECK(ag, "null agent");
   RLMD_HIP(hipDeviceSynchronize());
-  g_prof.enabled = on != 0;
+  rlmd::PhaseProfiler& pr = ag->prof;
+  pr.enabled = on != 0;
   // 2: only the events attached to the env kernel's own dispatch (phase 1): the
   // phase markers around acting / learning cost the stream ~25 us per C2 step
-  g_prof.mask = on == 2 ? 2 : 7;
-  for (int p = 0; p < 3; ++p) g_prof.used[p] = 0;
+  pr.mask = on == 2 ? 2 : 7;
+  for (int p = 0; p < 3; ++p) pr.used[p] = 0;
   return 0;
 }
 
-int rlmd_profile_read(double* ms_out3, int64_t* count_out3) {
-  RLMD_CHECK(ms_out3 && count_out3, "null argument");
+int rlmd_profile_read(rlmd_agent_t ag, double* ms_out3, int64_t* count_out3) {
+  RLMD_CHECK(ag && ms_out3 && count_out3, "null argument");
   RLMD_HIP(hipDeviceSynchronize());
+  const rlmd::PhaseProfiler& pr = ag->prof;
   for (int p = 0; p < 3; ++p) {
     double tot = 0.0;
-    for (size_t i = 0; i < g_prof.used[p]; ++i) {
+    for (size_t i = 0; i < pr.used[p]; ++i) {
       float ms = 0.f;
-      RLMD_HIP(hipEventElapsedTime(&ms, g_prof.ev[p][0][i], g_prof.ev[p][1][i]));
+      RLMD_HIP(hipEventElapsedTime(&ms, pr.ev[p][0][i], pr.ev[p][1][i]));
       tot += ms;
     }
     ms_out3[p] = tot;
-    count_out3[p] = (int64_t)g_prof.used[p];
+    count_out3[p] = (int64_t)pr.used[p];
   }
   return 0;
 }
-
-namespace {
-int g_last_fused = 0;  // whether the last rlmd_train_step ran the fused acting + env kernel
-}
-
-int rlmd_train_last_fused(void) { return g_last_fused; }
 
 int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlmd_train_cfg* cfg,
                     float* obs, float* actions, double* ep_stats, float* stats, void* stream) {
@@ -1361,11 +1358,11 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   }
   if (!random) {
     RLMD_CHECK(ag, "policy acting needs an agent");
-    RLMD_TRY(g_prof.record(0, 0, st));
+    RLMD_TRY(ag->prof.record(0, 0, st));
     // one refresh of every compute copy serves the acting and the K updates below
     RLMD_TRY(rlmd::refresh_copies(ag, st));
     if (!fused) RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st, true));
-    RLMD_TRY(g_prof.record(0, 1, st));
+    RLMD_TRY(ag->prof.record(0, 1, st));
   }
   double lo = -INFINITY, hi = INFINITY;
   if (window) {
@@ -1375,9 +1372,9 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
     hi = width * 0.99;
   }
   const int64_t base = rlmd::replay_mem_idx(rb);
-  hipEvent_t e0, e1;
-  RLMD_TRY(g_prof.pair(1, &e0, &e1));
-  g_last_fused = fused ? 1 : 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (ag) RLMD_TRY(ag->prof.pair(1, &e0, &e1));
+  rlmd::env_set_last_fused(env, fused);
   if (!fused) {
     RLMD_TRY(rlmd::env_train(env, v, base, (uint32_t)cs, actions, random ? 1 : 0, cfg->abs_warmup, window ? 1 : 0,
                              lo, hi, obs, ep_stats, st, e0, e1));
@@ -1389,9 +1386,9 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   }
   rlmd::replay_advance(rb, N);
   if (ag && cfg->k_updates > 0 && rlmd::replay_mem_idx(rb) > ag->cfg.batch) {
-    RLMD_TRY(g_prof.record(2, 0, st));
+    RLMD_TRY(ag->prof.record(2, 0, st));
     RLMD_TRY(rlmd::agent_learn_k(ag, rb, cfg->k_updates, stats, st, !random));
-    RLMD_TRY(g_prof.record(2, 1, st));
+    RLMD_TRY(ag->prof.record(2, 1, st));
   }
   return 0;
 }

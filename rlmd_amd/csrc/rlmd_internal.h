@@ -68,6 +68,7 @@ int env_market_eval_step(rlmd_env_t env, const float* actions, int window, doubl
                          double* reward, int32_t* steps, double* risk, uint8_t* live, hipStream_t stream);
 int env_episode_steps(rlmd_env_t env);  // market: steps until done_time
 int env_lanes(rlmd_env_t env);
+void env_set_last_fused(rlmd_env_t env, bool fused);  // rlmd_train_last_fused of this handle
 int env_state_dim(rlmd_env_t env);
 int env_action_dim(rlmd_env_t env);
 

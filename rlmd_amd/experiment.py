@@ -112,7 +112,8 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
                    warmup_steps=1000, smoothing_window=2000, buffer=1_000_000, multi_steps=1, precision="bf16",
                    seed=0, results_root=".", test_agent=True, device="cuda:0", test_days=250,
                    trainer_factory=None, gather_device=None, episode_rows=True, episode_cap=None, trail=50,
-                   checkpoint=True, continue_trials=False, max_episode_rows=1 << 22, **trainer_kw):
+                   checkpoint=True, continue_trials=False, max_episode_rows=1 << 22, schedule="updates",
+                   **trainer_kw):
     """Train n_trials independent vectorised agents (sharded over the ranks of an
     initialised process group, trial t on rank t % world) and save the
     reference's four log arrays on rank 0; returns (file stem, ExperimentLog),
@@ -130,6 +131,9 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
     per-episode trial rows of one trial (host memory and the logging gather:
     (19 + risk) x 4 B per row); a run that exceeds it raises, pointing at
     episode_rows=False (one aggregate row per logging interval).
+    schedule: warm-up / smoothing lengths in the reference's env steps mapped to
+    the same number of learner updates ("updates", trainer.schedule_steps) or
+    taken as vector steps per lane ("vector").
     checkpoint: trailing-`trail` checkpoints under the reference's models/ path.  continue_trials: inputs["continue"] — trial t starts from
     trial t-1's last checkpoint and final log temperature (run on one rank, as
     the chain is sequential).  trainer_factory(seed, init_logtemp) replaces the
@@ -146,7 +150,10 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
     rdim = (logs.market_log_dim(eid, n_gambles) if market else logs.multi_log_dim(eid, n_gambles))
     lg = logs.ExperimentLog(n_trials, n_rows, n_evals, n_eval, rdim, market=market, max_rows=max_episode_rows)
     if trainer_factory is None:
-        from .trainer import VecTrainer
+        from .trainer import VecTrainer, schedule_steps
+
+        warmup_steps = schedule_steps(warmup_steps, k_updates, schedule)
+        smoothing_window = schedule_steps(smoothing_window, k_updates, schedule)
 
         def trainer_factory(sd, init_logtemp=0.0):
             return VecTrainer(env, investor, n_lanes, n_gambles, algo=algo, loss=loss, k_updates=k_updates,

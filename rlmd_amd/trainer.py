@@ -26,6 +26,23 @@ DEFAULTS = {
 }
 
 
+def schedule_steps(steps, k_updates, schedule="updates"):
+    """The reference's warm-up / smoothing lengths (env steps of its single stream,
+    where one env step is one learner update: main.py:256-257) as vector steps.
+
+    "updates": the schedule ends after the same number of LEARNER UPDATES as in the
+    reference, ceil(steps / K) vector steps at K updates per vector step.  This is
+    the default of the vectorised drivers (tools/converge.py, run_experiment):
+    counted per lane in vector steps ("vector"), a 1e3-step warm-up at K = 8 is
+    8,000 updates on random-action data — measured: TD3 on Dice_SH_InvA then
+    saturates both actions at the tanh bounds (lev 1.98, no safe haven, -57 %/step)
+    and never recovers, where the reference's 800 warm-up updates leave it at
+    +0.4 %/step."""
+    if schedule == "vector" or k_updates <= 1:
+        return int(steps)
+    return -(-int(steps) // int(k_updates))
+
+
 class VecTrainer:
     def __init__(self, env="gbm", investor="A", n_lanes=65536, n_gambles=1, algo="SAC", loss="MSE",
                  k_updates=1, replay_capacity=1 << 20, seed=0, warmup_steps=1000,
@@ -33,6 +50,8 @@ class VecTrainer:
                  prices=None, obs_days=1, time_length=0, shuffle_days=5, sample_days=0,
                  device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99, s_dist="N",
                  initial_logtemp=0.0):
+        """warmup_steps / smoothing_window: vector steps per lane (the ABI's counters;
+        schedule_steps converts the reference's lengths)."""
         self.device = torch.device(device)
         self.env = VecEnv(env, investor, n_lanes, n_gambles, seed=seed, prices=prices, obs_days=obs_days,
                           time_length=time_length, shuffle_days=shuffle_days, sample_days=sample_days,
@@ -75,6 +94,27 @@ class VecTrainer:
     def run(self, n_steps):
         for _ in range(n_steps):
             self.step()
+
+    # per-handle switches (several trainers may share a process, each on its stream)
+    def set_fused(self, on):
+        """The acting + env fusion of this trainer's env (rlmd_train_set_fused)."""
+        check(_abi.lib().rlmd_train_set_fused(self.env.h, 1 if on else 0))
+
+    def last_fused(self):
+        return bool(_abi.lib().rlmd_train_last_fused(self.env.h))
+
+    def profile(self, mode):
+        """rlmd_profile_enable on this trainer's agent: 0 off, 1 every phase, 2 the
+        env kernel's dispatch only."""
+        check(_abi.lib().rlmd_profile_enable(self.agent.h, int(mode)))
+
+    def profile_read(self):
+        """(summed ms, launch count) per phase: 0 acting, 1 env kernel, 2 learn."""
+        import ctypes as C
+
+        ms, cnt = (C.c_double * 3)(), (C.c_int64 * 3)()
+        check(_abi.lib().rlmd_profile_read(self.agent.h, ms, cnt))
+        return list(ms), list(cnt)
 
     def last_stats(self, shadow=False, low_mul=1.0, high_mul=10.0):
         """loss[11] | logtemp | loss_params[4] of the last update (numpy f64).
@@ -182,7 +222,7 @@ class VecTrainer:
 
 
 def market_evaluate(agent, prices, investor, obs_days, test_days, starts, cum_step, warmup_steps,
-                    smoothing_window, shuffle_days=3, seed=0, action_days=1, device="cuda:0", env=None):
+                    smoothing_window, shuffle_days=3, seed=0, action_days=1, device="cuda:0", env=None, fused=None):
     """eval_market (tools/eval_episodes.py:402-611) on the device, one lane per
     episode: a Market_Inv?_D1/Dx env of time_length test_days + obs_days - 1
     starting at price row starts[i] (gap + eval_start_idx), its extract shuffled
@@ -200,6 +240,8 @@ def market_evaluate(agent, prices, investor, obs_days, test_days, starts, cum_st
                      sample_days=tl * action_days + 1, device=dev)
     assert env.n_lanes == n
     assert agent.S == env.state_dim and agent.A == env.action_dim, "agent / env dims differ"
+    if fused is not None:  # the env handle's one-launch switch (rlmd_train_set_fused)
+        check(_abi.lib().rlmd_train_set_fused(env.h, 1 if fused else 0))
     n_days = np.asarray(prices).shape[0]
     if starts.min() < 0 or starts.max() + tl * action_days + 1 > n_days:
         raise ValueError("an evaluation slice leaves the price table")
@@ -220,3 +262,44 @@ def market_evaluate(agent, prices, investor, obs_days, test_days, starts, cum_st
                               stream_ptr()))
     return {"reward": reward.cpu().numpy(), "steps": steps.cpu().numpy(), "risk": risk.cpu().numpy(),
             "risk_log": risk_log.cpu().numpy(), "stats": stats[1:15].cpu().numpy()}
+
+
+class SeedGroup:
+    """Several independent seeds of one workload on one GPU (GPU g runs
+    seeds {g, g + G, ...}; the reference's trial loop, rl_multiplicative.py:154-183,
+    rl_market.py:167-196, runs them one after another).
+
+    Each seed is a whole VecTrainer — its own lanes, replay ring, learner and
+    per-handle switches — launched on its own HIP stream, so the seeds' kernel
+    chains run concurrently on the chip (one learner's latency-bound update chain
+    leaves most CUs idle).  Nothing is shared between seeds: every seed computes
+    exactly what it computes alone (tests/test_seeds_gpu.py checks bit-equality)."""
+
+    def __init__(self, seeds, device="cuda:0", **kw):
+        import torch
+
+        self.device = torch.device(device)
+        self.seeds = list(seeds)
+        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.seeds]
+        self.trainers = []
+        for s, st in zip(self.seeds, self.streams):
+            with torch.cuda.stream(st):
+                kws = dict(kw)
+                kws.setdefault("init_seed", s)
+                self.trainers.append(VecTrainer(seed=s, device=device, **kws))
+        self.synchronize()
+
+    def step(self, k_updates=None):
+        """One vector step of every seed, each enqueued on its own stream."""
+        import torch
+
+        for tr, st in zip(self.trainers, self.streams):
+            with torch.cuda.stream(st):
+                tr.step(k_updates)
+
+    def synchronize(self):
+        for st in self.streams:
+            st.synchronize()
+
+    def __len__(self):
+        return len(self.trainers)

@@ -181,15 +181,10 @@ def test_eval_market_one_launch_matches_day_loop(golden, dev, algo, h1, h2, inv,
     test_days = 40
     starts = np.random.default_rng(7).integers(0, prices.shape[0] - test_days - d - 1, size=203)
     cum, warm, sw = (50, 10, 100) if window else (500, 10, 100)
-    lib = _abi.lib()
     outs = []
-    try:
-        for fused in (1, 0):
-            lib.rlmd_train_set_fused(fused)
-            outs.append(market_evaluate(ag, prices, inv, d, test_days, starts, cum, warm, sw, shuffle_days=3, seed=11,
-                                        device=dev))
-    finally:
-        lib.rlmd_train_set_fused(1)
+    for fused in (True, False):  # the evaluation env's switch (per handle)
+        outs.append(market_evaluate(ag, prices, inv, d, test_days, starts, cum, warm, sw, shuffle_days=3, seed=11,
+                                    device=dev, fused=fused))
     a, b = outs
     np.testing.assert_array_equal(a["steps"], b["steps"])
     np.testing.assert_array_equal(a["reward"], b["reward"])
@@ -210,23 +205,22 @@ def test_eval_market_one_launch_time(dev):
     prices = 100.0 * np.exp(np.cumsum(0.01 * rng.standard_normal((9167, 1)), axis=0))
     ag = DeviceAgent("SAC", 5, 1, 256, 256, 16, 8, precision="bf16", seed=1, device=dev)
     starts = rng.integers(0, 9167 - 260, size=100)
-    lib = _abi.lib()
+    from rlmd_amd.envs import VecEnv
+
     ms = {}
-    try:
-        for fused in (1, 0):
-            lib.rlmd_train_set_fused(fused)
-            market_evaluate(ag, prices, "A", 1, 250, starts, 5000, 10, 100, device=dev)
-            torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(5):
-                out = market_evaluate(ag, prices, "A", 1, 250, starts, 5000, 10, 100, device=dev)
-            e1.record()
-            torch.cuda.synchronize()
-            ms[fused] = e0.elapsed_time(e1) / 5
-            assert out["steps"].max() == 250
-    finally:
-        lib.rlmd_train_set_fused(1)
+    for fused in (1, 0):
+        env = VecEnv("market", "A", 100, 1, seed=1, prices=prices, obs_days=1, time_length=250, shuffle_days=3,
+                     sample_days=251, device=dev)
+        market_evaluate(ag, prices, "A", 1, 250, starts, 5000, 10, 100, device=dev, env=env, fused=bool(fused))
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            out = market_evaluate(ag, prices, "A", 1, 250, starts, 5000, 10, 100, device=dev, env=env)
+        e1.record()
+        torch.cuda.synchronize()
+        ms[fused] = e0.elapsed_time(e1) / 5
+        assert out["steps"].max() == 250
     print(f"C4 eval event: one launch {ms[1]:.3f} ms, per-day loop {ms[0]:.3f} ms")
     assert ms[1] < ms[0]
 
@@ -268,9 +262,8 @@ def test_eval_market_one_launch_matches_reference(golden, dev, c):
     init = reference_init(algo, S, A, h1, h2, seed=1)
     init["actor"] = [torch.from_numpy(g[f"case{c}/init/actor.{pn}"]) for pn in layer_names(algo, "actor")]
     ag = DeviceAgent(algo, S, A, h1, h2, 16, 8, precision="bf16", init=init, device=dev)
-    _abi.lib().rlmd_train_set_fused(1)
     out = market_evaluate(ag, g[f"case{c}/prices"], inv, d, test_days, g[f"case{c}/gaps"], cum, warm, sw,
-                          shuffle_days=1, device=dev)
+                          shuffle_days=1, device=dev, fused=True)
     head = "pi" if algo == "SAC" else "mu"
     pol = _bf16_actor(_golden_actor(g, c))
     rew, steps, risk = oev.market_rollout(algo, None, g[f"case{c}/prices"], inv, d, test_days, g[f"case{c}/gaps"],

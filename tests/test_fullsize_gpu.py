@@ -143,12 +143,11 @@ def test_c3_full_size_dice_sh_td3(dev, loss):
     from rlmd_amd.trainer import VecTrainer
 
     N, T, K, cap, seed = 65536, 4, 8, 1 << 20, 18
-    _abi.lib().rlmd_train_set_fused(1)
     tr = VecTrainer("dice_sh", "A", N, algo="TD3", loss=loss, k_updates=K, replay_capacity=cap, seed=seed,
                     warmup_steps=0, smoothing_window=0, precision="bf16", device=dev, init_seed=seed)
     ora = oe.OracleVecEnv(oe.DICE_SH, oe.INV_A, N, 1, seed=seed)
     a_r = _replay_steps(tr, ora, T, cap)
-    assert _abi.lib().rlmd_train_last_fused() == 1
+    assert tr.last_fused()
     assert tr.batch == 200 and tr.topk == 100 and a_r.shape == (N, 2)
     assert np.abs(a_r).max() <= 0.99 and np.unique(a_r[:, 0]).size > N // 4
     sc = tr.agent.scalars()
@@ -171,12 +170,11 @@ def test_c4_full_size_market_on_stooq_snp(golden, dev):
     N, T, K, cap, seed = 8192, 12, 8, 1 << 20, 0
     prices = golden("stooq_snp.npz")["prices"]
     kw = dict(prices=prices, obs_days=1, time_length=1000, shuffle_days=5, sample_days=1000 + 250 + 1 + 20 - 1)
-    _abi.lib().rlmd_train_set_fused(1)
     tr = VecTrainer("market", "A", N, algo="SAC", k_updates=K, replay_capacity=cap, seed=seed, warmup_steps=0,
                     smoothing_window=0, precision="bf16", device=dev, init_seed=seed, **kw)
     ora = oe.OracleVecEnv(oe.MARKET, oe.INV_A, N, 1, seed=seed, **kw)
     _replay_steps(tr, ora, T, cap, atol=1e-45)
-    assert _abi.lib().rlmd_train_last_fused() == 1
+    assert tr.last_fused()
     np.testing.assert_array_equal(tr.env.lane_start(), ora.start)
     sc = tr.agent.scalars()
     assert sc["learn_step_cntr"] == T * K and sc["nan_flag"] == 0

@@ -78,8 +78,8 @@ def test_wide_shapes_match_oracle(golden, dev, env, inv, n, obs_days, algo):
 
 def _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days):
     N, T, seed = 4000, 16, 11  # 4000 lanes: a ragged last 64-lane block
-    _lib().rlmd_train_set_fused(1)
     tr, kw = _trainer(dev, golden, env, inv, algo, N, T, seed=seed, n=n, obs_days=obs_days)
+    tr.set_fused(1)
     ora = oe.OracleVecEnv(FAMS[env], INVS[inv], N, n, seed=seed, **kw)
     obs = ora.reset()
     tr.episode_log(64)
@@ -89,7 +89,7 @@ def _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days):
     ended = 0
     for t in range(T):
         tr.step()
-        assert _lib().rlmd_train_last_fused() == int(expect_fused), "unexpected acting + env path"
+        assert tr.last_fused() == expect_fused, "unexpected acting + env path"
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
         assert np.all(np.abs(a_r) <= 0.99) and np.all(np.isfinite(a_r))
         ns, r, d, risk = ora.step(a_r.astype(np.float32))  # post-window policy actions: f32
@@ -128,19 +128,16 @@ def _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days):
 def test_fused_equals_unfused(golden, dev, env, inv, n, obs_days, algo):
     N, T = 2048, 12
     out = []
-    try:
-        for fused in (1, 0):
-            _lib().rlmd_train_set_fused(fused)
-            tr, _ = _trainer(dev, golden, env, inv, algo, N, T, k=1, seed=5, n=n, obs_days=obs_days)
-            for t in range(T):
-                tr.step()
-                assert _lib().rlmd_train_last_fused() == fused
-            ring = read_ring(tr, 0, N * T)
-            w, tt = tr.env.lane_state()
-            out.append((ring, w, tt, tr.obs.cpu().numpy(), tr.agent.params.cpu().numpy().copy()))
-            del tr
-    finally:
-        _lib().rlmd_train_set_fused(1)
+    for fused in (1, 0):
+        tr, _ = _trainer(dev, golden, env, inv, algo, N, T, k=1, seed=5, n=n, obs_days=obs_days)
+        tr.set_fused(fused)  # per env handle
+        for t in range(T):
+            tr.step()
+            assert tr.last_fused() == bool(fused)
+        ring = read_ring(tr, 0, N * T)
+        w, tt = tr.env.lane_state()
+        out.append((ring, w, tt, tr.obs.cpu().numpy(), tr.agent.params.cpu().numpy().copy()))
+        del tr
     (ra, wa, ta, oa, pa), (rb, wb, tb, ob, pb) = out
     for name, x, y in zip(("s", "a", "r", "s2", "d"), ra, rb):
         np.testing.assert_array_equal(x, y, err_msg=f"ring {name}")

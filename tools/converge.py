@@ -96,15 +96,18 @@ def kelly(env):
 
 
 def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eval_every=500, n_eval=4096,
-        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE"):
+        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE", schedule="updates"):
+    """warmup / smoothing: the reference's lengths (main.py gym_envs warm-up 1e3,
+    smoothing_window_mul 2e3), mapped to vector steps by trainer.schedule_steps."""
     import torch
 
-    from rlmd_amd.trainer import VecTrainer
+    from rlmd_amd.trainer import VecTrainer, schedule_steps
 
     fam, inv = FAMILY[env]
     tr = VecTrainer(env=fam, investor=inv, n_lanes=lanes, n_gambles=1, algo=algo, loss=loss, k_updates=k,
-                    replay_capacity=replay, seed=seed, warmup_steps=warmup, smoothing_window=smoothing,
-                    precision=precision, device=device, init_seed=seed)
+                    replay_capacity=replay, seed=seed, warmup_steps=schedule_steps(warmup, k, schedule),
+                    smoothing_window=schedule_steps(smoothing, k, schedule), precision=precision, device=device,
+                    init_seed=seed)
     l_star, g_star = kelly(env)
     reset_obs = tr.env.reset()[:1].float().clone()  # the reset state (identical for every lane)
     tr2 = None
@@ -149,11 +152,12 @@ def main():
     ap.add_argument("--replay", type=int, default=1 << 20)
     ap.add_argument("--algo", default="SAC", choices=["SAC", "TD3"])
     ap.add_argument("--loss", default="MSE")
+    ap.add_argument("--schedule", default="updates", choices=["updates", "vector"])
     ap.add_argument("--out", default=None, help="append JSON lines here")
     a = ap.parse_args()
     out = open(a.out, "a") if a.out else None
     run(a.env, a.lanes, a.k, a.steps, a.precision, a.warmup, a.smoothing, a.eval_every, a.n_eval, a.seed,
-        a.replay, a.algo, out, loss=a.loss)
+        a.replay, a.algo, out, loss=a.loss, schedule=a.schedule)
 
 
 if __name__ == "__main__":

@@ -1,27 +1,22 @@
 """Env-kernel timing probe (GPU): the C2 fused env step with and without the
 episode-statistics accumulator, K = 0 learner updates.  Prints phase times."""
-import ctypes as C
 import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
-from rlmd_amd import _abi
 from rlmd_amd.trainer import VecTrainer
 
 
 def run(tr, steps=50):
-    lib = _abi.lib()
     torch.cuda.synchronize()
-    _abi.check(lib.rlmd_profile_enable(1))
+    tr.profile(1)
     for _ in range(steps):
         tr.step()
     torch.cuda.synchronize()
-    ms = (C.c_double * 3)()
-    cnt = (C.c_int64 * 3)()
-    _abi.check(lib.rlmd_profile_read(ms, cnt))
-    _abi.check(lib.rlmd_profile_enable(0))
+    ms, cnt = tr.profile_read()
+    tr.profile(0)
     return [ms[i] / max(cnt[i], 1) for i in range(3)]
 
 

@@ -22,7 +22,7 @@ def main():
         tr.step()
     torch.cuda.synchronize()
     for prof in (0, 1):
-        _abi.check(_abi.lib().rlmd_profile_enable(prof))
+        tr.profile(prof)
         for n in (1, 3, 10):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -33,7 +33,7 @@ def main():
             t2 = time.perf_counter()
             print(f"profile {prof} steps {n}: host enqueue {1e6 * (t1 - t0) / n:8.1f} us/step, "
                   f"wall {1e6 * (t2 - t0) / n:8.1f} us/step", flush=True)
-        _abi.check(_abi.lib().rlmd_profile_enable(0))
+        tr.profile(0)
 
 
 if __name__ == "__main__":

@@ -138,12 +138,13 @@ def run_env():
     lib = _abi._LIB
     lib.rlmd_debug_ts_env.restype = C.c_int
     lib.rlmd_debug_ts_env.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    lib.rlmd_train_set_fused(0)
+    fused_mode = 0  # per env handle: set on the trainer below
     from rlmd_amd.trainer import VecTrainer
 
     fam = sys.argv[2] if len(sys.argv) > 2 else "gbm"
     tr = VecTrainer(fam, "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
                     replay_capacity=1 << 20, k_updates=1, device="cuda:0")
+    tr.set_fused(fused_mode)
     nb = 256
     buf = (C.c_ulonglong * (8 * nb))()
     spans, starts, ph = [], [], []
@@ -294,13 +295,14 @@ def run_actenv():
     lib = _abi._LIB
     lib.rlmd_debug_ts_actenv.restype = C.c_int
     lib.rlmd_debug_ts_actenv.argtypes = [C.POINTER(C.c_ulonglong), C.c_int]
-    lib.rlmd_train_set_fused(1)
+    fused_mode = 1  # per env handle: set on the trainer below
     from rlmd_amd.trainer import VecTrainer
 
     fam = sys.argv[2] if len(sys.argv) > 2 else "dice_sh"
     algo = "SAC" if fam == "gbm" else "TD3"
     tr = VecTrainer(fam, "A", 65536, algo=algo, precision="bf16", warmup_steps=0, smoothing_window=0,
                     replay_capacity=1 << 20, k_updates=0, device="cuda:0")
+    tr.set_fused(fused_mode)
     nb = 1024
     buf = (C.c_ulonglong * (8 * nb))()
     rows = []
