@@ -42,10 +42,10 @@ namespace rlmd {
 namespace {
 using namespace actrows;
 
-template <int H1P, int NB, int SP>
-__global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) fused_act_kernel(FusedActArgs a) {
+template <int H1P, int NB, int SP, int MA>
+__global__ void __launch_bounds__(256, H1P == 256 ? (MA == kMaxA ? 3 : 2) : 1) fused_act_kernel(FusedActArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  act_rows<H1P, NB, SP>(
+  act_rows<H1P, NB, SP, MA>(
       a, smem, [] {},
       [&](int, int b, const float* acts, const float*) {
         for (int j = 0; j < a.A; ++j) a.actions[(int64_t)b * a.A + j] = acts[j];
@@ -57,7 +57,7 @@ __global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) fused_act_kernel(Fuse
 bool fused_act_supported(const rlmd_agent_cfg& c) {
   int h1p, nb;
   return c.precision == RLMD_BF16 && fused_shape(c, h1p, nb) && (c.h2 + 31) / 32 * 32 <= 16 * 4 * nb &&
-         c.action_dim <= kMaxA && c.state_dim <= 16;
+         c.action_dim <= kMaxA4 && c.state_dim <= 16;
 }
 
 FusedActArgs fused_act_args(const rlmd_agent_cfg& c, const float* obs, int64_t n, float* actions,
@@ -97,20 +97,27 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
   const FusedActArgs a = fused_act_args(c, obs, n, actions, actor_params, off, w2bf, mode, seed, ctr, eps);
   const dim3 grid((unsigned)((n + kRows - 1) / kRows));
   const int sp = c.state_dim <= 8 ? 8 : 16;
-#define ACT_LAUNCH(H1P_, NB_, SP_)                                                                    \
-  hipExtLaunchKernelGGL((fused_act_kernel<H1P_, NB_, SP_>), grid, dim3(256), act_lds_bytes(H1P_, SP_), st, ev_start, \
-                        ev_stop, 0, a)
+  RLMD_CHECK(c.action_dim <= kMaxA4, "fused acting: at most 4 actions");
+#define ACT_LAUNCH1(H1P_, NB_, SP_, MA_)                                                                          \
+  hipExtLaunchKernelGGL((fused_act_kernel<H1P_, NB_, SP_, MA_>), grid, dim3(256), act_lds_bytes(H1P_, SP_, MA_), st, \
+                        ev_start, ev_stop, 0, a)
+#define ACT_LAUNCH(H1P_, NB_, SP_)                                            \
+  {                                                                           \
+    if (c.action_dim <= kMaxA) ACT_LAUNCH1(H1P_, NB_, SP_, kMaxA);            \
+    else ACT_LAUNCH1(H1P_, NB_, SP_, kMaxA4);                                 \
+  }
   if (h1p == 256) {
-    if (sp == 8) ACT_LAUNCH(256, 4, 8);
-    else ACT_LAUNCH(256, 4, 16);
+    if (sp == 8) ACT_LAUNCH(256, 4, 8)
+    else ACT_LAUNCH(256, 4, 16)
   } else if (h1p == 128) {
-    if (sp == 8) ACT_LAUNCH(128, 4, 8);
-    else ACT_LAUNCH(128, 4, 16);
+    if (sp == 8) ACT_LAUNCH(128, 4, 8)
+    else ACT_LAUNCH(128, 4, 16)
   } else {
-    if (sp == 8) ACT_LAUNCH(416, 5, 8);
-    else ACT_LAUNCH(416, 5, 16);
+    if (sp == 8) ACT_LAUNCH(416, 5, 8)
+    else ACT_LAUNCH(416, 5, 16)
   }
 #undef ACT_LAUNCH
+#undef ACT_LAUNCH1
   RLMD_LAUNCH_CHECK();
   return 0;
 }

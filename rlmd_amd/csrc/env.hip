@@ -716,8 +716,8 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
 // off (the env's NumPy rounding), and so does act.hip: the fused and two-launch
 // steps produce bit-equal actions, rings and wealth.
 // ---------------------------------------------------------------------------
-template <int FAM, int NG, int H1P, int NB, int SP>
-__global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
+template <int FAM, int NG, int H1P, int NB, int SP, int MA>
+__global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA ? 3 : 2) : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
                                                       StatFold sf) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -746,7 +746,11 @@ __global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) act_env_kernel(rlmd::
   };
   auto epi = [&](int, int b, const float* acts, const float* obs_row) {
     const int S = P.state_dim, A = P.action_dim;
-    auto act = [&](int i) -> float { return i == 0 ? acts[0] : acts[1]; };  // A <= 2
+    // the action by a fixed selection chain (no runtime-indexed register array)
+    auto act = [&](int i) -> float {
+      if constexpr (MA == 2) return i == 0 ? acts[0] : acts[1];
+      else return i == 0 ? acts[0] : i == 1 ? acts[1] : i == 2 ? acts[2] : acts[3];
+    };
     const int64_t row = ring_row(ring_base, b, rb.capacity);
     int64_t ep_slot = -1;
     const StepOut o = env_step_lane<FAM, NG, float>(
@@ -792,7 +796,7 @@ __global__ void __launch_bounds__(256, H1P == 256 ? 3 : 1) act_env_kernel(rlmd::
       P.time[b] = t + 1;
     }
   };
-  rlmd::actrows::act_rows<H1P, NB, SP>(a, smem, pro, epi);
+  rlmd::actrows::act_rows<H1P, NB, SP, MA>(a, smem, pro, epi);
   if (sf.part_out) {  // the block's finished-episode statistics, as env_train_kernel
     __shared__ double red[3][256 / 64];
 #pragma unroll
@@ -1356,7 +1360,10 @@ bool env_act_fusable(rlmd_env_t env) {
   // any n_gambles / assets / observation days whose action fits the acting body
   // (<= 2 actions) and whose state fits a 16-float staging row; the multi-asset
   // and Dx state widths above 8 take the 16-pitch market instantiation
-  if (env->fuse != 1 || P.action_dim > actrows::kMaxA || P.state_dim > 16) return false;
+  if (env->fuse != 1 || P.action_dim > actrows::kMaxA4 || P.state_dim > 16) return false;
+  // 3-4 actions (investors C, Dice_SH B / C): the one-gamble / one-day shapes
+  const bool ng1 = P.n == 1 && (P.fam != RLMD_MARKET || P.obs_days == 1);
+  if (P.action_dim > actrows::kMaxA && !(ng1 && P.state_dim <= 8)) return false;
   return P.state_dim <= 8 || P.fam == RLMD_MARKET;
 }
 
@@ -1388,12 +1395,21 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
   const bool ng1 = P.n == 1 && (P.fam != RLMD_MARKET || P.obs_days == 1);
   RLMD_CHECK(ng1 || P.fam != RLMD_DICE_SH, "fused acting + env step: dice_sh has one die");
   RLMD_CHECK(sp == 8 || P.fam == RLMD_MARKET, "fused acting + env step: state wider than 8 (market only)");
-#define FUSED(F, NG, H, B, SP)                                                                                     \
-  hipExtLaunchKernelGGL((act_env_kernel<F, NG, H, B, SP>), grid, block, actrows::act_lds_bytes(H, SP), stream,     \
+#define FUSEDM(F, NG, H, B, SP, MA)                                                                                 \
+  hipExtLaunchKernelGGL((act_env_kernel<F, NG, H, B, SP, MA>), grid, block, actrows::act_lds_bytes(H, SP, MA), stream, \
                         ev_start, ev_stop, 0, a, env->P, step, obs, rb, ring_base, sf)
+#define FUSED(F, NG, H, B, SP) FUSEDM(F, NG, H, B, SP, actrows::kMaxA)
+  // 3-4 actions: one gamble / asset and one observation day (env_act_fusable)
+  const bool ma4 = P.action_dim > actrows::kMaxA;
+#define FUSED4(F)                                                \
+  {                                                              \
+    if (h1p == 256) FUSEDM(F, 1, 256, 4, 8, actrows::kMaxA4);    \
+    else FUSEDM(F, 1, 416, 5, 8, actrows::kMaxA4);               \
+  }
 #define FUSED_FAM(F)                                 \
   {                                                  \
-    if (ng1) {                                       \
+    if (ma4) FUSED4(F)                               \
+    else if (ng1) {                                  \
       if (h1p == 256) FUSED(F, 1, 256, 4, 8);        \
       else FUSED(F, 1, 416, 5, 8);                   \
     } else {                                         \
@@ -1401,12 +1417,14 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
       else FUSED(F, 0, 416, 5, 8);                   \
     }                                                \
   }
+  RLMD_CHECK(!ma4 || (ng1 && sp == 8), "fused acting + env step: 3-4 actions need one gamble / asset and day");
   switch (P.fam) {
     case RLMD_COIN: FUSED_FAM(RLMD_COIN); break;
     case RLMD_DICE: FUSED_FAM(RLMD_DICE); break;
     case RLMD_GBM: FUSED_FAM(RLMD_GBM); break;
     case RLMD_DICE_SH:
-      if (h1p == 256) FUSED(RLMD_DICE_SH, 1, 256, 4, 8);
+      if (ma4) FUSED4(RLMD_DICE_SH)
+      else if (h1p == 256) FUSED(RLMD_DICE_SH, 1, 256, 4, 8);
       else FUSED(RLMD_DICE_SH, 1, 416, 5, 8);
       break;
     default:
@@ -1419,7 +1437,9 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
       break;
   }
 #undef FUSED_FAM
+#undef FUSED4
 #undef FUSED
+#undef FUSEDM
   RLMD_LAUNCH_CHECK();
   env->pending_dst = ep_stats;
   if (ep_stats) {

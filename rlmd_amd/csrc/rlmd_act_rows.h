@@ -24,7 +24,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kRows = 64;
-constexpr int kMaxA = 2;
+constexpr int kMaxA = 2;   // the headline shapes (one gamble / asset: investors A / B, Dice_SH A)
+constexpr int kMaxA4 = 4;  // the wide-action instantiation (investors C, Dice_SH B / C)
 
 
 // RNE f32 -> bf16, NaN kept quiet; branch-free (a select, not a divergent branch)
@@ -51,9 +52,11 @@ struct L1Tiles {
 // The acting body for one 64-row block.  pro() runs once every thread has issued
 // its epilogue loads (a fused caller issues its own per-row loads there); epi(r,
 // b, act, obs_row) runs on thread r < 64 of each valid row b with the row's
-// actions act[kMaxA] (f32) and its observation in LDS (obs_row[0 .. S)).
-template <int H1P, int NB, int SP, typename ProF, typename EpiF>
+// actions act[MA] (f32; MA = kMaxA, or kMaxA4 for 3-4 actions: twice the head
+// registers and partials) and its observation in LDS (obs_row[0 .. S)).
+template <int H1P, int NB, int SP, int MA, typename ProF, typename EpiF>
 __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* smem, ProF pro, EpiF epi) {
+  constexpr int kMaxA = MA;
   constexpr int HP = H1P + 8;  // bf16 row pitch: 16-B aligned fragment reads
   constexpr int NT = L1Tiles<H1P>::NT, NTP = L1Tiles<H1P>::NTP;
   unsigned short* h1s = reinterpret_cast<unsigned short*>(smem);                 // [64][HP]
@@ -242,7 +245,9 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
   // -- per row: sum the 4 wave partials, sample, write the action
   if (tid < kRows && row0 + tid < a.n) {
     const int r = tid, b = row0 + tid;
-    float acts[kMaxA] = {0.f, 0.f};
+    float acts[kMaxA];
+#pragma unroll
+    for (int j = 0; j < kMaxA; ++j) acts[j] = 0.f;
 #pragma unroll
     for (int j = 0; j < kMaxA; ++j) {
       if (j >= A) break;
@@ -276,11 +281,14 @@ inline bool fused_shape(const rlmd_agent_cfg& c, int& h1p, int& nb) {
   return (h1p == 128 && nb == 4) || (h1p == 256 && nb == 4) || (h1p == 416 && nb == 5);
 }
 
-// dynamic LDS of act_rows<h1p, *, sp>
-inline size_t act_lds_bytes(int h1p, int sp) {
+// dynamic LDS of act_rows<h1p, *, sp, ma>
+inline size_t act_lds_bytes(int h1p, int sp, int ma = kMaxA) {
   const int nt = h1p / 16, ntp = (nt + 7) / 8 * 8 + 4;
-  return (size_t)kRows * (h1p + 8) * 2 + 4 * kRows * 2 * kMaxA * 4 + ((size_t)sp * 16 * ntp + h1p + kRows * sp) * 4;
+  return (size_t)kRows * (h1p + 8) * 2 + 4 * kRows * 2 * ma * 4 + ((size_t)sp * 16 * ntp + h1p + kRows * sp) * 4;
 }
+
+// the acting body's action bound for an action count
+inline int act_ma(int action_dim) { return action_dim <= kMaxA ? kMaxA : kMaxA4; }
 
 }  // namespace actrows
 }  // namespace rlmd

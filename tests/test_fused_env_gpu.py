@@ -14,10 +14,11 @@ envs/gbm_envs.py:147-515, envs/market_envs.py:133-202 / :283-358 / :440-528
 (D1), dones tools/env_resources.py:26-200.
 
 Two gambles / assets and market Dx windows run the kernel's run-time-n
-instantiations (WIDE).  Shapes the fused kernel does not instantiate
-(action_dim > 2: the C investors and Dice_SH B/C) run the two-launch path
-(acting kernel + env_train_kernel); the test asserts which path ran
-(rlmd_train_last_fused) and checks both.
+instantiations (WIDE).  Three and four actions (the C investors, Dice_SH B / C,
+market InvC at one day) run the wide-action instantiation (act_env_kernel<...,
+MA = 4>: twice the head registers and partials); shapes with more actions AND
+run-time n keep the two-launch path (acting kernel + env_train_kernel); the test
+asserts which path ran (rlmd_train_last_fused) and checks both.
 
 Fused vs unfused: the same seeded loop with rlmd_train_set_fused(1) and (0),
 learning on (K = 1), must produce bit-identical rings, wealth and parameters
@@ -85,7 +86,9 @@ def _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days):
     tr.episode_log(64)
     at = 1e-45 if env == "market" else 1e-30
     length = np.ones(N, dtype=np.int64)
-    expect_fused = ora.A <= 2 and (ora.S <= 8 or (env == "market" and ora.S <= 16))
+    ng1 = n == 1 and obs_days == 1
+    expect_fused = (ora.A <= 2 and (ora.S <= 8 or (env == "market" and ora.S <= 16))) or (
+        ora.A <= 4 and ng1 and ora.S <= 8)
     ended = 0
     for t in range(T):
         tr.step()
@@ -124,7 +127,9 @@ def _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days):
 @pytest.mark.parametrize("algo", ["SAC", "TD3"])
 @pytest.mark.parametrize("env,inv,n,obs_days", [("coin", "B", 1, 1), ("dice", "A", 1, 1), ("gbm", "A", 1, 1),
                                                 ("dice_sh", "INSURED", 1, 1), ("dice_sh", "A", 1, 1),
-                                                ("market", "B", 1, 1), ("gbm", "A", 2, 1), ("market", "A", 1, 5)])
+                                                ("market", "B", 1, 1), ("gbm", "A", 2, 1), ("market", "A", 1, 5),
+                                                ("gbm", "C", 1, 1), ("coin", "C", 1, 1), ("dice_sh", "B", 1, 1),
+                                                ("dice_sh", "C", 1, 1), ("market", "C", 1, 1)])
 def test_fused_equals_unfused(golden, dev, env, inv, n, obs_days, algo):
     N, T = 2048, 12
     out = []
