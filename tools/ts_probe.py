@@ -48,8 +48,9 @@ def run():
         getattr(lib, fn).argtypes = [C.POINTER(C.c_ulonglong)]
     from rlmd_amd.trainer import VecTrainer
 
-    tr = VecTrainer("gbm", "A", 65536, algo="SAC", precision="bf16", warmup_steps=0, smoothing_window=0,
-                    replay_capacity=1 << 20, k_updates=1, device="cuda:0")
+    td3 = "--td3" in sys.argv  # C3: Dice_SH_InvA, TD3 400/300, B = 200
+    tr = VecTrainer("dice_sh" if td3 else "gbm", "A", 65536, algo="TD3" if td3 else "SAC", precision="bf16",
+                    warmup_steps=0, smoothing_window=0, replay_capacity=1 << 20, k_updates=1, device="cuda:0")
     for _ in range(20):
         tr.step()
     torch.cuda.synchronize()
