@@ -251,7 +251,7 @@ def reduce_ranks(elapsed, ep_stats, steps, world, device, extra=()):
     el_t = torch.tensor([elapsed], dtype=torch.float64, device=device)
     slab = torch.cat([ep_stats.to(device=device, dtype=torch.float64),
                       torch.tensor([steps, *extra], dtype=torch.float64, device=device)])
-    if world > 1:
+    if _dist_on():
         dist.all_reduce(el_t, op=dist.ReduceOp.MAX)
         gathered = [torch.empty_like(slab) for _ in range(world)]
         dist.all_gather(gathered, slab)
@@ -259,6 +259,15 @@ def reduce_ranks(elapsed, ep_stats, steps, world, device, extra=()):
     else:
         slab_all = slab[None]
     return float(el_t.item()), slab_all
+
+
+def _dist_on():
+    """A process group is up: world > 1, or RLMD_BENCH_FORCE_DIST=1 at world 1
+    (the nccl path's rendezvous, barriers, all_reduce and all_gather exercised
+    over RCCL on a one-GPU box)."""
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized()
 
 
 def spawn_ranks(n):
@@ -313,18 +322,18 @@ def timed_region(tr, steps, warmup, world, sync, on_start=None):
     for _ in range(warmup):
         tr.step()
     sync()
-    if world > 1:
+    if _dist_on():
         dist.barrier()
     if on_start is not None:
         on_start()
         sync()
-        if world > 1:
+        if _dist_on():
             dist.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
         tr.step()
     sync()
-    if world > 1:
+    if _dist_on():
         dist.barrier()
     return time.perf_counter() - t0
 
@@ -458,8 +467,13 @@ def main():
     local = local % max(ndev, 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    force_dist = os.environ.get("RLMD_BENCH_FORCE_DIST") == "1"
+    if world > 1 or force_dist:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", "29531")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         if shared:
             dist.init_process_group("gloo")
         else:
@@ -656,8 +670,10 @@ def main():
             out["cpu_baseline_utd1"] = {"all_cores": cpu_lines[2], "1core": cpu_lines[3]}
         else:
             out["cpu_baseline"] = None
+        if force_dist and world == 1:
+            out["process_group"] = f"{dist.get_backend()} at world 1 (RLMD_BENCH_FORCE_DIST)"
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if _dist_on():
         dist.barrier()
         dist.destroy_process_group()
 

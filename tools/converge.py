@@ -49,7 +49,16 @@ SH = dict(p=[1 / 6, 1 / 6, 2 / 3], r=[0.5, -0.5, 0.05], r_sh=[-0.99, 5.0, -0.99]
 # dice_roll_sh_envs.py:290-365); the eval risk row holds lev at column 3 and, for
 # Dice_SH_InvA, lev_sh at column 6 (the reference's eval_risk_log columns)
 FAMILY = {"coin": ("coin", "A"), "dice": ("dice", "A"), "dice_sh": ("dice_sh", "INSURED"), "gbm": ("gbm", "A"),
-          "dice_sh_a": ("dice_sh", "A")}
+          "dice_sh_a": ("dice_sh", "A"), "market": ("market", "A")}
+# C4 (key 21, SNP_InvA, D1): main.py's market schedule -- 1e3 training days per
+# episode, 250 test days, shuffled in 5 / 3-day intervals, a 5-20 day gap
+# (rl_market.py:56-60, eval_episodes.py:402-611); no analytic optimum
+
+
+def market_kw():
+    with np.load(os.path.join(ROOT, "tests", "golden", "stooq_snp.npz"), allow_pickle=False) as z:
+        prices = np.ascontiguousarray(z[z.files[0]], dtype=np.float64).reshape(-1, 1)
+    return dict(prices=prices, obs_days=1, time_length=1000, shuffle_days=5, sample_days=1000 + 250 + 1 + 20 - 1)
 # GBM log-return N(mu - sigma^2 / 2, sigma) (gbm_envs.py:43-63): expected log growth
 # lev * (mu - sigma^2 / 2) per step, monotone in lev (the optimum is the 4.95 corner,
 # tempered by the lev_max termination)
@@ -96,7 +105,7 @@ def kelly(env):
 
 
 def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eval_every=500, n_eval=4096,
-        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE", schedule="updates"):
+        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE", schedule="updates", multi_steps=1):
     """warmup / smoothing: the reference's lengths (main.py gym_envs warm-up 1e3,
     smoothing_window_mul 2e3), mapped to vector steps by trainer.schedule_steps."""
     import torch
@@ -104,12 +113,14 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
     from rlmd_amd.trainer import VecTrainer, schedule_steps
 
     fam, inv = FAMILY[env]
+    kw = market_kw() if env == "market" else {}
     tr = VecTrainer(env=fam, investor=inv, n_lanes=lanes, n_gambles=1, algo=algo, loss=loss, k_updates=k,
                     replay_capacity=replay, seed=seed, warmup_steps=schedule_steps(warmup, k, schedule),
                     smoothing_window=schedule_steps(smoothing, k, schedule), precision=precision, device=device,
-                    init_seed=seed)
-    l_star, g_star = kelly(env)
-    reset_obs = tr.env.reset()[:1].float().clone()  # the reset state (identical for every lane)
+                    init_seed=seed, multi_steps=multi_steps, **kw)
+    l_star, g_star = kelly(env) if env != "market" else (None, None)
+    # the reset state (identical for every lane; market lanes start on their own slices)
+    reset_obs = tr.env.reset()[:1].float().clone() if env != "market" else tr.obs[:1].float().clone()
     tr2 = None
     recs = []
     t0 = time.perf_counter()
@@ -117,16 +128,21 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
         tr.step()
         if step % eval_every == 0 or step == steps:
             a = tr.agent.act(reset_obs, mode=1)[0].cpu().numpy()
-            ev = tr.evaluate(n_eval=n_eval, max_steps=100, with_stats=False)
+            if env == "market":  # eval_risk_log = [gap, risk...] (eval_episodes.py:542-560)
+                ev = tr.evaluate_market(n_eval=min(n_eval, lanes), test_days=250)
+                lev = float(np.mean(ev["risk_log"][:, 3]))
+            else:
+                ev = tr.evaluate(n_eval=n_eval, max_steps=100, with_stats=False)
+                # the reference's statistic: the eval risk rows' leverage column
+                # (eval_episodes.py:267-274 -> eval_risk_log[..., 3]; lev_sh at 6)
+                lev = float(np.mean(ev["risk"][:, 3]))
             grow = 100.0 * float(np.mean(ev["reward"] - 1.0))
-            # the reference's statistic: the eval risk rows' leverage column
-            # (eval_episodes.py:267-274 -> eval_risk_log[..., 3]; lev_sh at 6)
-            lev = float(np.mean(ev["risk"][:, 3]))
             lev_sh = float(np.mean(ev["risk"][:, 6])) if env == "dice_sh_a" else None
             rec = {"env": env, "algo": algo, "loss": loss, "precision": precision, "lanes": lanes, "k": k,
-                   "replay": replay, "step": step, "updates": step * k, "env_steps": step * lanes,
+                   "replay": replay, "multi_steps": multi_steps, "step": step, "updates": step * k, "env_steps": step * lanes,
                    "action": [float(x) for x in a], "lev": lev, "lev_sh": lev_sh,
-                   "eval_growth_pct": grow, "analytic_growth_pct": 100.0 * math.expm1(growth(env, lev, lev_sh)),
+                   "eval_growth_pct": grow,
+                   "analytic_growth_pct": None if env == "market" else 100.0 * math.expm1(growth(env, lev, lev_sh)),
                    "kelly_lev": l_star, "kelly_growth_pct": g_star, "wall_s": time.perf_counter() - t0,
                    "nan_flag": tr.agent.scalars()["nan_flag"]}
             recs.append(rec)
@@ -153,11 +169,12 @@ def main():
     ap.add_argument("--algo", default="SAC", choices=["SAC", "TD3"])
     ap.add_argument("--loss", default="MSE")
     ap.add_argument("--schedule", default="updates", choices=["updates", "vector"])
+    ap.add_argument("--multi-steps", type=int, default=1)
     ap.add_argument("--out", default=None, help="append JSON lines here")
     a = ap.parse_args()
     out = open(a.out, "a") if a.out else None
     run(a.env, a.lanes, a.k, a.steps, a.precision, a.warmup, a.smoothing, a.eval_every, a.n_eval, a.seed,
-        a.replay, a.algo, out, loss=a.loss, schedule=a.schedule)
+        a.replay, a.algo, out, loss=a.loss, schedule=a.schedule, multi_steps=a.multi_steps)
 
 
 if __name__ == "__main__":

@@ -1,9 +1,17 @@
 #!/bin/bash
-# round 4 measurement: default bench line, the C2 profile round, C3 / C5 / C4 traces + MFMA passes
+# round 4 measurement: default bench line, the nccl process group at world 1,
+# the C2 profile round, C3 / C5 / C4 traces + MFMA passes.  Stops at the first
+# failing step (no GPU step after a fault / timeout).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 500 python -u bench.py > gpurun_out/r04_bench.log 2>&1; echo "bench rc=$?"; tail -n 1 gpurun_out/r04_bench.log | cut -c1-300
-timeout -k 10 700 bash tools/profile_round.sh r04 > gpurun_out/r04_prof.log 2>&1; echo "prof rc=$?"
-MFMA=1 CONFIGS="c3 c5 c4" timeout -k 10 900 bash tools/gpu_prof_configs.sh r04 > gpurun_out/r04_prof_cfg.log 2>&1; echo "cfg rc=$?"
+step() { local name=$1; shift; "$@"; local rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || exit $rc; }
+step bench timeout -k 10 500 python -u bench.py > gpurun_out/r04_bench.log 2>&1
+tail -n 1 gpurun_out/r04_bench.log | cut -c1-300
+step nccl1 env RLMD_BENCH_FORCE_DIST=1 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 \
+  --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 20 --warmup 5 \
+  --no-cpu-baseline --no-companion --k-sweep 8 --seeds-per-gpu "" > gpurun_out/r04_bench_nccl1.log 2>&1
+step prof timeout -k 10 700 bash tools/profile_round.sh r04 > gpurun_out/r04_prof.log 2>&1
+step cfg env MFMA=1 CONFIGS="c3 c5 c4" timeout -k 10 900 bash tools/gpu_prof_configs.sh r04 \
+  > gpurun_out/r04_prof_cfg.log 2>&1
 echo ALLDONE
