@@ -418,11 +418,15 @@ __device__ inline double philox_draw(const EnvParams& P, uint32_t lane, uint32_t
 // reset one lane: episode start (market: new slice), state element writer
 // start_at >= 0 (market): the episode's first price row is given (eval_market's
 // gap index) instead of drawn.
+// ep_now >= 0: the lane's current episode counter, already in a register (the
+// training step's epilogue loaded it with the lane state; re-reading it here put
+// a dependent global load into the tail of every wave with a finished lane).
 template <int FAM, typename StF>
-__device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st, int start_at = -1) {
+__device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st, int start_at = -1,
+                                      int64_t ep_now = -1) {
   P.wealth[lane] = kInitialValue;
   P.time[lane] = 1;
-  const uint32_t ep = P.episode[lane] + 1;
+  const uint32_t ep = (ep_now >= 0 ? (uint32_t)ep_now : P.episode[lane]) + 1;
   P.episode[lane] = ep;
   constexpr FamConst C = fam_const(FAM);
   st(0, kInitialValue / C.max_value);
@@ -670,7 +674,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
       st_n = 1.0;
       st_r = o.reward;
       st_t = (double)t;
-      env_reset_lane<FAM>(P, lane, [&](int k, double v) { obs[(int64_t)lane * S + k] = (float)v; });
+      env_reset_lane<FAM>(P, lane, [&](int k, double v) { obs[(int64_t)lane * S + k] = (float)v; }, -1, ep);
     } else {
       P.wealth[lane] = o.W;
       P.time[lane] = t + 1;
@@ -716,6 +720,29 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
 // off (the env's NumPy rounding), and so does act.hip: the fused and two-launch
 // steps produce bit-equal actions, rings and wealth.
 // ---------------------------------------------------------------------------
+// the state width when it is a compile-time constant (0: run time): Dice_SH 6,
+// coin / dice / GBM 4 + n at a fixed n; market rows depend on obs_days
+template <int FAM, int NG>
+constexpr int kStateRegs = FAM == RLMD_MARKET ? 0 : (FAM == RLMD_DICE_SH ? 6 : (NG > 0 ? 4 + NG : 0));
+
+typedef float f32x4u __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f32x2u __attribute__((ext_vector_type(2), aligned(4)));
+
+// one row of N floats at a 4-byte aligned address as 16-, 8- and 4-byte stores
+// (gfx950 global stores take dword alignment): a 5- or 6-float replay row is two
+// store instructions instead of five or six
+template <int N>
+__device__ __forceinline__ void store_row(float* dst, const float* v) {
+  int k = 0;
+#pragma unroll
+  for (; k + 4 <= N; k += 4) *reinterpret_cast<f32x4u*>(dst + k) = f32x4u{v[k], v[k + 1], v[k + 2], v[k + 3]};
+  if constexpr (N % 4 >= 2) {
+    *reinterpret_cast<f32x2u*>(dst + k) = f32x2u{v[k], v[k + 1]};
+    k += 2;
+  }
+  if constexpr (N % 2 == 1) dst[k] = v[k];
+}
+
 template <int FAM, int NG, int H1P, int NB, int SP, int MA>
 __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA ? 3 : 2) : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
@@ -753,12 +780,20 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
     };
     const int64_t row = ring_row(ring_base, b, rb.capacity);
     int64_t ep_slot = -1;
+    // a compile-time state width keeps the next state in registers (every put()
+    // index is a constant once env_step_lane is inlined) for row-wide stores
+    constexpr int SR = kStateRegs<FAM, NG>;
+    float ns[SR > 0 ? SR : 1];
     const StepOut o = env_step_lane<FAM, NG, float>(
         P, b, w0, t, start, ep, act, [&](int j) { return one_draw ? dr0 : philox_draw<FAM>(P, b, step, j); },
         [&](int k, double v) {
           const float f = (float)v;
-          rb.next_state[row * S + k] = f;
-          obs[(int64_t)b * S + k] = f;
+          if constexpr (SR > 0) {
+            ns[k] = f;
+          } else {
+            rb.next_state[row * S + k] = f;
+            obs[(int64_t)b * S + k] = f;
+          }
         },
         [&](int k, double v) {
           if (ep_slot >= 0 && k < P.ep_w - 4) P.ep_rows[ep_slot * P.ep_w + 4 + k] = (float)v;
@@ -781,8 +816,20 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
       er[2] = (float)o.reward;
       er[3] = (float)t;
     }
-    for (int j = 0; j < S; ++j) rb.state[row * S + j] = obs_row[j];
-    for (int i = 0; i < A; ++i) rb.action[row * A + i] = act(i);
+    if constexpr (SR > 0) {
+      float s0[SR];
+#pragma unroll
+      for (int j = 0; j < SR; ++j) s0[j] = obs_row[j];
+      store_row<SR>(rb.state + row * SR, s0);
+      store_row<SR>(rb.next_state + row * SR, ns);
+      if (!o.done) store_row<SR>(obs + (int64_t)b * SR, ns);  // a finished lane's obs is its reset state
+    } else {
+      for (int j = 0; j < S; ++j) rb.state[row * S + j] = obs_row[j];
+    }
+    if (A == 2)
+      *reinterpret_cast<f32x2u*>(rb.action + row * 2) = f32x2u{act(0), act(1)};
+    else
+      for (int i = 0; i < A; ++i) rb.action[row * A + i] = act(i);
     rb.reward[row] = (float)o.reward;
     rb.done[row] = o.learn_done;
     if (rb.n_steps > 1) rlmd::ms_record(rb, b, row, o.learn_done);
@@ -790,7 +837,7 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
       st_n = 1.0;
       st_r = o.reward;
       st_t = (double)t;
-      env_reset_lane<FAM>(P, b, [&](int k, double v) { obs[(int64_t)b * S + k] = (float)v; });
+      env_reset_lane<FAM>(P, b, [&](int k, double v) { obs[(int64_t)b * S + k] = (float)v; }, -1, ep);
     } else {
       P.wealth[b] = o.W;
       P.time[b] = t + 1;

@@ -8,6 +8,7 @@ Reference yardstick: the reference's rl_multiplicative loop run here on CPU
   key 14 GBM_InvA         SAC / MSE (C2)    converge_ref_14_s*.npz
   key 17 Dice_SH_INSURED  SAC / MSE         converge_ref_17_s*.npz
   key 18 Dice_SH_InvA     TD3 / MSE, HUB (C3)  converge_ref_18_TD3_{MSE,HUB}_s*.npz
+  key 14 GBM_InvA         TD3 / MSE, n = 5 (C5)  converge_ref_14_TD3_MSE_n5_s*.npz
 Per seed the statistic is the mean over the last third of its evaluations of
 (growth %/step = 100 (reward - 1), leverage = eval risk column 3).
 
@@ -19,14 +20,16 @@ steps on 4,096 device episodes; same statistic per seed; 3 seeds.
 
 Assertion (the stated statistic): the MEDIAN over the build seeds of each
 statistic lies inside [min, max] of the five reference seeds' values, with no
-widening.  GBM_InvA is one-sided (a measured deviation): its
-expected log growth is lev x 3.6 %/step, monotone up to the 4.95 leverage corner
-(19.5 %/step), the reference's single stream is still at leverage 0.28-1.41 after
-5e4 updates while every build update sees transitions of 65,536 lanes and climbs
-further — the build's median growth must lie in [reference min, analytic
-optimum] and its leverage in [reference min, 4.95].
+widening.  GBM_InvA (C2 SAC, C5 TD3 with 5-step returns) is one-sided (a
+measured deviation): its expected log growth is lev x 3.6
+%/step, monotone up to the 4.95 leverage corner (19.5 %/step); the reference's
+single SAC stream is still at leverage 0.28-1.41 after 5e4 updates, and its TD3
+n = 5 seeds split (three near the corner, one at 0.16, one diverged to -3.6),
+while every build update sees transitions of 65,536 lanes and climbs further —
+the build's median growth must lie in [reference MEDIAN, analytic optimum] and
+its leverage in [reference median, 4.95].
 Negative control: the same harness with K = 0 (no learning) must FAIL the band
-on Dice_SH_INSURED, Dice_SH_InvA and GBM_InvA.
+on Dice_SH_INSURED, Dice_SH_InvA and GBM_InvA (SAC and TD3 n = 5).
 """
 import math
 import os
@@ -42,15 +45,17 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 REF_SEEDS = (0, 1, 2, 3, 4)
 BUILD_SEEDS = (0, 1, 2)
 STEPS, EVAL_EVERY = 12000, 250
-# workload: (converge.py env, algo, loss, reference fixture stem)
+# workload: (converge.py env, algo, loss, reference fixture stem, n-step, lanes, reference steps)
 WORKLOADS = {
-    "coin": ("coin", "SAC", "MSE", "converge_ref_8"),
-    "dice": ("dice", "SAC", "MSE", "converge_ref_11"),
-    "gbm": ("gbm", "SAC", "MSE", "converge_ref_14"),
-    "dice_sh": ("dice_sh", "SAC", "MSE", "converge_ref_17"),
-    "dice_sh_a_mse": ("dice_sh_a", "TD3", "MSE", "converge_ref_18_TD3_MSE"),
-    "dice_sh_a_hub": ("dice_sh_a", "TD3", "HUB", "converge_ref_18_TD3_HUB"),
+    "coin": ("coin", "SAC", "MSE", "converge_ref_8", 1, 65536, 50000),
+    "dice": ("dice", "SAC", "MSE", "converge_ref_11", 1, 65536, 50000),
+    "gbm": ("gbm", "SAC", "MSE", "converge_ref_14", 1, 65536, 50000),
+    "dice_sh": ("dice_sh", "SAC", "MSE", "converge_ref_17", 1, 65536, 50000),
+    "dice_sh_a_mse": ("dice_sh_a", "TD3", "MSE", "converge_ref_18_TD3_MSE", 1, 65536, 50000),
+    "dice_sh_a_hub": ("dice_sh_a", "TD3", "HUB", "converge_ref_18_TD3_HUB", 1, 65536, 50000),
+    "gbm_td3_n5": ("gbm", "TD3", "MSE", "converge_ref_14_TD3_MSE_n5", 5, 65536, 50000),  # C5
 }
+ONE_SIDED = {"gbm", "gbm_td3_n5"}  # GBM_InvA: monotone growth up to the leverage corner
 GBM_LEV_MAX = 0.99 * 5  # the action bound times LEV_FACTOR (gbm_envs.py:43-90)
 
 
@@ -69,10 +74,11 @@ def ref_stats(golden, workload):
 def bands(golden, workload):
     st = ref_stats(golden, workload)
     g, lv = [x for x, _ in st], [x for _, x in st]
-    if workload == "gbm":
+    if workload in ONE_SIDED:
         import converge
 
-        return (min(g), 100.0 * math.expm1(converge.growth("gbm", GBM_LEV_MAX))), (min(lv), GBM_LEV_MAX)
+        return ((float(np.median(g)), 100.0 * math.expm1(converge.growth("gbm", GBM_LEV_MAX))),
+                (float(np.median(lv)), GBM_LEV_MAX))
     return (min(g), max(g)), (min(lv), max(lv))
 
 
@@ -84,11 +90,11 @@ def _third(recs, key):
 def build_medians(workload, k, precision="bf16"):
     import converge
 
-    env, algo, loss, _ = WORKLOADS[workload]
+    env, algo, loss, _, ms, lanes, _ = WORKLOADS[workload]
     got = []
     for seed in BUILD_SEEDS:
-        recs = converge.run(env, 65536, k, STEPS, precision=precision, eval_every=EVAL_EVERY, seed=seed, algo=algo,
-                            loss=loss, log=lambda s: None)
+        recs = converge.run(env, lanes, k, STEPS, precision=precision, eval_every=EVAL_EVERY, seed=seed, algo=algo,
+                            loss=loss, log=lambda s: None, multi_steps=ms)
         assert all(math.isfinite(r["eval_growth_pct"]) and r["nan_flag"] == 0 for r in recs)
         got.append((_third(recs, "eval_growth_pct"), _third(recs, "lev")))
     return float(np.median([g for g, _ in got])), float(np.median([lv for _, lv in got])), got
@@ -100,6 +106,7 @@ def inside(x, band):
 
 @pytest.mark.parametrize("workload,precision", [("dice_sh", "bf16"), ("dice_sh", "fp32"), ("gbm", "bf16"),
                                                 ("dice_sh_a_mse", "bf16"), ("dice_sh_a_hub", "bf16"),
+                                                ("gbm_td3_n5", "bf16"),
                                                 ("coin", "bf16"), ("dice", "bf16")])
 def test_build_median_in_reference_band(golden, dev, workload, precision):
     gb, lb = bands(golden, workload)
@@ -110,7 +117,7 @@ def test_build_median_in_reference_band(golden, dev, workload, precision):
     assert inside(lv, lb), (workload, precision, lv, lb)
 
 
-@pytest.mark.parametrize("workload", ["dice_sh", "dice_sh_a_mse", "gbm"])
+@pytest.mark.parametrize("workload", ["dice_sh", "dice_sh_a_mse", "gbm", "gbm_td3_n5"])
 def test_no_learning_fails_the_band(golden, dev, workload):
     """K = 0: the policy keeps its initial weights; the harness must reject it."""
     gb, lb = bands(golden, workload)

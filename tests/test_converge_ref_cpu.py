@@ -1,6 +1,7 @@
 """The reference convergence bands the GPU convergence test asserts against
 (tests/test_converge_gpu.py): five reference seeds per workload, made by the
-reference's own rl_multiplicative loop (tests/golden/run_reference_loop.py);
+reference's own rl_multiplicative loop (tests/golden/run_reference_loop.py; C5
+with 5-step returns);
 the last-third statistics (growth %/step, leverage) its docstring states."""
 import pytest
 
@@ -13,6 +14,7 @@ BAND = {  # (growth min, max %/step), (lev min, max): last thirds of the five se
     "dice_sh": ((-4.750, 2.037), (0.863, 0.929)),
     "dice_sh_a_mse": ((-6.244, 1.895), (0.481, 1.980)),
     "dice_sh_a_hub": ((-16.640, 0.756), (0.263, 1.980)),
+    "gbm_td3_n5": ((-17.530, 13.979), (-3.633, 4.165)),
 }
 
 
@@ -28,10 +30,13 @@ def test_reference_band(golden, workload):
     stem = WORKLOADS[workload][3]
     for s in REF_SEEDS:
         d = golden(f"{stem}_s{s}.npz")
-        assert int(d["seed"]) == s and int(d["steps"]) == 50000
+        assert int(d["seed"]) == s and int(d["steps"]) == WORKLOADS[workload][6]
+        assert int(d["multi_steps"]) == WORKLOADS[workload][4] if "multi_steps" in d else WORKLOADS[workload][4] == 1
 
 
-def test_gbm_band_is_one_sided_to_the_analytic_optimum(golden):
-    (g0, g1), (l0, l1) = bands(golden, "gbm")
-    assert g0 == pytest.approx(1.023, abs=1e-3) and g1 == pytest.approx(19.50, abs=0.01)
-    assert l0 == pytest.approx(0.279, abs=1e-3) and l1 == pytest.approx(4.95)
+@pytest.mark.parametrize("workload", ["gbm", "gbm_td3_n5"])
+def test_gbm_band_is_one_sided_to_the_analytic_optimum(golden, workload):
+    (g0, g1), (l0, l1) = bands(golden, workload)
+    med = {"gbm": (2.502, 0.679), "gbm_td3_n5": (13.796, 3.820)}[workload]  # the reference seeds' medians
+    assert g0 == pytest.approx(med[0], abs=1e-3) and g1 == pytest.approx(19.50, abs=0.01)
+    assert l0 == pytest.approx(med[1], abs=1e-3) and l1 == pytest.approx(4.95)
