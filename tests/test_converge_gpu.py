@@ -9,8 +9,11 @@ Reference yardstick: the reference's rl_multiplicative loop run here on CPU
   key 17 Dice_SH_INSURED  SAC / MSE         converge_ref_17_s*.npz
   key 18 Dice_SH_InvA     TD3 / MSE, HUB (C3)  converge_ref_18_TD3_{MSE,HUB}_s*.npz
   key 14 GBM_InvA         TD3 / MSE, n = 5 (C5)  converge_ref_14_TD3_MSE_n5_s*.npz
+  key 21 SNP_InvA (D1)    SAC / MSE (C4)    converge_ref_21_e20_s*.npz  (rl_market.market_env,
+                          1e5 steps, evaluations of 20 episodes x 250 test days)
 Per seed the statistic is the mean over the last third of its evaluations of
-(growth %/step = 100 (reward - 1), leverage = eval risk column 3).
+(growth %/step = 100 (reward - 1), leverage = eval risk column 3; for the market
+eval_market's [gap, risk...] rows, eval_episodes.py:542-560).
 
 Build: VecTrainer (65,536 lanes, K = 8 updates per vector step, bf16; the
 reference's hyper-parameters) for 12,000 vector steps (96,000 updates), the
@@ -54,6 +57,9 @@ WORKLOADS = {
     "dice_sh_a_mse": ("dice_sh_a", "TD3", "MSE", "converge_ref_18_TD3_MSE", 1, 65536, 50000),
     "dice_sh_a_hub": ("dice_sh_a", "TD3", "HUB", "converge_ref_18_TD3_HUB", 1, 65536, 50000),
     "gbm_td3_n5": ("gbm", "TD3", "MSE", "converge_ref_14_TD3_MSE_n5", 5, 65536, 50000),  # C5
+    # C4: SNP_InvA D1 (stooq_snp), 1e5 reference steps (main.py's n_cumsteps_mkt), 20 episodes
+    # of 250 test days per evaluation; the build at C4's 8,192 lanes
+    "market": ("market", "SAC", "MSE", "converge_ref_21_e20", 1, 8192, 100000),
 }
 ONE_SIDED = {"gbm", "gbm_td3_n5"}  # GBM_InvA: monotone growth up to the leverage corner
 GBM_LEV_MAX = 0.99 * 5  # the action bound times LEV_FACTOR (gbm_envs.py:43-90)
@@ -106,7 +112,7 @@ def inside(x, band):
 
 @pytest.mark.parametrize("workload,precision", [("dice_sh", "bf16"), ("dice_sh", "fp32"), ("gbm", "bf16"),
                                                 ("dice_sh_a_mse", "bf16"), ("dice_sh_a_hub", "bf16"),
-                                                ("gbm_td3_n5", "bf16"),
+                                                ("gbm_td3_n5", "bf16"), ("market", "bf16"),
                                                 ("coin", "bf16"), ("dice", "bf16")])
 def test_build_median_in_reference_band(golden, dev, workload, precision):
     gb, lb = bands(golden, workload)

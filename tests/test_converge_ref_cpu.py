@@ -1,7 +1,8 @@
 """The reference convergence bands the GPU convergence test asserts against
 (tests/test_converge_gpu.py): five reference seeds per workload, made by the
-reference's own rl_multiplicative loop (tests/golden/run_reference_loop.py; C5
-with 5-step returns);
+reference's own rl_multiplicative / rl_market loops
+(tests/golden/run_reference_loop.py; C5 with 5-step returns, C4 through
+market_env);
 the last-third statistics (growth %/step, leverage) its docstring states."""
 import pytest
 
@@ -15,6 +16,7 @@ BAND = {  # (growth min, max %/step), (lev min, max): last thirds of the five se
     "dice_sh_a_mse": ((-6.244, 1.895), (0.481, 1.980)),
     "dice_sh_a_hub": ((-16.640, 0.756), (0.263, 1.980)),
     "gbm_td3_n5": ((-17.530, 13.979), (-3.633, 4.165)),
+    "market": ((1.131, 5.921), (0.021, 0.085)),
 }
 
 
