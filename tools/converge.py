@@ -129,7 +129,8 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
         if step % eval_every == 0 or step == steps:
             a = tr.agent.act(reset_obs, mode=1)[0].cpu().numpy()
             if env == "market":  # eval_risk_log = [gap, risk...] (eval_episodes.py:542-560)
-                ev = tr.evaluate_market(n_eval=min(n_eval, lanes), test_days=250)
+                # one evaluation launch summarises at most 1,024 episodes (rlmd_eval_stats)
+                ev = tr.evaluate_market(n_eval=min(n_eval, lanes, 1024), test_days=250)
                 lev = float(np.mean(ev["risk_log"][:, 3]))
             else:
                 ev = tr.evaluate(n_eval=n_eval, max_steps=100, with_stats=False)
