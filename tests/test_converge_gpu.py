@@ -13,7 +13,8 @@ Reference yardstick: the reference's rl_multiplicative loop run here on CPU
                           1e5 steps, evaluations of 20 episodes x 250 test days)
 Per seed the statistic is the mean over the last third of its evaluations of
 (growth %/step = 100 (reward - 1), leverage = eval risk column 3; for the market
-eval_market's [gap, risk...] rows, eval_episodes.py:542-560).
+column 4 of eval_market's [gap, reward, wealth, step return, lev] rows,
+eval_episodes.py:542-543, market_envs.py:196).
 
 Build: VecTrainer (65,536 lanes, K = 8 updates per vector step, bf16; the
 reference's hyper-parameters) for 12,000 vector steps (96,000 updates), the
@@ -82,7 +83,10 @@ def ref_stats(golden, workload):
         d = golden(f"{stem}_s{s}.npz")
         n = d["reward"].shape[0]
         sl = slice(n - n // 3, n)
-        out.append((100.0 * float((d["reward"][sl] - 1.0).mean()), float(d["lev"][sl].mean())))
+        # market: eval_risk_log column 4 (the fixture's "lev" key holds the reference
+        # summary's column 3, the last step's return)
+        lev = d["risk"][sl][..., 4] if WORKLOADS[workload][0] == "market" else d["lev"][sl]
+        out.append((100.0 * float((d["reward"][sl] - 1.0).mean()), float(lev.mean())))
     return out
 
 

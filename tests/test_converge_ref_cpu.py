@@ -16,7 +16,7 @@ BAND = {  # (growth min, max %/step), (lev min, max): last thirds of the five se
     "dice_sh_a_mse": ((-6.244, 1.895), (0.481, 1.980)),
     "dice_sh_a_hub": ((-16.640, 0.756), (0.263, 1.980)),
     "gbm_td3_n5": ((-17.530, 13.979), (-3.633, 4.165)),
-    "market": ((1.131, 5.921), (0.021, 0.085)),
+    "market": ((1.131, 5.921), (0.207, 1.708)),
 }
 
 

@@ -128,10 +128,13 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
         tr.step()
         if step % eval_every == 0 or step == steps:
             a = tr.agent.act(reset_obs, mode=1)[0].cpu().numpy()
-            if env == "market":  # eval_risk_log = [gap, risk...] (eval_episodes.py:542-560)
-                # one evaluation launch summarises at most 1,024 episodes (rlmd_eval_stats)
+            if env == "market":
+                # eval_risk_log = [gap, reward, wealth, step return, mean lev, ...]
+                # (eval_episodes.py:542-543, market_envs.py:196): the leverage is column 4
+                # (the reference's summary prints column 3, the last step's return, as
+                # "lev"); one evaluation launch summarises at most 1,024 episodes
                 ev = tr.evaluate_market(n_eval=min(n_eval, lanes, 1024), test_days=250)
-                lev = float(np.mean(ev["risk_log"][:, 3]))
+                lev = float(np.mean(ev["risk_log"][:, 4]))
             else:
                 ev = tr.evaluate(n_eval=n_eval, max_steps=100, with_stats=False)
                 # the reference's statistic: the eval risk rows' leverage column
@@ -142,7 +145,7 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
             rec = {"env": env, "algo": algo, "loss": loss, "precision": precision, "lanes": lanes, "k": k,
                    "replay": replay, "multi_steps": multi_steps, "step": step, "updates": step * k, "env_steps": step * lanes,
                    "action": [float(x) for x in a], "lev": lev, "lev_sh": lev_sh,
-                   "eval_growth_pct": grow,
+                   "eval_growth_pct": grow, "eval_steps": float(np.mean(ev["steps"])),
                    "analytic_growth_pct": None if env == "market" else 100.0 * math.expm1(growth(env, lev, lev_sh)),
                    "kelly_lev": l_star, "kelly_growth_pct": g_star, "wall_s": time.perf_counter() - t0,
                    "nan_flag": tr.agent.scalars()["nan_flag"]}
