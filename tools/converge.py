@@ -157,6 +157,37 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
     return recs
 
 
+def market_single(seed, steps=100000, n_eval=20):
+    """C4's single-stream control: the build's reference-API market driver
+    (rlmd_amd.main.run -> scripts/rl_market.market_env: one env, one update per
+    env step, the device Agent_sac) on the reference's settings (key 21, SAC /
+    MSE, `steps` steps, evaluations of n_eval episodes x 250 test days, np.random
+    and torch seeded with `seed`).  Returns the per-evaluation growth %/step and
+    leverage (eval_risk_log column 4), averaged over the episodes."""
+    import tempfile
+
+    import torch
+
+    from rlmd_amd.config import INPUTS
+    from rlmd_amd.main import run as main_run
+
+    prices = market_kw()["prices"]
+    cwd = os.getcwd()
+    with tempfile.TemporaryDirectory() as tmp:
+        os.chdir(tmp)
+        try:
+            os.makedirs("market_data")
+            np.save("market_data/stooq_snp.npy", prices)
+            np.random.seed(seed)
+            torch.manual_seed(seed)
+            inputs = dict(INPUTS, n_trials_mkt=1, n_cumsteps_mkt=float(steps), n_eval_mkt=n_eval,
+                          market_dir="./market_data/", test_agent=True)
+            ((_, _, ev, _, ev_risk),), = main_run([21], ["SAC"], ["MSE"], [1], inputs=inputs, log=None)[21]
+        finally:
+            os.chdir(cwd)
+    return 100.0 * (ev[0, :, :, 1] - 1.0).mean(1), ev_risk[0, :, :, 4].mean(1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--env", default="coin", choices=sorted(FAMILY))
