@@ -161,6 +161,7 @@ def test_market_single_stream_in_reference_band(golden, dev):
         g, lv = converge.market_single(seed, WORKLOADS["market"][6])
         n = len(g)
         got.append((float(g[n - n // 3:].mean()), float(lv[n - n // 3:].mean())))
+        print(f"market single stream seed {seed}: {got[-1]}", flush=True)  # progress (~36 s per seed)
     gm, lm = float(np.median([x for x, _ in got])), float(np.median([x for _, x in got]))
     print(f"market single stream: median growth {gm:.3f} lev {lm:.4f}; seeds {got}; band {gb} {lb}")
     assert inside(gm, gb) and inside(lm, lb), (gm, lm, gb, lb, got)
