@@ -444,11 +444,13 @@ def main():
         cfg0 = CONFIGS[args.config]
         n0, rep0 = args.lanes or cfg0["lanes"], args.replay or cfg0["replay"]
         allc = min(16, os.cpu_count() or 1)  # this GPU's host-core share on the box
-        cpu_lines = (cpu_baseline_seeds(n0, args.k_updates, args.cpu_seconds, allc, replay=rep0),
-                     cpu_baseline(n0, args.k_updates, args.cpu_seconds, 1, replay=rep0),
-                     # BASELINE.md's plan: the reference's own loop semantics (one env,
-                     # UTD = 1, single stream), one seed per core and on one core
-                     cpu_baseline_seeds(1, 1, args.cpu_seconds, allc, replay=rep0),
+        # both worker pools first: the in-process runs import torch, which opens the
+        # device, and the box allows 16 processes on it (the pool's 16 + this one)
+        pool = cpu_baseline_seeds(n0, args.k_updates, args.cpu_seconds, allc, replay=rep0)
+        # BASELINE.md's plan: the reference's own loop semantics (one env, UTD = 1,
+        # single stream), one seed per core and on one core
+        pool1 = cpu_baseline_seeds(1, 1, args.cpu_seconds, allc, replay=rep0)
+        cpu_lines = (pool, cpu_baseline(n0, args.k_updates, args.cpu_seconds, 1, replay=rep0), pool1,
                      cpu_baseline(1, 1, args.cpu_seconds, 1, replay=rep0))
 
     import torch
