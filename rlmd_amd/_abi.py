@@ -143,7 +143,8 @@ _LIB = None
 def lib():
     global _LIB
     if _LIB is None:
-        _LIB = load()
+        # RLMD_LIB_PATH: another build of the same ABI (tools/ab_build.py A/B runs)
+        _LIB = load(os.environ.get("RLMD_LIB_PATH", LIB_PATH))
     return _LIB
 
 
