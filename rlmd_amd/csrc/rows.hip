@@ -387,31 +387,22 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
   const int nr = m.r1 - m.r0;
   const float* w = p + o.w1 + (int64_t)m.c * in;
   uint64_t mk[(MR + 7) / 8] = {};  // the thread's mask bytes, row r0 + rr at byte rr
-  // all of the thread's rows first (their LDS reads issue together and the MR
-  // FMA chains interleave), then the stores: a loop that stored a1 / m1s between
-  // rows waited on every row's reads in turn, since the stores may alias xs
-  // (TD3 400-wide: ≈9-11k cycles for 16 rows per thread).  Each row keeps its
-  // own sequential FMA order, so the values are unchanged.
-  float v[MR];
+  for (int r = m.r0; r < m.r1; ++r) {
+    float v = 0.f;
+    if (m.c < H1) {
+      float acc = 0.f;
+      // xs rows are zero padded to ldx >= W1P and k.w1[j] = 0 for j >= in: no branch
+      // between the LDS reads, so a row's W1P reads issue together
 #pragma unroll
-  for (int rr = 0; rr < MR; ++rr) {
-    const int r = rr < nr ? m.r0 + rr : m.r0;  // rows past nr read a live row, unused
-    float acc = 0.f;
-    // xs rows are zero padded to ldx >= W1P and k.w1[j] = 0 for j >= in: no branch
-    // between the LDS reads, so a row's W1P reads issue together
-#pragma unroll
-    for (int j = 0; j < W1P; ++j) acc = fmaf(xs[r * ldx + j], k.w1[j], acc);
-    for (int j = W1P; j < in; ++j) acc = fmaf(xs[r * ldx + j], m.c < H1 ? w[j] : 0.f, acc);
-    v[rr] = m.c < H1 ? fmaxf(acc + k.b1, 0.f) : 0.f;
-  }
-#pragma unroll
-  for (int rr = 0; rr < MR; ++rr) {
-    if (rr >= nr) break;
-    const int r = m.r0 + rr;
-    if (h1_out && m.c < H1 && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + m.c] = v[rr];
-    a1[r * lda1 + m.c] = CT<PREC>::cvt(v[rr]);
-    if (ex && ex->m1s) ex->m1s[r * H1p + m.c] = v[rr] > 0.f ? 1 : 0;
-    const uint64_t bit = (uint64_t)(v[rr] > 0.f ? 1u : 0u) << (8 * (rr & 7));
+      for (int j = 0; j < W1P; ++j) acc = fmaf(xs[r * ldx + j], k.w1[j], acc);
+      for (int j = W1P; j < in; ++j) acc = fmaf(xs[r * ldx + j], w[j], acc);
+      v = fmaxf(acc + k.b1, 0.f);
+      if (h1_out && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + m.c] = v;
+    }
+    a1[r * lda1 + m.c] = CT<PREC>::cvt(v);
+    if (ex && ex->m1s) ex->m1s[r * H1p + m.c] = v > 0.f ? 1 : 0;
+    const int rr = r - m.r0;
+    const uint64_t bit = (uint64_t)(v > 0.f ? 1u : 0u) << (8 * (rr & 7));
     if constexpr (MR > 8) {
       if (rr < 8) mk[0] |= bit;
       else mk[1] |= bit;
