@@ -1,7 +1,7 @@
 """A/B builds for same-box comparisons: librlmd_amd.so with some sources taken
 from another git revision, linked against the current build's other objects.
 
-    python tools/ab_build.py <rev> <tag> rows.hip [more.hip ...]
+    python tools/ab_build.py <rev> <tag> rows.hip [more.hip | header.h ...]
 writes tools/_abh/librlmd_amd_<tag>.so; load it with RLMD_LIB_PATH=<that path>
 (rlmd_amd/_abi.py), e.g. bench.py A/B runs on one box."""
 import os
@@ -20,6 +20,12 @@ def main():
     B.build()
     src_dir = os.path.join(OUT, tag)
     os.makedirs(src_dir, exist_ok=True)
+    # headers from the revision sit beside its sources: a quoted #include finds them first
+    for h in [f for f in files if f.endswith(".h")]:
+        text = subprocess.run(["git", "show", f"{rev}:rlmd_amd/csrc/{h}"], cwd=ROOT, capture_output=True, text=True,
+                              check=True).stdout
+        with open(os.path.join(src_dir, h), "w") as f:
+            f.write(text)
     objs = []
     for src in B.SOURCES:
         if src in files:
