@@ -232,6 +232,7 @@ struct Scratch {
   uint8_t* done;
   // target path: target q per row (no head bias), logp of the next actions
   float *logp_next, *tpart[2], *y;
+  float* tpartn[2];  // TD3 target pairing: the next update's target q (fwd_rows npair)
   float* qbias;  // [4] q_value.bias of the online, then target critics at loss time
   // critic path
   float *c1[2], *c2[2], *qpart[2], *dq[2], *dc2[2], *dc1[2];
@@ -336,6 +337,7 @@ struct rlmd_agent_s {
   // critic step as one launch (update.hip) for B <= 512; RLMD_NO_FUSED_UPDATE=1:
   // row backward + weight-gradient GEMM + Adam launches
   bool fused_update = false;
+  bool target_pair = true;  // TD3: next update's target path in this update's forward (RLMD_NO_TARGET_PAIR=1: off)
   bool fused_actor = false;  // the actor step too (actions <= 2)
   rlmd::PhaseProfiler prof;  // rlmd_profile_enable / _read
 };
@@ -540,8 +542,22 @@ struct Batch {
   const int32_t* eff;
 };
 
+// TD3 target pairing between consecutive updates of one call (algo_td3.py:
+// learn() forms the target from the target networks, which change only at
+// learn_step_cntr % td3_target_{critic,actor}_update == 0): when update n changes
+// no target network, update n + 1's target path — target actor on its s', the
+// clipped noise of its counter, both target critics — runs as two more jobs of
+// update n's forward (same kernel code, same parameters: bit-identical), and
+// update n + 1's forward skips jobs 0 / 1.  s2n: the next mini-batch's s'
+// (nullable: last update of the call); ready: this update's targets are in
+// tpartn; paired (out): the next update's targets were computed here.
+struct PairCtl {
+  const float* s2n;
+  bool ready, paired;
+};
+
 int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const float* eps_b, float* stats,
-               hipStream_t st) {
+               hipStream_t st, PairCtl* pc = nullptr) {
   const rlmd_agent_cfg& c = ag->cfg;
   Scratch& S_ = ag->sc;
   const int B = c.batch, S = c.state_dim, A = c.action_dim, X = S + A, H1 = c.h1, H2 = c.h2;
@@ -562,6 +578,11 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
   float* Gc[2] = {G + ag->off_c[0], G + ag->off_c[1]};
   float* Ga = G + ag->off_actor;
   const RowNet crit[2] = {row_net(ag, SLOT_C0), row_net(ag, SLOT_C0 + 1)};
+  const bool ready = pc && pc->ready;
+  const bool target_change = cntr % c.target_critic_update == 0 || (actor_step && cntr % c.target_actor_update == 0);
+  const bool pair = pc && pc->s2n && !ready && !sac && ag->target_pair && ag->fused_update && eps_a == nullptr &&
+                    !target_change;
+  if (pc) pc->paired = pair;
 
   // ---- forward rows: target path (algo_sac.py:300-367 / algo_td3.py:302-361),
   //      critics on (s, a) (algo_sac.py:413-417), policy on s for the actor step
@@ -617,6 +638,14 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       f.hp1a = S_.hp1a;
       f.hp2a = S_.hp2a;
     }
+    f.y0 = ready ? 2 : 0;
+    if (pair) {
+      f.npair = 1;
+      f.s2n = pc->s2n;
+      f.qtn[0] = S_.tpartn[0];
+      f.qtn[1] = S_.tpartn[1];
+      f.ctrn = (uint32_t)(cntr + 1);
+    }
     RLMD_TRY(fwd_rows_launch(f, st));
   }
   // ---- critic loss (algo_sac.py:413-465)
@@ -626,7 +655,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     for (int g = 0; g < 2; ++g) {
       la.qpart[g] = S_.qpart[g];
       la.qb[g] = Pc[g] + co.b3;
-      la.tpart[g] = S_.tpart[g];
+      la.tpart[g] = ready ? S_.tpartn[g] : S_.tpart[g];
       la.tb[g] = Tc[g] + co.b3;
     }
     la.r = mb.r;
@@ -951,11 +980,14 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
   RLMD_TRY(replay_sample_launch(v, M, B, k, c.seed ^ 0x5eed5eed5eedull, (uint64_t)ag->host_cntr, ag->kb_idx,
                                 ag->kb_s, ag->kb_a, ag->kb_r, ag->kb_s2, ag->kb_done, ag->kb_xsa,
                                 ms ? ag->kb_eff : nullptr, st));
+  PairCtl pc{nullptr, false, false};
   for (int i = 0; i < k; ++i) {
     const size_t o = (size_t)i * B;
     const Batch mb{ag->kb_s + o * S, ag->kb_r + o, ag->kb_s2 + o * S, ag->kb_xsa + o * (S + A), ag->kb_done + o,
                    ms ? ag->kb_eff + o : nullptr};
-    RLMD_TRY(learn_body(ag, mb, nullptr, nullptr, stats_slot(ag, stats, i), st));
+    pc.s2n = i + 1 < k ? ag->kb_s2 + (o + B) * S : nullptr;
+    RLMD_TRY(learn_body(ag, mb, nullptr, nullptr, stats_slot(ag, stats, i), st, &pc));
+    pc.ready = pc.paired;
   }
   return 0;
 }
@@ -1099,6 +1131,8 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
       RLMD_ALLOC(s.u1[g], e1);
       RLMD_ALLOC(s.w3s[g], H2);
     }
+    const char* np = getenv("RLMD_NO_TARGET_PAIR");
+    ag->target_pair = !(np && atoi(np) != 0);
     const char* nf = getenv("RLMD_NO_FUSED_UPDATE");
     ag->fused_update = B <= 512 && X <= 8 && !(nf && atoi(nf) != 0);
     const char* na = getenv("RLMD_NO_FUSED_ACTOR");
@@ -1126,6 +1160,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
   }
   for (int g = 0; g < 2; ++g) {
     RLMD_ALLOC(s.tpart[g], B);
+    RLMD_ALLOC(s.tpartn[g], B);
     RLMD_ALLOC(s.c1[g], B * H1);
     RLMD_ALLOC(s.c2[g], B * H2);
     RLMD_ALLOC(s.qpart[g], B);

@@ -172,6 +172,14 @@ struct FwdRowsArgs {
   // compute type (its masks go to am1 / am2; the bases are qeval_rows' head jobs)
   void* hp1a;
   void* hp2a;
+  // TD3 target pairing (learn.hip): with npair = 1 the launch also runs the NEXT
+  // update's target jobs (s2n, its noise counter ctrn, into qtn) — valid when no
+  // target network changes in between; y0 = 2 when the previous launch already
+  // computed this update's targets (jobs 0 / 1 skipped)
+  const float* s2n;
+  float* qtn[2];
+  uint32_t ctrn;
+  int32_t y0, npair;
 };
 
 // Critics evaluated on (s, a_new) after their update: y = g.

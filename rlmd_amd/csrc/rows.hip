@@ -735,7 +735,12 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
   const Lds L = lds_layout(d);
   float* xs = reinterpret_cast<float*>(smem + L.xs);
   const float* hout = reinterpret_cast<const float*>(smem + L.hout);
-  const int row0 = blockIdx.x * R, job = blockIdx.y, B = d.B;
+  const int row0 = blockIdx.x * R, B = d.B;
+  // jobs y0 .. nj - 1 of this update, then (npair) the next update's target jobs
+  const int nj = a.with_actor ? 5 : 4;
+  int job = (int)blockIdx.y + a.y0;
+  const bool nxt = job >= nj;
+  if (nxt) job -= nj;
   const bool sac = d.algo == RLMD_SAC;
   const int H1p = pad32(d.H1), H2p = pad32(d.H2);
   const int na = sac ? 2 * d.A : d.A;
@@ -744,32 +749,37 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     RLMD_TSR(16 * job + 0);
     const RowNet& an = a.tactor;
     const RowNet& cn = a.tcrit[job];
-    const StageReg sr = stage_issue(a.s2, d.S, L.ldx, row0, B);
+    const float* s2 = nxt ? a.s2n : a.s2;
+    const float* eps_next = nxt ? nullptr : a.eps_next;
+    SampleCfg smp = a.smp;
+    if (nxt) smp.ctr = a.ctrn;  // the next update's learn_step_cntr (its target noise draws)
+    const StageReg sr = stage_issue(s2, d.S, L.ldx, row0, B);
     const HeadBias hb = head_bias(an.p, a.ao, d);
-    const bool pre_nz = a.eps_next == nullptr;
+    const bool pre_nz = eps_next == nullptr;
     FwdConst<NBW> ka, kc;
     actor_const<NBW>(ka, an, a.ao, d);
     Pre<PREC, NBW, MULTI> pa, pc;
     pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
     critic_const<NBW>(kc, cn, a.co, d);
     pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
-    const Noise2 nz = pre_nz ? noise_pre(a.smp, d, a.t_tag, row0) : Noise2{{0.f, 0.f}};
+    const Noise2 nz = pre_nz ? noise_pre(smp, d, a.t_tag, row0) : Noise2{{0.f, 0.f}};
     RLMD_TSR(16 * job + 1);
-    stage_commit(sr, a.s2, d.S, xs, L.ldx, row0, B);
+    stage_commit(sr, s2, d.S, xs, L.ldx, row0, B);
     __syncthreads();
     RLMD_TSR(16 * job + 2);
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
                                d.A, smem, L, nullptr, nullptr, row0, B);
     RLMD_TSR(16 * job + 3);
-    sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, 0, a.t_tag, a.eps_next, a.t_noise_std, a.t_noise_clip,
-                a.t_clamp, job == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz, pre_nz);
+    sample_rows(an.p, a.ao, d, smp, xs, L.ldx, hout, 0, a.t_tag, eps_next, a.t_noise_std, a.t_noise_clip,
+                a.t_clamp, job == 0 && !nxt ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz, pre_nz);
     __syncthreads();
     RLMD_TSR(16 * job + 4);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
                                nullptr, row0, B);
     RLMD_TSR(16 * job + 5);
-    if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qt[job][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
-    if (a.bsnap && blockIdx.x == 0 && threadIdx.x == 0) a.bsnap[2 + job] = cn.p[a.co.b3];
+    float* qt = nxt ? a.qtn[job] : a.qt[job];
+    if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) qt[row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
+    if (!nxt && a.bsnap && blockIdx.x == 0 && threadIdx.x == 0) a.bsnap[2 + job] = cn.p[a.co.b3];
   } else if (job <= 3) {  // online critics on (s, a) (algo_sac.py:413-417)
     if (job == 2) RLMD_TSR(60);
     const int g = job - 2;
@@ -1520,7 +1530,9 @@ extern "C" int rlmd_debug_ts_rows(unsigned long long* out) {
 namespace rlmd {
 
 int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st) {
-  return launch_rows(a.d, 0, &a, a.with_actor ? 5 : 4, st);
+  RLMD_CHECK(a.y0 == 0 || a.y0 == 2, "fwd_rows: y0 is 0 or 2");
+  RLMD_CHECK(a.npair == 0 || (a.y0 == 0 && a.s2n && a.qtn[0] && a.qtn[1]), "fwd_rows: target pairing buffers");
+  return launch_rows(a.d, 0, &a, (a.with_actor ? 5 : 4) - a.y0 + 2 * a.npair, st);
 }
 int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st) {
   RLMD_CHECK(a.nq == nq && (a.nab == 0 || (a.ua && a.wheads && a.am1 && a.am2)), "qeval_rows: head jobs need their buffers");
