@@ -4,7 +4,7 @@ td3_target_actor_update = 2, main.py:243-244), the next update's target path —
 target actor on its s', clipped noise at its counter, both target critics — runs
 in the current update's forward launch.  Same kernel code on the same
 parameters: the training loop must be bit-identical with and without it
-(RLMD_NO_TARGET_PAIR=1), at C3's shape (Dice_SH_InvA) and C5's (GBM, 5-step
+(RLMD_TARGET_PAIR=1 against 0), at C3's shape (Dice_SH_InvA) and C5's (GBM, 5-step
 returns), through the warm-up / smoothing window into policy steps.
 Reference: algos/algo_td3.py:363-531 (learn), :302-361 (the target)."""
 import numpy as np
@@ -31,9 +31,9 @@ def _run(dev, env, ms, steps=14):
 
 @pytest.mark.parametrize("env,ms", [("dice_sh", 1), ("gbm", 5)])
 def test_td3_target_pairing_is_bit_identical(dev, monkeypatch, env, ms):
-    monkeypatch.setenv("RLMD_NO_TARGET_PAIR", "1")
+    monkeypatch.setenv("RLMD_TARGET_PAIR", "0")
     off = _run(dev, env, ms)
-    monkeypatch.setenv("RLMD_NO_TARGET_PAIR", "0")
+    monkeypatch.setenv("RLMD_TARGET_PAIR", "1")
     on = _run(dev, env, ms)
     for name, x, y in zip(("params", "target", "stats", "obs"), on, off):
         np.testing.assert_array_equal(x, y, err_msg=name)
