@@ -337,7 +337,7 @@ struct rlmd_agent_s {
   // critic step as one launch (update.hip) for B <= 512; RLMD_NO_FUSED_UPDATE=1:
   // row backward + weight-gradient GEMM + Adam launches
   bool fused_update = false;
-  bool target_pair = false;  // TD3: next update's target path in this update's forward (RLMD_TARGET_PAIR=1)
+  bool target_pair = true;  // TD3: next update's target path in this update's forward (RLMD_TARGET_PAIR=0: off)
   bool fused_actor = false;  // the actor step too (actions <= 2)
   rlmd::PhaseProfiler prof;  // rlmd_profile_enable / _read
 };
@@ -1131,8 +1131,8 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
       RLMD_ALLOC(s.u1[g], e1);
       RLMD_ALLOC(s.w3s[g], H2);
     }
-    const char* tp = getenv("RLMD_TARGET_PAIR");
-    ag->target_pair = tp && atoi(tp) != 0;
+    const char* tp = getenv("RLMD_TARGET_PAIR");  // default on; RLMD_TARGET_PAIR=0 turns it off
+    ag->target_pair = !(tp && atoi(tp) == 0);
     const char* nf = getenv("RLMD_NO_FUSED_UPDATE");
     ag->fused_update = B <= 512 && X <= 8 && !(nf && atoi(nf) != 0);
     const char* na = getenv("RLMD_NO_FUSED_ACTOR");
