@@ -418,6 +418,9 @@ def main():
     ap.add_argument("--seeds-per-gpu", default=None,
                     help="independent seeds per GPU timed after the headline (SeedGroup: one stream per seed); "
                          "default '2,4' (C4: '2,4,8'); '' = off")
+    ap.add_argument("--variants", default=None,
+                    help="BASELINE config variants timed after the headline, one trainer each: C3 the critic losses "
+                         "(default 'MSE,HUB,MAE,HSC'), C5 the multi-step n (default '3,5,7'); '' = off")
     ap.add_argument("--eval-every", type=int, default=1000,
                     help="vector steps between evaluations (eval_freq 1e3, main.py); amortised into value")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -562,6 +565,35 @@ def main():
                                "ms_per_group_step": 1e3 * dt / n_t,
                                "vs_one_seed": (T * N * n_t / dt) / (N * 1e3 / (1e3 * t_max / args.steps))}
             del grp
+    # BASELINE.json names variants of C3 (critic-loss sweep MSE/HUB/MAE/HSC,
+    # tools/critic_loss.py:143-205) and C5 (n = 3/5/7, tools/replay.py:251-332):
+    # each is timed as its own trainer (same lanes, K, ring), with its learn
+    # phase's MFMA fraction from a phase pass
+    variants = {}
+    if world == 1 and args.config in ("c3", "c5"):
+        spec = args.variants if args.variants is not None else ("MSE,HUB,MAE,HSC" if args.config == "c3" else "3,5,7")
+        for v in [x.strip() for x in spec.split(",") if x.strip()]:
+            loss_v, ms_v = (v.upper(), ms_n) if args.config == "c3" else (args.loss, int(v))
+            rep_v = (replay // N) * N if ms_v > 1 else replay
+            trv = VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"],
+                             loss=loss_v, k_updates=K, replay_capacity=rep_v, seed=430 + len(variants), warmup_steps=0,
+                             smoothing_window=0, precision=args.precision, device=dev, init_seed=430 + len(variants),
+                             multi_steps=ms_v, dynamics="A", **kw)
+            for _ in range(args.warmup):
+                trv.step()
+            ms_v_step = timed_steps(trv, max(10, min(args.steps, 30)))
+            trv.profile(1)
+            for _ in range(10):
+                trv.step()
+            pms, pcnt = trv.profile_read()
+            trv.profile(0)
+            lms = pms[2] / max(pcnt[2], 1)
+            upd_v = sac_update_flops if cfg["algo"] == "SAC" else td3_update_flops
+            fl = K * upd_v(trv.env.state_dim, trv.env.action_dim, trv.agent.h1, trv.agent.h2, trv.batch)
+            variants[v] = {"critic_loss": loss_v, "multi_steps": ms_v, "env_steps_per_s": N * 1e3 / ms_v_step,
+                           "ms_per_step": ms_v_step, "learn_ms_per_step": lms,
+                           "learn_mfma_frac": fl / (lms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS if lms > 0 else None}
+            del trv
     companion = None
     if not args.no_companion and world == 1 and args.precision == "bf16":
         tr32 = VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"],
@@ -658,6 +690,8 @@ def main():
                                       "replay and learner per seed, one HIP stream each), per-GPU totals; eval not "
                                       "amortised", **per_gpu} if per_gpu else None,
             "k_sweep": sweep,
+            "variants": {"note": "BASELINE.json's variants of this config, each its own trainer (same lanes, K, "
+                                 "ring), timed after the headline; eval not amortised", **variants} if variants else None,
             "fp32_companion": companion,
             "roofline": roofline,
             "roofline_fused_kernel": roofline_fused,

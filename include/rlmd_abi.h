@@ -45,7 +45,8 @@ typedef struct {
   int32_t action_days; /* market: days between actions (reference default 1) */
   int32_t shuffle_days;/* market: in-block shuffle interval (train 5, eval 3) */
   int32_t sample_days; /* market: days excluded from the start draw (rl_market.py:59) */
-  int32_t pad0;
+  int32_t slice_groups;/* market: lanes l, l' with l % G == l' % G draw the same episode
+                          slices and shuffles (0 = every lane its own; a probe switch) */
   uint64_t seed;       /* Philox key for env draws */
 } rlmd_env_cfg;
 

@@ -31,7 +31,7 @@ class EnvCfg(C.Structure):
     _fields_ = [("family", C.c_int32), ("investor", C.c_int32), ("n_lanes", C.c_int32),
                 ("n_gambles", C.c_int32), ("obs_days", C.c_int32), ("time_length", C.c_int32),
                 ("action_days", C.c_int32), ("shuffle_days", C.c_int32),
-                ("sample_days", C.c_int32), ("pad0", C.c_int32), ("seed", C.c_uint64)]
+                ("sample_days", C.c_int32), ("slice_groups", C.c_int32), ("seed", C.c_uint64)]
 
 
 class AgentCfg(C.Structure):

@@ -94,6 +94,7 @@ __device__ unsigned long long g_ts_env[2048][8];
 struct EnvParams {
   int fam, inv, n_lanes, n, obs_days, time_length, action_days, shuffle_days;
   int state_dim, action_dim, risk_dim, draw_dim, ext_len, start_range, n_days;
+  int slice_groups;  // market: lanes sharing slice draws in groups (lane % G; 0 = per lane)
   uint64_t seed;
   const double* prices;  // market [n_days, n]
   // lane state
@@ -143,13 +144,18 @@ __device__ inline int market_perm(uint64_t seed, uint32_t lane, uint32_t ep, uin
   return (int)((p >> (4 * pos)) & 15u);
 }
 
+// the Philox counter of a lane's market slice draws (start row, block shuffles)
+__device__ inline uint32_t slice_key(const EnvParams& P, uint32_t lane) {
+  return P.slice_groups > 0 ? lane % (uint32_t)P.slice_groups : lane;
+}
+
 // source price row of extract row e (time_slice + shuffle_data)
 __device__ inline int market_row(const EnvParams& P, uint32_t lane, int start, uint32_t ep, int e) {
   const int D = P.shuffle_days;
   if (D <= 1) return start + e;
   const int full = P.ext_len / D, blk = e / D, within = e % D;
   const int bs = blk < full ? D : P.ext_len - full * D;
-  return start + blk * D + market_perm(P.seed, lane, ep, (uint32_t)blk, bs, within);
+  return start + blk * D + market_perm(P.seed, slice_key(P, lane), ep, (uint32_t)blk, bs, within);
 }
 
 // observed_market_state element k (tools/env_resources.py:203-226): D1 -> row t*ad
@@ -434,7 +440,7 @@ __device__ inline void env_reset_lane(const EnvParams& P, uint32_t lane, StF st,
   st(2, 1.0 / C.max_value);
   st(3, 1.0 / C.max_value);
   if (FAM == RLMD_MARKET) {
-    const rlmd_u32x4 v = rlmd_philox(P.seed, lane, ep, RLMD_TAG_MKT_START, 0);
+    const rlmd_u32x4 v = rlmd_philox(P.seed, slice_key(P, lane), ep, RLMD_TAG_MKT_START, 0);
     const int start = start_at >= 0 ? start_at : (int)rlmd_below(v.x, v.y, (uint64_t)P.start_range);
     P.start[lane] = start;
     const int m = P.obs_days * P.n;
@@ -1609,6 +1615,7 @@ int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t 
   P.risk_dim = R;
   P.draw_dim = D;
   P.seed = cfg->seed;
+  P.slice_groups = cfg->slice_groups > 0 ? cfg->slice_groups : 0;
   const size_t N = (size_t)cfg->n_lanes;
   if (cfg->family == RLMD_MARKET) {
     if (!prices_host || n_days <= 1 || cfg->time_length <= 0 || P.shuffle_days > 16) {

@@ -226,7 +226,7 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
   if (b == 0 && part == 1) {  // critic 1's tail index only
     LearnState* st = a.st;
     a.stats[9] = 1.f / (s5[1] / a.zipf_x2);
-    if (isnan(a.stats[9]) && atomicOr(&st->nan_flag, RLMD_STATUS_NAN_STATS) == 0) st->nan_update = st->learn_cntr;
+    if (isnan(a.stats[9]) && atomicOr(&st->nan_flag, RLMD_STATUS_NAN_STATS) == 0) st->nan_update = a.cnt;
   }
   if (b == 0 && part != 1) {
     LearnState* st = a.st;
@@ -256,7 +256,7 @@ __device__ __forceinline__ void critic_loss_block(const LossArgs& a, uint64_t* r
       if (v < 6 || v == 8 || (v == 9 && part < 0)) sn |= isnan(a.stats[v]);
     if (sn) fl |= RLMD_STATUS_NAN_STATS;
     // sticky; atomic: with part 1 running alongside, the first to set it stamps nan_update
-    if (fl && atomicOr(&st->nan_flag, fl) == 0) st->nan_update = st->learn_cntr;
+    if (fl && atomicOr(&st->nan_flag, fl) == 0) st->nan_update = a.cnt;
     if (!a.keep_actor_slot) a.stats[10] = NAN;
     // no temperature step in this update: log alpha is the value it started from
     if (!a.keep_logtemp_slot) a.stats[11] = a.algo == RLMD_SAC ? st->log_alpha[slot_rd(a.cnt)] : NAN;

@@ -27,19 +27,32 @@ _SEED_CTR = [0]
 
 
 def private_seed():
-    """A Philox seed for a device env created without one.  Drawn from a private
-    counter, never from np.random: the reference's env constructors consume no
-    NumPy draws, so taking one here would shift the global stream the drivers
-    consume in the reference's order (time_slice, shuffle_data, eval gaps)."""
+    """A Philox seed for a device env created without one.
+
+    It is a hash of NumPy's global MT19937 state together with a private
+    counter.  Reading the state (np.random.get_state) does not advance the
+    stream: the reference's env constructors consume no NumPy draws, so drawing
+    one here would shift the global stream the drivers consume in the
+    reference's order (time_slice, shuffle_data, eval gaps).  Hashing the state
+    makes the device env's noise follow the driver's np.random.seed(s) (the
+    reference's seeds control its env noise), and the counter keeps two envs
+    created at the same stream position apart."""
+    import hashlib
+
     _SEED_CTR[0] += 1
-    return (0x6576616C * _SEED_CTR[0] + 0x2545F491) & 0x7FFFFFFF
+    _, keys, pos, _, _ = np.random.get_state()
+    h = hashlib.blake2b(np.ascontiguousarray(keys, dtype=np.uint32).tobytes(), digest_size=8)
+    h.update(np.array([pos, _SEED_CTR[0]], dtype=np.int64).tobytes())
+    return int.from_bytes(h.digest(), "little") & 0x7FFFFFFF
 
 
 class VecEnv:
     """N lanes of one reference env class, stepped by one HIP kernel launch."""
 
     def __init__(self, family, investor, n_lanes, n_gambles=1, seed=0, prices=None, obs_days=1,
-                 time_length=0, action_days=1, shuffle_days=1, sample_days=0, device="cuda:0"):
+                 time_length=0, action_days=1, shuffle_days=1, sample_days=0, device="cuda:0", slice_groups=0):
+        """slice_groups (market, a probe switch): lanes l and l' with l % G == l' % G
+        draw the same episode slices and block shuffles; 0 = every lane its own."""
         self.family = FAMILY[family] if isinstance(family, str) else family
         self.investor = INVESTOR[investor] if isinstance(investor, str) else investor
         self.n_lanes, self.n_gambles, self.device = n_lanes, n_gambles, torch.device(device)
@@ -47,7 +60,7 @@ class VecEnv:
         self.make_kw = dict(prices=prices, obs_days=obs_days, time_length=time_length, action_days=action_days,
                             shuffle_days=shuffle_days, sample_days=sample_days)
         cfg = _abi.EnvCfg(self.family, self.investor, n_lanes, n_gambles, obs_days, time_length,
-                          action_days, shuffle_days, sample_days, 0, seed)
+                          action_days, shuffle_days, sample_days, int(slice_groups), seed)
         self._prices = None
         n_days = 0
         pp = None

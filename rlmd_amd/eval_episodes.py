@@ -66,7 +66,7 @@ def _eval_env(inputs, n_gambles, n_eval, device):
     key = (cls.family, cls.investor, n_gambles, n_eval, str(device))
     env = _EVAL_ENVS.get(key)
     if env is None:
-        seed = int(inputs.get("eval_seed", private_seed()))
+        seed = int(inputs["eval_seed"]) if "eval_seed" in inputs else private_seed()
         env = VecEnv(cls.family, cls.investor, n_eval, n_gambles, seed=seed, device=device)
         _cache_put(_EVAL_ENVS, key, env)
     return env

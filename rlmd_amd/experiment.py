@@ -131,9 +131,15 @@ def run_experiment(env="gbm", investor="A", n_gambles=1, algo="SAC", loss="MSE",
     per-episode trial rows of one trial (host memory and the logging gather:
     (19 + risk) x 4 B per row); a run that exceeds it raises, pointing at
     episode_rows=False (one aggregate row per logging interval).
-    schedule: warm-up / smoothing lengths in the reference's env steps mapped to
-    the same number of learner updates ("updates", trainer.schedule_steps) or
-    taken as vector steps per lane ("vector").
+    warmup_steps / smoothing_window: UNITS depend on `schedule`.  With the
+    default schedule="updates" they are the reference's lengths in its env steps
+    (one learner update per env step, main.py:256-257) and are converted to the
+    same number of learner updates: ceil(steps / k_updates) vector steps
+    (trainer.schedule_steps).  With schedule="vector" they are vector steps per
+    lane, the unit VecTrainer itself takes (rounds 1-3's behaviour).  Callers
+    that passed per-lane vector-step counts before round 4 must pass
+    schedule="vector" or their warm-up becomes k_updates times shorter
+    (INTEGRATION.md, "Units of the warm-up / smoothing arguments").
     checkpoint: trailing-`trail` checkpoints under the reference's models/ path.  continue_trials: inputs["continue"] — trial t starts from
     trial t-1's last checkpoint and final log temperature (run on one rank, as
     the chain is sequential).  trainer_factory(seed, init_logtemp) replaces the

@@ -6,8 +6,10 @@ One ``step()`` is one fused vector step of scripts/rl_multiplicative.py:190-227
 action_window clip, the env step, the replay insert of (s, a, r, s',
 learn_done), auto-reset of finished lanes, then K learn() updates.
 
-Semantics decisions versus the reference's single stream: warm-up
-and smoothing schedules count vector steps per lane; K updates of batch B per
+Semantics decisions versus the reference's single stream: the
+warm-up and smoothing counters of this class are vector steps per lane (the
+vectorised drivers pass the reference's lengths through schedule_steps, which
+converts them to the same number of learner updates); K updates of batch B per
 vector step (UTD = K / N per env step, reported with every metric); one agent
 shared by all lanes; uniform sampling over all lanes' transitions.
 """
@@ -49,13 +51,14 @@ class VecTrainer:
                  smoothing_window=2000, precision="bf16", hidden=None, batch=None, topk=None,
                  prices=None, obs_days=1, time_length=0, shuffle_days=5, sample_days=0,
                  device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99, s_dist="N",
-                 initial_logtemp=0.0):
+                 initial_logtemp=0.0, agent_kw=None, slice_groups=0):
         """warmup_steps / smoothing_window: vector steps per lane (the ABI's counters;
-        schedule_steps converts the reference's lengths)."""
+        schedule_steps converts the reference's lengths).  agent_kw: further
+        DeviceAgent settings (update intervals, learning rates, ...)."""
         self.device = torch.device(device)
         self.env = VecEnv(env, investor, n_lanes, n_gambles, seed=seed, prices=prices, obs_days=obs_days,
                           time_length=time_length, shuffle_days=shuffle_days, sample_days=sample_days,
-                          device=device)
+                          device=device, slice_groups=slice_groups)
         d = DEFAULTS[algo]
         h1, h2 = hidden or (d["h1"], d["h2"])
         self.batch = batch or d["batch"]
@@ -63,7 +66,7 @@ class VecTrainer:
         S, A = self.env.state_dim, self.env.action_dim
         self.agent = DeviceAgent(algo, S, A, h1, h2, self.batch, self.topk, loss=loss, precision=precision,
                                  seed=seed, init_seed=init_seed, policy_dist=s_dist, device=device,
-                                 initial_logtemp=initial_logtemp)
+                                 initial_logtemp=initial_logtemp, **(agent_kw or {}))
         self.replay = ReplayMemory(replay_capacity, S, A, device=device, multi_steps=multi_steps, lanes=n_lanes,
                                    dynamics=dynamics, gamma=gamma)
         self.n_lanes, self.k_updates = n_lanes, k_updates

@@ -105,7 +105,8 @@ def kelly(env):
 
 
 def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eval_every=500, n_eval=4096,
-        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE", schedule="updates", multi_steps=1):
+        seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE", schedule="updates", multi_steps=1,
+        slice_groups=0):
     """warmup / smoothing: the reference's lengths (main.py gym_envs warm-up 1e3,
     smoothing_window_mul 2e3), mapped to vector steps by trainer.schedule_steps."""
     import torch
@@ -117,7 +118,7 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
     tr = VecTrainer(env=fam, investor=inv, n_lanes=lanes, n_gambles=1, algo=algo, loss=loss, k_updates=k,
                     replay_capacity=replay, seed=seed, warmup_steps=schedule_steps(warmup, k, schedule),
                     smoothing_window=schedule_steps(smoothing, k, schedule), precision=precision, device=device,
-                    init_seed=seed, multi_steps=multi_steps, **kw)
+                    init_seed=seed, multi_steps=multi_steps, slice_groups=slice_groups, **kw)
     l_star, g_star = kelly(env) if env != "market" else (None, None)
     # the reset state (identical for every lane; market lanes start on their own slices)
     reset_obs = tr.env.reset()[:1].float().clone() if env != "market" else tr.obs[:1].float().clone()
@@ -132,8 +133,10 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
                 # eval_risk_log = [gap, reward, wealth, step return, mean lev, ...]
                 # (eval_episodes.py:542-543, market_envs.py:196): the leverage is column 4
                 # (the reference's summary prints column 3, the last step's return, as
-                # "lev"); one evaluation launch summarises at most 1,024 episodes
-                ev = tr.evaluate_market(n_eval=min(n_eval, lanes, 1024), test_days=250)
+                # "lev")
+                # episode i starts from lane (i mod N)'s position plus a gap (one
+                # evaluation launch summarises at most 1,024 episodes)
+                ev = tr.evaluate_market(n_eval=min(n_eval, 1024), test_days=250)
                 lev = float(np.mean(ev["risk_log"][:, 4]))
             else:
                 ev = tr.evaluate(n_eval=n_eval, max_steps=100, with_stats=False)

@@ -59,6 +59,30 @@ def mfma_summary(path, stat_rows, dst):
     print(json.dumps(out, indent=1))
 
 
+def trace_roofline(path, lanes=65536, bytes_per_lane=103):
+    """The headline roofline recomputed from the per-dispatch kernel trace of the
+    same bench command: act_env_kernel's average dispatch duration minus the
+    standalone fused_act_kernel's on full-size launches only (grid = 4 x lanes
+    work-items: the 20 acting-only reference launches and the unfused steps; the
+    100-row evaluation launches are excluded), against 103 B x lanes."""
+    dur = {"act_env_kernel": [], "fused_act_kernel": []}
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            m = re.search(r"(\w+_kernel)", row["Kernel_Name"])
+            k = m.group(1) if m else ""
+            if k in dur and int(row["Grid_Size_X"]) == 4 * lanes:
+                dur[k].append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-3)
+    if not dur["act_env_kernel"] or not dur["fused_act_kernel"]:
+        return None
+    fa, act = statistics.mean(dur["act_env_kernel"]), statistics.mean(dur["fused_act_kernel"])
+    marg = fa - act
+    gbs = bytes_per_lane * lanes / (marg * 1e-6) / 1e9
+    return {"act_env_us": fa, "act_env_launches": len(dur["act_env_kernel"]), "fused_act_us": act,
+            "fused_act_launches": len(dur["fused_act_kernel"]), "marginal_us": marg,
+            "algorithmic_bytes_per_launch": bytes_per_lane * lanes, "achieved_GBs": gbs, "frac": gbs / 8000.0,
+            "method": f"means over dispatches with grid {4 * lanes} work-items (full-size launches only)"}
+
+
 def main(tag, config="c2"):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
@@ -67,12 +91,19 @@ def main(tag, config="c2"):
     shutil.copy(stats, os.path.join(dst, f"{tag}_kernel_stats.csv"))
     rows = list(csv.DictReader(open(stats)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
-    lines = [f"rocprofv3 --kernel-trace --stats: python bench.py --no-cpu-baseline --steps 25 --warmup 5 "
+    lines = [f"rocprofv3 --kernel-trace --stats: python bench.py --no-cpu-baseline --no-companion --k-sweep= "
+             f"--seeds-per-gpu= --steps 25 --warmup 5 "
              f"(C2, 65,536 GBM lanes, SAC 256/256 bf16, K=8)", "",
              f"{'calls':>6} {'avg_us':>9} {'total_ms':>9} {'pct':>6}  kernel"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
         n, t = int(r["Calls"]), float(r["TotalDurationNs"])
         lines.append(f"{n:6d} {t / n / 1e3:9.2f} {t / 1e6:9.3f} {100 * t / tot:6.2f}  {r['Name'][:120]}")
+    tpath = os.path.join(src, "trace", "trace_kernel_trace.csv")
+    roof = trace_roofline(tpath) if config == "c2" and os.path.exists(tpath) else None
+    if roof:
+        lines += ["", "headline roofline from this trace (act_env_kernel - fused_act_kernel, full-size launches):",
+                  json.dumps(roof)]
+        json.dump(roof, open(os.path.join(dst, f"{tag}_roofline_trace.json"), "w"), indent=1)
     open(os.path.join(dst, f"{tag}_kernel_summary.txt"), "w").write("\n".join(lines) + "\n")
     fpath = os.path.join(src, "fetch", "fetch_counter_collection.csv")
     wpath = os.path.join(src, "write", "write_counter_collection.csv")
