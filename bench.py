@@ -423,6 +423,9 @@ def main():
                          "(default 'MSE,HUB,MAE,HSC'), C5 the multi-step n (default '3,5,7'); '' = off")
     ap.add_argument("--eval-every", type=int, default=1000,
                     help="vector steps between evaluations (eval_freq 1e3, main.py); amortised into value")
+    ap.add_argument("--event-stride", type=int, default=10,
+                    help="time every n-th env-kernel dispatch of the timed region with attached HIP events (each "
+                         "attached pair costs the stream ~11 us at C2: stamping every step would tax the headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dry-run", action="store_true",
@@ -503,12 +506,19 @@ def main():
                     smoothing_window=0, precision=args.precision, device=dev, init_seed=420 + rank,
                     multi_steps=ms_n, dynamics="A", **kw)
     # inside the timed region only the events attached to the env kernel's own
-    # dispatch are recorded (profile mode 2): the phase markers around acting and
-    # learning cost the stream ~25 us per C2 step (5 %), so the phase times come
-    # from a separate pass after the headline
-    elapsed = timed_region(tr, args.steps, args.warmup, world, torch.cuda.synchronize, on_start=lambda: tr.profile(2))
+    # dispatch are recorded (profile mode 2), on every event_stride-th step: the
+    # phase markers around acting and learning cost the stream ~25 us per C2 step
+    # (5 %) and an attached pair ~11 us (2.4 %), so the phase times come from a
+    # separate pass after the headline and the live kernel timing samples the region
+    def _prof_on():
+        tr.profile(2)
+        tr.profile_stride(max(args.event_stride, 1))
+
+    elapsed = timed_region(tr, args.steps, args.warmup, world, torch.cuda.synchronize, on_start=_prof_on)
     ms, cnt = tr.profile_read()
     env_ms = ms[1] / max(cnt[1], 1)
+    env_samples = cnt[1]
+    tr.profile_stride(1)
     tr.profile(1)  # the phase pass (untimed)
     for _ in range(10):
         tr.step()
@@ -642,8 +652,9 @@ def main():
                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc and pmc["source"],
                     "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": marginal_ms,
-                    "timing": "marginal: act_env_kernel (kernel-attached HIP events, every timed step) minus the "
-                              "standalone fused acting kernel on the same rows (kernel-attached events, 20 launches)",
+                    "timing": f"marginal: act_env_kernel (kernel-attached HIP events on every {args.event_stride}-th "
+                              f"step of the timed region: {env_samples} launches) minus the standalone fused acting "
+                              "kernel on the same rows (kernel-attached events, 20 launches)",
                     "fused_kernel_ms": fused_ms, "act_only_kernel_ms": act_only_ms,
                     "separate_env_kernel": {"avg_launch_ms": sep_env_ms, "algorithmic_bytes_per_launch": sep_bytes,
                                             "achieved": sep_bytes / (sep_env_ms * 1e-3) / 1e9,
@@ -662,8 +673,9 @@ def main():
                     "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": pmc and pmc["source"],
                     "algorithmic_bytes_per_launch": env_bytes, "avg_launch_ms": env_ms,
-                    "timing": "HIP events attached to every env_train_kernel dispatch of the timed region "
-                              "(hipExtLaunchKernelGGL start/stop: the dispatch's own begin/end)"}
+                    "timing": f"HIP events attached to every {args.event_stride}-th env_train_kernel dispatch of the "
+                              f"timed region ({env_samples} launches; hipExtLaunchKernelGGL start/stop: the "
+                              "dispatch's own begin/end)"}
         roofline_fused = None
     upd = sac_update_flops if cfg["algo"] == "SAC" else td3_update_flops
     flops = K * upd(S, A, H1, H2, tr.batch)

@@ -11,8 +11,13 @@ from concurrent.futures import ThreadPoolExecutor
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-BUILD = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "librlmd_amd.so")
+# experiment builds (A/B on one box): RLMD_BUILD_TAG=<tag> RLMD_EXTRA_FLAGS="-D..." writes
+# tools/_abh/librlmd_amd_<tag>.so from objects in rlmd_amd/_build_<tag>; load it with RLMD_LIB_PATH
+_TAG = os.environ.get("RLMD_BUILD_TAG", "")
+EXTRA = os.environ.get("RLMD_EXTRA_FLAGS", "").split()
+BUILD = os.path.join(HERE, "_build" + (f"_{_TAG}" if _TAG else ""))
+LIB = (os.path.join(HERE, "..", "tools", "_abh", f"librlmd_amd_{_TAG}.so") if _TAG
+       else os.path.join(HERE, "librlmd_amd.so"))
 ARCH = os.environ.get("RLMD_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = ["abi.hip", "env.hip", "replay.hip", "gemm.hip", "learn.hip", "act.hip", "rows.hip", "eval.hip", "shadow.hip", "lev.hip", "lev_sort.hip", "update.hip"]
@@ -44,7 +49,7 @@ def _compile(src):
     path = os.path.join(CSRC, src)
     if not _stale(obj, path, _headers()):
         return obj, None
-    cmd = [HIPCC, *FLAGS, *PER_FILE.get(src, DEFAULT_EXTRA), "-c", path, "-o", obj]
+    cmd = [HIPCC, *FLAGS, *PER_FILE.get(src, DEFAULT_EXTRA), *EXTRA, "-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
@@ -53,6 +58,7 @@ def _compile(src):
 
 def build(verbose=False, jobs=None):
     os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
     jobs = jobs or min(len(SOURCES), max(1, (os.cpu_count() or 4) // 2), 8)
     with ThreadPoolExecutor(jobs) as ex:
         res = list(ex.map(_compile, SOURCES))

@@ -44,6 +44,7 @@ using namespace actrows;
 
 template <int H1P, int NB, int SP, int MA>
 __global__ void __launch_bounds__(256, H1P == 256 ? (MA == kMaxA ? 3 : 2) : 1) fused_act_kernel(FusedActArgs a) {
+  RLMD_KERNARG_PREFETCH(a);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   act_rows<H1P, NB, SP, MA>(
       a, smem, [] {},

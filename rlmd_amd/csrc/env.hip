@@ -753,6 +753,7 @@ template <int FAM, int NG, int H1P, int NB, int SP, int MA>
 __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA ? 3 : 2) : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
                                                       StatFold sf) {
+  rlmd_kernarg_prefetch<(int)(sizeof(a) + sizeof(P) + sizeof(rb) + sizeof(sf) + 32)>();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (blockIdx.x == 0 && sf.fold_src)
     fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst, reinterpret_cast<double(*)[256]>(smem));

@@ -266,8 +266,17 @@ struct PhaseProfiler {
   int mask = 7;  // phases recorded: bit p = phase p (rlmd_profile_enable: 1 all, 2 the env kernel's only)
   std::vector<hipEvent_t> ev[3][2];  // phase x {start, stop}: 0 act, 1 env, 2 learn
   size_t used[3] = {0, 0, 0};
+  // sampling (rlmd_profile_stride): only every stride-th occurrence of a phase is
+  // timed — each attached event pair costs the stream a few us, so the headline's
+  // live kernel timing samples the timed region instead of stamping every step
+  int stride = 1;
+  uint64_t seen[3] = {0, 0, 0};
+  bool skip[3] = {false, false, false};
+  bool sample(int phase) { return (seen[phase]++ % (uint64_t)stride) == 0; }
   int record(int phase, int which, hipStream_t s) {
     if (!enabled || !(mask >> phase & 1)) return 0;
+    if (which == 0) skip[phase] = !sample(phase);
+    if (skip[phase]) return 0;
     auto& v = ev[phase][which];
     const size_t i = which == 0 ? used[phase] : used[phase] - 1;
     if (i >= v.size()) {
@@ -285,6 +294,7 @@ struct PhaseProfiler {
   int pair(int phase, hipEvent_t* start, hipEvent_t* stop) {
     *start = *stop = nullptr;
     if (!enabled || !(mask >> phase & 1)) return 0;
+    if (!sample(phase)) return 0;
     const size_t i = used[phase];
     for (int w = 0; w < 2; ++w)
       if (i >= ev[phase][w].size()) {
@@ -339,6 +349,8 @@ struct rlmd_agent_s {
   bool fused_update = false;
   bool target_pair = true;  // TD3: next update's target path in this update's forward (RLMD_TARGET_PAIR=0: off)
   bool fused_actor = false;  // the actor step too (actions <= 2)
+  int n_cu = 256;            // compute units of the device (column-split decisions)
+  int qsplit_max = 2;        // qeval_rows column split allowed (RLMD_QSPLIT=1: off)
   rlmd::PhaseProfiler prof;  // rlmd_profile_enable / _read
 };
 
@@ -804,7 +816,14 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       qe.ua = S_.ua;
       qe.wheads = S_.wheads;
     }
-    RLMD_TRY(qeval_rows_launch(qe, nq, st));
+    // column split of the critic / basis jobs: two workgroups per (rows, job), each
+    // streaming half of an fc2 copy, when the halves are whole K-steps and the
+    // grid still fits the chip in one round
+    int qsplit = 1;
+    if (ag->fused_actor && ag->qsplit_max > 1 && d.H2p % 64 == 0 &&
+        2 * ((B + 15) / 16) * (nq + qe.nab) <= ag->n_cu)
+      qsplit = 2;
+    RLMD_TRY(qeval_rows_launch(qe, nq, st, qsplit));
     if (ag->fused_actor) {
       // the actor (+ temperature) step in one launch (update.hip)
       ActUpdArgs au{};
@@ -860,6 +879,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       au.ti = d.H2p / 32;
       au.n_w2 = au.ti * au.tj;
       au.n_w1 = d.H1p / 32;
+      au.qsplit = qsplit;
       RLMD_TRY(actor_update_launch(au, st));
       return 0;
     }
@@ -1140,9 +1160,18 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
     const int nh = c.algo == RLMD_SAC ? 2 * A : A;
     RLMD_ALLOC(s.hp1a, e1 * ts);
     RLMD_ALLOC(s.hp2a, e2 * ts);
-    RLMD_ALLOC(s.ua, e1 * nh);
+    // two halves of the partial bases, dq/da and q (qeval_rows column split)
+    RLMD_ALLOC(s.ua, 2 * e1 * nh);
     RLMD_ALLOC(s.wheads, nh * H2);
-    for (int g = 0; g < 2; ++g) RLMD_ALLOC(s.dqda[g], B * A);
+    for (int g = 0; g < 2; ++g) RLMD_ALLOC(s.dqda[g], 2 * B * A);
+    {
+      int dev = 0, ncu = 0;
+      if (hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && ncu > 0)
+        ag->n_cu = ncu;
+      const char* qs = getenv("RLMD_QSPLIT");
+      ag->qsplit_max = qs ? std::max(1, std::min(2, atoi(qs))) : 2;
+    }
     RLMD_ALLOC(s.rank1, B);
   }
   {  // weight-gradient tiles of the larger phase (critics: both nets; actor)
@@ -1169,7 +1198,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
     RLMD_ALLOC(s.dc1[g], B * H1);
     RLMD_ALLOC(s.e1[g], B * H1);
     RLMD_ALLOC(s.e2[g], B * H2);
-    RLMD_ALLOC(s.qnpart[g], B);
+    RLMD_ALLOC(s.qnpart[g], 2 * B);
     RLMD_ALLOC(s.dqn[g], B);
   }
   ag->wcopy_bytes = (size_t)rlmd::pad32(H1) * rlmd::pad32(H2) * (c.precision == RLMD_BF16 ? 2 : 4);
@@ -1342,7 +1371,17 @@ int rlmd_profile_enable(rlmd_agent_t ag, int32_t on) {
   // 2: only the events attached to the env kernel's own dispatch (phase 1): the
   // phase markers around acting / learning cost the stream ~25 us per C2 step
   pr.mask = on == 2 ? 2 : 7;
-  for (int p = 0; p < 3; ++p) pr.used[p] = 0;
+  for (int p = 0; p < 3; ++p) {
+    pr.used[p] = 0;
+    pr.seen[p] = 0;
+    pr.skip[p] = false;
+  }
+  return 0;
+}
+
+int rlmd_profile_stride(rlmd_agent_t ag, int32_t stride) {
+  RLMD_CHECK(ag && stride >= 1, "bad profile stride");
+  ag->prof.stride = stride;
   return 0;
 }
 

@@ -289,7 +289,7 @@ struct ABwdArgs {
 
 size_t rows_lds_bytes(const RowDims& d);
 int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st);
-int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st);
+int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st, int split = 1);  // split: gridDim.z column halves
 int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st);
 int abwd_rows_launch(const ABwdArgs& a, hipStream_t st);
 // Compute copies (wc, wt) of fc2.weight for n nets; refresh from the masters.

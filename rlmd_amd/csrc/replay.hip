@@ -166,6 +166,7 @@ __global__ void __launch_bounds__(kSampleThreads)
     replay_sample_kernel(rlmd::ReplayView rb, int64_t M, int B, int G, uint64_t seed, uint32_t ctr_lo,
                          uint32_t ctr_hi, int64_t* idx_out, float* s, float* a,
                          float* r, float* s2, uint8_t* done, float* xsa, int32_t* eff) {
+  rlmd_kernarg_prefetch<(int)sizeof(rb) + 112>();
   __shared__ uint64_t keys[kSortPopulation];
   __shared__ int64_t cand[kSampleThreads];
   __shared__ int any_dup;

@@ -125,6 +125,72 @@ __device__ __forceinline__ float rlmd_ldf(__amdgpu_buffer_rsrc_t r, int64_t idx,
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? (int)(idx * 4) : 0x7fffffff, 0, 0));
 }
 
+// Kernel-argument prefetch.  The learner kernels take structs of 0.5-1 KB by
+// value; the compiler loads each field (s_load) next to its first use, behind the
+// role branches, so a prologue walked ~6-9 dependent scalar round trips, each a
+// miss on a fresh kernarg line (the host writes the segment per dispatch: no
+// cache holds it).  One dword of every 64-byte line, loaded together at entry and
+// waited for once, turns those into scalar-cache hits.  Loads only (the scalar
+// cache is never written).  The loads and their wait are ONE asm statement with
+// early-clobber outputs: left to the compiler they came in clauses of 8 with a
+// wait after each, and split asm loads would let it reuse an output register
+// while its load is still in flight.
+template <int NL>
+__device__ __forceinline__ void rlmd_karg_lines(const void* kp);
+template <>
+__device__ __forceinline__ void rlmd_karg_lines<4>(const void* kp) {
+  uint32_t v[4];
+  __asm__ volatile("s_load_dword %0, %4, 0\n""s_load_dword %1, %4, 64\n""s_load_dword %2, %4, 128\n""s_load_dword %3, %4, 192\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3])
+                   : "s"(kp)
+                   : "memory");
+}
+template <>
+__device__ __forceinline__ void rlmd_karg_lines<8>(const void* kp) {
+  uint32_t v[8];
+  __asm__ volatile("s_load_dword %0, %8, 0\n""s_load_dword %1, %8, 64\n""s_load_dword %2, %8, 128\n""s_load_dword %3, %8, 192\n""s_load_dword %4, %8, 256\n""s_load_dword %5, %8, 320\n""s_load_dword %6, %8, 384\n""s_load_dword %7, %8, 448\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3]), "=&s"(v[4]), "=&s"(v[5]), "=&s"(v[6]), "=&s"(v[7])
+                   : "s"(kp)
+                   : "memory");
+}
+template <>
+__device__ __forceinline__ void rlmd_karg_lines<12>(const void* kp) {
+  uint32_t v[12];
+  __asm__ volatile("s_load_dword %0, %12, 0\n""s_load_dword %1, %12, 64\n""s_load_dword %2, %12, 128\n""s_load_dword %3, %12, 192\n""s_load_dword %4, %12, 256\n""s_load_dword %5, %12, 320\n""s_load_dword %6, %12, 384\n""s_load_dword %7, %12, 448\n""s_load_dword %8, %12, 512\n""s_load_dword %9, %12, 576\n""s_load_dword %10, %12, 640\n""s_load_dword %11, %12, 704\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3]), "=&s"(v[4]), "=&s"(v[5]), "=&s"(v[6]), "=&s"(v[7]), "=&s"(v[8]), "=&s"(v[9]), "=&s"(v[10]), "=&s"(v[11])
+                   : "s"(kp)
+                   : "memory");
+}
+template <>
+__device__ __forceinline__ void rlmd_karg_lines<16>(const void* kp) {
+  uint32_t v[16];
+  __asm__ volatile("s_load_dword %0, %16, 0\n""s_load_dword %1, %16, 64\n""s_load_dword %2, %16, 128\n""s_load_dword %3, %16, 192\n""s_load_dword %4, %16, 256\n""s_load_dword %5, %16, 320\n""s_load_dword %6, %16, 384\n""s_load_dword %7, %16, 448\n""s_load_dword %8, %16, 512\n""s_load_dword %9, %16, 576\n""s_load_dword %10, %16, 640\n""s_load_dword %11, %16, 704\n""s_load_dword %12, %16, 768\n""s_load_dword %13, %16, 832\n""s_load_dword %14, %16, 896\n""s_load_dword %15, %16, 960\n"
+                   "s_waitcnt lgkmcnt(0)"
+                   : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3]), "=&s"(v[4]), "=&s"(v[5]), "=&s"(v[6]), "=&s"(v[7]), "=&s"(v[8]), "=&s"(v[9]), "=&s"(v[10]), "=&s"(v[11]), "=&s"(v[12]), "=&s"(v[13]), "=&s"(v[14]), "=&s"(v[15])
+                   : "s"(kp)
+                   : "memory");
+}
+template <int BYTES>
+__device__ __forceinline__ void rlmd_kernarg_prefetch() {
+  // lines of the explicit arguments, rounded up to a multiple of 4 (<= 16: 1 KB)
+  constexpr int nl = (BYTES + 63) / 64, n4 = ((nl + 3) / 4) * 4;
+  static_assert(n4 <= 16, "kernel arguments above 1 KB");
+  rlmd_karg_lines<n4>((const void*)__builtin_amdgcn_kernarg_segment_ptr());
+}
+#ifndef RLMD_KARG_PF
+#define RLMD_KARG_PF 1
+#endif
+#if RLMD_KARG_PF
+#define RLMD_KERNARG_PREFETCH(args) rlmd_kernarg_prefetch<(int)sizeof(args)>()
+#else
+#define RLMD_KERNARG_PREFETCH(args) \
+  do {                              \
+  } while (0)
+#endif
+
 // Write-through stores for data the next kernel reads (optimiser state, compute
 // copies, row-packed activations, bases): a device-scope store (sc1) sends each
 // line on to memory as it is written, instead of leaving it dirty in the XCD's

@@ -184,10 +184,13 @@ __device__ __forceinline__ void frag_load(FragArr<PREC, NBW, MULTI>& f,
     }
 }
 
+// K-steps [ks0, K / KS) of output bands nb0 .. nb0 + nblk - 1 (a K split: ks0 > 0
+// with K short of the full depth; a column split: nb0 > 0 with fewer bands)
 template <int PREC, int NBW, bool MULTI>
 __device__ __forceinline__ void pre_issue(Pre<PREC, NBW, MULTI>& p, const void* Bg, int ldb, int K, int nblk,
-                                          int nb0 = 0) {
-  frag_load<PREC, NBW, MULTI>(p.f, static_cast<const typename CT<PREC>::T*>(Bg), ldb, 0, K / CT<PREC>::KS, nblk, nb0);
+                                          int nb0 = 0, int ks0 = 0) {
+  frag_load<PREC, NBW, MULTI>(p.f, static_cast<const typename CT<PREC>::T*>(Bg), ldb, ks0, K / CT<PREC>::KS, nblk,
+                              nb0);
 }
 
 template <int PREC, int NBW, bool MULTI>
@@ -212,10 +215,11 @@ __device__ __forceinline__ void frag_mfma(const FragArr<PREC, NBW, MULTI>& f,
 
 // acc[i] = A[16 x K] B^T for output column block nb = wave + 8 i (A: LDS rows of
 // pitch lda; B: compute copy, one row of K elements per output column, pitch ldb).
+// ks0: the first K-step (pre issued with the same origin); K / KS the end
 template <int PREC, int NBW, bool MULTI>
 __device__ __forceinline__ void mfma_rows(Pre<PREC, NBW, MULTI>& pre, const typename CT<PREC>::T* As, int lda,
                                           const void* Bv, int ldb, int K, int nblk, f32x4 (&acc)[NBW],
-                                          int nb0 = 0) {
+                                          int nb0 = 0, int ks0 = 0) {
   constexpr int G = Pre<PREC, NBW, MULTI>::G;
   const auto* Bg = static_cast<const typename CT<PREC>::T*>(Bv);
   const int nsteps = K / CT<PREC>::KS;
@@ -223,10 +227,10 @@ __device__ __forceinline__ void mfma_rows(Pre<PREC, NBW, MULTI>& pre, const type
   for (int i = 0; i < NBW; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   if constexpr (!MULTI) {
     (void)Bg;
-    frag_mfma<PREC, NBW, MULTI>(pre.f, As, lda, 0, nsteps, nblk, acc);
+    frag_mfma<PREC, NBW, MULTI>(pre.f, As, lda, ks0, nsteps, nblk, acc);
   } else {
     FragArr<PREC, NBW, MULTI> b1;
-    for (int s = 0; s < nsteps; s += 2 * G) {
+    for (int s = ks0; s < nsteps; s += 2 * G) {
       frag_load<PREC, NBW, MULTI>(b1, Bg, ldb, s + G, nsteps, nblk, nb0);
       frag_mfma<PREC, NBW, MULTI>(pre.f, As, lda, s, nsteps, nblk, acc);
       frag_load<PREC, NBW, MULTI>(pre.f, Bg, ldb, s + 2 * G, nsteps, nblk, nb0);
@@ -276,7 +280,7 @@ struct FwdConst {
 
 template <int NBW>
 __device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, const NetOff& o, int in, int nh,
-                                          const float* wa, const float* wb, int na) {
+                                          const float* wa, const float* wb, int na, int nb0 = 0) {
   const ElemMap m = elem_map(pad32(o.h1));
   const bool own = m.c < o.h1 && m.r0 < R;
   const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(p, o.size * 4);
@@ -299,7 +303,7 @@ __device__ __forceinline__ void fwd_const(FwdConst<NBW>& k, const float* p, cons
   const int64_t oa = wa - p, ob = (wb ? wb : wa) - p;  // head rows relative to p
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
-    const int col = acc_col(i);
+    const int col = acc_col(i, nb0);
     const bool cin = col < o.h2;
     k.b2[i] = rlmd_ldf(rp, o.b2 + col, cin);
 #pragma unroll
@@ -443,8 +447,9 @@ template <int NBW, int PREC = RLMD_BF16>
 __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdConst<NBW>& k, const NetOff& o,
                                              int nh, float* h2_out, uint8_t* m2_out, float* h2s, int ldh2,
                                              float* part, int row0, int B, const FwdExtra<PREC>* ex = nullptr,
-                                             int lda1 = 0) {
-  const int H2 = o.h2, nblk = pad32(H2) / 16;
+                                             int lda1 = 0, int nb0 = 0, int nbw = 0) {
+  // output bands nb0 .. nb0 + nbw - 1 (a column split; nbw = 0: all of them)
+  const int H2 = o.h2, nblk = nbw ? nbw : pad32(H2) / 16;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float ph[4][NHF];
 #pragma unroll
@@ -454,7 +459,7 @@ __device__ __forceinline__ void fwd_epilogue(const f32x4 (&acc)[NBW], const FwdC
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
     if (wave + NW * i < nblk) {
-      const int col = acc_col(i);
+      const int col = acc_col(i, nb0);
       const bool cin = col < H2;
       uint32_t mw = 0;
       typename CT<PREC>::T hz[4];
@@ -521,7 +526,8 @@ template <int PREC, int NBW, bool MULTI>
 __device__ __forceinline__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>& k, Pre<PREC, NBW, MULTI>& pre,
                          const float* xs, int ldx, int in, int nh, const float* wa, const float* wb, int na,
                          unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B,
-                         uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr, const FwdExtra<PREC>* ex = nullptr) {
+                         uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr, const FwdExtra<PREC>* ex = nullptr,
+                         int nb0 = 0, int nbw = 0) {
   using T = typename CT<PREC>::T;
   T* a1 = reinterpret_cast<T*>(smem + L.a1);
   float* part = reinterpret_cast<float*>(smem + L.part);
@@ -535,11 +541,12 @@ __device__ __forceinline__ void mlp_rows(const RowNet& net, const NetOff& o, con
   if (blockIdx.y == 4) RLMD_TSR(88);
   f32x4 acc[NBW];
   const int H1p = pad32(o.h1);
-  mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, pad32(o.h2) / 16, acc);
+  mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, nbw ? nbw : pad32(o.h2) / 16, acc, nb0);
   if (blockIdx.y == 2) RLMD_TSR(65);
   if (blockIdx.y == 4) RLMD_TSR(89);
   const bool fused = nh <= NHF;
-  fwd_epilogue<NBW, PREC>(acc, k, o, nh, h2_out, m2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B, ex, L.lda1);
+  fwd_epilogue<NBW, PREC>(acc, k, o, nh, h2_out, m2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B, ex, L.lda1,
+                          nb0, nbw);
   if (blockIdx.y == 2) RLMD_TSR(66);
   if (blockIdx.y == 4) RLMD_TSR(90);
   __syncthreads();
@@ -696,8 +703,9 @@ __device__ __forceinline__ void actor_const(FwdConst<NBW>& k, const RowNet& n, c
   fwd_const<NBW>(k, n.p, ao, d.S, sac ? 2 * d.A : d.A, n.p + ao.w3, sac ? n.p + ao.w4 : n.p + ao.w3, d.A);
 }
 template <int NBW>
-__device__ __forceinline__ void critic_const(FwdConst<NBW>& k, const RowNet& n, const NetOff& co, const RowDims& d) {
-  fwd_const<NBW>(k, n.p, co, d.X, 1, n.p + co.w3, n.p + co.w3, 1);
+__device__ __forceinline__ void critic_const(FwdConst<NBW>& k, const RowNet& n, const NetOff& co, const RowDims& d,
+                                             int nb0 = 0) {
+  fwd_const<NBW>(k, n.p, co, d.X, 1, n.p + co.w3, n.p + co.w3, 1, nb0);
 }
 
 // The backward-basis pass of one net over the block's rows: acc = aU (LDS,
@@ -730,6 +738,7 @@ __device__ __forceinline__ void basis_pass(Pre<PREC, NBW, MULTI>& pw, const type
 // critic y - 2 on (s, a); y = 4: policy on s for the actor step.
 template <int PREC, int NBW, bool MULTI>
 __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
+  RLMD_KERNARG_PREFETCH(a);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowDims& d = a.d;
   const Lds L = lds_layout(d);
@@ -898,6 +907,7 @@ __device__ __forceinline__ void bwd_mask(BwdMask<NBW>& k, const uint8_t* m1, con
 
 template <int PREC, int NBW, bool MULTI>
 __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
+  RLMD_KERNARG_PREFETCH(a);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const RowDims& d = a.d;
   const Lds L = lds_layout(d);
@@ -905,6 +915,12 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   const float* hout = reinterpret_cast<const float*>(smem + L.hout);
   const int row0 = blockIdx.x * R, g = blockIdx.y, B = d.B;
   const int H1p = pad32(d.H1), H2p = pad32(d.H2);
+  // column split (gridDim.z = P halves of the fc2 output columns, P <= 2): the
+  // workgroup of half p streams half of each fc2 copy — the per-workgroup weight
+  // stream is this kernel's cost — and writes partial q, dq/da and bases at
+  // offset p, which the actor step sums in half order
+  const int P = (int)gridDim.z, p = (int)blockIdx.z;
+  const int kh = H2p / P, ks0 = p * kh / CT<PREC>::KS, ke = (p + 1) * kh;  // this half's fc2 columns as K-steps
   if (g >= a.nq) {
     // the policy's backward basis of head h over the block's rows (fused actor
     // update): aU = [h2 > 0] * W_head[h] from the forward's masks, times fc2.weight
@@ -913,13 +929,13 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     const int h = g - a.nq, nrb = (B + R - 1) / R;
     const RowNet& an = a.actor;
     Pre<PREC, NBW, MULTI> pw;
-    pre_issue<PREC, NBW, MULTI>(pw, an.wt, H2p, H2p, H1p / 16);
+    pre_issue<PREC, NBW, MULTI>(pw, an.wt, H2p, ke, H1p / 16, 0, ks0);
     BwdMask<NBW> k;
     bwd_mask<NBW>(k, a.am1, a.am2, nullptr, a.ao, row0, B);
     const ElemMap m = elem_map(H2p);
     const int64_t wrow = h < d.A ? a.ao.w3 + (int64_t)h * d.H2 : a.ao.w4 + (int64_t)(h - d.A) * d.H2;
     const float wk = rlmd_ldf(rlmd_rsrc(an.p, a.ao.size * 4), wrow + m.c, m.c < d.H2);
-    if (blockIdx.x == 0 && m.r0 == 0 && m.c < d.H2) a.wheads[(int64_t)h * d.H2 + m.c] = wk;
+    if (blockIdx.x == 0 && p == 0 && m.r0 == 0 && m.c < d.H2) a.wheads[(int64_t)h * d.H2 + m.c] = wk;
     T* aU = reinterpret_cast<T*>(smem + L.aU);
 #pragma unroll
     for (int rr = 0; rr < kMR<NBW>; ++rr) {
@@ -928,8 +944,8 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     }
     __syncthreads();
     f32x4 acc[NBW];
-    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, an.wt, H2p, H2p, H1p / 16, acc);
-    float* u = a.ua + (int64_t)h * nrb * H1p * R;
+    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, an.wt, H2p, ke, H1p / 16, acc, 0, ks0);
+    float* u = a.ua + (int64_t)(p * a.nab + h) * nrb * H1p * R;
     const int wave = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
@@ -945,13 +961,14 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   }
   const RowNet& cn = a.crit[g];
   const bool upd = a.dqda[0] != nullptr;
+  const int nbw = H2p / 16 / P, nb0 = p * nbw;  // this half's fc2 output bands
   Pre<PREC, NBW, MULTI> pc, pw;
-  pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+  pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
   FwdConst<NBW> kc;
-  critic_const<NBW>(kc, cn, a.co, d);
+  critic_const<NBW>(kc, cn, a.co, d, nb0);
   float w1a[NBW][NHF];  // W1[c][S + j] of this lane's accumulator columns (fused actor update)
   if (upd) {
-    pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
+    pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
     const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(cn.p, a.co.size * 4);
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
@@ -965,7 +982,7 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   __syncthreads();
   if (!upd) {
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.e1[g],
-                               a.e2[g], row0, B, a.em1[g], a.em2[g]);
+                               a.e2[g], row0, B, a.em1[g], a.em2[g], nullptr, nb0, nbw);
   } else {
     // the critic on (s, a_new) and its input gradient dq/da per row: the basis
     // pass [h1 > 0] * (([h2 > 0] w3) W2) contracted with W1[:, S:S+A] (the
@@ -976,9 +993,9 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     float* part = reinterpret_cast<float*>(smem + L.part);
     const FwdExtra<PREC> ex{nullptr, nullptr, reinterpret_cast<uint8_t*>(smem + L.m1s), aU};
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
-                               nullptr, row0, B, nullptr, nullptr, &ex);
+                               nullptr, row0, B, nullptr, nullptr, &ex, nb0, nbw);
     f32x4 acc[NBW];
-    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H2p, H2p, H1p / 16, acc);
+    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H2p, ke, H1p / 16, acc, 0, ks0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     float pd[4][NHF];
 #pragma unroll
@@ -1009,10 +1026,10 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     __syncthreads();
     if ((int)threadIdx.x < R * d.A) {
       const int r = threadIdx.x % R, j = threadIdx.x / R;
-      if (row0 + r < B) a.dqda[g][(int64_t)(row0 + r) * d.A + j] = head_sum(part, r, j);
+      if (row0 + r < B) a.dqda[g][(int64_t)(p * B + row0 + r) * d.A + j] = head_sum(part, r, j);
     }
   }
-  if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qn[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
+  if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.qn[g][p * B + row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
 }
 
 // ---------------------------------------------------------------------------
@@ -1088,6 +1105,7 @@ __device__ __forceinline__ void dh1_rows(Pre<PREC, NBW, MULTI>& pre, const RowNe
 
 template <int PREC, int NBW, bool MULTI>
 __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
+  RLMD_KERNARG_PREFETCH(a);
   using T = typename CT<PREC>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const Lds L = lds_layout(a.d);
@@ -1161,6 +1179,7 @@ __global__ void __launch_bounds__(NT) cbwd_rows_kernel(CBwdArgs a) {
 // count, so TD3's instantiations hold no second critic's fragments or masks.
 template <int PREC, int NBW, bool MULTI, int NQ>
 __global__ void __launch_bounds__(NT) abwd_rows_kernel(ABwdArgs a) {
+  RLMD_KERNARG_PREFETCH(a);
   const int nq = NQ == 1 ? 1 : a.nq;  // NQ = 2 keeps the runtime count (its register allocation measured best)
   using T = typename CT<PREC>::T;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1534,9 +1553,11 @@ int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st) {
   RLMD_CHECK(a.npair == 0 || (a.y0 == 0 && a.s2n && a.qtn[0] && a.qtn[1]), "fwd_rows: target pairing buffers");
   return launch_rows(a.d, 0, &a, (a.with_actor ? 5 : 4) - a.y0 + 2 * a.npair, st);
 }
-int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st) {
+int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st, int split) {
   RLMD_CHECK(a.nq == nq && (a.nab == 0 || (a.ua && a.wheads && a.am1 && a.am2)), "qeval_rows: head jobs need their buffers");
-  return launch_rows(a.d, 1, &a, nq + a.nab, st);
+  RLMD_CHECK(split == 1 || (split == 2 && a.dqda[0] && a.d.H2p % 64 == 0),
+             "qeval_rows: a column split needs the fused actor path and H2p a multiple of 64");
+  return launch_rows(a.d, 1, &a, nq + a.nab, st, 0, split);
 }
 // cbwd: dh1 columns in halves when each half is a whole number of column blocks
 // per wave (the per-workgroup W2^T stream is the kernel's cost)

@@ -208,6 +208,7 @@ struct ULds {
 // exceed the 256 CUs at one workgroup per CU (a second dispatch round); 2 x 88 do not.
 template <int PREC, bool WIDE>
 __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
+  RLMD_KERNARG_PREFETCH(a);
   using K = KT<PREC>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* dqs = reinterpret_cast<float*>(smem + ULds::dq);
@@ -543,6 +544,7 @@ struct ALds {
 
 template <int PREC>
 __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
+  RLMD_KERNARG_PREFETCH(a);
   using K = KT<PREC>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* ghs = reinterpret_cast<float*>(smem + ALds::gh);
@@ -615,18 +617,24 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   //      tile operands, Adam state, the fc1 block's states and first two bases
   const bool in = tid < B;
   const int64_t nB = (int64_t)B * 4;
-  const float q1r = rlmd_ldf(rlmd_rsrc(a.qn[0], nB), tid, in);
-  const float q2r = rlmd_ldf(rlmd_rsrc(a.qn[1], a.nq > 1 ? nB : 0), tid, in);
+  const int QP = a.qsplit > 1 ? 2 : 1;  // partial halves of q / dq/da / bases (qeval_rows column split)
+  const bool h2nd = QP > 1;
+  const __amdgpu_buffer_rsrc_t rq0 = rlmd_rsrc(a.qn[0], nB * QP), rq1 = rlmd_rsrc(a.qn[1], a.nq > 1 ? nB * QP : 0);
+  const float q1r = rlmd_ldf(rq0, tid, in) + rlmd_ldf(rq0, B + tid, in && h2nd);
+  const float q2r = rlmd_ldf(rq1, tid, in) + rlmd_ldf(rq1, B + tid, in && h2nd);
   lpv = rlmd_ldf(rlmd_rsrc(a.logp, sac ? nB : 0), tid, in);
   float dqda[2][kAM], sv[5][kAM];
   {
     const bool rin = in && !stats_wg;
-    const __amdgpu_buffer_rsrc_t r0 = rlmd_rsrc(a.dqda[0], nB * A), r1 = rlmd_rsrc(a.dqda[1], a.nq > 1 ? nB * A : 0),
+    const __amdgpu_buffer_rsrc_t r0 = rlmd_rsrc(a.dqda[0], nB * A * QP),
+                                 r1 = rlmd_rsrc(a.dqda[1], a.nq > 1 ? nB * A * QP : 0),
                                  rs = rlmd_rsrc(a.save, nB * 5 * A);
 #pragma unroll
     for (int j = 0; j < kAM; ++j) {
-      dqda[0][j] = rlmd_ldf(r0, (int64_t)tid * A + j, rin && j < A);
-      dqda[1][j] = rlmd_ldf(r1, (int64_t)tid * A + j, rin && j < A);
+      dqda[0][j] = rlmd_ldf(r0, (int64_t)tid * A + j, rin && j < A) +
+                   rlmd_ldf(r0, (int64_t)(B + tid) * A + j, rin && h2nd && j < A);
+      dqda[1][j] = rlmd_ldf(r1, (int64_t)tid * A + j, rin && j < A) +
+                   rlmd_ldf(r1, (int64_t)(B + tid) * A + j, rin && h2nd && j < A);
 #pragma unroll
       for (int q = 0; q < 5; ++q) sv[q][j] = rlmd_ldf(rs, (int64_t)tid * 5 * A + q * A + j, rin && j < A);
     }
@@ -677,7 +685,11 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   constexpr int kUP = 2;  // bases prefetched per fc1-block thread (the rest load in the loop)
   f32x4 uv[kUP][8];
   const int64_t ustride = (int64_t)nrb * H1p * 16;
-  const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * 4);
+  const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * QP * 4);
+  // bases in summation order hv = h * QP + half: U_h = sum over the halves, each
+  // half's term added with the head's gradient (layout [half][head])
+  const int nhv = nh * QP;
+  auto uoff = [&](int hv) { return (int64_t)((hv % QP) * nh + hv / QP) * ustride; };
   {
     const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
     const float log_alpha = sac ? st->log_alpha[slot_rd(a.adam.cnt)] : 0.f;
@@ -709,9 +721,9 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int r = 32 * p + 4 * q;
-          const bool ok = w1blk && h < nh && r < nrb * 16 && j < H1p;
+          const bool ok = w1blk && h < nhv && r < nrb * 16 && j < H1p;
           uv[h][q] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((uoff(h) + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
                                                            0, 0));
         }
     }
@@ -911,24 +923,27 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
       const int r = 32 * p + 4 * q;
       du[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int h = 0; h < kUP; ++h)
+      for (int h = 0; h < kUP; ++h) {
+        const int hg = h / QP;  // this term's head
 #pragma unroll
-        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(r + e) * kHM + h], uv[h][q][e], du[q][e]);
+        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(r + e) * kHM + hg], uv[h][q][e], du[q][e]);
+      }
     }
-    for (int h = kUP; h < nh; ++h) {
+    for (int hv = kUP; hv < nhv; ++hv) {
       f32x4 u[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int r = 32 * p + 4 * q;
         const bool ok = r < nrb * 16 && j < H1p;
         u[q] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((uoff(hv) + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
                                                          0, 0));
       }
+      const int hg = hv / QP;
 #pragma unroll
       for (int q = 0; q < 8; ++q)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(32 * p + 4 * q + e) * kHM + h], u[q][e], du[q][e]);
+        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(32 * p + 4 * q + e) * kHM + hg], u[q][e], du[q][e]);
     }
     float acc[9];
 #pragma unroll

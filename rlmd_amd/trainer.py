@@ -111,6 +111,10 @@ class VecTrainer:
         env kernel's dispatch only."""
         check(_abi.lib().rlmd_profile_enable(self.agent.h, int(mode)))
 
+    def profile_stride(self, stride):
+        """Time only every stride-th launch of each phase (rlmd_profile_stride)."""
+        check(_abi.lib().rlmd_profile_stride(self.agent.h, int(stride)))
+
     def profile_read(self):
         """(summed ms, launch count) per phase: 0 acting, 1 env kernel, 2 learn."""
         import ctypes as C

@@ -24,23 +24,29 @@ steps on 4,096 device episodes; same statistic per seed; 3 seeds.
 
 Assertion (the stated statistic): the MEDIAN over the build seeds of each
 statistic lies inside [min, max] of the five reference seeds' values, with no
-widening.  GBM_InvA (C2 SAC, C5 TD3 with 5-step returns) is one-sided (a
-measured deviation): its expected log growth is lev x 3.6
-%/step, monotone up to the 4.95 leverage corner; the reference's single SAC
-stream is still at leverage 0.28-1.41 after 5e4 updates while every build update
-sees transitions of 65,536 lanes and climbs further — the build's median growth
-must be >= the reference MEDIAN and its leverage in [reference median, 4.95].
-No upper bound on growth: at the corner the reference's lev_max termination
-(Q4) ends an evaluation episode after one step, whose reward exp(R) has mean
-exp(l (mu - s^2/2) + l^2 s^2 / 2) - 1 = 86 %, not the 19.5 % time-average.
+widening.  GBM_InvA (C2 SAC) is one-sided (a measured deviation):
+its expected log growth is lev x 3.6 %/step, monotone up to the 4.95 leverage
+corner; the reference's single SAC stream is still at leverage 0.28-1.41 after 5e4
+updates while every build update sees transitions of 65,536 lanes and climbs
+further — the build's median growth must be >= the reference MEDIAN and its
+leverage in [reference median, 4.95].  No upper bound on growth: at the corner the
+reference's lev_max termination (Q4) ends an evaluation episode after one step,
+whose reward exp(R) has mean exp(l (mu - s^2/2) + l^2 s^2 / 2) - 1 = 86 %, not the
+19.5 % time-average.  Dice_SH_InvA (C3's env) also needs two of three seeds inside
+the band individually.  Dice_InvA is uninformative (its band contains 0; kept as
+a divergence check).
 C5 is bimodal in the reference (three seeds near the corner, one at 0.16, one
-diverged to -3.6) and in the build (seed 0 at the corner, seeds 1-2 diverged to
--3.1 / -3.9): its check is that the build's best seed reaches the upper mode
-(the one-sided band above); 2 of 3 against 2 of 5 seeds outside it is not a
-difference at these sample sizes.
-Negative control: the same harness with K = 0 (no learning) must FAIL the band
-on Dice_SH_INSURED, Dice_SH_InvA and GBM_InvA (SAC and TD3 n = 5).
+diverged to -3.6) and in the build: the statistic is the number of 5 build seeds
+in the reference's upper mode, >= 1 (P(0 of 5) = 1 % at the reference's 3/5).
+C4 (market): the vectorised loop at C4's shape is held to the level bound of the
+round-5 N-sweep; the reference's single-stream semantics (N = 1, K = 1) through
+the same vectorised path is compared with the reference seeds by a Mann-Whitney
+test; the build's reference-API single-stream driver keeps the median band test.
+Negative control: the same harness with K = 0 (no learning) must FAIL on
+Dice_SH_INSURED, Dice_SH_InvA, GBM_InvA (SAC), Coin_InvA, C5 and both C4 checks.
+Per-seed records go to $RLMD_CONVERGE_LOG (profiles/r05_converge.jsonl).
 """
+import json
 import math
 import os
 import sys
@@ -103,16 +109,28 @@ def _third(recs, key):
     return float(v[-max(len(v) // 3, 1):].mean())
 
 
-def build_medians(workload, k, precision="bf16"):
+def record(workload, **kw):
+    """Per-seed convergence records, appended to $RLMD_CONVERGE_LOG when set (the
+    round's committed profiles/rNN_converge.jsonl is this file)."""
+    path = os.environ.get("RLMD_CONVERGE_LOG")
+    if path:
+        with open(path, "a") as f:
+            f.write(json.dumps({"workload": workload, **kw}) + "\n")
+
+
+def build_medians(workload, k, precision="bf16", seeds=BUILD_SEEDS):
     import converge
 
     env, algo, loss, _, ms, lanes, _ = WORKLOADS[workload]
     got = []
-    for seed in BUILD_SEEDS:
+    for seed in seeds:
         recs = converge.run(env, lanes, k, STEPS, precision=precision, eval_every=EVAL_EVERY, seed=seed, algo=algo,
                             loss=loss, log=lambda s: None, multi_steps=ms)
         assert all(math.isfinite(r["eval_growth_pct"]) and r["nan_flag"] == 0 for r in recs)
         got.append((_third(recs, "eval_growth_pct"), _third(recs, "lev")))
+        record(workload, k=k, precision=precision, seed=seed, lanes=lanes, updates=STEPS * k,
+               growth_pct=got[-1][0], lev=got[-1][1])
+        print(f"{workload} K={k} {precision} seed {seed}: growth {got[-1][0]:.3f} lev {got[-1][1]:.4f}", flush=True)
     return float(np.median([g for g, _ in got])), float(np.median([lv for _, lv in got])), got
 
 
@@ -120,31 +138,69 @@ def inside(x, band):
     return band[0] <= x <= band[1]
 
 
+# Dice_InvA (key 11) is UNINFORMATIVE: the reference's own band (lev -0.040 .. 0.123,
+# growth -0.136 .. 0.303 %/step) contains zero, and the no-learning control
+# (K = 0: -0.026 %/step, lev -0.008) lands inside it too — the reference's 5e4
+# steps do not learn this gamble's Kelly leverage (0.379) either.  It stays as a
+# check that the build does not diverge, not as evidence of learning.
+UNINFORMATIVE = {"dice"}
+
+
 @pytest.mark.parametrize("workload,precision", [("dice_sh", "bf16"), ("dice_sh", "fp32"), ("gbm", "bf16"),
                                                 ("dice_sh_a_mse", "bf16"), ("dice_sh_a_hub", "bf16"),
-                                                ("gbm_td3_n5", "bf16"),
                                                 ("coin", "bf16"), ("dice", "bf16")])
 def test_build_median_in_reference_band(golden, dev, workload, precision):
     gb, lb = bands(golden, workload)
     g, lv, seeds = build_medians(workload, 8, precision)
     print(f"{workload} {precision}: build median growth {g:.3f} %/step lev {lv:.4f}; seeds {seeds}; "
-          f"band growth {gb} lev {lb}")
-    if workload in BIMODAL:
-        # the upper mode is reached: the best build seed inside the one-sided band
-        g, lv = max(seeds, key=lambda x: x[1])
-        assert all(math.isfinite(x) and abs(x) <= GBM_LEV_MAX for _, x in seeds), (workload, seeds)
+          f"band growth {gb} lev {lb}" + (" (uninformative: the band contains 0)" if workload in UNINFORMATIVE else ""))
     assert inside(g, gb), (workload, precision, g, gb)
     assert inside(lv, lb), (workload, precision, lv, lb)
+    if workload.startswith("dice_sh_a"):
+        # the band admits a wide range (lev 0.26 .. 1.98): also per seed, at least
+        # two of the three build seeds inside both bands
+        n_in = sum(inside(x, gb) and inside(y, lb) for x, y in seeds)
+        assert n_in >= 2, (workload, seeds, gb, lb)
 
 
-@pytest.mark.parametrize("workload", ["dice_sh", "dice_sh_a_mse", "gbm", "gbm_td3_n5"])
+# C5 (TD3, 5-step returns, GBM_InvA): the reference's seeds split into an upper
+# mode near the leverage corner (3 of 5: lev 3.82 / 4.09 / 4.17, growth >= 13.8
+# %/step) and a lower one (0.16, -3.63).  Statistic: the number of build seeds in
+# the upper mode (lev >= the reference's upper-mode minimum 3.82 and growth >= its
+# minimum 13.80 %/step) out of 5.  If the build's upper-mode probability were the
+# reference's 3/5, P(0 of 5) = 0.4^5 = 1.0 %: the test asserts >= 1 of 5, which
+# fails a build that never reaches the upper mode at the 1 % level; the K = 0
+# control must have 0 of 5.  (Fisher's exact test cannot separate 3/5 from 1/5 at
+# these sizes; this bound is what five seeds per side can establish.)
+C5_SEEDS = (0, 1, 2, 3, 4)
+C5_UPPER = (13.80, 3.82)
+
+
+def c5_upper_count(seeds):
+    return sum(g >= C5_UPPER[0] and lv >= C5_UPPER[1] for g, lv in seeds)
+
+
+def test_c5_upper_mode_frequency(golden, dev):
+    ref = ref_stats(golden, "gbm_td3_n5")
+    assert sum(g >= C5_UPPER[0] and lv >= C5_UPPER[1] for g, lv in ref) == 3, ref  # the reference's 3 of 5
+    _, _, seeds = build_medians("gbm_td3_n5", 8, seeds=C5_SEEDS)
+    assert all(math.isfinite(x) and abs(x) <= GBM_LEV_MAX for _, x in seeds), seeds
+    n_up = c5_upper_count(seeds)
+    print(f"C5 upper mode: build {n_up} of 5 (reference 3 of 5); seeds {seeds}")
+    assert n_up >= 1, seeds
+
+
+@pytest.mark.parametrize("workload", ["dice_sh", "dice_sh_a_mse", "gbm", "gbm_td3_n5", "coin"])
 def test_no_learning_fails_the_band(golden, dev, workload):
     """K = 0: the policy keeps its initial weights; the harness must reject it."""
     gb, lb = bands(golden, workload)
+    if workload in BIMODAL:  # the C5 statistic: no seed of five in the upper mode
+        _, _, seeds = build_medians(workload, 0, seeds=C5_SEEDS)
+        print(f"{workload} K=0: seeds {seeds}")
+        assert c5_upper_count(seeds) == 0, seeds
+        return
     g, lv, seeds = build_medians(workload, 0)
     print(f"{workload} K=0: median growth {g:.3f} lev {lv:.4f}; seeds {seeds}")
-    if workload in BIMODAL:  # as the learning test: the best seed
-        g, lv = max(seeds, key=lambda x: x[1])
     assert not (inside(g, gb) and inside(lv, lb)), (workload, g, lv, gb, lb)
 
 
@@ -167,22 +223,60 @@ def test_market_single_stream_in_reference_band(golden, dev):
     assert inside(gm, gb) and inside(lm, lb), (gm, lm, gb, lb, got)
 
 
-def test_market_vectorised_learns_the_drift(golden, dev):
-    """C4 at its own shape (8,192 lanes, K = 8, 12,000 vector steps): a measured
-    deviation in level (late leverage ~0.06-0.13 against the
-    reference's 0.21-1.71; the single-stream control above lands in the band, so
-    the learner is not the cause), held to what does agree: the learned policy
-    follows the data's positive drift — median over three seeds of the
-    last-third leverage and evaluation growth both > 0."""
+# C4 at its own shape (8,192 lanes, K = 8, the 1M ring, 12,000 vector steps):
+# the level bound derived from the round-5 N-sweep (profiles/r05_market_sweep.jsonl,
+# DESIGN.md §5a): 12 of 13 seeds (bf16 and fp32) ended at last-third leverage
+# 0.042 .. 0.094 and growth 0.19 .. 0.49 %/step (one seed at 1.16 / 5.2).  The
+# median of three seeds must lie in [0.03, 0.15] x [0.15, 0.75]; the no-learning
+# control (K = 0: the initial policies, leverage -0.06 .. 0.15) must not.
+C4_LEV_BAND, C4_GROWTH_BAND = (0.03, 0.15), (0.15, 0.75)
+
+
+def _market_run(lanes, k, seed, updates=96000):
     import converge
 
-    got = []
-    for seed in BUILD_SEEDS:
-        recs = converge.run("market", WORKLOADS["market"][5], 8, STEPS, eval_every=EVAL_EVERY, seed=seed,
-                            log=lambda s: None)
-        got.append((_third(recs, "eval_growth_pct"), _third(recs, "lev")))
-        print(f"market vectorised seed {seed}: {got[-1]}", flush=True)
-    assert float(np.median([g for g, _ in got])) > 0.0 and float(np.median([x for _, x in got])) > 0.0, got
+    ke = k if k > 0 else 8
+    recs = converge.run("market", lanes, k, updates // ke, eval_every=max(1000 // ke, 1), n_eval=100, seed=seed,
+                        log=lambda s: None)
+    got = (_third(recs, "eval_growth_pct"), _third(recs, "lev"))
+    record("market", lanes=lanes, k=k, seed=seed, updates=updates if k > 0 else 0, growth_pct=got[0], lev=got[1])
+    print(f"market N={lanes} K={k} seed {seed}: growth {got[0]:.3f} lev {got[1]:.4f}", flush=True)
+    return got
+
+
+def test_market_vectorised_level(golden, dev):
+    got = [_market_run(8192, 8, s) for s in BUILD_SEEDS]
+    g, lv = float(np.median([x for x, _ in got])), float(np.median([y for _, y in got]))
+    assert inside(lv, C4_LEV_BAND) and inside(g, C4_GROWTH_BAND), got
+    k0 = [_market_run(8192, 0, s) for s in BUILD_SEEDS]
+    g0, l0 = float(np.median([x for x, _ in k0])), float(np.median([y for _, y in k0]))
+    assert not (inside(l0, C4_LEV_BAND) and inside(g0, C4_GROWTH_BAND)), k0
+
+
+# The reference's single-stream semantics through the vectorised path: N = 1 lane,
+# K = 1 update per vector step, 96,000 updates.  The single stream is chaotic (the
+# round-5 sweep: 19 seeds from -2.1 to the 2.97 leverage corner, about half of them
+# near it), so a median against five reference seeds cannot decide; the statistic
+# is the two-sided Mann-Whitney U test of 8 build seeds against the reference's 5,
+# on last-third leverage and growth: consistent at p >= 0.05.  The no-learning
+# control (K = 0) must be rejected (p < 0.05 on leverage).
+N1_SEEDS = tuple(range(8))
+
+
+def test_market_single_lane_consistent_with_reference(golden, dev):
+    from scipy.stats import mannwhitneyu
+
+    ref = ref_stats(golden, "market")
+    got = [_market_run(1, 1, s) for s in N1_SEEDS]
+    p_lev = mannwhitneyu([y for _, y in got], [y for _, y in ref], alternative="two-sided", method="exact").pvalue
+    p_g = mannwhitneyu([x for x, _ in got], [x for x, _ in ref], alternative="two-sided", method="exact").pvalue
+    print(f"market N=1 K=1: Mann-Whitney p lev {p_lev:.3f} growth {p_g:.3f}; build {got}; reference {ref}")
+    record("market_n1_test", p_lev=p_lev, p_growth=p_g)
+    assert p_lev >= 0.05 and p_g >= 0.05, (p_lev, p_g, got, ref)
+    k0 = [_market_run(1, 0, s) for s in N1_SEEDS]
+    p0 = mannwhitneyu([y for _, y in k0], [y for _, y in ref], alternative="two-sided", method="exact").pvalue
+    print(f"market N=1 K=0: Mann-Whitney p lev {p0:.4f}; {k0}")
+    assert p0 < 0.05, (p0, k0)
 
 
 def test_kelly_optima():

@@ -263,8 +263,10 @@ def test_nan_guard_sets_status(dev, algo):
 def test_fused_actor_statistics_use_prestep_scalars(dev, monkeypatch, loss):
     """The fused actor step runs its two critic-statistics workgroups beside the
     workgroups that write log_alpha (temperature step) and the Nagy Cauchy scales
-    in the same launch.  They read the pre-step snapshot critic_update_kernel
-    takes (LearnState::snap_*), so their statistics, the Cauchy scales (the next
+    in the same launch.  The scalars live in update-parity slots of LearnState
+    (update n reads slot (n - 1) & 1 and writes slot n & 1), so the statistics
+    read the starting values without ordering against their writers; their
+    statistics, the Cauchy scales (the next
     update's CAU / TCAU loss scale) and log alpha must match the launch chain
     (RLMD_NO_FUSED_ACTOR=1: statistics in abwd_rows' own workgroup, temperature in
     adam_kernel after it) over consecutive SAC updates with a temperature step."""

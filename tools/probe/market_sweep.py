@@ -39,8 +39,9 @@ def main():
     for lanes, k, replay, shared, prec in cases:
         for seed in seeds:
             t0 = time.perf_counter()
-            steps = updates // k
-            recs = converge.run("market", lanes, k, steps, eval_every=max(1000 // k, 1), n_eval=100, seed=seed,
+            ke = k if k > 0 else 8  # K = 0 (no learning): the C4 schedule's vector steps
+            steps = updates // ke
+            recs = converge.run("market", lanes, k, steps, eval_every=max(1000 // ke, 1), n_eval=100, seed=seed,
                                 replay=replay, log=lambda s: None, slice_groups=shared, precision=prec)
             g = np.array([r["eval_growth_pct"] for r in recs])
             lv = np.array([r["lev"] for r in recs])

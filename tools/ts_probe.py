@@ -13,7 +13,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 OUT = os.path.join(ROOT, "tools", "_probe")
-LIB = os.path.join(OUT, "librlmd_timing.so")
+LIB = os.path.join(OUT, f"librlmd_timing{os.environ.get('RLMD_TS_TAG', '')}.so")
 
 
 def build():
