@@ -351,6 +351,7 @@ struct rlmd_agent_s {
   bool fused_actor = false;  // the actor step too (actions <= 2)
   int n_cu = 256;            // compute units of the device (column-split decisions)
   int qsplit_max = 2;        // qeval_rows column split allowed (RLMD_QSPLIT=1: off)
+  int fsplit_max = 2;        // fwd_rows critic column split allowed (RLMD_FSPLIT=1: off)
   rlmd::PhaseProfiler prof;  // rlmd_profile_enable / _read
 };
 
@@ -566,6 +567,7 @@ struct Batch {
 struct PairCtl {
   const float* s2n;
   bool ready, paired;
+  int split;  // the pairing update's fwd column split: its target halves are this update's
 };
 
 int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const float* eps_b, float* stats,
@@ -595,6 +597,19 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
   const bool pair = pc && pc->s2n && !ready && !sac && ag->target_pair && ag->fused_update && eps_a == nullptr &&
                     !target_change;
   if (pc) pc->paired = pair;
+  // column split of the forward's critic streams (target critics, online critics
+  // + their U1 bases): two workgroups per (rows, job) when the grid still fits
+  // the chip in one round; the halves' partial sums meet in the critic step
+  int fsplit = 1;
+  {
+    const int ny = (actor_step ? 5 : 4) - (ready ? 2 : 0) + (pair ? 2 : 0);
+    if (ag->fused_update && ag->fsplit_max > 1 && d.H2p % 64 == 0 && 2 * ((B + 15) / 16) * ny <= ag->n_cu)
+      fsplit = 2;
+    // targets computed by the previous update's forward carry its split (the
+    // partial layout of tpartn); this update's fewer jobs fit whenever its did
+    if (ready) fsplit = pc->split;
+    if (pc) pc->split = fsplit;
+  }
 
   // ---- forward rows: target path (algo_sac.py:300-367 / algo_td3.py:302-361),
   //      critics on (s, a) (algo_sac.py:413-417), policy on s for the actor step
@@ -658,7 +673,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       f.qtn[1] = S_.tpartn[1];
       f.ctrn = (uint32_t)(cntr + 1);
     }
-    RLMD_TRY(fwd_rows_launch(f, st));
+    RLMD_TRY(fwd_rows_launch(f, st, fsplit));
   }
   // ---- critic loss (algo_sac.py:413-465)
   LossArgs loss_fused{}, loss_stats{};  // B == 0: not used
@@ -690,6 +705,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     la.log_noise = c.log_noise;
     la.grad_scale = sac ? 0.5f : 1.0f;  // SAC: 0.5 (q1_loss + q2_loss)
     la.cnt = (int32_t)cntr;
+    la.qsplit = fsplit;
     if (B > 512) {
       hipLaunchKernelGGL(critic_loss_kernel<1024>, dim3(1), dim3(1024), 0, st, la);
       RLMD_LAUNCH_CHECK();
@@ -1000,7 +1016,7 @@ int agent_learn_k(rlmd_agent_s* ag, rlmd_replay_t rb, int k, float* stats, hipSt
   RLMD_TRY(replay_sample_launch(v, M, B, k, c.seed ^ 0x5eed5eed5eedull, (uint64_t)ag->host_cntr, ag->kb_idx,
                                 ag->kb_s, ag->kb_a, ag->kb_r, ag->kb_s2, ag->kb_done, ag->kb_xsa,
                                 ms ? ag->kb_eff : nullptr, st));
-  PairCtl pc{nullptr, false, false};
+  PairCtl pc{nullptr, false, false, 1};
   for (int i = 0; i < k; ++i) {
     const size_t o = (size_t)i * B;
     const Batch mb{ag->kb_s + o * S, ag->kb_r + o, ag->kb_s2 + o * S, ag->kb_xsa + o * (S + A), ag->kb_done + o,
@@ -1148,7 +1164,7 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
     for (int g = 0; g < 2; ++g) {
       RLMD_ALLOC(s.hp1[g], e1 * ts);
       RLMD_ALLOC(s.hp2[g], e2 * ts);
-      RLMD_ALLOC(s.u1[g], e1);
+      RLMD_ALLOC(s.u1[g], 2 * e1);  // two partial halves (fwd_rows column split)
       RLMD_ALLOC(s.w3s[g], H2);
     }
     const char* tp = getenv("RLMD_TARGET_PAIR");  // default on; RLMD_TARGET_PAIR=0 turns it off
@@ -1171,6 +1187,8 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
         ag->n_cu = ncu;
       const char* qs = getenv("RLMD_QSPLIT");
       ag->qsplit_max = qs ? std::max(1, std::min(2, atoi(qs))) : 2;
+      const char* fs = getenv("RLMD_FSPLIT");
+      ag->fsplit_max = fs ? std::max(1, std::min(2, atoi(fs))) : 2;
     }
     RLMD_ALLOC(s.rank1, B);
   }
@@ -1188,11 +1206,11 @@ int rlmd_agent_create(const rlmd_agent_cfg* cfg, float* params, float* target, f
     ag->fuse_splits = fs ? std::max(1, std::min(RLMD_GRAD_SPLITS, atoi(fs))) : RLMD_GRAD_SPLITS;
   }
   for (int g = 0; g < 2; ++g) {
-    RLMD_ALLOC(s.tpart[g], B);
-    RLMD_ALLOC(s.tpartn[g], B);
+    RLMD_ALLOC(s.tpart[g], 2 * B);
+    RLMD_ALLOC(s.tpartn[g], 2 * B);
     RLMD_ALLOC(s.c1[g], B * H1);
     RLMD_ALLOC(s.c2[g], B * H2);
-    RLMD_ALLOC(s.qpart[g], B);
+    RLMD_ALLOC(s.qpart[g], 2 * B);
     RLMD_ALLOC(s.dq[g], B);
     RLMD_ALLOC(s.dc2[g], B * H2);
     RLMD_ALLOC(s.dc1[g], B * H1);

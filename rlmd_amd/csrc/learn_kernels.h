@@ -235,6 +235,9 @@ struct LossArgs {
   int32_t keep_actor_slot;  // 1: leave stats[10] (actor loss) alone
   int32_t keep_logtemp_slot;  // 1: leave stats[11] (log temperature) to the temperature step
   int32_t cnt;  // learn_step_cntr of this update: LearnState slots slot_rd(cnt) / slot_wr(cnt)
+  // fwd_rows' column split (1 or 2): qpart / tpart hold P partial sums at offsets
+  // p * B, added in half order (and the critic step's U1 slabs likewise)
+  int32_t qsplit;
 };
 
 struct CBwdArgs {
@@ -288,7 +291,7 @@ struct ABwdArgs {
 };
 
 size_t rows_lds_bytes(const RowDims& d);
-int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st);
+int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st, int split = 1);  // split: critic column halves (gridDim.z)
 int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st, int split = 1);  // split: gridDim.z column halves
 int cbwd_rows_launch(const CBwdArgs& a, hipStream_t st);
 int abwd_rows_launch(const ABwdArgs& a, hipStream_t st);

@@ -711,12 +711,13 @@ __device__ __forceinline__ void critic_const(FwdConst<NBW>& k, const RowNet& n, 
 // The backward-basis pass of one net over the block's rows: acc = aU (LDS,
 // [R][H2p]) times fc2.weight through the transposed compute copy, masked by
 // [h1 > 0] (m1s) and stored row-packed in f32 (u, [nrb][H1p][16]).
+// K-steps [ks0, ke / KS) of the contraction (a column split: this half's fc2 columns).
 template <int PREC, int NBW, bool MULTI>
 __device__ __forceinline__ void basis_pass(Pre<PREC, NBW, MULTI>& pw, const typename CT<PREC>::T* aU, int lda,
                                            const void* wt, int H1p, int H2p, const uint8_t* m1s, float* u, int row0,
-                                           int B) {
+                                           int B, int ks0 = 0, int ke = 0) {
   f32x4 acc[NBW];
-  mfma_rows<PREC, NBW, MULTI>(pw, aU, lda, wt, H2p, H2p, H1p / 16, acc);
+  mfma_rows<PREC, NBW, MULTI>(pw, aU, lda, wt, H2p, ke ? ke : H2p, H1p / 16, acc, 0, ks0);
   const int wave = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < NBW; ++i) {
@@ -753,6 +754,16 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
   const bool sac = d.algo == RLMD_SAC;
   const int H1p = pad32(d.H1), H2p = pad32(d.H2);
   const int na = sac ? 2 * d.A : d.A;
+  // column split of the critics' fc2 (gridDim.z = P <= 2, as qeval_rows): the
+  // workgroup of half p streams half of each critic's fc2 copies and writes
+  // partial q / target q / U1 at offset p, summed in half order by the critic
+  // step.  The policy (target path, job 4) is not split: its heads need every
+  // column before tanh; job 4's second half has nothing to do.
+  const int P = (int)gridDim.z, p = (int)blockIdx.z;
+  const int nbw = H2p / 16 / P, nb0 = p * nbw;              // this half's fc2 output bands
+  const int ks0 = p * (H2p / P) / CT<PREC>::KS, ke = (p + 1) * (H2p / P);  // and its basis K-steps
+  const int64_t ustr = (int64_t)((B + R - 1) / R) * H1p * R;  // one U1 slab
+  if (job == 4 && p > 0) return;
   RLMD_TSJ(40 + job);
   if (job <= 1) {  // target path (algo_sac.py:300-367 / algo_td3.py:302-361)
     RLMD_TSR(16 * job + 0);
@@ -769,8 +780,8 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     actor_const<NBW>(ka, an, a.ao, d);
     Pre<PREC, NBW, MULTI> pa, pc;
     pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
-    critic_const<NBW>(kc, cn, a.co, d);
-    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
+    critic_const<NBW>(kc, cn, a.co, d, nb0);
+    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
     const Noise2 nz = pre_nz ? noise_pre(smp, d, a.t_tag, row0) : Noise2{{0.f, 0.f}};
     RLMD_TSR(16 * job + 1);
     stage_commit(sr, s2, d.S, xs, L.ldx, row0, B);
@@ -780,15 +791,16 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
                                d.A, smem, L, nullptr, nullptr, row0, B);
     RLMD_TSR(16 * job + 3);
     sample_rows(an.p, a.ao, d, smp, xs, L.ldx, hout, 0, a.t_tag, eps_next, a.t_noise_std, a.t_noise_clip,
-                a.t_clamp, job == 0 && !nxt ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz, pre_nz);
+                a.t_clamp, job == 0 && !nxt && p == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz,
+                pre_nz);
     __syncthreads();
     RLMD_TSR(16 * job + 4);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
-                               nullptr, row0, B);
+                               nullptr, row0, B, nullptr, nullptr, nullptr, nb0, nbw);
     RLMD_TSR(16 * job + 5);
-    float* qt = nxt ? a.qtn[job] : a.qt[job];
+    float* qt = (nxt ? a.qtn[job] : a.qt[job]) + p * B;
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) qt[row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
-    if (!nxt && a.bsnap && blockIdx.x == 0 && threadIdx.x == 0) a.bsnap[2 + job] = cn.p[a.co.b3];
+    if (!nxt && a.bsnap && blockIdx.x == 0 && p == 0 && threadIdx.x == 0) a.bsnap[2 + job] = cn.p[a.co.b3];
   } else if (job <= 3) {  // online critics on (s, a) (algo_sac.py:413-417)
     if (job == 2) RLMD_TSR(60);
     const int g = job - 2;
@@ -796,33 +808,35 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     const bool upd = a.u1[0] != nullptr;
     const StageReg sr = stage_issue(a.xsa, d.X, L.ldx, row0, B);
     FwdConst<NBW> kc;
-    critic_const<NBW>(kc, cn, a.co, d);
+    critic_const<NBW>(kc, cn, a.co, d, nb0);
     Pre<PREC, NBW, MULTI> pc, pw;
-    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, H2p / 16);
-    if (upd) pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, H2p, H1p / 16);
+    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
+    if (upd) pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
     stage_commit(sr, a.xsa, d.X, xs, L.ldx, row0, B);
     __syncthreads();
     if (job == 2) RLMD_TSR(61);
     if (!upd) {
       mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, a.c1[g],
-                                 a.c2[g], row0, B, a.cm1[g], a.cm2[g]);
+                                 a.c2[g], row0, B, a.cm1[g], a.cm2[g], nullptr, nb0, nbw);
     } else {
       using T = typename CT<PREC>::T;
       T* aU = reinterpret_cast<T*>(smem + L.aU);
       uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + L.m1s);
-      const FwdExtra<PREC> ex{static_cast<T*>(a.hp1[g]), static_cast<T*>(a.hp2[g]), m1s, aU};
+      // h1 is the same in both halves: half 0 writes it
+      const FwdExtra<PREC> ex{p == 0 ? static_cast<T*>(a.hp1[g]) : nullptr, static_cast<T*>(a.hp2[g]), m1s, aU};
       mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
-                                 nullptr, row0, B, nullptr, a.cm2[g], &ex);
+                                 nullptr, row0, B, nullptr, a.cm2[g], &ex, nb0, nbw);
       // the backward basis of these rows: U1 = [h1 > 0] * (([h2 > 0] w3) W2), so
-      // that the critic update forms dh1 = dq * U1 once dq is known (update.hip)
-      basis_pass<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H1p, H2p, m1s, a.u1[g], row0, B);
-      if (blockIdx.x == 0) {  // snapshots of what the update reads while stepping it
+      // that the critic update forms dh1 = dq * U1 once dq is known (update.hip);
+      // a half's partial U1 over its fc2 columns
+      basis_pass<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H1p, H2p, m1s, a.u1[g] + p * ustr, row0, B, ks0, ke);
+      if (blockIdx.x == 0 && p == 0) {  // snapshots of what the update reads while stepping it
         for (int c = threadIdx.x; c < d.H2; c += NT) a.w3s[g][c] = cn.p[a.co.w3 + c];
         if (threadIdx.x == 0) a.bsnap[g] = cn.p[a.co.b3];
       }
     }
     if (job == 2) RLMD_TSR(62);
-    if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
+    if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) a.q[g][p * B + row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];
   } else {  // policy on s for the actor update (algo_sac.py:524-535 / algo_td3.py:507-515)
     RLMD_TSR(80);
     const RowNet& an = a.actor;
@@ -1548,10 +1562,12 @@ extern "C" int rlmd_debug_ts_rows(unsigned long long* out) {
 
 namespace rlmd {
 
-int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st) {
+int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st, int split) {
   RLMD_CHECK(a.y0 == 0 || a.y0 == 2, "fwd_rows: y0 is 0 or 2");
   RLMD_CHECK(a.npair == 0 || (a.y0 == 0 && a.s2n && a.qtn[0] && a.qtn[1]), "fwd_rows: target pairing buffers");
-  return launch_rows(a.d, 0, &a, (a.with_actor ? 5 : 4) - a.y0 + 2 * a.npair, st);
+  RLMD_CHECK(split == 1 || (split == 2 && a.u1[0] && a.d.H2p % 64 == 0),
+             "fwd_rows: a column split needs the fused critic path and H2p a multiple of 64");
+  return launch_rows(a.d, 0, &a, (a.with_actor ? 5 : 4) - a.y0 + 2 * a.npair, st, 0, split);
 }
 int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st, int split) {
   RLMD_CHECK(a.nq == nq && (a.nab == 0 || (a.ua && a.wheads && a.am1 && a.am2)), "qeval_rows: head jobs need their buffers");

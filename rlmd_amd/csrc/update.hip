@@ -334,7 +334,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   //     column over its 32 rows
   float* xs = reinterpret_cast<float*>(smem + ULds::xs);
   float xv[8];
-  f32x4 u1v[8];
+  f32x4 u1v[8], u1w[8];  // U1, and its second partial half (fwd_rows column split)
   {
     const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.x, (int64_t)B * X * 4);
 #pragma unroll
@@ -343,13 +343,17 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       xv[q] = rlmd_ldf(rx, (int64_t)r * X + c, w1blk && r < B && c < X);
     }
     const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
-    const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.u1[g], (int64_t)nrb * H1p * 16 * 4);
+    const bool us = a.loss.qsplit > 1;
+    const int64_t ustr = (int64_t)nrb * H1p * 16;
+    const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.u1[g], ustr * (us ? 2 : 1) * 4);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const int r = 32 * p + 4 * q;
+      const bool ok = w1blk && r < nrb * 16 && j < H1p;
       u1v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             ru, (w1blk && r < nrb * 16 && j < H1p) ? (int)(rp_idx(r, H1p, j) * 4)
-                                                                                        : 0x7fffffff, 0, 0));
+                                             ru, ok ? (int)(rp_idx(r, H1p, j) * 4) : 0x7fffffff, 0, 0));
+      u1w[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             ru, (ok && us) ? (int)((ustr + rp_idx(r, H1p, j)) * 4) : 0x7fffffff, 0, 0));
     }
   }
 
@@ -482,7 +486,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int r = 32 * p + 4 * q + e;
-        const float du = dqs[r] * u[q][e];
+        const float du = dqs[r] * (u[q][e] + u1w[q][e]);  // halves in order (u1w = 0 unsplit)
         acc[8] += du;
 #pragma unroll
         for (int c = 0; c < 8; ++c) acc[c] = fmaf(du, xs[r * 8 + c], acc[c]);
