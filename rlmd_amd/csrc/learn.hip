@@ -837,8 +837,9 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
     // grid still fits the chip in one round
     int qsplit = 1;
     if (ag->fused_actor && ag->qsplit_max > 1 && d.H2p % 64 == 0 &&
-        2 * ((B + 15) / 16) * (nq + qe.nab) <= ag->n_cu)
+        ((B + 15) / 16) * (2 * nq + qe.nab) <= ag->n_cu)
       qsplit = 2;
+    qe.split = qsplit;
     RLMD_TRY(qeval_rows_launch(qe, nq, st, qsplit));
     if (ag->fused_actor) {
       // the actor (+ temperature) step in one launch (update.hip)

@@ -206,6 +206,7 @@ struct QEvalArgs {
   const uint8_t* am2;
   float* ua;
   float* wheads;
+  int32_t split;  // column split of the critic jobs (1 or 2): grid y = nq * split + nab
 };
 
 // Critic data-gradients: y = g.  dh2 = dq w3 * [h2 > 0], dh1 = (dh2 W2) * [h1 > 0].

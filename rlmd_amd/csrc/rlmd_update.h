@@ -53,8 +53,8 @@ struct ActUpdArgs {
   AdamArgs adam;           // the actor (+ temperature when adam.temp)
   LossArgs cstats;         // critic statistics workgroup (B == 0: none)
   int32_t ti, tj, n_w2, n_w1;
-  // qeval_rows' column split (1 or 2): q, dq/da and the bases arrive as P partial
-  // sums, at offsets p * B (q), p * B * A (dq/da) and p * nh (bases)
+  // qeval_rows' column split (1 or 2): q and dq/da arrive as P partial sums, at
+  // offsets p * B (q) and p * B * A (dq/da)
   int32_t qsplit;
 };
 

@@ -927,13 +927,18 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   const Lds L = lds_layout(d);
   float* xs = reinterpret_cast<float*>(smem + L.xs);
   const float* hout = reinterpret_cast<const float*>(smem + L.hout);
-  const int row0 = blockIdx.x * R, g = blockIdx.y, B = d.B;
+  const int row0 = blockIdx.x * R, B = d.B;
   const int H1p = pad32(d.H1), H2p = pad32(d.H2);
-  // column split (gridDim.z = P halves of the fc2 output columns, P <= 2): the
-  // workgroup of half p streams half of each fc2 copy — the per-workgroup weight
-  // stream is this kernel's cost — and writes partial q, dq/da and bases at
-  // offset p, which the actor step sums in half order
-  const int P = (int)gridDim.z, p = (int)blockIdx.z;
+  // column split (a.split = P halves of the fc2 output columns, P <= 2): the
+  // critic workgroup of half p streams half of each fc2 copy — the per-workgroup
+  // weight stream is this kernel's cost — and writes partial q and dq/da at
+  // offset p, which the actor step sums in half order.  The head jobs' stream
+  // (the policy's transposed copy) is one copy already, no more than a critic
+  // half's two: they are not split (their second half returns at once), so the
+  // actor step reads one basis per head.  Grid y: critic g half p at g * P + p,
+  // then the head jobs.
+  const int P = a.split > 1 ? 2 : 1, y = (int)blockIdx.y;
+  const int g = y < a.nq * P ? y / P : y - a.nq * P + a.nq, p = y < a.nq * P ? y % P : 0;
   const int kh = H2p / P, ks0 = p * kh / CT<PREC>::KS, ke = (p + 1) * kh;  // this half's fc2 columns as K-steps
   if (g >= a.nq) {
     // the policy's backward basis of head h over the block's rows (fused actor
@@ -943,13 +948,13 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     const int h = g - a.nq, nrb = (B + R - 1) / R;
     const RowNet& an = a.actor;
     Pre<PREC, NBW, MULTI> pw;
-    pre_issue<PREC, NBW, MULTI>(pw, an.wt, H2p, ke, H1p / 16, 0, ks0);
+    pre_issue<PREC, NBW, MULTI>(pw, an.wt, H2p, H2p, H1p / 16);
     BwdMask<NBW> k;
     bwd_mask<NBW>(k, a.am1, a.am2, nullptr, a.ao, row0, B);
     const ElemMap m = elem_map(H2p);
     const int64_t wrow = h < d.A ? a.ao.w3 + (int64_t)h * d.H2 : a.ao.w4 + (int64_t)(h - d.A) * d.H2;
     const float wk = rlmd_ldf(rlmd_rsrc(an.p, a.ao.size * 4), wrow + m.c, m.c < d.H2);
-    if (blockIdx.x == 0 && p == 0 && m.r0 == 0 && m.c < d.H2) a.wheads[(int64_t)h * d.H2 + m.c] = wk;
+    if (blockIdx.x == 0 && m.r0 == 0 && m.c < d.H2) a.wheads[(int64_t)h * d.H2 + m.c] = wk;
     T* aU = reinterpret_cast<T*>(smem + L.aU);
 #pragma unroll
     for (int rr = 0; rr < kMR<NBW>; ++rr) {
@@ -958,8 +963,8 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     }
     __syncthreads();
     f32x4 acc[NBW];
-    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, an.wt, H2p, ke, H1p / 16, acc, 0, ks0);
-    float* u = a.ua + (int64_t)(p * a.nab + h) * nrb * H1p * R;
+    mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, an.wt, H2p, H2p, H1p / 16, acc);
+    float* u = a.ua + (int64_t)h * nrb * H1p * R;
     const int wave = threadIdx.x >> 6;
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
@@ -1571,9 +1576,9 @@ int fwd_rows_launch(const FwdRowsArgs& a, hipStream_t st, int split) {
 }
 int qeval_rows_launch(const QEvalArgs& a, int nq, hipStream_t st, int split) {
   RLMD_CHECK(a.nq == nq && (a.nab == 0 || (a.ua && a.wheads && a.am1 && a.am2)), "qeval_rows: head jobs need their buffers");
-  RLMD_CHECK(split == 1 || (split == 2 && a.dqda[0] && a.d.H2p % 64 == 0),
+  RLMD_CHECK(a.split == split && (split == 1 || (split == 2 && a.dqda[0] && a.d.H2p % 64 == 0)),
              "qeval_rows: a column split needs the fused actor path and H2p a multiple of 64");
-  return launch_rows(a.d, 1, &a, nq + a.nab, st, 0, split);
+  return launch_rows(a.d, 1, &a, nq * split + a.nab, st);
 }
 // cbwd: dh1 columns in halves when each half is a whole number of column blocks
 // per wave (the per-workgroup W2^T stream is the kernel's cost)

@@ -689,11 +689,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   constexpr int kUP = 2;  // bases prefetched per fc1-block thread (the rest load in the loop)
   f32x4 uv[kUP][8];
   const int64_t ustride = (int64_t)nrb * H1p * 16;
-  const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * QP * 4);
-  // bases in summation order hv = h * QP + half: U_h = sum over the halves, each
-  // half's term added with the head's gradient (layout [half][head])
-  const int nhv = nh * QP;
-  auto uoff = [&](int hv) { return (int64_t)((hv % QP) * nh + hv / QP) * ustride; };
+  const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * 4);
   {
     const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
     const float log_alpha = sac ? st->log_alpha[slot_rd(a.adam.cnt)] : 0.f;
@@ -725,9 +721,9 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const int r = 32 * p + 4 * q;
-          const bool ok = w1blk && h < nhv && r < nrb * 16 && j < H1p;
+          const bool ok = w1blk && h < nh && r < nrb * 16 && j < H1p;
           uv[h][q] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((uoff(h) + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
                                                            0, 0));
         }
     }
@@ -927,27 +923,24 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
       const int r = 32 * p + 4 * q;
       du[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int h = 0; h < kUP; ++h) {
-        const int hg = h / QP;  // this term's head
+      for (int h = 0; h < kUP; ++h)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(r + e) * kHM + hg], uv[h][q][e], du[q][e]);
-      }
+        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(r + e) * kHM + h], uv[h][q][e], du[q][e]);
     }
-    for (int hv = kUP; hv < nhv; ++hv) {
+    for (int h = kUP; h < nh; ++h) {
       f32x4 u[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int r = 32 * p + 4 * q;
         const bool ok = r < nrb * 16 && j < H1p;
         u[q] = __builtin_bit_cast(
-            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((uoff(hv) + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
                                                          0, 0));
       }
-      const int hg = hv / QP;
 #pragma unroll
       for (int q = 0; q < 8; ++q)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(32 * p + 4 * q + e) * kHM + hg], u[q][e], du[q][e]);
+        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(32 * p + 4 * q + e) * kHM + h], u[q][e], du[q][e]);
     }
     float acc[9];
 #pragma unroll
