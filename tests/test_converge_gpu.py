@@ -74,6 +74,17 @@ WORKLOADS = {
     # of 250 test days per evaluation; the build at C4's 8,192 lanes
     "market": ("market", "SAC", "MSE", "converge_ref_21_e20", 1, 8192, 100000),
 }
+# C4's band test runs at a stated vectorised shape: 8,192 lanes on ONE shared
+# market-slice stream (VecTrainer slice_groups=1: every lane trades the same
+# shuffled price path, the reference's single-stream data regime, vectorised over
+# the lanes' policy noise), K = 8, the median of 8 seeds.  The round-5 N-sweep
+# (profiles/r05_market_sweep.jsonl) pins the cause of the level
+# deviation at C4's own shape (independent slices per lane) to that one change:
+# shared slices give Mann-Whitney p = 0.28 / 0.44 against the reference seeds,
+# independent ones 0.019 / 0.008.  The independent-slice shape keeps its own
+# level test below.
+WORKLOAD_KW = {"market": dict(slice_groups=1)}
+WORKLOAD_SEEDS = {"market": tuple(range(8))}
 ONE_SIDED = {"gbm", "gbm_td3_n5"}  # GBM_InvA: monotone growth up to the leverage corner
 # TD3 n = 5 on GBM_InvA splits into two modes in the reference (three seeds near the
 # corner, one at 0.16, one diverged to -3.6) and in the build: the check is per mode
@@ -118,18 +129,23 @@ def record(workload, **kw):
             f.write(json.dumps({"workload": workload, **kw}) + "\n")
 
 
-def build_medians(workload, k, precision="bf16", seeds=BUILD_SEEDS):
+def build_medians(workload, k, precision="bf16", seeds=None):
     import converge
 
     env, algo, loss, _, ms, lanes, _ = WORKLOADS[workload]
+    seeds = seeds or WORKLOAD_SEEDS.get(workload, BUILD_SEEDS)
+    kw = WORKLOAD_KW.get(workload, {})
+    ee = EVAL_EVERY
+    if env == "market":  # the reference's evaluations: every 1e3 updates, 100 episodes of 250 test days
+        kw, ee = dict(kw, n_eval=100), 1000 // 8
     got = []
     for seed in seeds:
-        recs = converge.run(env, lanes, k, STEPS, precision=precision, eval_every=EVAL_EVERY, seed=seed, algo=algo,
-                            loss=loss, log=lambda s: None, multi_steps=ms)
+        recs = converge.run(env, lanes, k, STEPS, precision=precision, eval_every=ee, seed=seed, algo=algo,
+                            loss=loss, log=lambda s: None, multi_steps=ms, **kw)
         assert all(math.isfinite(r["eval_growth_pct"]) and r["nan_flag"] == 0 for r in recs)
         got.append((_third(recs, "eval_growth_pct"), _third(recs, "lev")))
         record(workload, k=k, precision=precision, seed=seed, lanes=lanes, updates=STEPS * k,
-               growth_pct=got[-1][0], lev=got[-1][1])
+               growth_pct=got[-1][0], lev=got[-1][1], **{k2: v for k2, v in kw.items() if k2 == "slice_groups"})
         print(f"{workload} K={k} {precision} seed {seed}: growth {got[-1][0]:.3f} lev {got[-1][1]:.4f}", flush=True)
     return float(np.median([g for g, _ in got])), float(np.median([lv for _, lv in got])), got
 
@@ -148,7 +164,7 @@ UNINFORMATIVE = {"dice"}
 
 @pytest.mark.parametrize("workload,precision", [("dice_sh", "bf16"), ("dice_sh", "fp32"), ("gbm", "bf16"),
                                                 ("dice_sh_a_mse", "bf16"), ("dice_sh_a_hub", "bf16"),
-                                                ("coin", "bf16"), ("dice", "bf16")])
+                                                ("coin", "bf16"), ("dice", "bf16"), ("market", "bf16")])
 def test_build_median_in_reference_band(golden, dev, workload, precision):
     gb, lb = bands(golden, workload)
     g, lv, seeds = build_medians(workload, 8, precision)
@@ -190,7 +206,7 @@ def test_c5_upper_mode_frequency(golden, dev):
     assert n_up >= 1, seeds
 
 
-@pytest.mark.parametrize("workload", ["dice_sh", "dice_sh_a_mse", "gbm", "gbm_td3_n5", "coin"])
+@pytest.mark.parametrize("workload", ["dice_sh", "dice_sh_a_mse", "gbm", "gbm_td3_n5", "coin", "market"])
 def test_no_learning_fails_the_band(golden, dev, workload):
     """K = 0: the policy keeps its initial weights; the harness must reject it."""
     gb, lb = bands(golden, workload)
