@@ -241,10 +241,10 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
   const int64_t a_cols = MODE == rlmd::GEMM_BWD_W ? s.M : s.K;
   const int64_t b_rows = MODE == rlmd::GEMM_FWD ? s.N : s.K;
   const int64_t b_cols = MODE == rlmd::GEMM_FWD ? s.K : s.N;
-  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)p.A, (short)0, (int)(((a_rows - 1) * p.lda + a_cols) * 4), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)p.B, (short)0, (int)(((b_rows - 1) * p.ldb + b_cols) * 4), 0x00020000);
+  const __amdgpu_buffer_rsrc_t ra = rlmd_rsrc_wave(
+      (void*)p.A, (int)(((a_rows - 1) * p.lda + a_cols) * 4));
+  const __amdgpu_buffer_rsrc_t rb = rlmd_rsrc_wave(
+      (void*)p.B, (int)(((b_rows - 1) * p.ldb + b_cols) * 4));
   // K-steps in flight: D register stages.  One: every split-K workgroup has a
   // single K-step at B <= 512, and a deeper ring (4: a fused tile's whole
   // reduction at once) doubles the VGPRs and halves the resident waves.
@@ -375,8 +375,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
         return;
       }
       // one uniform resource over the tile's slabs; the lane offset in voffset
-      const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
-          batch.slabs + (int64_t)tg * ns * 256, (short)0, ns * 256 * 16, 0x00020000);
+      const __amdgpu_buffer_rsrc_t rsl = rlmd_rsrc_wave(
+          batch.slabs + (int64_t)tg * ns * 256, ns * 256 * 16);
       const int lo = (int)threadIdx.x * 16;
       __builtin_amdgcn_raw_buffer_store_b128(
           __builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, tot[0][0]), rsl, lo + sp0 * 4096, 0, kSC1);
@@ -411,10 +411,9 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
   // C/D map (16x16 MFMA, every dtype): col = lane & 15, row = 4*(lane >> 4) + reg
   __amdgpu_buffer_rsrc_t rx = ra;
   if (MODE == rlmd::GEMM_FWD && p.bias)
-    rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.bias, (short)0, s.N * 4, 0x00020000);
+    rx = rlmd_rsrc_wave((void*)p.bias, s.N * 4);
   if (MODE == rlmd::GEMM_BWD_X && p.mask)
-    rx = __builtin_amdgcn_make_buffer_rsrc((void*)p.mask, (short)0,
-                                           (int)(((int64_t)(s.M - 1) * p.ldm + s.N) * 4), 0x00020000);
+    rx = rlmd_rsrc_wave((void*)p.mask, (int)(((int64_t)(s.M - 1) * p.ldm + s.N) * 4));
   float out[MB][MB][4];
 #pragma unroll
   for (int mi = 0; mi < MB; ++mi)
@@ -430,7 +429,7 @@ __global__ void __launch_bounds__(256) gemm_kernel(rlmd::GemmBatch batch) {
     if (p.head_w) {  // fused q head: per-row partial over this tile's 32 columns
       __shared__ float hp[2][32];
       const int j = j0 + col0 + (lane & 15);
-      const float w = buf_load(__builtin_amdgcn_make_buffer_rsrc((void*)p.head_w, (short)0, s.N * 4, 0x00020000),
+      const float w = buf_load(rlmd_rsrc_wave((void*)p.head_w, s.N * 4),
                                j < s.N ? j * 4 : kOutOfRange);
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {

@@ -73,13 +73,13 @@ __device__ __forceinline__ AdamIn adam_load(const AdamArgs& a, int i, bool polya
   const int n4 = (int)(a.n * 4), off = i >= 0 ? i * 4 : 0x7fffffff;
   AdamIn o;
   o.m = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                     __builtin_amdgcn_make_buffer_rsrc(a.m, (short)0, n4, 0x00020000), off, 0, 0));
+                                     rlmd_rsrc_wave(a.m, n4), off, 0, 0));
   o.v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                     __builtin_amdgcn_make_buffer_rsrc(a.v, (short)0, n4, 0x00020000), off, 0, 0));
+                                     rlmd_rsrc_wave(a.v, n4), off, 0, 0));
   o.p = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                     __builtin_amdgcn_make_buffer_rsrc(a.p, (short)0, n4, 0x00020000), off, 0, 0));
+                                     rlmd_rsrc_wave(a.p, n4), off, 0, 0));
   o.t = polyak ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                               __builtin_amdgcn_make_buffer_rsrc(a.target, (short)0, n4, 0x00020000),
+                                               rlmd_rsrc_wave(a.target, n4),
                                                off, 0, 0))
                : 0.f;
   return o;

@@ -117,9 +117,24 @@ __device__ __forceinline__ uint64_t rlmd_shfl_xor_u64(uint64_t v, int m) {
 // Range-checked buffer loads: an element load is always issued (no exec-masked
 // branch, whose s_waitcnt vmcnt(0) would serialise a run of conditional loads);
 // ok == false turns the byte offset out of range and the hardware returns 0.
+//
+// A buffer resource must sit in scalar registers.  Every resource here is
+// wave-uniform by construction (workgroup / job / wave pointers and sizes), but
+// where the compiler cannot prove it — a size chosen by a select it placed on the
+// VALU, a pointer picked by the wave index — it wraps each load in a
+// readfirstlane "waterfall" loop (one trip per distinct value, a dependent round
+// of scalar moves, compares and exec branches around every single load).  The
+// explicit readfirstlane below states the uniformity; on values already in
+// scalar registers it folds to a move.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rlmd_rsrc_wave(const void* base, int bytes) {
+  const uint64_t b = (uint64_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rlmd_rsrc(const void* base, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0,
-                                           (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff), 0x00020000);
+  return rlmd_rsrc_wave(base, (int)(bytes < 0x7fffffff ? bytes : 0x7fffffff));
 }
 __device__ __forceinline__ float rlmd_ldf(__amdgpu_buffer_rsrc_t r, int64_t idx, bool ok) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, ok ? (int)(idx * 4) : 0x7fffffff, 0, 0));

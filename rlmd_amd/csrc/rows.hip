@@ -354,7 +354,7 @@ __device__ __forceinline__ void store_rp_rows(typename CT<PREC>::T* base, int64_
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
   constexpr int TS = sizeof(typename CT<PREC>::T);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rs = rlmd_rsrc_wave(base, 0x7fffffff);
   const int off = (int)(idx * TS);
   uint32_t w[(MR * TS + 3) / 4];
   if constexpr (PREC == RLMD_BF16) {

@@ -120,7 +120,7 @@ __device__ __forceinline__ void tile_copies(const float* pcl, const CopyDst& cd,
 #pragma unroll
       for (int q = 0; q < 4; ++q) w[q] = __float_as_uint(v[q]);
     }
-    __builtin_amdgcn_raw_buffer_store_b128(w, __builtin_amdgcn_make_buffer_rsrc(dst, (short)0, 0x7fffffff, 0x00020000),
+    __builtin_amdgcn_raw_buffer_store_b128(w, rlmd_rsrc_wave(dst, 0x7fffffff),
                                            (int)(at * (BF ? 2 : 4)), 0, RLMD_WT_AUX);
   }
 }
