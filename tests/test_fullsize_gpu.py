@@ -61,10 +61,11 @@ def test_c5_full_ring_multistep_gathers(dev):
     N, T, n, cap = 65536, 250, 5, 1 << 24
 
     def make():
-        return VecTrainer("gbm", "A", N, algo="TD3", k_updates=0, replay_capacity=cap, seed=7, warmup_steps=0,
-                          smoothing_window=0, precision="bf16", device=dev, multi_steps=n, dynamics="A")
+        return VecTrainer("gbm", "A", N, algo="TD3", k_updates=0, replay_capacity=cap, seed=7, init_seed=7,
+                          warmup_steps=0, smoothing_window=0, precision="bf16", device=dev, multi_steps=n,
+                          dynamics="A")
 
-    # the run is deterministic (seeded Philox, no updates): a first pass finds the
+    # the run is deterministic (seeded Philox and initial parameters, no updates): a first pass finds the
     # lanes whose episodes end (rare: |action| < 1e-5 / lev_factor), so that the
     # tracked lanes include episode boundaries inside the n-step histories
     tr = make()
