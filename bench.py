@@ -417,7 +417,7 @@ def main():
     ap.add_argument("--no-companion", action="store_true", help="skip the fp32 companion measurement")
     ap.add_argument("--seeds-per-gpu", default=None,
                     help="independent seeds per GPU timed after the headline (SeedGroup: one stream per seed); "
-                         "default '2,4' (C4: '2,4,8'); '' = off")
+                         "default '2,3,4' (C2, C4), '2,4' otherwise; '' = off")
     ap.add_argument("--variants", default=None,
                     help="BASELINE config variants timed after the headline, one trainer each: C3 the critic losses "
                          "(default 'MSE,HUB,MAE,HSC'), C5 the multi-step n (default '3,5,7'); '' = off")
@@ -552,7 +552,7 @@ def main():
     tr.step(K)
     # several independent seeds per GPU (§8e "GPU g runs seeds {g, g+G, ...}"):
     # T whole trainers on T streams, the per-GPU throughput of a trial sweep
-    seeds_spec = args.seeds_per_gpu if args.seeds_per_gpu is not None else ("2,4,8" if args.config == "c4" else "2,4")
+    seeds_spec = args.seeds_per_gpu if args.seeds_per_gpu is not None else ("2,3,4" if args.config in ("c2", "c4") else "2,4")
     per_gpu = {}
     if world == 1:
         from rlmd_amd.trainer import SeedGroup

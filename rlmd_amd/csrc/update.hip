@@ -37,7 +37,21 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int NT = 512;
-constexpr int TW = 32;  // tile edge (fc2.weight tiles TW x TW, fc1 blocks of TW rows)
+constexpr int TW = 32;
+// timing ablations (experiment builds only, RLMD_EXTRA_FLAGS=-DRLMD_ABL=<bits>; the
+// results are wrong): 1 no ranking (rank = row), 2 no optimiser step / copies
+#ifndef RLMD_ABL
+#define RLMD_ABL 0
+#endif
+template <int NW>
+__device__ __forceinline__ void upd_rank(uint64_t key, uint64_t* runs, int* out) {
+  if constexpr ((RLMD_ABL & 1) != 0) {
+    out[threadIdx.x] = (int)threadIdx.x;
+    __syncthreads();
+  } else {
+    block_rank<NW>(key, runs, out);
+  }
+}  // tile edge (fc2.weight tiles TW x TW, fc1 blocks of TW rows)
 
 #ifdef RLMD_TIMING
 // experiment builds only (tools/ts_probe.py upd): thread-0 s_memtime stamps of
@@ -244,7 +258,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   // Adam on an element of this critic (fc2.weight elements also refresh the copies)
   auto step = [&](int pi, float gv, const AdamIn& in) {
     const int j = pi - (int)pbase - (int)co.w2;
-    adam_apply_dst(a.adam, pi, gv, in, polyak, (j >= 0 && j < H1 * H2) ? j : -1, cd);
+    if (!(RLMD_ABL & 2)) adam_apply_dst(a.adam, pi, gv, in, polyak, (j >= 0 && j < H1 * H2) ? j : -1, cd);
   };
   const int bx = blockIdx.x, pb = a.n_w2 + a.n_w1 + a.ti;
   const int ts_slot = bx == 0 ? 0 : bx == 1 ? 1 : bx == a.n_w2 ? 2 : bx == a.n_w2 + a.n_w1 ? 3 : bx == pb ? 4
@@ -369,7 +383,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     bool sel = o.in;
     if (B > a.loss.k) {
       int* rank_of = reinterpret_cast<int*>(smem + ULds::rank);
-      block_rank<NT / 64>(critic_sel_key(o), reinterpret_cast<uint64_t*>(smem + ULds::runs), rank_of);
+      upd_rank<NT / 64>(critic_sel_key(o), reinterpret_cast<uint64_t*>(smem + ULds::runs), rank_of);
       sel = o.in && rank_of[tid] < kk;
       if (blockIdx.x == 0 && a.rank_out && o.in) a.rank_out[tid] = rank_of[tid];  // for the statistics
     }
@@ -419,7 +433,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 #pragma unroll
         for (int w = 0; w < 8 / NH; ++w) gs += part[(hf * (8 / NH) + w) * 1024 + el];
         float pn = 0.f, tn = 0.f;  // padding elements: zero in the copies
-        if (pidx[hf][e] >= 0) adam_core(a.adam, pidx[hf][e], gs, ain[hf][e], polyak, pn, tn);
+        if (pidx[hf][e] >= 0 && !(RLMD_ABL & 2)) adam_core(a.adam, pidx[hf][e], gs, ain[hf][e], polyak, pn, tn);
         float* ph = pcl + hf * 2 * 32 * 33;
         ph[ii * 33 + jj] = pn;
         ph[32 * 33 + ii * 33 + jj] = tn;
@@ -428,7 +442,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
 #pragma unroll
     for (int hf = 0; hf < NH; ++hf)
       if (j0 + 32 * hf < H1p)  // WIDE: the last tile's second half may lie past the padded width
-        tile_copies<PREC>(pcl + hf * 2 * 32 * 33, cd, polyak && cd.twc, i0, j0 + 32 * hf, H1p, H2p);
+        if (!(RLMD_ABL & 2)) tile_copies<PREC>(pcl + hf * 2 * 32 * 33, cd, polyak && cd.twc, i0, j0 + 32 * hf, H1p, H2p);
     RLMD_TSU(5);
   } else if (first_col) {
     {
@@ -586,7 +600,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const CopyDst cd = copy_dst(a.adam, 0);
   auto step = [&](int pi, float gv, const AdamIn& in) {
     const int j = pi - (int)ao.w2;
-    adam_apply_dst(a.adam, pi, gv, in, polyak, (j >= 0 && j < H1 * H2) ? j : -1, cd);
+    if (!(RLMD_ABL & 2)) adam_apply_dst(a.adam, pi, gv, in, polyak, (j >= 0 && j < H1 * H2) ? j : -1, cd);
   };
   float v = 0.f, lpv = 0.f, alpha = 0.f;
   bool sel = false;
@@ -702,7 +716,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     sel = in;
     if (a.topk) {
       int* rank_of = reinterpret_cast<int*>(smem + ALds::rank);
-      block_rank<NT / 64>(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
+      upd_rank<NT / 64>(in ? ((uint64_t)(sac ? ~f2key(v) : f2key(v)) << 32) | (uint32_t)tid : ~0ull,
                  reinterpret_cast<uint64_t*>(smem + ALds::runs), rank_of);
       sel = in && rank_of[tid] < kk;
     }
@@ -846,12 +860,12 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
 #pragma unroll
       for (int w = 0; w < 8; ++w) gs += part[w * 1024 + el];
       float pn = 0.f, tn = 0.f;
-      if (pidx[e] >= 0) adam_core(a.adam, pidx[e], gs, ain[e], polyak, pn, tn);
+      if (pidx[e] >= 0 && !(RLMD_ABL & 2)) adam_core(a.adam, pidx[e], gs, ain[e], polyak, pn, tn);
       pcl[ii * 33 + jj] = pn;
       pcl[32 * 33 + ii * 33 + jj] = tn;
     }
     __syncthreads();
-    tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
+    if (!(RLMD_ABL & 2)) tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
     RLMD_TSA(6);
   } else if (first_col) {
     {
