@@ -282,7 +282,7 @@ def test_market_single_stream_in_reference_band(golden, dev):
 # the level bound derived from the round-5 N-sweep (profiles/r05_market_sweep.jsonl,
 # DESIGN.md §5a): 12 of 13 seeds (bf16 and fp32) ended at last-third leverage
 # 0.042 .. 0.094 and growth 0.19 .. 0.49 %/step (one seed at 1.16 / 5.2).  The
-# median of three seeds must lie in [0.03, 0.15] x [0.15, 0.75]; the no-learning
+# median of the five build seeds must lie in [0.03, 0.15] x [0.15, 0.75]; the no-learning
 # control (K = 0: the initial policies, leverage -0.06 .. 0.15) must not.
 C4_LEV_BAND, C4_GROWTH_BAND = (0.03, 0.15), (0.15, 0.75)
 
