@@ -395,7 +395,9 @@ int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
  * begin / end to phase 0.
  * enable(1) resets the counters and records every phase; enable(2) records
  * only phase 1 (events attached to the env kernel's dispatch, no markers on the
- * stream); enable(0) stops.  read() synchronises and returns the summed
+ * stream); enable(3) records kernel-attached pairs only: phase 1 as in (2)
+ * and, in unfused train steps, phase 0 as the acting kernel's own dispatch (no
+ * markers); enable(0) stops.  read() synchronises and returns the summed
  * milliseconds and the number of timed launches per phase. */
 int rlmd_profile_enable(rlmd_agent_t ag, int32_t on);
 int rlmd_profile_read(rlmd_agent_t ag, double* ms_out3, int64_t* count_out3);
@@ -404,6 +406,13 @@ int rlmd_profile_read(rlmd_agent_t ag, double* ms_out3, int64_t* count_out3);
  * region is sampled rather than stamped on every step.  Counting restarts at
  * rlmd_profile_enable. */
 int rlmd_profile_stride(rlmd_agent_t ag, int32_t stride);
+/* The compute units this agent's launches may count on (default: the device's).
+ * The learner splits a critic's layer-2 columns over two workgroups only while
+ * the doubled grid still fits that many CUs (one 512-thread workgroup per CU);
+ * several trainers sharing a GPU (SeedGroup) each get a share, so the split is
+ * not taken where the trainers' grids would queue behind each other.  It changes
+ * f32 summation order, so runs compared bit for bit must use the same budget. */
+int rlmd_agent_set_cu_budget(rlmd_agent_t ag, int32_t n_cu);
 
 /* ------------------------------------------------------------- test hooks */
 /* Copy ring rows (start + i) % capacity, i < n, into caller buffers (nullable). */

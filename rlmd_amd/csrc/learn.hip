@@ -264,6 +264,11 @@ struct PhaseProfiler {
   }
   bool enabled = false;
   int mask = 7;  // phases recorded: bit p = phase p (rlmd_profile_enable: 1 all, 2 the env kernel's only)
+  // rlmd_profile_enable(3): kernel-attached pairs only — the env kernel's dispatch
+  // (phase 1) and, in unfused train steps, the acting kernel's own dispatch (phase
+  // 0) instead of markers around acting: the in-step acting-only reference of the
+  // fused kernel's marginal (same cache state as act_env_kernel, after K updates)
+  bool kernel_pairs = false;
   std::vector<hipEvent_t> ev[3][2];  // phase x {start, stop}: 0 act, 1 env, 2 learn
   size_t used[3] = {0, 0, 0};
   // sampling (rlmd_profile_stride): only every stride-th occurrence of a phase is
@@ -349,7 +354,8 @@ struct rlmd_agent_s {
   bool fused_update = false;
   bool target_pair = true;  // TD3: next update's target path in this update's forward (RLMD_TARGET_PAIR=0: off)
   bool fused_actor = false;  // the actor step too (actions <= 2)
-  int n_cu = 256;            // compute units of the device (column-split decisions)
+  int n_cu = 256;            // compute units this agent may count on (column-split decisions;
+                             // the device's, or rlmd_agent_set_cu_budget)
   int qsplit_max = 2;        // qeval_rows column split allowed (RLMD_QSPLIT=1: off)
   int fsplit_max = 2;        // fwd_rows critic column split allowed (RLMD_FSPLIT=1: off)
   rlmd::PhaseProfiler prof;  // rlmd_profile_enable / _read
@@ -1388,8 +1394,10 @@ int rlmd_profile_enable(rlmd_agent_t ag, int32_t on) {
   rlmd::PhaseProfiler& pr = ag->prof;
   pr.enabled = on != 0;
   // 2: only the events attached to the env kernel's own dispatch (phase 1): the
-  // phase markers around acting / learning cost the stream ~25 us per C2 step
-  pr.mask = on == 2 ? 2 : 7;
+  // phase markers around acting / learning cost the stream ~25 us per C2 step.
+  // 3: kernel-attached pairs on the env kernel and the unfused acting kernel
+  pr.mask = on == 2 ? 2 : on == 3 ? 3 : 7;
+  pr.kernel_pairs = on == 3;
   for (int p = 0; p < 3; ++p) {
     pr.used[p] = 0;
     pr.seen[p] = 0;
@@ -1401,6 +1409,12 @@ int rlmd_profile_enable(rlmd_agent_t ag, int32_t on) {
 int rlmd_profile_stride(rlmd_agent_t ag, int32_t stride) {
   RLMD_CHECK(ag && stride >= 1, "bad profile stride");
   ag->prof.stride = stride;
+  return 0;
+}
+
+int rlmd_agent_set_cu_budget(rlmd_agent_t ag, int32_t n_cu) {
+  RLMD_CHECK(ag && n_cu >= 1, "bad CU budget");
+  ag->n_cu = n_cu;
   return 0;
 }
 
@@ -1451,11 +1465,16 @@ int rlmd_train_step(rlmd_env_t env, rlmd_replay_t rb, rlmd_agent_t ag, const rlm
   }
   if (!random) {
     RLMD_CHECK(ag, "policy acting needs an agent");
-    RLMD_TRY(ag->prof.record(0, 0, st));
+    const bool kp = ag->prof.kernel_pairs;
+    if (!kp) RLMD_TRY(ag->prof.record(0, 0, st));
     // one refresh of every compute copy serves the acting and the K updates below
     RLMD_TRY(rlmd::refresh_copies(ag, st));
-    if (!fused) RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st, true));
-    RLMD_TRY(ag->prof.record(0, 1, st));
+    if (!fused) {
+      hipEvent_t a0 = nullptr, a1 = nullptr;
+      if (kp) RLMD_TRY(ag->prof.pair(0, &a0, &a1));
+      RLMD_TRY(rlmd::agent_act(ag, obs, N, actions, 0, (uint64_t)cs, nullptr, st, true, a0, a1));
+    }
+    if (!kp) RLMD_TRY(ag->prof.record(0, 1, st));
   }
   double lo = -INFINITY, hi = INFINITY;
   if (window) {

@@ -13,13 +13,13 @@ namespace {
 // 64-lane sum: DPP within each 16-lane row, then two cross-row shuffles
 __device__ __forceinline__ float wave_sum(float v) {
   v = rlmd_row16_sum(v);
-  v += __shfl_xor(v, 16, 64);
+  v += __uint_as_float(rlmd_xor_lane<16>(__float_as_uint(v)));
   v += __shfl_xor(v, 32, 64);
   return v;
 }
 __device__ __forceinline__ float wave_max(float v) {
   v = rlmd_row16_max(v);
-  v = fmaxf(v, __shfl_xor(v, 16, 64));
+  v = fmaxf(v, __uint_as_float(rlmd_xor_lane<16>(__float_as_uint(v))));
   v = fmaxf(v, __shfl_xor(v, 32, 64));
   return v;
 }
@@ -66,19 +66,23 @@ __device__ __forceinline__ void block_allreduce(float* sm, float* mx, float* red
   __syncthreads();  // red / res reusable
 }
 
-// Ascending bitonic sort of one 64-bit key per lane across the wave (registers).
+// Ascending bitonic sort of one 64-bit key per lane across the wave (registers):
+// merge stage (K, J) exchanges with lane l ^ J, the stride a compile-time
+// constant so that 18 of the 21 stages move lanes by DPP (rlmd_xor_lane).
+template <int K, int J>
+__device__ __forceinline__ uint64_t bitonic_stage(uint64_t key, int l) {
+  const uint64_t other = rlmd_xor_lane_u64<J>(key);
+  const bool up = (l & K) == 0 || K == 64;
+  const bool keep_min = ((l & J) == 0) == up;
+  // one compare: this lane keeps its own key exactly when (key < other) agrees
+  // with keeping the minimum (keys are distinct but for absent ~0 ones)
+  key = ((key < other) == keep_min) ? key : other;
+  if constexpr (J > 1) return bitonic_stage<K, J / 2>(key, l);
+  else if constexpr (K < 64) return bitonic_stage<2 * K, K>(key, l);
+  else return key;
+}
 __device__ __forceinline__ uint64_t wave_sort64(uint64_t key) {
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int k = 2; k <= 64; k <<= 1)
-#pragma unroll
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      const uint64_t other = rlmd_shfl_xor_u64(key, j);
-      const bool up = (l & k) == 0 || k == 64;
-      const bool keep_min = ((l & j) == 0) == up;
-      key = keep_min ? (key < other ? key : other) : (key < other ? other : key);
-    }
-  return key;
+  return bitonic_stage<2, 1>(key, (int)(threadIdx.x & 63));
 }
 
 // Ranks of distinct 64-bit keys across the block (ascending; key ~0 = absent):

@@ -114,6 +114,30 @@ __device__ __forceinline__ uint64_t rlmd_shfl_xor_u64(uint64_t v, int m) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+// The value of lane (l ^ J) for a compile-time J, by the cheapest lane move:
+// DPP for J < 16 (quad permutes [1,0,3,2] / [2,3,0,1]; J = 4 as the half-row
+// mirror l ^ 7 then the quad reversal l ^ 3; J = 8 as row_ror:8), ds_swizzle's
+// xor mode for J = 16 (no address VGPR), ds_bpermute only for J = 32.  A
+// bitonic stage otherwise waits a bpermute round trip per 32-bit half.
+template <int J>
+__device__ __forceinline__ uint32_t rlmd_xor_lane(uint32_t v) {
+  // every lane's source lies inside its row, so no lane keeps an old value
+  // (mov_dpp: no "old" operand to initialise)
+  const int x = (int)v;
+  if constexpr (J == 1) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0xB1, 0xF, 0xF, false);
+  else if constexpr (J == 2) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x4E, 0xF, 0xF, false);
+  else if constexpr (J == 4)
+    return (uint32_t)__builtin_amdgcn_mov_dpp(__builtin_amdgcn_mov_dpp(x, 0x141, 0xF, 0xF, false), 0x1B, 0xF, 0xF,
+                                              false);
+  else if constexpr (J == 8) return (uint32_t)__builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false);
+  else if constexpr (J == 16) return (uint32_t)__builtin_amdgcn_ds_swizzle(x, 0x401F);
+  else return (uint32_t)__shfl_xor(x, J, 64);
+}
+template <int J>
+__device__ __forceinline__ uint64_t rlmd_xor_lane_u64(uint64_t v) {
+  return ((uint64_t)rlmd_xor_lane<J>((uint32_t)(v >> 32)) << 32) | rlmd_xor_lane<J>((uint32_t)v);
+}
+
 // Range-checked buffer loads: an element load is always issued (no exec-masked
 // branch, whose s_waitcnt vmcnt(0) would serialise a run of conditional loads);
 // ok == false turns the byte offset out of range and the hardware returns 0.

@@ -51,10 +51,12 @@ class VecTrainer:
                  smoothing_window=2000, precision="bf16", hidden=None, batch=None, topk=None,
                  prices=None, obs_days=1, time_length=0, shuffle_days=5, sample_days=0,
                  device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99, s_dist="N",
-                 initial_logtemp=0.0, agent_kw=None, slice_groups=0):
+                 initial_logtemp=0.0, agent_kw=None, slice_groups=0, cu_budget=None):
         """warmup_steps / smoothing_window: vector steps per lane (the ABI's counters;
         schedule_steps converts the reference's lengths).  agent_kw: further
-        DeviceAgent settings (update intervals, learning rates, ...)."""
+        DeviceAgent settings (update intervals, learning rates, ...).  cu_budget:
+        the CUs this trainer's learner may count on (rlmd_agent_set_cu_budget;
+        None = the device's)."""
         self.device = torch.device(device)
         self.env = VecEnv(env, investor, n_lanes, n_gambles, seed=seed, prices=prices, obs_days=obs_days,
                           time_length=time_length, shuffle_days=shuffle_days, sample_days=sample_days,
@@ -67,6 +69,8 @@ class VecTrainer:
         self.agent = DeviceAgent(algo, S, A, h1, h2, self.batch, self.topk, loss=loss, precision=precision,
                                  seed=seed, init_seed=init_seed, policy_dist=s_dist, device=device,
                                  initial_logtemp=initial_logtemp, **(agent_kw or {}))
+        if cu_budget is not None:
+            check(_abi.lib().rlmd_agent_set_cu_budget(self.agent.h, int(cu_budget)))
         self.replay = ReplayMemory(replay_capacity, S, A, device=device, multi_steps=multi_steps, lanes=n_lanes,
                                    dynamics=dynamics, gamma=gamma)
         self.n_lanes, self.k_updates = n_lanes, k_updates
@@ -108,7 +112,8 @@ class VecTrainer:
 
     def profile(self, mode):
         """rlmd_profile_enable on this trainer's agent: 0 off, 1 every phase, 2 the
-        env kernel's dispatch only."""
+        env kernel's dispatch only, 3 kernel-attached pairs on the env kernel and
+        (unfused steps) the acting kernel."""
         check(_abi.lib().rlmd_profile_enable(self.agent.h, int(mode)))
 
     def profile_stride(self, stride):
@@ -280,20 +285,32 @@ class SeedGroup:
     per-handle switches — launched on its own HIP stream, so the seeds' kernel
     chains run concurrently on the chip (one learner's latency-bound update chain
     leaves most CUs idle).  Nothing is shared between seeds: every seed computes
-    exactly what it computes alone (tests/test_seeds_gpu.py checks bit-equality)."""
+    exactly what it computes alone with the same CU budget (tests/test_seeds_gpu.py
+    checks bit-equality).
 
-    def __init__(self, seeds, device="cuda:0", **kw):
+    cu_budget ("auto"): each seed's learner counts on 1/T of the device's CUs, so
+    the layer-2 column split (twice the workgroups of a row kernel) is not taken
+    where T learners' grids would queue for the same CUs (round-5 measurement at
+    C2: T = 2 1.60 x one seed with the split, 1.71 x without)."""
+
+    def __init__(self, seeds, device="cuda:0", cu_budget="auto", **kw):
         import torch
 
         self.device = torch.device(device)
         self.seeds = list(seeds)
+        if cu_budget == "auto":
+            cu_budget = None
+            if len(self.seeds) > 1:
+                ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+                cu_budget = max(1, ncu // len(self.seeds))
+        self.cu_budget = cu_budget
         self.streams = [torch.cuda.Stream(device=self.device) for _ in self.seeds]
         self.trainers = []
         for s, st in zip(self.seeds, self.streams):
             with torch.cuda.stream(st):
                 kws = dict(kw)
                 kws.setdefault("init_seed", s)
-                self.trainers.append(VecTrainer(seed=s, device=device, **kws))
+                self.trainers.append(VecTrainer(seed=s, device=device, cu_budget=cu_budget, **kws))
         self.synchronize()
 
     def step(self, k_updates=None):

@@ -2,7 +2,9 @@
 independent trainers on their own HIP streams, stepped together, each
 bit-equal to the same seed run alone — replay ring rows, lane wealth / time,
 learner parameters and statistics — for the C2 shape (GBM_InvA, SAC 256/256
-bf16, fused acting + env) and the C4 shape (Market_InvA_D1 on stooq_snp)."""
+bf16, fused acting + env) and the C4 shape (Market_InvA_D1 on stooq_snp).  The
+solo run takes the group's CU budget (rlmd_agent_set_cu_budget): the budget
+decides the learner's column split, which changes f32 summation order."""
 import numpy as np
 import pytest
 import torch
@@ -51,7 +53,7 @@ def test_seed_group_bit_equal_to_solo(golden, dev, config, T):
     got = [_state(tr, steps, kw["n_lanes"]) for tr in grp.trainers]
     assert all(tr.last_fused() for tr in grp.trainers)  # the post-window steps fused, per handle
     for i, s in enumerate(seeds):
-        solo = VecTrainer(seed=s, init_seed=s, device=dev, **kw)
+        solo = VecTrainer(seed=s, init_seed=s, device=dev, cu_budget=grp.cu_budget, **kw)
         for _ in range(steps):
             solo.step()
         torch.cuda.synchronize()
