@@ -68,54 +68,81 @@ __device__ __forceinline__ void block_allreduce(float* sm, float* mx, float* red
 
 // Ascending bitonic sort of one 64-bit key per lane across the wave (registers):
 // merge stage (K, J) exchanges with lane l ^ J, the stride a compile-time
-// constant so that 18 of the 21 stages move lanes by DPP (rlmd_xor_lane).
+// constant so that 18 of the 21 stages move lanes by DPP (rlmd_xor_lane).  Which
+// lanes keep the minimum depends on the lane index only: a 64-bit constant per
+// stage, applied to the compare's lane mask on the scalar unit (ballot ->
+// s_xnor -> inverse ballot), so a stage costs the two lane moves, one 64-bit
+// compare and two selects on the VALU.
 template <int K, int J>
-__device__ __forceinline__ uint64_t bitonic_stage(uint64_t key, int l) {
+constexpr uint64_t bitonic_keep_min() {
+  uint64_t m = 0;
+  for (int l = 0; l < 64; ++l) {
+    const bool up = (l & K) == 0 || K == 64;
+    if (((l & J) == 0) == up) m |= 1ull << l;
+  }
+  return m;
+}
+template <int K, int J>
+__device__ __forceinline__ uint64_t bitonic_stage(uint64_t key) {
   const uint64_t other = rlmd_xor_lane_u64<J>(key);
-  const bool up = (l & K) == 0 || K == 64;
-  const bool keep_min = ((l & J) == 0) == up;
-  // one compare: this lane keeps its own key exactly when (key < other) agrees
-  // with keeping the minimum (keys are distinct but for absent ~0 ones)
-  key = ((key < other) == keep_min) ? key : other;
-  if constexpr (J > 1) return bitonic_stage<K, J / 2>(key, l);
-  else if constexpr (K < 64) return bitonic_stage<2 * K, K>(key, l);
+  // this lane keeps its own key exactly when (key < other) agrees with keeping
+  // the minimum (keys are distinct but for absent ~0 ones)
+  const uint64_t lt = __builtin_amdgcn_ballot_w64(key < other);
+  key = __builtin_amdgcn_inverse_ballot_w64(~(lt ^ bitonic_keep_min<K, J>())) ? key : other;
+  if constexpr (J > 1) return bitonic_stage<K, J / 2>(key);
+  else if constexpr (K < 64) return bitonic_stage<2 * K, K>(key);
   else return key;
 }
-__device__ __forceinline__ uint64_t wave_sort64(uint64_t key) {
-  return bitonic_stage<2, 1>(key, (int)(threadIdx.x & 63));
-}
+__device__ __forceinline__ uint64_t wave_sort64(uint64_t key) { return bitonic_stage<2, 1>(key); }
 
 // Ranks of distinct 64-bit keys across the block (ascending; key ~0 = absent):
 // each wave sorts its 64 keys in registers, parks the sorted run in LDS, and the
-// key at lane l of run w gets rank l + sum over the other runs of a binary
-// search (6 probes over the first 63 entries + the last entry).  The searches
-// over the other runs are independent: each probe step reads all of them at
-// once, so the dependent LDS chain is 6 probes long, not 6 per run.  The rank is
+// key at lane l of run w gets rank l + sum over the other NW - 1 runs of a
+// binary search (6 probes over the first 63 entries + the last entry).  The
+// searches over the other runs are independent: each probe step reads all of
+// them at once, so the dependent LDS chain is 6 probes long, not 6 per run.  A
+// search position is kept as a byte address (the run's base folded in), so a
+// probe is one LDS read with a constant offset, one 64-bit compare, one select
+// and one add: the rank is VALU-bound at two waves per SIMD.  The rank is
 // scattered to out[key & 0xffffffff] (the caller's index in the low word) and
 // read back by the key's owner after the barrier.
 // runs: LDS [blockDim.x] uint64; out: LDS int [blockDim.x].  NW: the block's
-// waves (blockDim.x == 64 NW), a compile-time constant so that every probe is
-// an unconditional LDS read (one wait per probe step for all runs).
+// waves (blockDim.x == 64 NW), a compile-time constant.
 template <int NW>
 __device__ __forceinline__ void block_rank(uint64_t key, uint64_t* runs, int* out) {
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  typedef const __attribute__((address_space(3))) uint64_t lds_u64;
+  const int l = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform: scalar run bases
   const uint64_t sk = wave_sort64(key);
   runs[threadIdx.x] = sk;
   __syncthreads();
-  int pos[NW];
+  if constexpr (NW == 1) {
+    if (sk != ~0ull) out[(int)(sk & 0xffffffffu)] = l;
+    __syncthreads();
+    return;
+  }
+  // LDS byte address of each other run's search position
+  const uint32_t r0 = (uint32_t)(uintptr_t)(lds_u64*)runs;
+  uint32_t at[NW > 1 ? NW - 1 : 1];
 #pragma unroll
-  for (int v = 0; v < NW; ++v) pos[v] = 0;
+  for (int i = 0; i < NW - 1; ++i) at[i] = r0 + (uint32_t)(512 * ((w + 1 + i) % NW));
 #pragma unroll
   for (int st = 32; st > 0; st >>= 1) {
-    uint64_t probe[NW];
+    uint64_t probe[NW > 1 ? NW - 1 : 1];
 #pragma unroll
-    for (int v = 0; v < NW; ++v) probe[v] = runs[64 * v + pos[v] + st - 1];
+    for (int i = 0; i < NW - 1; ++i) probe[i] = *(lds_u64*)(uintptr_t)(at[i] + 8u * (st - 1));
 #pragma unroll
-    for (int v = 0; v < NW; ++v) pos[v] += probe[v] < sk ? st : 0;
+    for (int i = 0; i < NW - 1; ++i) at[i] += probe[i] < sk ? 8u * st : 0u;
+    // keep each step's reads together (one LDS round per step): unconstrained,
+    // the scheduler ran one run's six dependent probes after another
+    __builtin_amdgcn_sched_barrier(0);
   }
   int rank = l;
 #pragma unroll
-  for (int v = 0; v < NW; ++v) rank += v == w ? 0 : pos[v] + (runs[64 * v + 63] < sk ? 1 : 0);
+  for (int i = 0; i < NW - 1; ++i) {
+    const uint32_t run0 = r0 + (uint32_t)(512 * ((w + 1 + i) % NW));
+    rank += (int)((at[i] - run0) >> 3) + (*(lds_u64*)(uintptr_t)(run0 + 504u) < sk ? 1 : 0);
+  }
   if (sk != ~0ull) out[(int)(sk & 0xffffffffu)] = rank;
   __syncthreads();
 }
