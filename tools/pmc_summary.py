@@ -152,5 +152,49 @@ def main(tag, config="c2"):
     print("\n".join(lines[:14]))
 
 
+CONFIG_NAMES = {"c3": "C3, 65,536 Dice_SH_InvA lanes, TD3 400/300 bf16, B = 200, K = 8",
+                "c4": "C4, 8,192 Market_InvA_D1 lanes on stooq_snp, SAC 256/256 bf16, K = 8",
+                "c5": "C5, 65,536 GBM_InvA lanes, TD3 400/300 bf16, 5-step returns, 2^24-row ring, K = 8"}
+LEARN = ("fwd_rows_kernel", "critic_update_kernel", "qeval_rows_kernel", "actor_update_kernel")
+
+
+def config_summaries(tag):
+    """profiles/<tag>_<cfg>_kernel_summary.txt (+ _pmc_mfma.json) for the C3 / C4 / C5
+    traces of tools/gpu_prof_configs.sh (headline region only: no seed groups or
+    variants), with the learner's time per update (launch counts weight the TD3
+    kernels that run every second update)."""
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    for cfg, name in CONFIG_NAMES.items():
+        stats = os.path.join(src, f"trace_{cfg}", "trace_kernel_stats.csv")
+        if not os.path.exists(stats):
+            continue
+        rows = list(csv.DictReader(open(stats)))
+        tot = sum(float(r["TotalDurationNs"]) for r in rows)
+        lines = [f"rocprofv3 --kernel-trace --stats: python bench.py --config {cfg} --no-cpu-baseline --no-companion "
+                 f"--k-sweep= --seeds-per-gpu= --variants= --steps 25 --warmup 5 ({name})", "",
+                 f"{'calls':>6} {'avg_us':>9} {'total_ms':>9} {'pct':>6}  kernel"]
+        per_kernel = {}
+        for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
+            n, t = int(r["Calls"]), float(r["TotalDurationNs"])
+            lines.append(f"{n:6d} {t / n / 1e3:9.2f} {t / 1e6:9.3f} {100 * t / tot:6.2f}  {r['Name'][:120]}")
+            m = re.search(r"(\w+_kernel)", r["Name"])
+            if m and m.group(1) in LEARN:
+                c, tt = per_kernel.get(m.group(1), (0, 0.0))
+                per_kernel[m.group(1)] = (c + n, tt + t)
+        if "critic_update_kernel" in per_kernel:
+            n_upd = per_kernel["critic_update_kernel"][0]  # one critic step per update
+            per_upd = sum(t for _, t in per_kernel.values()) / n_upd / 1e3
+            lines += ["", f"learner time per update: {per_upd:.2f} us over {n_upd} updates "
+                          "(sum of the four learner kernels' total time / critic steps)"]
+        open(os.path.join(ROOT, "profiles", f"{tag}_{cfg}_kernel_summary.txt"), "w").write("\n".join(lines) + "\n")
+        print("\n".join(lines[:10] + lines[-1:]))
+        mf = os.path.join(src, f"mfma_{cfg}", "mfma_counter_collection.csv")
+        if os.path.exists(mf):
+            mfma_summary(mf, rows, os.path.join(ROOT, "profiles", f"{tag}_{cfg}_pmc_mfma.json"))
+
+
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else "c2")
+    if len(sys.argv) > 2 and sys.argv[2] == "configs":
+        config_summaries(sys.argv[1])
+    else:
+        main(sys.argv[1] if len(sys.argv) > 1 else "r01", sys.argv[2] if len(sys.argv) > 2 else "c2")
