@@ -27,6 +27,11 @@ extern "C" {
 /* ------------------------------------------------------------------ errors */
 const char* rlmd_last_error(void);
 int rlmd_device_sync(void);
+/* A non-blocking HIP stream of this library's runtime (for several trainers in
+ * one process, each on its own stream: rlmd_amd.trainer.SeedGroup) and its
+ * release; *out receives the hipStream_t. */
+int rlmd_stream_create(void** out);
+int rlmd_stream_destroy(void* stream);
 
 /* --------------------------------------------------------------------- env */
 /* families (envs/<family>_envs.py) and investors */

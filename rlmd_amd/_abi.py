@@ -62,6 +62,8 @@ I32, I64, U64 = C.c_int32, C.c_int64, C.c_uint64
 SIGNATURES = {
     "rlmd_last_error": (C.c_char_p, []),
     "rlmd_device_sync": (C.c_int, []),
+    "rlmd_stream_create": (C.c_int, [P]),
+    "rlmd_stream_destroy": (C.c_int, [P]),
     "rlmd_env_create": (C.c_int, [C.POINTER(EnvCfg), P, I64, C.POINTER(P)]),
     "rlmd_env_destroy": (C.c_int, [P]),
     "rlmd_env_dims": (C.c_int, [P, C.POINTER(I32), C.POINTER(I32), C.POINTER(I32), C.POINTER(I32)]),

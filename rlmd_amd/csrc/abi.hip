@@ -21,4 +21,21 @@ int rlmd_device_sync(void) {
   return 0;
 }
 
+// Streams created by the HIP runtime this library launches on (SeedGroup wraps
+// them as torch external streams): non-blocking, each placed on the process's
+// hardware queues by HIP at creation.
+int rlmd_stream_create(void** out) {
+  RLMD_CHECK(out, "null argument");
+  hipStream_t s = nullptr;
+  RLMD_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  *out = s;
+  return 0;
+}
+
+int rlmd_stream_destroy(void* stream) {
+  RLMD_CHECK(stream, "null stream");
+  RLMD_HIP(hipStreamDestroy((hipStream_t)stream));
+  return 0;
+}
+
 }  // extern "C"

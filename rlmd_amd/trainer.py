@@ -13,6 +13,8 @@ converts them to the same number of learner updates); K updates of batch B per
 vector step (UTD = K / N per env step, reported with every metric); one agent
 shared by all lanes; uniform sampling over all lanes' transitions.
 """
+import ctypes
+
 import numpy as np
 import torch
 
@@ -276,6 +278,27 @@ def market_evaluate(agent, prices, investor, obs_days, test_days, starts, cum_st
             "risk_log": risk_log.cpu().numpy(), "stats": stats[1:15].cpu().numpy()}
 
 
+_HIP_STREAMS = {}
+
+
+def _hip_streams(device, n):
+    """The first n of this process's group streams on `device`, created on first
+    use by the library's HIP runtime and kept for the process (the trainers'
+    tensors were allocated on them; torch's caching allocator keys its blocks by
+    stream).  HIP places each new stream on one of the process's hardware queues
+    as it is created, so every group reuses the same placement: seed i of any
+    group runs on the i-th stream created.  Round 5 measured torch pool streams
+    taken by consecutive groups at 1.36 - 1.96 x one seed for T = 3 depending on
+    which pool slots they got (tools/probe/seeds_queue_probe.py)."""
+    lst = _HIP_STREAMS.setdefault(str(device), [])
+    with torch.cuda.device(device):
+        while len(lst) < n:
+            h = ctypes.c_void_p()
+            check(_abi.lib().rlmd_stream_create(ctypes.byref(h)))
+            lst.append(torch.cuda.ExternalStream(h.value, device=device))
+    return lst[:n]
+
+
 class SeedGroup:
     """Several independent seeds of one workload on one GPU (GPU g runs
     seeds {g, g + G, ...}; the reference's trial loop, rl_multiplicative.py:154-183,
@@ -293,7 +316,12 @@ class SeedGroup:
     where T learners' grids would queue for the same CUs (round-5 measurement at
     C2: T = 2 1.60 x one seed with the split, 1.71 x without)."""
 
-    def __init__(self, seeds, device="cuda:0", cu_budget="auto", **kw):
+    def __init__(self, seeds, device="cuda:0", cu_budget="auto", streams="pool", **kw):
+        """streams: "pool" — torch's stream pool; a list — the caller's streams, one
+        per seed; "hip" — streams created for the
+        group by the library's HIP runtime (rlmd_stream_create), wrapped as torch
+        external streams: one process-wide list per device, seed i of every group
+        on its i-th stream (see _hip_streams)."""
         import torch
 
         self.device = torch.device(device)
@@ -304,7 +332,13 @@ class SeedGroup:
                 ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
                 cu_budget = max(1, ncu // len(self.seeds))
         self.cu_budget = cu_budget
-        self.streams = [torch.cuda.Stream(device=self.device) for _ in self.seeds]
+        if streams == "hip":
+            self.streams = _hip_streams(self.device, len(self.seeds))
+        elif isinstance(streams, (list, tuple)):
+            assert len(streams) == len(self.seeds), "one stream per seed"
+            self.streams = list(streams)
+        else:
+            self.streams = [torch.cuda.Stream(device=self.device) for _ in self.seeds]
         self.trainers = []
         for s, st in zip(self.seeds, self.streams):
             with torch.cuda.stream(st):

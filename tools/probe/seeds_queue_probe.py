@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--T", default="2,3,4")
     ap.add_argument("--offsets", default="0,1,2,3")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--streams", default="pool", help="SeedGroup streams: pool (torch) or hip (rlmd_stream_create)")
     args = ap.parse_args()
     dev = "cuda:0"
     kw = dict(env="gbm", investor="A", n_lanes=65536, algo="SAC", k_updates=8, replay_capacity=1 << 20,
@@ -48,7 +49,7 @@ def main():
                 with torch.cuda.stream(st):
                     torch.zeros(1, device=dev).add_(1)
             keep += extra
-            grp = SeedGroup([420 + 1000 * i for i in range(T)], device=dev, **kw)
+            grp = SeedGroup([420 + 1000 * i for i in range(T)], device=dev, streams=args.streams, **kw)
             for _ in range(5):
                 grp.step()
             grp.synchronize()
@@ -57,7 +58,7 @@ def main():
                 grp.step()
             grp.synchronize()
             dt = time.perf_counter() - t0
-            print(json.dumps({"T": T, "offset": off, "vs_one_seed": T * 65536 * args.steps / dt / one,
+            print(json.dumps({"T": T, "offset": off, "streams": args.streams, "vs_one_seed": T * 65536 * args.steps / dt / one,
                               "ms_per_group_step": 1e3 * dt / args.steps}), flush=True)
             del grp
             torch.cuda.synchronize()
