@@ -37,16 +37,18 @@ def _kw(golden, config):
                 shuffle_days=5, sample_days=1000 + 250 + 1 + 20 - 1)
 
 
-@pytest.mark.parametrize("config", ["c2", "c4"])
-@pytest.mark.parametrize("T", [2, 4])
-def test_seed_group_bit_equal_to_solo(golden, dev, config, T):
+@pytest.mark.parametrize("config,T,streams", [("c2", 2, "pool"), ("c2", 4, "pool"), ("c4", 2, "pool"), ("c4", 4, "pool"),
+                                              ("c2", 3, "hip")])
+def test_seed_group_bit_equal_to_solo(golden, dev, config, T, streams):
+    """streams="hip": the group's streams come from the library's runtime
+    (rlmd_stream_create) instead of torch's pool."""
     from rlmd_amd.trainer import SeedGroup, VecTrainer
 
     steps, K = 6, 4
     kw = dict(_kw(golden, config), k_updates=K, replay_capacity=1 << 16, warmup_steps=2, smoothing_window=4,
               precision="bf16")
     seeds = [420 + i for i in range(T)]
-    grp = SeedGroup(seeds, device=dev, **kw)
+    grp = SeedGroup(seeds, device=dev, streams=streams, **kw)
     for _ in range(steps):
         grp.step()
     grp.synchronize()

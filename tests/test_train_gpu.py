@@ -246,6 +246,33 @@ def test_policy_steps_apply_action_window_and_learn(dev):
     assert tr.agent.scalars()["nan_flag"] == 0
 
 
+def test_profile_modes_count_the_timed_launches(dev):
+    """rlmd_profile_enable: 2 times only the env kernel's dispatch (fused steps:
+    act_env_kernel), every stride-th; 3 times the acting and the env kernel of
+    unfused steps by their own dispatches (bench.py's in-step acting reference)."""
+    from rlmd_amd.trainer import VecTrainer
+
+    tr = VecTrainer(env="gbm", investor="A", n_lanes=4096, algo="SAC", k_updates=1, seed=5, warmup_steps=0,
+                    smoothing_window=0, replay_capacity=4096 * 8, precision="bf16", device=dev)
+    tr.step()
+    tr.profile(2)
+    tr.profile_stride(2)
+    for _ in range(6):
+        tr.step()
+    ms, cnt = tr.profile_read()
+    assert list(cnt) == [0, 3, 0] and ms[1] > 0
+    assert tr.last_fused()
+    tr.profile_stride(1)
+    tr.set_fused(0)
+    tr.profile(3)
+    for _ in range(4):
+        tr.step()
+    ms, cnt = tr.profile_read()
+    tr.profile(0)
+    tr.set_fused(1)
+    assert list(cnt) == [4, 4, 0] and ms[0] > 0 and ms[1] > 0, (ms, cnt)
+
+
 @pytest.mark.parametrize("env,inv,fam,oinv", [("gbm", "A", oe.GBM, oe.INV_A), ("dice_sh", "B", oe.DICE_SH, oe.INV_B)])
 def test_window_steps_feed_the_env_float64_actions(dev, env, inv, fam, oinv):
     """During warm-up (float64 action space sample) and inside the smoothing window
