@@ -75,64 +75,77 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
   // past H2 read 0): issued first, so their latency hides under layers 1-2
   const int nh = a.algo == RLMD_SAC ? 2 * A : A;  // heads: pi (+ log_scale)
   const int col0 = 16 * NB * wave;
+  // every load of this round through a range-checked buffer resource (an
+  // excluded element reads 0): no load sits in a branch, whose merge would wait
+  // for it (four such waits had serialised this prologue's load round)
+  const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(a.params, 0x7fffffff);
   float hw[NB][2 * kMaxA];
   float b2v[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int c = col0 + 16 * nb + (lane & 15);
     const bool live = c < H2;
-    b2v[nb] = live ? a.params[o.b2 + c] : 0.f;
+    b2v[nb] = rlmd_ldf(rp, o.b2 + c, live);
 #pragma unroll
     for (int h = 0; h < 2 * kMaxA; ++h) {
       const int64_t base = h < A ? o.w3 + (int64_t)h * H2 : o.w4 + (int64_t)(h - A) * H2;
-      hw[nb][h] = live && h < nh ? a.params[base + c] : 0.f;
+      hw[nb][h] = rlmd_ldf(rp, base + c, live && h < nh);
     }
   }
   // the sampling threads' head biases and policy noise (Philox -> f64 Box-Muller):
   // independent of the forward pass, so drawn here, under the load latency, not
   // in the epilogue's tail
   float mu_b[kMaxA], ls_b[kMaxA], nz[kMaxA];
+  const __amdgpu_buffer_rsrc_t re = rlmd_rsrc(a.eps_in, a.eps_in ? (int64_t)a.n * A * 4 : 0);
 #pragma unroll
   for (int j = 0; j < kMaxA; ++j) {
     const bool mine = tid < kRows && row0 + tid < a.n && j < A;
-    mu_b[j] = mine ? a.params[o.b3 + j] : 0.f;
-    ls_b[j] = mine && a.algo == RLMD_SAC ? a.params[o.b4 + j] : 0.f;
-    nz[j] = 0.f;
-    if (mine && a.mode == 0)
-      nz[j] = a.eps_in ? a.eps_in[(int64_t)(row0 + tid) * A + j]
-                       : policy_draw(a.algo == RLMD_SAC ? a.dist : RLMD_DIST_N, a.seed, (uint32_t)(row0 + tid), a.ctr,
-                                     a.tag, j);
+    mu_b[j] = rlmd_ldf(rp, o.b3 + j, mine);
+    ls_b[j] = rlmd_ldf(rp, o.b4 + j, mine && a.algo == RLMD_SAC);
+    const float ein = rlmd_ldf(re, (int64_t)(row0 + tid) * A + j, mine && a.mode == 0);
+    // drawn by every thread and selected: a draw in a branch overwrote the
+    // register the speculatively issued eps load targets, which waited on it
+    const float drawn = policy_draw(a.algo == RLMD_SAC ? a.dist : RLMD_DIST_N, a.seed, (uint32_t)(row0 + tid), a.ctr,
+                                    a.tag, j);
+    nz[j] = mine && a.mode == 0 ? (a.eps_in ? ein : drawn) : 0.f;
   }
   pro();
   // -- stage W1, b1 and this block's observations into the zero-padded LDS
   //    tiles (destination-indexed gathers, compile-time index math; padding
-  //    reads 0 through the predicate), 8 loads per thread in flight per pass
+  //    reads 0 through the predicate): every thread's loads in one round, all
+  //    issued before its first LDS store
   {
     constexpr int nW = SP * 16 * NTP + H1P, nO = kRows * SP;
-    constexpr int nmax = nW > nO ? nW : nO;
+    constexpr int PW = (nW + 255) / 256, PO = (nO + 255) / 256;
     const int rows = a.n - row0 < kRows ? a.n - row0 : kRows;
     const __amdgpu_buffer_rsrc_t rw = rlmd_rsrc(a.params + o.w1, (int64_t)(H1 * S + H1) * 4);
     const __amdgpu_buffer_rsrc_t ro = rlmd_rsrc(a.obs + (int64_t)row0 * S, (int64_t)rows * S * 4);
-    for (int base = 0; base < nmax; base += 8 * 256) {
-      float vw[8], vo[8];
+    float vw[PW], vo[PO];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int e = base + j * 256 + tid;
-        const bool isb = e >= SP * 16 * NTP;  // the b1 tail
-        const int k = e / (16 * NTP), jt = e - k * (16 * NTP);
-        const int jj = jt / NTP, t = jt - jj * NTP;
-        const int c = isb ? e - SP * 16 * NTP : 16 * t + jj;
-        const bool wl = e < nW && c < H1 && (isb || (t < NT && k < S));
-        vw[j] = rlmd_ldf(rw, isb ? H1 * S + c : c * S + k, wl);
-        const int r = e / SP, ko = e - r * SP;
-        vo[j] = rlmd_ldf(ro, r * S + ko, e < nO && ko < S && r < rows);
-      }
+    for (int j = 0; j < PW; ++j) {
+      const int e = j * 256 + tid;
+      const bool isb = e >= SP * 16 * NTP;  // the b1 tail
+      const int k = e / (16 * NTP), jt = e - k * (16 * NTP);
+      const int jj = jt / NTP, t = jt - jj * NTP;
+      const int c = isb ? e - SP * 16 * NTP : 16 * t + jj;
+      const bool wl = e < nW && c < H1 && (isb || (t < NT && k < S));
+      vw[j] = rlmd_ldf(rw, isb ? H1 * S + c : c * S + k, wl);
+    }
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int e = base + j * 256 + tid;
-        if (e < nW) w1s[e] = vw[j];  // b1 follows w1g contiguously
-        if (e < nO) obs_s[e] = vo[j];
-      }
+    for (int j = 0; j < PO; ++j) {
+      const int e = j * 256 + tid;
+      const int r = e / SP, ko = e - r * SP;
+      vo[j] = rlmd_ldf(ro, r * S + ko, e < nO && ko < S && r < rows);
+    }
+#pragma unroll
+    for (int j = 0; j < PW; ++j) {
+      const int e = j * 256 + tid;
+      if (e < nW) w1s[e] = vw[j];  // b1 follows w1g contiguously
+    }
+#pragma unroll
+    for (int j = 0; j < PO; ++j) {
+      const int e = j * 256 + tid;
+      if (e < nO) obs_s[e] = vo[j];
     }
   }
   // layer-2 B fragments of the first K step: issued now, consumed after layer 1
@@ -201,10 +214,12 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
     bf16x8 bcur[NB];
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) bcur[nb] = bnext[nb];
+#if !defined(RLMD_ABL_ACT)
     if (k0 + 32 < H1P) {
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) bnext[nb] = wf[(nb * nS + k0 / 32 + 1) * 64];
     }
+#endif  // timing ablation (experiment builds only; results wrong): layer 2 without its fragment stream
 #pragma unroll
     for (int m = 0; m < 4; ++m) {
       const bf16x8 af = *reinterpret_cast<const bf16x8*>(&h1s[(16 * m + (lane & 15)) * HP + k0 + kq]);
