@@ -406,6 +406,9 @@ int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
  * milliseconds and the number of timed launches per phase. */
 int rlmd_profile_enable(rlmd_agent_t ag, int32_t on);
 int rlmd_profile_read(rlmd_agent_t ag, double* ms_out3, int64_t* count_out3);
+/* The individual timed launches of one phase since rlmd_profile_enable (up to
+ * cap of them, milliseconds each); *count_out = how many were timed. */
+int rlmd_profile_samples(rlmd_agent_t ag, int32_t phase, double* ms_out, int64_t cap, int64_t* count_out);
 /* Sample every stride-th occurrence of each phase (default 1 = every one): each
  * timed launch's event pair costs the stream a few microseconds, so a timed
  * region is sampled rather than stamped on every step.  Counting restarts at

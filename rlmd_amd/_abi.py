@@ -114,6 +114,7 @@ SIGNATURES = {
     "rlmd_profile_enable": (C.c_int, [P, I32]),
     "rlmd_profile_read": (C.c_int, [P, P, P]),
     "rlmd_profile_stride": (C.c_int, [P, I32]),
+    "rlmd_profile_samples": (C.c_int, [P, I32, P, C.c_int64, P]),
     "rlmd_agent_set_cu_budget": (C.c_int, [P, I32]),
     "rlmd_gemm": (C.c_int, [I32, I32, I32, I32, I32, I32, P, I32, P, I32, P, P, I32, P, I32, P, P]),
 }

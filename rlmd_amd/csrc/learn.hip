@@ -1412,6 +1412,20 @@ int rlmd_profile_stride(rlmd_agent_t ag, int32_t stride) {
   return 0;
 }
 
+int rlmd_profile_samples(rlmd_agent_t ag, int32_t phase, double* ms_out, int64_t cap, int64_t* count_out) {
+  RLMD_CHECK(ag && count_out && phase >= 0 && phase < 3 && (cap == 0 || ms_out), "bad argument");
+  RLMD_HIP(hipDeviceSynchronize());
+  const rlmd::PhaseProfiler& pr = ag->prof;
+  const int64_t n = (int64_t)pr.used[phase];
+  for (int64_t i = 0; i < n && i < cap; ++i) {
+    float ms = 0.f;
+    RLMD_HIP(hipEventElapsedTime(&ms, pr.ev[phase][0][i], pr.ev[phase][1][i]));
+    ms_out[i] = ms;
+  }
+  *count_out = n;
+  return 0;
+}
+
 int rlmd_agent_set_cu_budget(rlmd_agent_t ag, int32_t n_cu) {
   RLMD_CHECK(ag && n_cu >= 1, "bad CU budget");
   ag->n_cu = n_cu;

@@ -130,6 +130,16 @@ class VecTrainer:
         check(_abi.lib().rlmd_profile_read(self.agent.h, ms, cnt))
         return list(ms), list(cnt)
 
+    def profile_samples(self, phase):
+        """The individual timed launches of one phase (ms), rlmd_profile_samples."""
+        import ctypes as C
+
+        n = C.c_int64()
+        check(_abi.lib().rlmd_profile_samples(self.agent.h, int(phase), None, 0, C.byref(n)))
+        buf = (C.c_double * max(n.value, 1))()
+        check(_abi.lib().rlmd_profile_samples(self.agent.h, int(phase), buf, n.value, C.byref(n)))
+        return list(buf[:n.value])
+
     def last_stats(self, shadow=False, low_mul=1.0, high_mul=10.0):
         """loss[11] | logtemp | loss_params[4] of the last update (numpy f64).
         shadow: first fill loss[6:8] with the critics' power-law shadow means on

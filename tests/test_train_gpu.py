@@ -261,6 +261,8 @@ def test_profile_modes_count_the_timed_launches(dev):
         tr.step()
     ms, cnt = tr.profile_read()
     assert list(cnt) == [0, 3, 0] and ms[1] > 0
+    samples = tr.profile_samples(1)
+    assert len(samples) == 3 and abs(sum(samples) - ms[1]) < 1e-6 * max(ms[1], 1.0)
     assert tr.last_fused()
     tr.profile_stride(1)
     tr.set_fused(0)

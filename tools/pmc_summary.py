@@ -85,15 +85,16 @@ def trace_roofline(path, lanes=65536, bytes_per_lane=103):
             (in_step if nxt == "env_train_kernel" else b2b).append((t1 - t0) * 1e-3)
     if not fused or not in_step:
         return None
-    fa, act = statistics.mean(fused), statistics.mean(in_step)
+    fa, act = statistics.median(fused), statistics.median(in_step)
     marg = fa - act
     gbs = bytes_per_lane * lanes / (marg * 1e-6) / 1e9
-    return {"act_env_us": fa, "act_env_launches": len(fused), "fused_act_in_step_us": act,
+    return {"act_env_us": fa, "act_env_mean_us": statistics.mean(fused), "act_env_launches": len(fused),
+            "fused_act_in_step_us": act, "fused_act_in_step_mean_us": statistics.mean(in_step),
             "fused_act_in_step_launches": len(in_step),
-            "fused_act_back_to_back_us": statistics.mean(b2b) if b2b else None, "marginal_us": marg,
+            "fused_act_back_to_back_us": statistics.median(b2b) if b2b else None, "marginal_us": marg,
             "algorithmic_bytes_per_launch": bytes_per_lane * lanes, "achieved_GBs": gbs, "frac": gbs / 8000.0,
-            "method": f"means over dispatches with grid {4 * lanes} work-items; acting-only = fused_act_kernel "
-                      "dispatches followed by env_train_kernel (in whole unfused steps)"}
+            "method": f"medians over dispatches with grid {4 * lanes} work-items (as bench.py's live samples); "
+                      "acting-only = fused_act_kernel dispatches followed by env_train_kernel (in whole unfused steps)"}
 
 
 def main(tag, config="c2"):
