@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--loss", default="MSE")
     ap.add_argument("--multi-steps", type=int, default=1, help="n-step returns (C5: 5)")
     ap.add_argument("--n-eval", type=int, default=0, help="evaluation episodes (0: main.py's)")
+    ap.add_argument("--out", default="", help="output path (default: the fixture name under tests/golden)")
     a = ap.parse_args()
     market = 21 <= a.key <= 26
     _refshim.install()
@@ -80,7 +81,7 @@ def main():
     tag = "" if (a.algo, a.loss) == ("SAC", "MSE") else f"_{a.algo}_{a.loss}"
     tag += f"_n{a.multi_steps}" if a.multi_steps != 1 else ""
     tag += f"_e{a.n_eval}" if a.n_eval else ""
-    out = os.path.join(HERE, f"converge_ref_{a.key}{tag}_s{a.seed}.npz")
+    out = a.out or os.path.join(HERE, f"converge_ref_{a.key}{tag}_s{a.seed}.npz")
     np.random.seed(a.seed)
     torch.manual_seed(a.seed)
     cwd = os.getcwd()
@@ -99,12 +100,16 @@ def main():
                 multiplicative_env(ref_main.gym_envs, inputs, n_gambles=1)
             ev = np.load(glob.glob("results/**/*_eval.npy", recursive=True)[0])
             er = np.load(glob.glob("results/**/*_eval_risk.npy", recursive=True)[0])
+            # per training episode (rl_multiplicative.py:419-429): length, logtemp, last risk row
+            tr = np.load(glob.glob("results/**/*_trial.npy", recursive=True)[0])
+            trr = np.load(glob.glob("results/**/*_trial_risk.npy", recursive=True)[0])
         finally:
             os.chdir(cwd)
     np.savez_compressed(out, key=a.key, seed=a.seed, steps=a.steps, env=ref_main.gym_envs[str(a.key)][0],
                         cum_steps=ev[0, :, 0, 19], reward=ev[0, :, :, 1], eval_steps=ev[0, :, :, 2],
                         lev=er[0, :, :, 3], risk=er[0].astype(np.float32), algo=a.algo, loss=a.loss,
-                        multi_steps=a.multi_steps)
+                        multi_steps=a.multi_steps, **({"trial_steps": tr[0, :, 2], "trial_logtemp": tr[0, :, 14],
+                                                       "trial_lev": trr[0, :, 3]} if a.out else {}))
     print("wrote", out, "final mean lev", er[0, -5:, :, 3].mean(), "final mean reward", ev[0, -5:, :, 1].mean())
 
 
