@@ -21,6 +21,23 @@ from . import _abi
 from ._abi import check, ptr, stream_ptr
 
 HEADS = {"SAC": ("pi", "log_scale"), "TD3": ("mu",)}
+_AGENT_CTR = [0]
+
+
+def private_agent_seed():
+    """The Philox key of an agent built without one (acting noise, the
+    update's policy noise, replay indices).  The reference draws these from
+    torch's and NumPy's generators, so they follow the driver's
+    torch.manual_seed / np.random.seed: the key hashes torch.initial_seed(),
+    NumPy's MT19937 state (read, not advanced) and a private counter (two
+    agents of one process apart)."""
+    import hashlib
+
+    _AGENT_CTR[0] += 1
+    _, keys, pos, _, _ = np.random.get_state()
+    h = hashlib.blake2b(np.ascontiguousarray(keys, dtype=np.uint32).tobytes(), digest_size=8)
+    h.update(np.array([pos, torch.initial_seed() & 0x7FFFFFFFFFFFFFFF, _AGENT_CTR[0]], dtype=np.int64).tobytes())
+    return int.from_bytes(h.digest(), "little") & 0x7FFFFFFF
 
 
 def layer_names(algo, net):
@@ -286,8 +303,9 @@ class _Agent:
 
     algo = None
 
-    def __init__(self, inputs, device=None, precision="fp32", seed=0):
+    def __init__(self, inputs, device=None, precision="fp32", seed=None):
         sac = self.algo == "SAC"
+        seed = private_agent_seed() if seed is None else seed
         device = device or ("cuda:0" if torch.cuda.is_available() else None)
         if device is None:
             raise _abi.RlmdError("rlmd_amd agents need a GPU (no CPU fallback)")
