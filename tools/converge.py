@@ -151,7 +151,7 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
                    "eval_growth_pct": grow, "eval_steps": float(np.mean(ev["steps"])),
                    "analytic_growth_pct": None if env == "market" else 100.0 * math.expm1(growth(env, lev, lev_sh)),
                    "kelly_lev": l_star, "kelly_growth_pct": g_star, "wall_s": time.perf_counter() - t0,
-                   "nan_flag": tr.agent.scalars()["nan_flag"]}
+                   "nan_flag": tr.agent.scalars()["nan_flag"], "log_alpha": tr.agent.scalars()["log_alpha"]}
             recs.append(rec)
             log(json.dumps(rec))
             if out is not None:

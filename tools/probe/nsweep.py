@@ -46,7 +46,8 @@ def main():
             assert all(math.isfinite(r["eval_growth_pct"]) for r in recs)
             got.append((t._third(recs, "eval_growth_pct"), t._third(recs, "lev")))
             t.record(w + "_nsweep", lanes=n, k=k, seed=seed, updates=updates, precision=precision, growth_pct=got[-1][0],
-                     lev=got[-1][1], lev_curve=[round(r["lev"], 3) for r in recs])
+                     lev=got[-1][1], lev_curve=[round(r["lev"], 3) for r in recs],
+                     logtemp_curve=[round(r["log_alpha"], 3) for r in recs])
             print(f"{w} N={n} K={k} seed {seed}: growth {got[-1][0]:.3f} lev {got[-1][1]:.4f}", flush=True)
         pg, pl = t.mw_p(got, ref)
         print(f"{w} N={n} K={k}: Mann-Whitney p growth {pg:.3f} lev {pl:.3f}; lev median {np.median([x for _, x in got]):.3f}",
