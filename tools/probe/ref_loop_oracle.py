@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--steps", type=int, default=50000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--philox-env", action="store_true",
+                    help="GBM returns from the build's Philox normals (oracle/philox.py) instead of np.random")
     a = ap.parse_args()
     _refshim.install()
     import torch
@@ -75,6 +77,31 @@ def main():
         return [np.float32(x) for x in loss], np.array(logtemp, dtype=np.float32), lp
 
     asac.Agent_sac.learn = learn
+    if a.philox_env:
+        import envs.gbm_envs as gbm_mod
+
+        from oracle import philox as px
+
+        ctr = [0]
+
+        class _PhiloxRandom:
+            def normal(self, loc=0.0, scale=1.0, size=None):
+                n = int(np.prod(size)) if size is not None else 1
+                z = np.asarray(px.normal_draws(a.seed, np.zeros(1, dtype=np.uint64), ctr[0], px.TAG_ENV_DRAW, n)).ravel()[:n]
+                ctr[0] += 1
+                out = loc + scale * z
+                return out.reshape(size) if size is not None else float(out[0])
+
+            def __getattr__(self, name):
+                return getattr(np.random, name)
+
+        class _Np:
+            random = _PhiloxRandom()
+
+            def __getattr__(self, name):
+                return getattr(np, name)
+
+        gbm_mod.np = _Np()
 
     inputs = dict(ref_main.inputs)
     inputs.update({"n_trials_mul": 1, "n_cumsteps_mul": float(a.steps), "gpu": "cpu", "buffer_gpu": False})
