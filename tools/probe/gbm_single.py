@@ -66,6 +66,24 @@ def main():
     import test_converge_gpu as t
 
     args = sys.argv[1:]
+    if "--alias" in args:
+        # the reference envs return one next_state array, mutated in place by every
+        # step (e.g. gbm_envs.py:179-181, 212), and the loop keeps `state = next_state`
+        # (rl_multiplicative.py:218-245): from an episode's second step on, the
+        # stored state IS the stored next state.  Reproduce that in the driver's env.
+        from rlmd_amd import envs as envs_mod
+
+        base_step = envs_mod._SingleEnv.step
+
+        def aliased_step(self, action):
+            ns, r, d, risk = base_step(self, action)
+            buf = getattr(self, "_ns_buf", None)
+            if buf is None or buf.shape != ns.shape:
+                buf = self._ns_buf = np.empty_like(ns)
+            buf[...] = ns
+            return buf, r, d, risk
+
+        envs_mod._SingleEnv.step = aliased_step
     steps = 50000
     for a in [a for a in args if a.startswith("--steps=")]:
         steps = int(a.split("=")[1])
