@@ -373,6 +373,20 @@ def dry_run(args):
     """The N-rank launch path of main() with DryTrainer: gloo on the host,
     rank 0 prints the headline fields it would print for the real loop,
     labelled DRY-RUN (never a measurement)."""
+    # the per-seed processes start now, before this process opens the GPU (they
+    # wait on stdin until the headline and its companions are done)
+    procs_spec = args.seed_procs if args.seed_procs is not None else ("1,2,3,4" if args.config in ("c2", "c4") else "")
+    procs_T = [int(v) for v in procs_spec.split(",") if v.strip()]
+    seed_procs = None
+    if procs_T and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        child = ["--config", args.config, "--k-updates", str(args.k_updates), "--precision", args.precision,
+                 "--loss", args.loss, "--warmup", str(args.warmup)]
+        if args.lanes:
+            child += ["--lanes", str(args.lanes)]
+        if args.replay:
+            child += ["--replay", str(args.replay)]
+        seed_procs = SeedProcs(max(procs_T), child)
+
     import torch
     import torch.distributed as dist
 
@@ -386,19 +400,135 @@ def dry_run(args):
     cfg = CONFIGS[args.config]
     N = args.lanes or cfg["lanes"]
     ms_n = parse_multi_steps(args.multi_steps, rank, cfg["multi_steps"])
+    procs_T = [int(v) for v in (args.seed_procs or "").split(",") if v.strip()]
+    sp = SeedProcs(max(procs_T), ["--dry-run", "--warmup", "1"]) if procs_T and world == 1 else None
     tr = DryTrainer(rank)
     elapsed = timed_region(tr, args.steps, args.warmup, world, lambda: None)
     t_max, value, ms_per_rank = whole_job(elapsed, tr, N, args.steps, world, torch.device("cpu"), ms_n)
+    per_proc = {}
+    if sp is not None:
+        per_proc = {str(T): sp.round(T, 5, N) for T in procs_T}
+        assert sp.close() == 0
     if rank == 0:
         print(json.dumps({"metric": "DRY-RUN (host stand-in trainer; not a measurement)", "value": value,
                           "unit": "env steps/sec", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": 1e3 * t_max / args.steps, "t_max_s": t_max,
-                          "rank0_elapsed_s": elapsed, "scaling": "weak",
+                          "rank0_elapsed_s": elapsed, "scaling": "weak", "seeds_per_gpu_processes": per_proc,
                           "config": {"config": args.config, "lanes_per_gpu": N, "global_lanes": N * world,
                                      "multi_steps_per_rank": ms_per_rank}}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+class SeedProcs:
+    """Several seeds per GPU as one PROCESS per seed (§8e "GPU g runs seeds
+    {g, g+G, ...}"): each seed process gets its own HIP hardware queues, which
+    SeedGroup's streams inside one process share (4 queues per process; two busy
+    seeds placed on one queue serialise).  The children are started
+    before this process opens the GPU (subprocess children of a process that has
+    not initialised HIP) and wait on stdin; each builds its trainer when first
+    asked to run.  One round of T seeds: "run" to children 0..T-1 (build or reuse
+    the trainer, warm up, synchronize, answer "ready"), then "go" to all of them
+    together (n_t timed steps bracketed by synchronize, answer with the
+    wall-clock start and end); the group's rate is T x lanes x n_t over the span
+    from the first start to the last end."""
+
+    def __init__(self, n, argv):
+        import subprocess
+
+        self.procs = []
+        for i in range(n):
+            env = dict(os.environ)
+            for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+                env.pop(k, None)
+            self.procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--seed-worker",
+                                                "--seed", str(420 + 1000 * (i + 1))] + argv, env=env,
+                                               stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1))
+
+    def _ask(self, procs, msg):
+        for p in procs:
+            p.stdin.write(msg + "\n")
+            p.stdin.flush()
+        out = []
+        for p in procs:
+            line = p.stdout.readline()
+            if not line:
+                raise RuntimeError(f"seed process exited (rc {p.poll()})")
+            out.append(json.loads(line))
+        return out
+
+    def round(self, T, n_t, lanes):
+        ps = self.procs[:T]
+        self._ask(ps, f"run {n_t}")
+        res = self._ask(ps, "go")
+        span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
+        return {"env_steps_per_s": T * lanes * n_t / span, "span_s": span,
+                "per_seed_ms_per_step": [1e3 * (r["t1"] - r["t0"]) / n_t for r in res]}
+
+    def close(self):
+        for p in self.procs:
+            try:
+                p.stdin.write("exit\n")
+                p.stdin.flush()
+            except OSError:
+                pass
+        return max((p.wait() for p in self.procs), key=abs, default=0)
+
+
+def seed_worker(args):
+    """One seed process of SeedProcs: the headline workload's trainer (own lanes,
+    replay and learner, seed --seed) driven by stdin commands."""
+    tr = None
+    n_t = 0
+    for line in sys.stdin:
+        cmd = line.split()
+        if not cmd or cmd[0] == "exit":
+            break
+        import torch
+
+        sync = (lambda: None) if args.dry_run else torch.cuda.synchronize
+        if cmd[0] == "run":
+            n_t = int(cmd[1])
+            if tr is None:
+                tr = DryTrainer(0) if args.dry_run else make_trainer(args, torch.device("cuda", 0), args.seed)
+                for _ in range(max(args.warmup, 3)):
+                    tr.step()
+            sync()
+            print(json.dumps({"ready": True}), flush=True)
+        elif cmd[0] == "go":
+            t0 = time.time()
+            for _ in range(n_t):
+                tr.step()
+            sync()
+            print(json.dumps({"t0": t0, "t1": time.time()}), flush=True)
+    return 0
+
+
+def make_trainer(args, dev, seed, **over):
+    """The configuration's trainer as the headline builds it (steady state:
+    warm-up and smoothing off)."""
+    from rlmd_amd.trainer import VecTrainer
+
+    cfg = CONFIGS[args.config]
+    N = args.lanes or cfg["lanes"]
+    replay = args.replay or cfg["replay"]
+    ms_n = over.pop("multi_steps", cfg["multi_steps"])
+    if ms_n > 1:
+        replay = (replay // N) * N
+    kw = market_kwargs() if cfg["env"] == "market" else {}
+    kw.update(over)
+    return VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"],
+                      loss=args.loss, k_updates=args.k_updates, replay_capacity=replay, seed=seed, warmup_steps=0,
+                      smoothing_window=0, precision=args.precision, device=dev, init_seed=seed, multi_steps=ms_n,
+                      dynamics="A", **kw)
+
+
+def market_kwargs():
+    """C4's market env: stooq_snp, train 1000 d (obs_days 1), shuffle 5, the
+    start draw excluding train + test + gap days (rl_market.py:54-62)."""
+    return dict(prices=stooq_snp_prices(), obs_days=1, time_length=1000, shuffle_days=5,
+                sample_days=1000 + 250 + 1 + 20 - 1)
 
 
 def main():
@@ -419,6 +549,10 @@ def main():
     ap.add_argument("--seeds-per-gpu", default=None,
                     help="independent seeds per GPU timed after the headline (SeedGroup: one stream per seed); "
                          "default '2,3,4' (C2, C4), '2,4' otherwise; '' = off")
+    ap.add_argument("--seed-procs", default=None,
+                    help="independent seeds per GPU as one process each (own HIP queues), timed after the headline; "
+                         "default '1,2,3,4' (C2, C4), '' otherwise; '' = off")
+    ap.add_argument("--seed-worker", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--variants", default=None,
                     help="BASELINE config variants timed after the headline, one trainer each: C3 the critic losses "
                          "(default 'MSE,HUB,MAE,HSC'), C5 the multi-step n (default '3,5,7'); '' = off")
@@ -440,6 +574,8 @@ def main():
         print(json.dumps(r), flush=True)
         return 0
 
+    if args.seed_worker:
+        return seed_worker(args)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
     if args.dry_run:
@@ -459,6 +595,20 @@ def main():
         pool1 = cpu_baseline_seeds(1, 1, args.cpu_seconds, allc, replay=rep0)
         cpu_lines = (pool, cpu_baseline(n0, args.k_updates, args.cpu_seconds, 1, replay=rep0), pool1,
                      cpu_baseline(1, 1, args.cpu_seconds, 1, replay=rep0))
+
+    # the per-seed processes start now, before this process opens the GPU (they
+    # wait on stdin until the headline and its companions are done)
+    procs_spec = args.seed_procs if args.seed_procs is not None else ("1,2,3,4" if args.config in ("c2", "c4") else "")
+    procs_T = [int(v) for v in procs_spec.split(",") if v.strip()]
+    seed_procs = None
+    if procs_T and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        child = ["--config", args.config, "--k-updates", str(args.k_updates), "--precision", args.precision,
+                 "--loss", args.loss, "--warmup", str(args.warmup)]
+        if args.lanes:
+            child += ["--lanes", str(args.lanes)]
+        if args.replay:
+            child += ["--replay", str(args.replay)]
+        seed_procs = SeedProcs(max(procs_T), child)
 
     import torch
     import torch.distributed as dist
@@ -498,8 +648,7 @@ def main():
     ms_n = parse_multi_steps(args.multi_steps, rank, cfg["multi_steps"])
     kw = {}
     if cfg["env"] == "market":
-        kw = dict(prices=stooq_snp_prices(), obs_days=1, time_length=1000, shuffle_days=5,
-                  sample_days=1000 + 250 + 1 + 20 - 1)
+        kw = market_kwargs()
     if ms_n > 1:
         replay = (replay // N) * N  # per-lane rings: capacity a multiple of the lanes
     tr = VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"],
@@ -579,6 +728,13 @@ def main():
                                "ms_per_group_step": 1e3 * dt / n_t,
                                "vs_one_seed": (T * N * n_t / dt) / (N * 1e3 / (1e3 * t_max / args.steps))}
             del grp
+    per_proc = {}
+    if seed_procs is not None:
+        one = N * 1e3 / (1e3 * t_max / args.steps)
+        for T in procs_T:
+            r = seed_procs.round(T, max(10, min(args.steps, 30)), N)
+            per_proc[str(T)] = dict(r, vs_one_seed=r["env_steps_per_s"] / one)
+        seed_procs.close()
     # BASELINE.json names variants of C3 (critic-loss sweep MSE/HUB/MAE/HSC,
     # tools/critic_loss.py:143-205) and C5 (n = 3/5/7, tools/replay.py:251-332):
     # each is timed as its own trainer (same lanes, K, ring), with its learn
@@ -713,6 +869,12 @@ def main():
             "seeds_per_gpu": {"note": "T independent seeds of this workload on one GPU (SeedGroup: own lanes, "
                                       "replay and learner per seed, one HIP stream each), per-GPU totals; eval not "
                                       "amortised", **per_gpu} if per_gpu else None,
+            "seeds_per_gpu_processes": {"note": "T independent seeds of this workload on one GPU, one process each "
+                                                "(own HIP hardware queues; the process-per-seed alternative to "
+                                                "SeedGroup's streams); per-GPU totals over the span from the first "
+                                                "seed's start to the last one's end; vs_one_seed against the "
+                                                "headline's one seed; eval not amortised", **per_proc}
+            if per_proc else None,
             "k_sweep": sweep,
             "variants": {"note": "BASELINE.json's variants of this config, each its own trainer (same lanes, K, "
                                  "ring), timed after the headline; eval not amortised", **variants} if variants else None,

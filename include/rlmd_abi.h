@@ -389,6 +389,21 @@ int rlmd_train_episode_drain(rlmd_env_t env, float* out_dev, int64_t out_cap, in
 int rlmd_train_set_fused(rlmd_env_t env, int32_t on);
 int rlmd_train_last_fused(rlmd_env_t env);
 
+/* What the replay row's `s` holds in rlmd_train_step (default
+ * RLMD_STORE_REFERENCE).  The reference's coin / dice / GBM / market envs return
+ * one self.next_state array that step() mutates in place (gbm_envs.py:125,
+ * 184-186, 212; market_envs.py:111, 172-174, 202), and its loop stores `state`
+ * after `state = next_state` (rl_multiplicative.py:213-245, rl_market.py:240-273),
+ * so from an episode's second step on the stored state IS the post-step state
+ * (s == s'); reset() returns a fresh array, so the first row holds the reset
+ * state.  Dice_SH returns a fresh array per step: rows hold the pre-step state.
+ * RLMD_STORE_REFERENCE reproduces this; RLMD_STORE_PRESTEP stores the true
+ * pre-step state for every family (a diagnostic, not the reference).
+ * rlmd_train_stored_state returns the mode in effect. */
+enum { RLMD_STORE_REFERENCE = 0, RLMD_STORE_PRESTEP = 1 };
+int rlmd_train_set_stored_state(rlmd_env_t env, int32_t mode);
+int rlmd_train_stored_state(rlmd_env_t env);
+
 /* Initialise obs_dev f32 [N, S] with every lane reset (episode start). */
 int rlmd_train_reset(rlmd_env_t env, float* obs_dev, void* stream);
 

@@ -24,6 +24,7 @@ import numpy as np
 from . import philox as px
 
 COIN, DICE, GBM, DICE_SH, MARKET = range(5)
+ALIAS_FAMILIES = (COIN, DICE, GBM, MARKET)  # reference envs with an in-place self.next_state
 INV_A, INV_B, INV_C, INV_INSURED = range(4)
 
 INITIAL_VALUE = 1e4
@@ -326,4 +327,19 @@ class OracleVecEnv:
                 risk[:, k:k + n] = levs
         self.wealth = W
         self.time = t + 1
+        self.last_time = t
         return ns, reward, np.stack([done, learn_done], 1), risk
+
+    def stored_state(self, obs, ns):
+        """The state the reference's loop stores for the step just taken (obs: the
+        pre-step observation, ns: step()'s next state).  Coin / dice / GBM / market
+        envs return one self.next_state array that step() mutates in place
+        (gbm_envs.py:125, 184-186, 212; market_envs.py:111, 172-174, 202); the loop
+        keeps state = next_state and stores state after the next step
+        (rl_multiplicative.py:213-245, rl_market.py:240-273; replay.py:164-167
+        copies then), so from an episode's second step (t > 1) the stored state
+        is the post-step state.  The first step stores reset()'s fresh array.
+        Dice_SH returns a new array per step (dice_roll_sh_envs.py:336-339)."""
+        if self.f not in ALIAS_FAMILIES:
+            return obs
+        return np.where((self.last_time > 1)[:, None], ns, obs)

@@ -97,6 +97,8 @@ SIGNATURES = {
     "rlmd_train_episode_log": (C.c_int, [P, C.c_int32]),
     "rlmd_train_set_fused": (C.c_int, [P, C.c_int32]),
     "rlmd_train_last_fused": (C.c_int, [P]),
+    "rlmd_train_set_stored_state": (C.c_int, [P, C.c_int32]),
+    "rlmd_train_stored_state": (C.c_int, [P]),
     "rlmd_train_episode_drain": (C.c_int, [P, P, C.c_int64, P, P, P]),
     "rlmd_env_lane_start": (C.c_int, [P, P]),
     "rlmd_env_write_prices": (C.c_int, [P, P, I64, I64, P]),

@@ -1,9 +1,12 @@
 """Build librlmd_amd.so (gfx950) in-tree with hipcc.
 
 The .so is the product: a C-ABI shared library (include/rlmd_abi.h) loaded by
-rlmd_amd/_abi.py with ctypes.  Objects are rebuilt only when a source or
-header is newer than the object.
+rlmd_amd/_abi.py with ctypes.  Objects are rebuilt when a source or header is
+newer than the object, or when the compile command differs from the one the
+object was built with (a per-object flags stamp): an experiment build's flags
+never leak into the production library.
 """
+import json
 import os
 import subprocess
 import sys
@@ -15,6 +18,9 @@ CSRC = os.path.join(HERE, "csrc")
 # tools/_abh/librlmd_amd_<tag>.so from objects in rlmd_amd/_build_<tag>; load it with RLMD_LIB_PATH
 _TAG = os.environ.get("RLMD_BUILD_TAG", "")
 EXTRA = os.environ.get("RLMD_EXTRA_FLAGS", "").split()
+if EXTRA and not _TAG:
+    raise RuntimeError("RLMD_EXTRA_FLAGS needs RLMD_BUILD_TAG: experiment flags never build the production "
+                       "library (rlmd_amd/librlmd_amd.so)")
 BUILD = os.path.join(HERE, "_build" + (f"_{_TAG}" if _TAG else ""))
 LIB = (os.path.join(HERE, "..", "tools", "_abh", f"librlmd_amd_{_TAG}.so") if _TAG
        else os.path.join(HERE, "librlmd_amd.so"))
@@ -36,8 +42,18 @@ def _headers():
         os.path.join(HERE, "..", "include", "rlmd_abi.h")]
 
 
-def _stale(obj, src, deps):
+def _stamp_path(obj):
+    return obj + ".flags"
+
+
+def _stale(obj, src, deps, cmd):
     if not os.path.exists(obj):
+        return True
+    try:
+        with open(_stamp_path(obj)) as f:
+            if json.load(f) != cmd:
+                return True
+    except (OSError, ValueError):
         return True
     deps = deps + [os.path.abspath(__file__)]
     t = os.path.getmtime(obj)
@@ -47,12 +63,14 @@ def _stale(obj, src, deps):
 def _compile(src):
     obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
     path = os.path.join(CSRC, src)
-    if not _stale(obj, path, _headers()):
-        return obj, None
     cmd = [HIPCC, *FLAGS, *PER_FILE.get(src, DEFAULT_EXTRA), *EXTRA, "-c", path, "-o", obj]
+    if not _stale(obj, path, _headers(), cmd):
+        return obj, None
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"$ {' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
+    with open(_stamp_path(obj), "w") as f:
+        json.dump(cmd, f)
     return obj, None
 
 

@@ -24,6 +24,7 @@
 #pragma clang fp contract(off)
 #include <math.h>
 #include <stdlib.h>
+#include <stddef.h>
 #include <string.h>
 #include <hip/hip_ext.h>
 
@@ -95,6 +96,14 @@ struct EnvParams {
   int fam, inv, n_lanes, n, obs_days, time_length, action_days, shuffle_days;
   int state_dim, action_dim, risk_dim, draw_dim, ext_len, start_range, n_days;
   int slice_groups;  // market: lanes sharing slice draws in groups (lane % G; 0 = per lane)
+  // replay rows store s = s' from an episode's second step on: the reference's
+  // coin / dice / GBM / market envs return one self.next_state array mutated in
+  // place (e.g. gbm_envs.py:125, 184-186, 212), its loop keeps state = next_state
+  // (rl_multiplicative.py:245, rl_market.py:273) and stores state after the
+  // next env.step (:218-220; replay.py:164-167 copies then); reset() returns a
+  // fresh array (gbm_envs.py:224-229), so an episode's first row keeps the reset
+  // state.  Dice_SH builds a new array per step (dice_roll_sh_envs.py:336): 0.
+  int alias_state;
   uint64_t seed;
   const double* prices;  // market [n_days, n]
   // lane state
@@ -614,22 +623,26 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
       }
     };
     const int64_t row = ring_row(ring_base, lane, rb.capacity);
-    // s (the current obs) goes to the ring unchanged.  gfx9 counts stores in
-    // vmcnt, so a store issued before the compute would be waited on at the first
-    // use of a loaded value: the first 8 obs elements are loaded now and stored
-    // after the step; the rest (market Dx only) are copied here, before the
-    // next-state writes overwrite obs.
+    // the stored s: the reference's aliased post-step state from an episode's
+    // second step on (EnvParams::alias_state), else the current obs unchanged
+    const bool alias = P.alias_state && t > 1;
+    // gfx9 counts stores in vmcnt, so a store issued before the compute would be
+    // waited on at the first use of a loaded value: the first 8 obs elements are
+    // loaded now and stored after the step; the rest (market Dx only) are copied
+    // here, before the next-state writes overwrite obs.
     const __amdgpu_buffer_rsrc_t ro = rlmd_rsrc(obs, (int64_t)P.n_lanes * S * 4);
     float s0[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) s0[j] = rlmd_ldf(ro, (int64_t)lane * S + j, j < S);
-    for (int k0 = 8; k0 < S; k0 += 8) {
-      float v[8];
+    for (int j = 0; j < 8; ++j) s0[j] = rlmd_ldf(ro, (int64_t)lane * S + j, j < S && !alias);
+    if (!alias) {
+      for (int k0 = 8; k0 < S; k0 += 8) {
+        float v[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = rlmd_ldf(ro, (int64_t)lane * S + k0 + j, k0 + j < S);
+        for (int j = 0; j < 8; ++j) v[j] = rlmd_ldf(ro, (int64_t)lane * S + k0 + j, k0 + j < S);
 #pragma unroll
-      for (int j = 0; j < 8; ++j)
-        if (k0 + j < S) rb.state[row * S + k0 + j] = v[j];
+        for (int j = 0; j < 8; ++j)
+          if (k0 + j < S) rb.state[row * S + k0 + j] = v[j];
+      }
     }
 
     // the one draw of a single-gamble lane depends on (seed, lane, step) only: its
@@ -643,6 +656,7 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
         [&](int k, double v) {
           const float f = (float)v;
           rb.next_state[row * S + k] = f;
+          if (alias) rb.state[row * S + k] = f;
           obs[(int64_t)lane * S + k] = f;
         },
         [&](int k, double v) {
@@ -669,9 +683,11 @@ __global__ void __launch_bounds__(256) env_train_kernel(EnvParams P, uint32_t st
       er[2] = (float)o.reward;
       er[3] = (float)t;
     }
+    if (!alias) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < S) rb.state[row * S + j] = s0[j];
+      for (int j = 0; j < 8; ++j)
+        if (j < S) rb.state[row * S + j] = s0[j];
+    }
     for (int i = 0; i < A; ++i) rb.action[row * A + i] = (float)act(i);
     rb.reward[row] = (float)o.reward;  // max(reward, r_abs_zero = -inf)
     rb.done[row] = o.learn_done;
@@ -749,11 +765,24 @@ __device__ __forceinline__ void store_row(float* dst, const float* v) {
   if constexpr (N % 2 == 1) dst[k] = v[k];
 }
 
+// act_env_kernel's explicit arguments as laid out in the kernarg segment (in
+// order, each at its natural alignment): their exact byte count bounds the
+// argument prefetch
+struct ActEnvKargs {
+  rlmd::FusedActArgs a;
+  EnvParams P;
+  uint32_t step;
+  float* obs;
+  rlmd::ReplayView rb;
+  int64_t ring_base;
+  StatFold sf;
+};
+
 template <int FAM, int NG, int H1P, int NB, int SP, int MA>
 __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA ? 3 : 2) : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
                                                       StatFold sf) {
-  rlmd_kernarg_prefetch<(int)(sizeof(a) + sizeof(P) + sizeof(rb) + sizeof(sf) + 32)>();
+  rlmd_kernarg_prefetch<(int)(offsetof(ActEnvKargs, sf) + sizeof(StatFold))>();
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if (blockIdx.x == 0 && sf.fold_src)
     fold_stat_rows(sf.fold_src, sf.rows, sf.fold_dst, reinterpret_cast<double(*)[256]>(smem));
@@ -786,6 +815,9 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
       else return i == 0 ? acts[0] : i == 1 ? acts[1] : i == 2 ? acts[2] : acts[3];
     };
     const int64_t row = ring_row(ring_base, b, rb.capacity);
+    // the stored s: the aliased post-step state from an episode's second step on
+    // (EnvParams::alias_state, env_train_kernel), else this row's observation
+    const bool alias = P.alias_state && t > 1;
     int64_t ep_slot = -1;
     // a compile-time state width keeps the next state in registers (every put()
     // index is a constant once env_step_lane is inlined) for row-wide stores
@@ -799,6 +831,7 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
             ns[k] = f;
           } else {
             rb.next_state[row * S + k] = f;
+            if (alias) rb.state[row * S + k] = f;
             obs[(int64_t)b * S + k] = f;
           }
         },
@@ -826,11 +859,11 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
     if constexpr (SR > 0) {
       float s0[SR];
 #pragma unroll
-      for (int j = 0; j < SR; ++j) s0[j] = obs_row[j];
+      for (int j = 0; j < SR; ++j) s0[j] = alias ? ns[j] : obs_row[j];
       store_row<SR>(rb.state + row * SR, s0);
       store_row<SR>(rb.next_state + row * SR, ns);
       if (!o.done) store_row<SR>(obs + (int64_t)b * SR, ns);  // a finished lane's obs is its reset state
-    } else {
+    } else if (!alias) {
       for (int j = 0; j < S; ++j) rb.state[row * S + j] = obs_row[j];
     }
     if (A == 2)
@@ -1617,6 +1650,7 @@ int rlmd_env_create(const rlmd_env_cfg* cfg, const double* prices_host, int64_t 
   P.draw_dim = D;
   P.seed = cfg->seed;
   P.slice_groups = cfg->slice_groups > 0 ? cfg->slice_groups : 0;
+  P.alias_state = cfg->family != RLMD_DICE_SH;
   const size_t N = (size_t)cfg->n_lanes;
   if (cfg->family == RLMD_MARKET) {
     if (!prices_host || n_days <= 1 || cfg->time_length <= 0 || P.shuffle_days > 16) {
@@ -1796,6 +1830,17 @@ int rlmd_train_set_fused(rlmd_env_t env, int32_t on) {
 }
 
 int rlmd_train_last_fused(rlmd_env_t env) { return env ? env->last_fused : 0; }
+
+int rlmd_train_set_stored_state(rlmd_env_t env, int32_t mode) {
+  RLMD_CHECK(env, "null env");
+  RLMD_CHECK(mode == RLMD_STORE_REFERENCE || mode == RLMD_STORE_PRESTEP, "bad stored-state mode");
+  env->P.alias_state = mode == RLMD_STORE_REFERENCE && env->P.fam != RLMD_DICE_SH;
+  return 0;
+}
+
+int rlmd_train_stored_state(rlmd_env_t env) {
+  return env && !env->P.alias_state && env->P.fam != RLMD_DICE_SH ? RLMD_STORE_PRESTEP : RLMD_STORE_REFERENCE;
+}
 
 int rlmd_train_episode_log(rlmd_env_t env, int32_t cap_per_wave) {
   RLMD_CHECK(env, "null env");

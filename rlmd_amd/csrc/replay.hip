@@ -25,6 +25,7 @@
 #include <string>
 #include <vector>
 
+#include <stddef.h>
 #include "rlmd_common.h"
 #include "rlmd_internal.h"
 
@@ -162,11 +163,27 @@ __device__ __forceinline__ void gather_row1(const rlmd::ReplayView& rb, int64_t 
 constexpr int kMaxRounds = 64;
 constexpr int kSortPopulation = 8192;  // M at or below: sort-based subset
 
+// replay_sample_kernel's explicit arguments as laid out in the kernarg segment
+// (each at its natural alignment, in order): their exact byte count bounds the
+// argument prefetch
+struct SampleKargs {
+  rlmd::ReplayView rb;
+  int64_t M;
+  int B, G;
+  uint64_t seed;
+  uint32_t ctr_lo, ctr_hi;
+  int64_t* idx_out;
+  float *s, *a, *r, *s2;
+  uint8_t* done;
+  float* xsa;
+  int32_t* eff;
+};
+
 __global__ void __launch_bounds__(kSampleThreads)
     replay_sample_kernel(rlmd::ReplayView rb, int64_t M, int B, int G, uint64_t seed, uint32_t ctr_lo,
                          uint32_t ctr_hi, int64_t* idx_out, float* s, float* a,
                          float* r, float* s2, uint8_t* done, float* xsa, int32_t* eff) {
-  rlmd_kernarg_prefetch<(int)sizeof(rb) + 112>();
+  rlmd_kernarg_prefetch<(int)(offsetof(SampleKargs, eff) + sizeof(int32_t*))>();
   __shared__ uint64_t keys[kSortPopulation];
   __shared__ int64_t cand[kSampleThreads];
   __shared__ int any_dup;

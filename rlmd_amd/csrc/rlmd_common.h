@@ -174,50 +174,63 @@ __device__ __forceinline__ float rlmd_ldf(__amdgpu_buffer_rsrc_t r, int64_t idx,
 // early-clobber outputs: left to the compiler they came in clauses of 8 with a
 // wait after each, and split asm loads would let it reuse an output register
 // while its load is still in flight.
-template <int NL>
-__device__ __forceinline__ void rlmd_karg_lines(const void* kp);
-template <>
-__device__ __forceinline__ void rlmd_karg_lines<4>(const void* kp) {
+// Line offsets are clamped to the last dword of the explicit arguments
+// (LAST = BYTES - 4, rounded down to a dword): lines past the end repeat that
+// dword instead of reading past the arguments, where the kernarg allocation of a
+// kernel whose hidden arguments the compiler trimmed may end.
+template <int NL, int LAST>
+struct rlmd_karg_lines;
+template <int LAST>
+struct rlmd_karg_lines<4, LAST> {
+  static __device__ __forceinline__ void run(const void* kp) {
   uint32_t v[4];
-  __asm__ volatile("s_load_dword %0, %4, 0\n""s_load_dword %1, %4, 64\n""s_load_dword %2, %4, 128\n""s_load_dword %3, %4, 192\n"
+  __asm__ volatile("s_load_dword %0, %4, %5\n""s_load_dword %1, %4, %6\n""s_load_dword %2, %4, %7\n""s_load_dword %3, %4, %8\n"
                    "s_waitcnt lgkmcnt(0)"
                    : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3])
-                   : "s"(kp)
+                   : "s"(kp), "i"(0 < LAST ? 0 : LAST), "i"(64 < LAST ? 64 : LAST), "i"(128 < LAST ? 128 : LAST), "i"(192 < LAST ? 192 : LAST)
                    : "memory");
-}
-template <>
-__device__ __forceinline__ void rlmd_karg_lines<8>(const void* kp) {
+  }
+};
+template <int LAST>
+struct rlmd_karg_lines<8, LAST> {
+  static __device__ __forceinline__ void run(const void* kp) {
   uint32_t v[8];
-  __asm__ volatile("s_load_dword %0, %8, 0\n""s_load_dword %1, %8, 64\n""s_load_dword %2, %8, 128\n""s_load_dword %3, %8, 192\n""s_load_dword %4, %8, 256\n""s_load_dword %5, %8, 320\n""s_load_dword %6, %8, 384\n""s_load_dword %7, %8, 448\n"
+  __asm__ volatile("s_load_dword %0, %8, %9\n""s_load_dword %1, %8, %10\n""s_load_dword %2, %8, %11\n""s_load_dword %3, %8, %12\n""s_load_dword %4, %8, %13\n""s_load_dword %5, %8, %14\n""s_load_dword %6, %8, %15\n""s_load_dword %7, %8, %16\n"
                    "s_waitcnt lgkmcnt(0)"
                    : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3]), "=&s"(v[4]), "=&s"(v[5]), "=&s"(v[6]), "=&s"(v[7])
-                   : "s"(kp)
+                   : "s"(kp), "i"(0 < LAST ? 0 : LAST), "i"(64 < LAST ? 64 : LAST), "i"(128 < LAST ? 128 : LAST), "i"(192 < LAST ? 192 : LAST), "i"(256 < LAST ? 256 : LAST), "i"(320 < LAST ? 320 : LAST), "i"(384 < LAST ? 384 : LAST), "i"(448 < LAST ? 448 : LAST)
                    : "memory");
-}
-template <>
-__device__ __forceinline__ void rlmd_karg_lines<12>(const void* kp) {
+  }
+};
+template <int LAST>
+struct rlmd_karg_lines<12, LAST> {
+  static __device__ __forceinline__ void run(const void* kp) {
   uint32_t v[12];
-  __asm__ volatile("s_load_dword %0, %12, 0\n""s_load_dword %1, %12, 64\n""s_load_dword %2, %12, 128\n""s_load_dword %3, %12, 192\n""s_load_dword %4, %12, 256\n""s_load_dword %5, %12, 320\n""s_load_dword %6, %12, 384\n""s_load_dword %7, %12, 448\n""s_load_dword %8, %12, 512\n""s_load_dword %9, %12, 576\n""s_load_dword %10, %12, 640\n""s_load_dword %11, %12, 704\n"
+  __asm__ volatile("s_load_dword %0, %12, %13\n""s_load_dword %1, %12, %14\n""s_load_dword %2, %12, %15\n""s_load_dword %3, %12, %16\n""s_load_dword %4, %12, %17\n""s_load_dword %5, %12, %18\n""s_load_dword %6, %12, %19\n""s_load_dword %7, %12, %20\n""s_load_dword %8, %12, %21\n""s_load_dword %9, %12, %22\n""s_load_dword %10, %12, %23\n""s_load_dword %11, %12, %24\n"
                    "s_waitcnt lgkmcnt(0)"
                    : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3]), "=&s"(v[4]), "=&s"(v[5]), "=&s"(v[6]), "=&s"(v[7]), "=&s"(v[8]), "=&s"(v[9]), "=&s"(v[10]), "=&s"(v[11])
-                   : "s"(kp)
+                   : "s"(kp), "i"(0 < LAST ? 0 : LAST), "i"(64 < LAST ? 64 : LAST), "i"(128 < LAST ? 128 : LAST), "i"(192 < LAST ? 192 : LAST), "i"(256 < LAST ? 256 : LAST), "i"(320 < LAST ? 320 : LAST), "i"(384 < LAST ? 384 : LAST), "i"(448 < LAST ? 448 : LAST), "i"(512 < LAST ? 512 : LAST), "i"(576 < LAST ? 576 : LAST), "i"(640 < LAST ? 640 : LAST), "i"(704 < LAST ? 704 : LAST)
                    : "memory");
-}
-template <>
-__device__ __forceinline__ void rlmd_karg_lines<16>(const void* kp) {
+  }
+};
+template <int LAST>
+struct rlmd_karg_lines<16, LAST> {
+  static __device__ __forceinline__ void run(const void* kp) {
   uint32_t v[16];
-  __asm__ volatile("s_load_dword %0, %16, 0\n""s_load_dword %1, %16, 64\n""s_load_dword %2, %16, 128\n""s_load_dword %3, %16, 192\n""s_load_dword %4, %16, 256\n""s_load_dword %5, %16, 320\n""s_load_dword %6, %16, 384\n""s_load_dword %7, %16, 448\n""s_load_dword %8, %16, 512\n""s_load_dword %9, %16, 576\n""s_load_dword %10, %16, 640\n""s_load_dword %11, %16, 704\n""s_load_dword %12, %16, 768\n""s_load_dword %13, %16, 832\n""s_load_dword %14, %16, 896\n""s_load_dword %15, %16, 960\n"
+  __asm__ volatile("s_load_dword %0, %16, %17\n""s_load_dword %1, %16, %18\n""s_load_dword %2, %16, %19\n""s_load_dword %3, %16, %20\n""s_load_dword %4, %16, %21\n""s_load_dword %5, %16, %22\n""s_load_dword %6, %16, %23\n""s_load_dword %7, %16, %24\n""s_load_dword %8, %16, %25\n""s_load_dword %9, %16, %26\n""s_load_dword %10, %16, %27\n""s_load_dword %11, %16, %28\n""s_load_dword %12, %16, %29\n""s_load_dword %13, %16, %30\n""s_load_dword %14, %16, %31\n""s_load_dword %15, %16, %32\n"
                    "s_waitcnt lgkmcnt(0)"
                    : "=&s"(v[0]), "=&s"(v[1]), "=&s"(v[2]), "=&s"(v[3]), "=&s"(v[4]), "=&s"(v[5]), "=&s"(v[6]), "=&s"(v[7]), "=&s"(v[8]), "=&s"(v[9]), "=&s"(v[10]), "=&s"(v[11]), "=&s"(v[12]), "=&s"(v[13]), "=&s"(v[14]), "=&s"(v[15])
-                   : "s"(kp)
+                   : "s"(kp), "i"(0 < LAST ? 0 : LAST), "i"(64 < LAST ? 64 : LAST), "i"(128 < LAST ? 128 : LAST), "i"(192 < LAST ? 192 : LAST), "i"(256 < LAST ? 256 : LAST), "i"(320 < LAST ? 320 : LAST), "i"(384 < LAST ? 384 : LAST), "i"(448 < LAST ? 448 : LAST), "i"(512 < LAST ? 512 : LAST), "i"(576 < LAST ? 576 : LAST), "i"(640 < LAST ? 640 : LAST), "i"(704 < LAST ? 704 : LAST), "i"(768 < LAST ? 768 : LAST), "i"(832 < LAST ? 832 : LAST), "i"(896 < LAST ? 896 : LAST), "i"(960 < LAST ? 960 : LAST)
                    : "memory");
-}
+  }
+};
 template <int BYTES>
 __device__ __forceinline__ void rlmd_kernarg_prefetch() {
   // lines of the explicit arguments, rounded up to a multiple of 4 (<= 16: 1 KB)
   constexpr int nl = (BYTES + 63) / 64, n4 = ((nl + 3) / 4) * 4;
   static_assert(n4 <= 16, "kernel arguments above 1 KB");
-  rlmd_karg_lines<n4>((const void*)__builtin_amdgcn_kernarg_segment_ptr());
+  static_assert(BYTES >= 4, "kernel arguments below one dword");
+  rlmd_karg_lines<n4, ((BYTES - 4) / 4) * 4>::run((const void*)__builtin_amdgcn_kernarg_segment_ptr());
 }
 #ifndef RLMD_KARG_PF
 #define RLMD_KARG_PF 1

@@ -22,6 +22,10 @@ INVESTOR = {"A": _abi.INV_A, "B": _abi.INV_B, "C": _abi.INV_C, "INSURED": _abi.I
 MAX_VALUE = {_abi.COIN: 1e18, _abi.DICE: 1e18, _abi.GBM: 1e18, _abi.DICE_SH: 1e18, _abi.MARKET: 1e34}
 MIN_REWARD = {_abi.COIN: 1e-3, _abi.DICE: 1e-3, _abi.GBM: 1e-3, _abi.DICE_SH: 1e-6, _abi.MARKET: 1e-3}
 MAX_ABS_ACTION = 0.99
+# families whose reference env returns one self.next_state array mutated in place by
+# every step (Dice_SH builds a new one per step); the vectorised trainer's replay
+# rows follow the same rule (rlmd_train_set_stored_state)
+ALIAS_FAMILIES = frozenset({_abi.COIN, _abi.DICE, _abi.GBM, _abi.MARKET})
 
 _SEED_CTR = [0]
 
@@ -151,17 +155,39 @@ class _SingleEnv:
         self.reward_range = (MIN_REWARD[self._v.family], np.inf)
         self.observation_space = Box(-np.inf, np.inf, (self._v.state_dim,))
         self.action_space = Box(-MAX_ABS_ACTION, MAX_ABS_ACTION, (self._v.action_dim,))
+        # the reference env's reused self.next_state buffer (None: a new array per step)
+        self._next_state = (np.empty(self._v.state_dim, dtype=np.float64) if self._v.family in ALIAS_FAMILIES
+                            else None)
 
     def reset(self):
+        """A fresh array per call (gbm_envs.py:224-229)."""
         return self._v.reset()[0].cpu().numpy().copy()
 
     def step(self, action):
+        """(next_state, reward, [done, learn_done], risk).  next_state is ONE array
+        per env that every step overwrites in place for the families whose
+        reference env does so (self.next_state: coin_flip_envs.py:128, 188-190,
+        216; dice_roll_envs.py:131, 191-193; gbm_envs.py:125, 184-186, 212;
+        market_envs.py:111, 172-174, 202): a driver that keeps
+        ``state = next_state`` and stores ``state`` after the next step stores the
+        post-step state, as the reference's loop does (rl_multiplicative.py:
+        213-245).  Dice_SH returns a new array per step (dice_roll_sh_envs.py:
+        336-339)."""
+        return self._step(action, None)
+
+    def _step(self, action, draws):
+        """step() with optional injected draws f64 [1, D] (test hook)."""
         arr = np.asarray(action)
         a = torch.as_tensor(arr.astype(np.float64 if arr.dtype == np.float64 else np.float32).reshape(1, -1))
-        ns, r, d, risk = self._v.step(a)
+        ns, r, d, risk = self._v.step(a, draws=draws)
         d = d[0].cpu().numpy()
-        return (ns[0].cpu().numpy().copy(), np.float64(r[0].item()), [bool(d[0]), bool(d[1])],
-                risk[0].cpu().numpy().copy())
+        s2 = ns[0].cpu().numpy()
+        if self._next_state is not None:
+            self._next_state[:] = s2
+            s2 = self._next_state
+        else:
+            s2 = s2.copy()
+        return s2, np.float64(r[0].item()), [bool(d[0]), bool(d[1])], risk[0].cpu().numpy().copy()
 
 
 def _make(name, fam, inv, sh=False):

@@ -53,12 +53,12 @@ class VecTrainer:
                  smoothing_window=2000, precision="bf16", hidden=None, batch=None, topk=None,
                  prices=None, obs_days=1, time_length=0, shuffle_days=5, sample_days=0,
                  device="cuda:0", init_seed=None, multi_steps=1, dynamics="A", gamma=0.99, s_dist="N",
-                 initial_logtemp=0.0, agent_kw=None, slice_groups=0, cu_budget=None):
+                 initial_logtemp=0.0, agent_kw=None, slice_groups=0, cu_budget=None, stored_state="reference"):
         """warmup_steps / smoothing_window: vector steps per lane (the ABI's counters;
         schedule_steps converts the reference's lengths).  agent_kw: further
         DeviceAgent settings (update intervals, learning rates, ...).  cu_budget:
         the CUs this trainer's learner may count on (rlmd_agent_set_cu_budget;
-        None = the device's)."""
+        None = the device's).  stored_state: see set_stored_state."""
         self.device = torch.device(device)
         self.env = VecEnv(env, investor, n_lanes, n_gambles, seed=seed, prices=prices, obs_days=obs_days,
                           time_length=time_length, shuffle_days=shuffle_days, sample_days=sample_days,
@@ -87,6 +87,8 @@ class VecTrainer:
         self.ep_stats = torch.zeros(4, dtype=torch.float64, device=self.device)
         self.stats = torch.full((max(k_updates, 1), 16), float("nan"), dtype=torch.float32, device=self.device)
         check(_abi.lib().rlmd_train_reset(self.env.h, ptr(self.obs), stream_ptr()))
+        if stored_state != "reference":
+            self.set_stored_state(stored_state)
 
     @property
     def cum_step(self):
@@ -111,6 +113,17 @@ class VecTrainer:
 
     def last_fused(self):
         return bool(_abi.lib().rlmd_train_last_fused(self.env.h))
+
+    def set_stored_state(self, mode):
+        """What replay rows store as `s` (rlmd_train_set_stored_state):
+        "reference" (default) = the reference loop's aliased post-step state from
+        an episode's second step on (coin / dice / GBM / market; Dice_SH keeps the
+        pre-step state), "prestep" = the true pre-step state (a diagnostic)."""
+        code = {"reference": 0, "prestep": 1}[mode]
+        check(_abi.lib().rlmd_train_set_stored_state(self.env.h, code))
+
+    def stored_state(self):
+        return ("reference", "prestep")[_abi.lib().rlmd_train_stored_state(self.env.h)]
 
     def profile(self, mode):
         """rlmd_profile_enable on this trainer's agent: 0 off, 1 every phase, 2 the

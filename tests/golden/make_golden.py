@@ -933,34 +933,51 @@ class _RecordingRandom:
         cdf /= cdf[-1]
         return np.asarray(a)[cdf.searchsorted(u, side="right")]
 
+    def normal(self, loc=0.0, scale=1.0, size=None):
+        # legacy normal(loc, scale) = loc + scale * gauss(), gauss being the stream
+        # standard_normal draws from: bit-identical (checked over 20,000 draws)
+        z = np.random.standard_normal(size)
+        self.sink(np.atleast_1d(z).astype(np.float64))
+        return loc + scale * z
 
-def c1_trace(n_steps=2500, seed=0):
-    """Config C1 as the reference runs it: main.py's tables (Coin_InvA, key 8),
-    SAC, MSE, one trial of n_steps with eval_freq 1e3, seeded np.random + torch,
-    through scripts/rl_multiplicative.multiplicative_env.  n_steps = 2500 covers
-    the warm-up (|sample|, <= 1e3), the smoothing window (f64 clip, <= 2e3) and
-    the policy phase.  Recorded for the TRAINING env instance: every step's
-    action as the env received it, the coin draw u, state / next_state / reward /
-    done / risk; every select_next_action output (pre-window) and learn() return;
-    the cum_steps of every save_models(); and the saved trial / trial_risk logs."""
+
+def c1_trace(n_steps=2500, seed=0, key=8):
+    """Config C1 as the reference runs it: main.py's tables (key 8 = Coin_InvA;
+    key 14 = GBM_InvA, C2's env), SAC, MSE, one trial of n_steps with eval_freq
+    1e3, seeded np.random + torch, through
+    scripts/rl_multiplicative.multiplicative_env.  n_steps = 2500 covers the
+    warm-up (|sample| except GBM, <= 1e3), the smoothing window (f64 clip,
+    <= 2e3) and the policy phase.  Recorded for the TRAINING env instance: every
+    step's action as the env received it, the env draw (coin: the choice uniform
+    u; GBM: the standard normal z of normal(LOG_MEAN, VOL)), the pre-step state /
+    next_state / reward / done / risk; what store_transistion RECEIVED, copied
+    at call time (stored_state / stored_next_state: the reference's env mutates
+    one self.next_state array and the loop stores state after state =
+    next_state, rl_multiplicative.py:213-245, so from an episode's second step
+    the stored state is the post-step state); every select_next_action output
+    (pre-window) and learn() return; the cum_steps of every save_models(); and
+    the saved trial / trial_risk logs."""
     import importlib
 
     import main as ref_main
-    import envs.coin_flip_envs as cf
     from algos import algo_sac
     from tools import utils
 
-    rec = {k: [] for k in ("action", "u", "state", "next_state", "reward", "done", "risk", "policy",
-                           "learn_loss", "learn_logtemp", "learn_params", "learn_step", "save_step")}
+    name = ref_main.gym_envs[str(key)][0]
+    cf = importlib.import_module({"Coin": "envs.coin_flip_envs", "GBM_": "envs.gbm_envs"}[name[:4]])
+    rec = {k: [] for k in ("action", "draw", "state", "next_state", "reward", "done", "risk", "policy",
+                           "learn_loss", "learn_logtemp", "learn_params", "learn_step", "save_step",
+                           "stored_state", "stored_next_state")}
     env_ids = []
     ctr = {"steps": 0}
     cur_u = []
     cf_np = _NpProxy(_RecordingRandom(cur_u.append))
     saved_np = cf.np
-    cls = cf.Coin_InvA
+    cls = getattr(cf, name)
     orig_init, orig_step, orig_reset = cls.__init__, cls.step, cls.reset
     orig_sel, orig_learn, orig_save = algo_sac.Agent_sac.select_next_action, algo_sac.Agent_sac.learn, \
         algo_sac.Agent_sac.save_models
+    orig_store = algo_sac.Agent_sac.store_transistion
 
     def init(self, *a, **kw):
         orig_init(self, *a, **kw)
@@ -975,7 +992,7 @@ def c1_trace(n_steps=2500, seed=0):
         cur_u.clear()
         s2, r, d, risk = orig_step(self, action)
         if train:
-            rec["u"].append(np.array(cur_u[0], dtype=np.float64).copy())
+            rec["draw"].append(np.array(cur_u[0], dtype=np.float64).copy())
             rec["next_state"].append(np.asarray(s2, np.float64).copy())
             rec["reward"].append(float(r))
             rec["done"].append(list(d))
@@ -994,6 +1011,11 @@ def c1_trace(n_steps=2500, seed=0):
         rec["policy"].append(np.asarray(a).astype(np.float64).copy())
         return a
 
+    def store(self, state, action, reward, next_state, done):
+        rec["stored_state"].append(np.asarray(state, np.float64).copy())
+        rec["stored_next_state"].append(np.asarray(next_state, np.float64).copy())
+        return orig_store(self, state, action, reward, next_state, done)
+
     def learn(self):
         loss, logtemp, params = orig_learn(self)
         rec["learn_loss"].append(np.asarray([float(x) for x in loss], np.float64))
@@ -1009,7 +1031,7 @@ def c1_trace(n_steps=2500, seed=0):
     cf.np = cf_np
     cls.__init__, cls.step, cls.reset = init, step, reset
     algo_sac.Agent_sac.select_next_action, algo_sac.Agent_sac.learn = sel, learn
-    algo_sac.Agent_sac.save_models = save
+    algo_sac.Agent_sac.save_models, algo_sac.Agent_sac.store_transistion = save, store
     rl = importlib.import_module("scripts.rl_multiplicative")
     rl.Agent_sac = algo_sac.Agent_sac
     import contextlib
@@ -1017,11 +1039,13 @@ def c1_trace(n_steps=2500, seed=0):
     import io
 
     try:
+        for f in glob.glob("results/test_multiplicative/**/*.npy", recursive=True):
+            os.remove(f)
         inputs = dict(ref_main.inputs)
         inputs.update({"n_trials_mul": 1, "n_cumsteps_mul": float(n_steps), "gpu": "cpu", "buffer_gpu": False})
-        inputs = utils.input_initialisation(inputs, [8], ["SAC"], ["MSE"], [1])
+        inputs = utils.input_initialisation(inputs, [key], ["SAC"], ["MSE"], [1])
         inputs["test_agent"] = True
-        inputs["ENV_KEY"] = 8
+        inputs["ENV_KEY"] = key
         np.random.seed(seed)
         T.manual_seed(seed)
         with contextlib.redirect_stdout(io.StringIO()):
@@ -1032,13 +1056,21 @@ def c1_trace(n_steps=2500, seed=0):
         cf.np = saved_np
         cls.__init__, cls.step, cls.reset = orig_init, orig_step, orig_reset
         algo_sac.Agent_sac.select_next_action, algo_sac.Agent_sac.learn = orig_sel, orig_learn
-        algo_sac.Agent_sac.save_models = orig_save
+        algo_sac.Agent_sac.save_models, algo_sac.Agent_sac.store_transistion = orig_save, orig_store
     out = {k: np.asarray(v) for k, v in rec.items()}
     out["trial"] = trial
     out["trial_risk"] = trial_risk
     out["n_steps"] = np.array(n_steps)
     out["seed"] = np.array(seed)
+    out["key"] = np.array(key)
     return out
+
+
+def c1_gbm_trace():
+    """F6-GBM: c1_trace on GBM_InvA (key 14, C2's env): the family whose state
+    (wealth / 1e18) is not negligible, so the stored-state aliasing changes the
+    critic's input."""
+    return c1_trace(key=14)
 
 
 # ----------------------------------------------------------------------------
@@ -1070,11 +1102,12 @@ def market_trace(obs_days, n_steps=2500, seed=0, key=22, algo="TD3", loss_fn="HU
     rec = {k: [] for k in ("action", "action_dtype", "obs", "state", "next_state", "reward", "done", "risk",
                            "policy", "learn_loss", "learn_logtemp", "learn_params", "save_step", "start_idx",
                            "extract", "reset_obs", "eval_start_idx", "eval_cum_steps", "eval_loss",
-                           "eval_logtemp", "eval_params")}
+                           "eval_logtemp", "eval_params", "stored_state", "stored_next_state")}
     env_ids, ctx = [], {"eval": False, "steps": 0}
     cls = getattr(me, "Market_" + ref_main.gym_envs[str(key)][0][-4:] + ("_D1" if obs_days == 1 else "_Dx"))
     orig = dict(init=cls.__init__, step=cls.step, reset=cls.reset, ts=er.time_slice, sd=er.shuffle_data,
-                ev=ev.eval_market, sel=agent_cls.select_next_action, learn=agent_cls.learn, save=agent_cls.save_models)
+                ev=ev.eval_market, sel=agent_cls.select_next_action, learn=agent_cls.learn, save=agent_cls.save_models,
+                store=agent_cls.store_transistion)
 
     def init(self, *a, **kw):
         env_ids.append(id(self))  # before the constructor's own reset(assets=None)
@@ -1137,6 +1170,11 @@ def market_trace(obs_days, n_steps=2500, seed=0, key=22, algo="TD3", loss_fn="HU
         rec["policy"].append(np.asarray(a).astype(np.float64).copy())
         return a
 
+    def store(self, state, action, reward, next_state, done):
+        rec["stored_state"].append(np.asarray(state, np.float64).copy())
+        rec["stored_next_state"].append(np.asarray(next_state, np.float64).copy())
+        return orig["store"](self, state, action, reward, next_state, done)
+
     def learn(self):
         loss, logtemp, params = orig["learn"](self)
         rec["learn_loss"].append(np.asarray([float(x) for x in loss], np.float64))
@@ -1151,6 +1189,7 @@ def market_trace(obs_days, n_steps=2500, seed=0, key=22, algo="TD3", loss_fn="HU
     cls.__init__, cls.step, cls.reset = init, step, reset
     er.time_slice, er.shuffle_data, ev.eval_market = time_slice, shuffle_data, eval_market
     agent_cls.select_next_action, agent_cls.learn, agent_cls.save_models = sel, learn, save
+    agent_cls.store_transistion = store
     rl = importlib.import_module("scripts.rl_market")
     import contextlib
     import glob
@@ -1176,6 +1215,7 @@ def market_trace(obs_days, n_steps=2500, seed=0, key=22, algo="TD3", loss_fn="HU
         cls.__init__, cls.step, cls.reset = orig["init"], orig["step"], orig["reset"]
         er.time_slice, er.shuffle_data, ev.eval_market = orig["ts"], orig["sd"], orig["ev"]
         agent_cls.select_next_action, agent_cls.learn, agent_cls.save_models = orig["sel"], orig["learn"], orig["save"]
+        agent_cls.store_transistion = orig["store"]
     out = {k: np.asarray(v) for k, v in rec.items() if k != "extract"}
     out["extract"] = np.stack(rec["extract"])  # every slice has train_length + 1 rows
     for nm, v in logs_out.items():
@@ -1378,6 +1418,7 @@ def main():
         "learn.npz": learn_fixtures,
         "lev.npz": lev_fixtures,
         "c1_trace.npz": c1_trace,
+        "c1_gbm_trace.npz": c1_gbm_trace,
         "market_trace.npz": market_traces,
         "env_resources_kat.npz": env_resources_kat,
         "aggregate.npz": aggregate_fixtures,

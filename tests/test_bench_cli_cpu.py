@@ -53,3 +53,18 @@ def test_gpus_world_mismatch_refused():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--dry-run", "--gpus", "2"],
                        capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
     assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_seed_processes_protocol():
+    """--seed-procs: one child process per seed (SeedProcs / seed_worker), built
+    and warmed on "run", started together on "go"; the group's rate is T x
+    lanes x n_t over the span from the first start to the last end."""
+    lanes = 64
+    out = _run("--steps", "3", "--warmup", "1", "--lanes", str(lanes), "--seed-procs", "1,2,3")
+    sp = out["seeds_per_gpu_processes"]
+    assert sorted(sp) == ["1", "2", "3"]
+    for T, r in sp.items():
+        assert len(r["per_seed_ms_per_step"]) == int(T)
+        assert r["env_steps_per_s"] == pytest.approx(int(T) * lanes * 5 / r["span_s"], rel=1e-12)
+        # the stand-in sleeps 2 ms per step in every process: the seeds overlap
+        assert r["span_s"] < int(T) * 5 * 0.002 * 0.9 or int(T) == 1

@@ -2,9 +2,11 @@
 
 F6 (tests/golden/c1_trace.npz, make_golden.c1_trace) is the reference's own
 scripts/rl_multiplicative.py loop (Coin_InvA, SAC, MSE, 2,500 steps: warm-up,
-smoothing window and policy phases), recorded step by step.  The replay test
-drives rlmd_amd.scripts.rl_multiplicative with
-  * an env that is the device Coin_InvA fed the reference's coin draws, and
+smoothing window and policy phases), recorded step by step, including what
+store_transistion received (the aliased post-step state from an episode's
+second step); F6-GBM (c1_gbm_trace.npz) is the same on GBM_InvA (key 14, C2's
+env).  The replay test drives rlmd_amd.scripts.rl_multiplicative with
+  * an env that is the device Coin_InvA / GBM_InvA fed the reference's draws, and
   * an agent that returns the reference's own policy outputs and learn() values,
 so everything in between is the build's: the warm-up |sample| rule, the
 float64 action window, the env step on the device, the episode bookkeeping,
@@ -38,14 +40,16 @@ def _c1_inputs(n_steps, n_trials=1, key=8, **kw):
     return inputs
 
 
-class _ReplayCoin:
-    """The device Coin_InvA with the reference's coin draws injected in order and
-    its warm-up samples replayed."""
+class _ReplayEnv:
+    """The device env of the trace (Coin_InvA / GBM_InvA) with the reference's
+    draws injected in order and its warm-up samples replayed.  Steps go through
+    the facade's own step (``_step`` with injected draws), so the driver gets
+    the facade's in-place next_state buffer, as it would from env.step."""
 
-    def __init__(self, f, dev):
-        from rlmd_amd.envs import Coin_InvA
+    def __init__(self, f, dev, name):
+        from rlmd_amd.envs import ENV_CLASSES
 
-        self._env = Coin_InvA(1, device=dev, seed=0)
+        self._env = ENV_CLASSES[name](1, device=dev, seed=0)
         self.observation_space = self._env.observation_space
         self.reward_range = self._env.reward_range
         self.f = f
@@ -69,12 +73,9 @@ class _ReplayCoin:
     def step(self, action):
         a = np.asarray(action)
         self.seen.append(a.copy())
-        u = torch.tensor(self.f["u"][self.t].reshape(1, -1), dtype=torch.float64)
-        at = torch.as_tensor(a.astype(np.float64 if a.dtype == np.float64 else np.float32).reshape(1, -1))
-        ns, r, d, risk = self._env._v.step(at, draws=u)
+        draw = torch.tensor(self.f["draw"][self.t].reshape(1, -1), dtype=torch.float64)
         self.t += 1
-        d = d[0].cpu().numpy()
-        return ns[0].cpu().numpy().copy(), float(r[0].item()), [bool(d[0]), bool(d[1])], risk[0].cpu().numpy().copy()
+        return self._env._step(a, draw)
 
 
 class _ScriptedAgent:
@@ -101,7 +102,8 @@ class _ScriptedAgent:
         return a
 
     def store_transistion(self, s, a, r, s2, d):
-        self.stored.append((np.asarray(s, np.float64).copy(), float(r), bool(d)))
+        # copied at call time, as the reference's ReplayBuffer.store_exp does (replay.py:164-167)
+        self.stored.append((np.asarray(s, np.float64).copy(), float(r), bool(d), np.asarray(s2, np.float64).copy()))
         self.n_store += 1
 
     def learn(self):
@@ -113,21 +115,25 @@ class _ScriptedAgent:
         self.saves.append(self.n_store)
 
 
-def test_c1_driver_replays_reference_loop(golden, dev, tmp_path, monkeypatch):
+@pytest.mark.parametrize("fixture", ["c1_trace.npz", "c1_gbm_trace.npz"])
+def test_c1_driver_replays_reference_loop(golden, dev, tmp_path, monkeypatch, fixture):
+    """F6 (Coin_InvA, key 8) and F6-GBM (GBM_InvA, key 14, C2's env)."""
     from rlmd_amd.config import GYM_ENVS
     from rlmd_amd.scripts.rl_multiplicative import multiplicative_env
 
-    f = golden("c1_trace.npz")
+    f = golden(fixture)
     n = int(f["n_steps"])
+    key = int(f["key"])
+    name = GYM_ENVS[str(key)][0]
     monkeypatch.chdir(tmp_path)
-    env = _ReplayCoin(f, dev)
+    env = _ReplayEnv(f, dev, name)
     holder = {}
 
     def factory(inputs):
         holder["agent"] = _ScriptedAgent(f, dev, inputs)
         return holder["agent"]
 
-    inputs = _c1_inputs(n, n_eval_mul=16)
+    inputs = _c1_inputs(n, n_eval_mul=16, key=key)
     (directory, trial, _, trial_risk, _), = multiplicative_env(GYM_ENVS, inputs, 1, env=env, agent_factory=factory,
                                                                log=None)
     ag = holder["agent"]
@@ -135,10 +141,18 @@ def test_c1_driver_replays_reference_loop(golden, dev, tmp_path, monkeypatch):
     seen = np.stack([np.asarray(a, np.float64).reshape(-1) for a in env.seen])
     np.testing.assert_array_equal(seen, f["action"].reshape(n, -1))  # warm-up |sample|, f64 window, policy
     np.testing.assert_array_equal(np.array([np.asarray(a).dtype == np.float64 for a in env.seen]), f["action_dtype"])
-    st = np.stack([s for s, _, _ in ag.stored])
-    np.testing.assert_allclose(st, f["state"], rtol=1e-12, atol=0)
-    np.testing.assert_allclose(np.array([r for _, r, _ in ag.stored]), f["reward"], rtol=1e-12, atol=0)
-    np.testing.assert_array_equal(np.array([d for _, _, d in ag.stored]), f["done"][:, 1])
+    # what store_transistion received: the reference's env mutates one next_state
+    # array and its loop stores state after state = next_state, so from an
+    # episode's second step the stored state IS the post-step state
+    # (rl_multiplicative.py:213-245, gbm_envs.py:184-186); the facade's in-place
+    # buffer reproduces it through the build's driver
+    st = np.stack([s for s, _, _, _ in ag.stored])
+    np.testing.assert_allclose(st, f["stored_state"], rtol=1e-12, atol=0)
+    np.testing.assert_allclose(np.stack([s2 for _, _, _, s2 in ag.stored]), f["stored_next_state"], rtol=1e-12, atol=0)
+    aliased = np.all(f["stored_state"] == f["stored_next_state"], 1)
+    assert aliased.sum() > n // 2 and not np.array_equal(f["stored_state"], f["state"])  # the fixture shows it
+    np.testing.assert_allclose(np.array([r for _, r, _, _ in ag.stored]), f["reward"], rtol=1e-12, atol=0)
+    np.testing.assert_array_equal(np.array([d for _, _, d, _ in ag.stored]), f["done"][:, 1])
     assert ag.i_learn == len(f["learn_loss"])
     assert ag.saves == f["save_step"].tolist()
     ref, ref_risk = f["trial"], f["trial_risk"]
@@ -162,7 +176,7 @@ def test_c1_driver_replays_reference_loop(golden, dev, tmp_path, monkeypatch):
     # own final risk vector, the values the reference's rows held when appended
     np.testing.assert_allclose(trial_risk[0], f["risk"][ends].astype(np.float32), rtol=1e-6, atol=0)
     assert np.all(ref_risk[0] == f["risk"][-1].astype(np.float32))
-    assert directory.startswith("./results/test_multiplicative/data/Coin_InvA_n1/")
+    assert directory.startswith(f"./results/test_multiplicative/data/{name}_n1/")
     for suffix in ("_trial.npy", "_eval.npy", "_trial_risk.npy", "_eval_risk.npy"):
         assert os.path.exists(directory + suffix)
 

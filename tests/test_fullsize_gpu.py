@@ -38,7 +38,7 @@ def test_c2_full_size_ring_and_learner(dev):
         tr.step()
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, (t * N) % cap, N)
         ns, r, d, _ = ora.step(a_r.astype(np.float32))  # policy actions: f32 (NumPy-2 dtype flow)
-        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s")
+        np.testing.assert_allclose(s_r, ora.stored_state(obs, ns).astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s")
         np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6, err_msg=f"t={t} r")
         np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=1e-30, err_msg=f"t={t} s2")
         np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
@@ -119,7 +119,7 @@ def _replay_steps(tr, ora, T, cap, atol=1e-30):
         tr.step()
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, (t * N) % cap, N)
         ns, r, d, _ = ora.step(a_r.astype(np.float32))
-        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=atol, err_msg=f"t={t} s")
+        np.testing.assert_allclose(s_r, ora.stored_state(obs, ns).astype(np.float32), rtol=1e-6, atol=atol, err_msg=f"t={t} s")
         np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6, err_msg=f"t={t} r")
         np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=atol, err_msg=f"t={t} s2")
         np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")

@@ -96,7 +96,7 @@ def _replay_policy_steps(golden, dev, env, inv, algo, n, obs_days):
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
         assert np.all(np.abs(a_r) <= 0.99) and np.all(np.isfinite(a_r))
         ns, r, d, risk = ora.step(a_r.astype(np.float32))  # post-window policy actions: f32
-        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s")
+        np.testing.assert_allclose(s_r, ora.stored_state(obs, ns).astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s")
         np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6, err_msg=f"t={t} r")
         np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s2")
         np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")
@@ -150,3 +150,46 @@ def test_fused_equals_unfused(golden, dev, env, inv, n, obs_days, algo):
     np.testing.assert_array_equal(ta, tb)
     np.testing.assert_array_equal(oa, ob)
     np.testing.assert_array_equal(pa, pb)  # the K = 1 updates learned from identical rings
+
+
+@pytest.mark.parametrize("fused", [1, 0])
+@pytest.mark.parametrize("env,inv,n,obs_days", [("gbm", "A", 1, 1), ("coin", "B", 1, 1), ("dice", "C", 1, 1),
+                                                ("market", "A", 1, 1), ("market", "B", 1, 5),
+                                                ("dice_sh", "A", 1, 1)])
+def test_stored_state_modes(golden, dev, env, inv, n, obs_days, fused):
+    """rlmd_train_set_stored_state: RLMD_STORE_REFERENCE (the default) stores the
+    reference loop's aliased state — s == s' from an episode's second step on
+    for coin / dice / GBM / market (their envs mutate one self.next_state,
+    gbm_envs.py:184-186; the loop stores state after state = next_state,
+    rl_multiplicative.py:213-245), the reset state on an episode's first step,
+    and the pre-step state for Dice_SH (a new array per step,
+    dice_roll_sh_envs.py:336).  RLMD_STORE_PRESTEP stores the pre-step state
+    everywhere.  Everything else in the two runs is bit-identical (no updates:
+    the same policy acts on the same observations).  market B at obs_days 5 has
+    S = 9 > 8 (the run-time-width store path of both kernels)."""
+    N, T = 1000, 14
+    rings, times = {}, {}
+    for mode in ("reference", "prestep"):
+        tr, _ = _trainer(dev, golden, env, inv, "SAC", N, T, k=0, seed=3, n=n, obs_days=obs_days)
+        tr.set_fused(fused)
+        if mode == "prestep":
+            tr.set_stored_state("prestep")
+        assert tr.stored_state() == ("prestep" if mode == "prestep" and env != "dice_sh" else "reference")
+        tb = []
+        for _ in range(T):
+            tb.append(tr.env.lane_state()[1].copy())
+            tr.step()
+        rings[mode], times[mode] = read_ring(tr, 0, N * T), np.concatenate(tb)
+        del tr
+    ref, pre = rings["reference"], rings["prestep"]
+    np.testing.assert_array_equal(times["reference"], times["prestep"])
+    for i, name in ((1, "a"), (2, "r"), (3, "s2"), (4, "d")):
+        np.testing.assert_array_equal(ref[i], pre[i], err_msg=name)
+    later = times["reference"] > 1
+    assert later.any() and (~later).any()  # both first steps (incl. auto-resets) and later steps
+    if env == "dice_sh":
+        np.testing.assert_array_equal(ref[0], pre[0])
+    else:
+        np.testing.assert_array_equal(ref[0][later], ref[3][later])  # s == s' (aliased)
+        np.testing.assert_array_equal(ref[0][~later], pre[0][~later])  # the reset state
+        assert not np.array_equal(pre[0][later], pre[3][later])

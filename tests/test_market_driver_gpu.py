@@ -50,6 +50,8 @@ def test_reference_api_market_env_matches_reference_episode(golden, dev, name):
         np.testing.assert_allclose(r, g[name + "/reward"][t], rtol=RTOL)
         assert dn == list(g[name + "/done"][t])
         np.testing.assert_allclose(risk, g[name + "/risk"][t], rtol=RTOL, equal_nan=True)
+        if t > 0:
+            assert ns is state  # one next_state array, overwritten in place (market_envs.py:111, 202)
         state = ns
     assert dn[0]  # the episode ends where the reference's did
     with pytest.raises(ValueError):
@@ -115,7 +117,8 @@ class _ScriptedAgent:
         return a
 
     def store_transistion(self, s, a, r, s2, d):
-        self.stored.append((np.asarray(s, np.float64).copy(), float(r), bool(d)))
+        # copied at call time (replay.py:164-167)
+        self.stored.append((np.asarray(s, np.float64).copy(), float(r), bool(d), np.asarray(s2, np.float64).copy()))
 
     def learn(self):
         i = self.i_learn
@@ -183,10 +186,16 @@ def test_market_driver_replays_reference_loop(golden, dev, tmp_path, monkeypatch
     np.testing.assert_array_equal(seen, f["action"])  # raw warm-up samples, f64 window, f32 policy
     np.testing.assert_array_equal(np.array([np.asarray(a).dtype == np.float64 for a in env.seen]), f["action_dtype"])
     # the device env's outputs
-    st = np.stack([s for s, _, _ in ag.stored])
-    np.testing.assert_allclose(st, f["state"], rtol=RTOL, atol=0)
-    np.testing.assert_allclose(np.array([r for _, r, _ in ag.stored]), f["reward"], rtol=RTOL, atol=0)
-    np.testing.assert_array_equal(np.array([d for _, _, d in ag.stored]), f["done"][:, 1])
+    # what store_transistion received: the market env mutates one next_state array
+    # (market_envs.py:111, 172-174, 202) and rl_market.py:240-273 stores state after
+    # state = next_state, so from an episode's second step the stored state is the
+    # post-step state; the facade's in-place buffer reproduces it
+    st = np.stack([s for s, _, _, _ in ag.stored])
+    np.testing.assert_allclose(st, f["stored_state"], rtol=RTOL, atol=0)
+    np.testing.assert_allclose(np.stack([s2 for _, _, _, s2 in ag.stored]), f["stored_next_state"], rtol=RTOL, atol=0)
+    assert np.all(f["stored_state"] == f["stored_next_state"], 1).sum() > n // 2
+    np.testing.assert_allclose(np.array([r for _, r, _, _ in ag.stored]), f["reward"], rtol=RTOL, atol=0)
+    np.testing.assert_array_equal(np.array([d for _, _, d, _ in ag.stored]), f["done"][:, 1])
     assert ag.i_learn == len(f["learn_loss"]) and ag.i_pol == len(f["policy"])
     assert ag.saves == f["save_step"].tolist()
     # evaluations: from start_idx + step, at the reference's cum_steps, shadow means filled on the device

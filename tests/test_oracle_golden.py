@@ -262,3 +262,30 @@ def test_shadow_equiv_matches_reference(golden):
         got = np.array([osh.shadow_equiv(m, a, lo, m, 1) for m, a, lo in zip(g["eq_mean"], g["eq_alpha"], g["eq_min"])])
     np.testing.assert_allclose(got, g["eq_out"], rtol=1e-12)
     assert (g["eq_out"][g["eq_alpha"] >= 1] == 1).all()
+
+
+@pytest.mark.parametrize("fixture,fam", [("c1_trace.npz", oe.COIN), ("c1_gbm_trace.npz", oe.GBM)])
+def test_stored_state_rule_matches_reference_loop(golden, fixture, fam):
+    """F6 / F6-GBM: the reference's own C1 loop (scripts/rl_multiplicative.py,
+    2,500 steps), recorded at store_transistion.  The oracle env replays its
+    actions and draws (dtype as received: f64 in warm-up / window, f32 after);
+    OracleVecEnv.stored_state gives what the loop stored — the reset state on an
+    episode's first step, the aliased post-step state after (the env's one
+    self.next_state array, gbm_envs.py:125, 184-186, 212; rl_multiplicative.py:
+    213-245) — and step() gives the stored next states and rewards."""
+    f = golden(fixture)
+    ora = oe.OracleVecEnv(fam, oe.INV_A, 1, 1)
+    obs = ora.reset()
+    n = int(f["n_steps"])
+    for t in range(n):
+        a = f["action"][t].reshape(1, -1)
+        a = a.astype(np.float64) if f["action_dtype"][t] else a.astype(np.float32)
+        ns, r, d, _ = ora.step(a, draws=f["draw"][t].reshape(1, -1))
+        np.testing.assert_allclose(ora.stored_state(obs, ns)[0], f["stored_state"][t], rtol=1e-12, atol=0,
+                                   err_msg=f"t={t}")
+        np.testing.assert_allclose(ns[0], f["stored_next_state"][t], rtol=1e-12, atol=0, err_msg=f"t={t}")
+        np.testing.assert_allclose(r[0], f["reward"][t], rtol=1e-12, atol=0)
+        assert list(d[0]) == list(f["done"][t]), t
+        obs = ora.reset() if d[0, 0] else ns.copy()
+    aliased = np.all(f["stored_state"] == f["stored_next_state"], 1)
+    assert aliased.sum() == n - int(f["done"][:, 0].sum()) - (0 if f["done"][-1, 0] else 1)

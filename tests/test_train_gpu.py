@@ -77,7 +77,7 @@ def test_warmup_steps_fill_ring_like_oracle(golden, dev, env, inv, fam, oinv, n)
         ns, r, d, risk = ora.step(a)  # float64 actions, as action_space.sample() gives
         s_r, a_r, r_r, s2_r, d_r = read_ring(tr, t * N, N)
         np.testing.assert_array_equal(a_r, a.astype(np.float32), err_msg=f"t={t} actions")
-        np.testing.assert_allclose(s_r, obs.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s")
+        np.testing.assert_allclose(s_r, ora.stored_state(obs, ns).astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s")
         np.testing.assert_allclose(s2_r, ns.astype(np.float32), rtol=1e-6, atol=at, err_msg=f"t={t} s2")
         np.testing.assert_allclose(r_r, r.astype(np.float32), rtol=1e-6)
         np.testing.assert_array_equal(d_r.astype(bool), d[:, 1], err_msg=f"t={t} learn_done")

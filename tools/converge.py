@@ -106,9 +106,11 @@ def kelly(env):
 
 def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eval_every=500, n_eval=4096,
         seed=0, replay=1 << 20, algo="SAC", out=None, log=print, device="cuda:0", loss="MSE", schedule="updates", multi_steps=1,
-        slice_groups=0):
+        slice_groups=0, stored_state="reference"):
     """warmup / smoothing: the reference's lengths (main.py gym_envs warm-up 1e3,
-    smoothing_window_mul 2e3), mapped to vector steps by trainer.schedule_steps."""
+    smoothing_window_mul 2e3), mapped to vector steps by trainer.schedule_steps.
+    stored_state: the replay rows' s (VecTrainer.set_stored_state; "reference" =
+    the reference loop's aliased post-step state)."""
     import torch
 
     from rlmd_amd.trainer import VecTrainer, schedule_steps
@@ -118,7 +120,7 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
     tr = VecTrainer(env=fam, investor=inv, n_lanes=lanes, n_gambles=1, algo=algo, loss=loss, k_updates=k,
                     replay_capacity=replay, seed=seed, warmup_steps=schedule_steps(warmup, k, schedule),
                     smoothing_window=schedule_steps(smoothing, k, schedule), precision=precision, device=device,
-                    init_seed=seed, multi_steps=multi_steps, slice_groups=slice_groups, **kw)
+                    init_seed=seed, multi_steps=multi_steps, slice_groups=slice_groups, stored_state=stored_state, **kw)
     l_star, g_star = kelly(env) if env != "market" else (None, None)
     # the reset state (identical for every lane; market lanes start on their own slices)
     reset_obs = tr.env.reset()[:1].float().clone() if env != "market" else tr.obs[:1].float().clone()
@@ -146,7 +148,7 @@ def run(env, lanes, k, steps, precision="bf16", warmup=1000, smoothing=2000, eva
             grow = 100.0 * float(np.mean(ev["reward"] - 1.0))
             lev_sh = float(np.mean(ev["risk"][:, 6])) if env == "dice_sh_a" else None
             rec = {"env": env, "algo": algo, "loss": loss, "precision": precision, "lanes": lanes, "k": k,
-                   "replay": replay, "multi_steps": multi_steps, "step": step, "updates": step * k, "env_steps": step * lanes,
+                   "replay": replay, "multi_steps": multi_steps, "stored_state": stored_state, "step": step, "updates": step * k, "env_steps": step * lanes,
                    "action": [float(x) for x in a], "lev": lev, "lev_sh": lev_sh,
                    "eval_growth_pct": grow, "eval_steps": float(np.mean(ev["steps"])),
                    "analytic_growth_pct": None if env == "market" else 100.0 * math.expm1(growth(env, lev, lev_sh)),

@@ -2,7 +2,8 @@
 on the GPU box) and append every evaluation record as a JSON line.
 
     python tools/converge_batch.py OUT.jsonl "env=gbm,algo=SAC,k=8,seed=0" "env=dice_sh_a,algo=TD3,k=0" ...
-Keys: env, algo, loss, k, seed, lanes, steps, replay, precision, eval_every, warmup, smoothing.
+Keys: env, algo, loss, k, seed, lanes, steps, replay, precision, eval_every, warmup, smoothing, ms (n-step
+returns), stored (reference | prestep: the replay rows' s), sg (market slice_groups), n_eval.
 """
 import json
 import os
@@ -15,10 +16,11 @@ import converge  # noqa: E402
 
 def parse(spec):
     d = dict(env="gbm", algo="SAC", loss="MSE", k=8, seed=0, lanes=65536, steps=12000, replay=1 << 20,
-             precision="bf16", eval_every=250, warmup=1000, smoothing=2000, schedule="updates")
+             precision="bf16", eval_every=250, warmup=1000, smoothing=2000, schedule="updates", ms=1,
+             stored="reference", sg=0, n_eval=4096)
     for kv in spec.split(","):
         k, v = kv.split("=")
-        d[k] = v if k in ("env", "algo", "loss", "precision", "schedule") else int(float(v))
+        d[k] = v if k in ("env", "algo", "loss", "precision", "schedule", "stored") else int(float(v))
     return d
 
 
@@ -30,7 +32,8 @@ def main():
         recs = converge.run(d["env"], d["lanes"], d["k"], d["steps"], precision=d["precision"],
                             warmup=d["warmup"], smoothing=d["smoothing"], eval_every=d["eval_every"], seed=d["seed"],
                             replay=d["replay"], algo=d["algo"], loss=d["loss"], log=lambda s: None,
-                            schedule=d["schedule"])
+                            schedule=d["schedule"], multi_steps=d["ms"], stored_state=d["stored"],
+                            slice_groups=d["sg"], n_eval=d["n_eval"])
         for r in recs:
             r["spec"] = spec
             out.write(json.dumps(r) + "\n")
