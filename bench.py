@@ -104,7 +104,8 @@ CONFIGS = {
                workload="C3: Dice_SH_InvA (key 18, S=6,A=2), TD3 400/300, B=200/k=100, replay 1M/GPU"),
     "c4": dict(env="market", investor="A", n=1, algo="SAC", lanes=8192, replay=1 << 20, multi_steps=1,
                workload="C4: Market_InvA_D1 on stooq_snp (9167 S&P 500 daily closes), "
-                        "train 1000 d, shuffle 5, SAC 256/256, 8192 lanes/GPU (one seed shard per GPU)"),
+                        "train 1000 d, shuffle 5, SAC 256/256, 8192 lanes/GPU on one shared slice stream "
+                        "(one seed shard per GPU)"),
     "c5": dict(env="gbm", investor="A", n=1, algo="TD3", lanes=65536, replay=1 << 24, multi_steps=5,
                workload="C5: GBM_InvA, TD3 400/300, multi-step n=5 (A), replay 16,777,216 transitions/GPU"),
 }
@@ -380,7 +381,7 @@ def dry_run(args):
     seed_procs = None
     if procs_T and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         child = ["--config", args.config, "--k-updates", str(args.k_updates), "--precision", args.precision,
-                 "--loss", args.loss, "--warmup", str(args.warmup)]
+                 "--loss", args.loss, "--warmup", str(args.warmup), "--slice-groups", str(args.slice_groups)]
         if args.lanes:
             child += ["--lanes", str(args.lanes)]
         if args.replay:
@@ -516,7 +517,7 @@ def make_trainer(args, dev, seed, **over):
     ms_n = over.pop("multi_steps", cfg["multi_steps"])
     if ms_n > 1:
         replay = (replay // N) * N
-    kw = market_kwargs() if cfg["env"] == "market" else {}
+    kw = market_kwargs(args.slice_groups) if cfg["env"] == "market" else {}
     kw.update(over)
     return VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"],
                       loss=args.loss, k_updates=args.k_updates, replay_capacity=replay, seed=seed, warmup_steps=0,
@@ -524,11 +525,15 @@ def make_trainer(args, dev, seed, **over):
                       dynamics="A", **kw)
 
 
-def market_kwargs():
+def market_kwargs(slice_groups=1):
     """C4's market env: stooq_snp, train 1000 d (obs_days 1), shuffle 5, the
-    start draw excluding train + test + gap days (rl_market.py:54-62)."""
+    start draw excluding train + test + gap days (rl_market.py:54-62).  The lanes
+    trade one shared shuffled slice stream (slice_groups = 1): the reference's
+    single-stream data regime (one time_slice + shuffle_data per episode,
+    rl_market.py:202-214), vectorised over the lanes' policy noise.  Independent
+    slices per lane (0) learn a leverage outside the reference's."""
     return dict(prices=stooq_snp_prices(), obs_days=1, time_length=1000, shuffle_days=5,
-                sample_days=1000 + 250 + 1 + 20 - 1)
+                sample_days=1000 + 250 + 1 + 20 - 1, slice_groups=slice_groups)
 
 
 def main():
@@ -553,6 +558,9 @@ def main():
                     help="independent seeds per GPU as one process each (own HIP queues), timed after the headline; "
                          "default '1,2,3,4' (C2, C4), '' otherwise; '' = off")
     ap.add_argument("--seed-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--slice-groups", type=int, default=1,
+                    help="C4: lanes l, l' with l %% G == l' %% G trade the same shuffled slices; 1 (default) = one "
+                         "shared stream, the reference's data regime; 0 = every lane its own")
     ap.add_argument("--variants", default=None,
                     help="BASELINE config variants timed after the headline, one trainer each: C3 the critic losses "
                          "(default 'MSE,HUB,MAE,HSC'), C5 the multi-step n (default '3,5,7'); '' = off")
@@ -603,7 +611,7 @@ def main():
     seed_procs = None
     if procs_T and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         child = ["--config", args.config, "--k-updates", str(args.k_updates), "--precision", args.precision,
-                 "--loss", args.loss, "--warmup", str(args.warmup)]
+                 "--loss", args.loss, "--warmup", str(args.warmup), "--slice-groups", str(args.slice_groups)]
         if args.lanes:
             child += ["--lanes", str(args.lanes)]
         if args.replay:
@@ -648,7 +656,7 @@ def main():
     ms_n = parse_multi_steps(args.multi_steps, rank, cfg["multi_steps"])
     kw = {}
     if cfg["env"] == "market":
-        kw = market_kwargs()
+        kw = market_kwargs(args.slice_groups)
     if ms_n > 1:
         replay = (replay // N) * N  # per-lane rings: capacity a multiple of the lanes
     tr = VecTrainer(env=cfg["env"], investor=cfg["investor"], n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"],

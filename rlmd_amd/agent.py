@@ -19,25 +19,18 @@ import torch
 
 from . import _abi
 from ._abi import check, ptr, stream_ptr
+from .envs import _StateKeyed
 
 HEADS = {"SAC": ("pi", "log_scale"), "TD3": ("mu",)}
-_AGENT_CTR = [0]
-
-
+_AGENT_SEEDS = _StateKeyed(b"agent")
 def private_agent_seed():
-    """The Philox key of an agent built without one (acting noise, the
-    update's policy noise, replay indices).  The reference draws these from
-    torch's and NumPy's generators, so they follow the driver's
-    torch.manual_seed / np.random.seed: the key hashes torch.initial_seed(),
-    NumPy's MT19937 state (read, not advanced) and a private counter (two
-    agents of one process apart)."""
-    import hashlib
-
-    _AGENT_CTR[0] += 1
-    _, keys, pos, _, _ = np.random.get_state()
-    h = hashlib.blake2b(np.ascontiguousarray(keys, dtype=np.uint32).tobytes(), digest_size=8)
-    h.update(np.array([pos, torch.initial_seed() & 0x7FFFFFFFFFFFFFFF, _AGENT_CTR[0]], dtype=np.int64).tobytes())
-    return int.from_bytes(h.digest(), "little") & 0x7FFFFFFF
+    """The Philox key of an agent built without one (acting noise, the update's
+    policy noise, replay indices).  The reference draws these from torch's and
+    NumPy's generators, so they follow the driver's torch.manual_seed /
+    np.random.seed: the key hashes both generators' states (read, not advanced).
+    Agent construction draws the initial parameters from torch's generator
+    (reference_init), so consecutive agents see different states."""
+    return _AGENT_SEEDS()
 
 
 def layer_names(algo, net):

@@ -27,27 +27,50 @@ MAX_ABS_ACTION = 0.99
 # rows follow the same rule (rlmd_train_set_stored_state)
 ALIAS_FAMILIES = frozenset({_abi.COIN, _abi.DICE, _abi.GBM, _abi.MARKET})
 
-_SEED_CTR = [0]
+def generator_state_key():
+    """A hash of the driver-visible random state: NumPy's global MT19937 state and
+    torch's CPU generator state, both read without advancing them."""
+    import hashlib
+
+    _, keys, pos, _, _ = np.random.get_state()
+    h = hashlib.blake2b(np.ascontiguousarray(keys, dtype=np.uint32).tobytes(), digest_size=8)
+    h.update(np.array([pos], dtype=np.int64).tobytes())
+    h.update(torch.get_rng_state().numpy().tobytes())
+    return h.digest()
+
+
+class _StateKeyed:
+    """Philox keys from the generator state.  Two objects created while the state
+    has not moved (no draw in between) are kept apart by their position in that
+    run of creations; the position restarts whenever the state moves, so a seed's
+    keys do not depend on what the process created before it was seeded."""
+
+    def __init__(self, tag):
+        self.tag, self.last, self.n = tag, None, 0
+
+    def __call__(self):
+        import hashlib
+
+        st = generator_state_key()
+        if st == self.last:
+            self.n += 1
+        else:
+            self.last, self.n = st, 0
+        h = hashlib.blake2b(st + self.tag + self.n.to_bytes(4, "little"), digest_size=8)
+        return int.from_bytes(h.digest(), "little") & 0x7FFFFFFF
+
+
+_ENV_SEEDS = _StateKeyed(b"env")
 
 
 def private_seed():
-    """A Philox seed for a device env created without one.
-
-    It is a hash of NumPy's global MT19937 state together with a private
-    counter.  Reading the state (np.random.get_state) does not advance the
-    stream: the reference's env constructors consume no NumPy draws, so drawing
-    one here would shift the global stream the drivers consume in the
-    reference's order (time_slice, shuffle_data, eval gaps).  Hashing the state
-    makes the device env's noise follow the driver's np.random.seed(s) (the
-    reference's seeds control its env noise), and the counter keeps two envs
-    created at the same stream position apart."""
-    import hashlib
-
-    _SEED_CTR[0] += 1
-    _, keys, pos, _, _ = np.random.get_state()
-    h = hashlib.blake2b(np.ascontiguousarray(keys, dtype=np.uint32).tobytes(), digest_size=8)
-    h.update(np.array([pos, _SEED_CTR[0]], dtype=np.int64).tobytes())
-    return int.from_bytes(h.digest(), "little") & 0x7FFFFFFF
+    """A Philox seed for a device env created without one.  Reading the generator
+    states does not advance them: the reference's env constructors consume no
+    draws, so drawing one here would shift the global stream the drivers consume
+    in the reference's order (time_slice, shuffle_data, eval gaps).  Hashing the
+    state makes the device env's noise follow the driver's np.random.seed(s) /
+    torch.manual_seed(s), as the reference's env noise does."""
+    return _ENV_SEEDS()
 
 
 class VecEnv:

@@ -19,7 +19,7 @@ for cfg in ${CONFIGS:-c2 c3}; do
         if [ -n "$ENVB" ]; then EXTRA=$ENVB; else export RLMD_LIB_PATH=$PWD/tools/_abh/librlmd_amd_${TAG}.so; fi
       else unset RLMD_LIB_PATH; fi
       env $EXTRA timeout -k 10 150 python -u bench.py --config $cfg --steps 40 --warmup 10 --no-cpu-baseline --no-companion \
-        --k-sweep 8 --seeds-per-gpu "" > gpurun_out/ab_run.log 2>&1 || { echo "run failed $cfg $rep $side"; tail -5 gpurun_out/ab_run.log; exit 1; }
+        --k-sweep 8 --seeds-per-gpu "" --seed-procs "" > gpurun_out/ab_run.log 2>&1 || { echo "run failed $cfg $rep $side"; tail -5 gpurun_out/ab_run.log; exit 1; }
       python - "$cfg" "$rep" "$side" "$OUT" <<'PY'
 import json, sys
 cfg, rep, side, out = sys.argv[1:]

@@ -16,7 +16,7 @@ if [ "$WHAT" = lines ]; then
   step bench timeout -k 10 420 python -u bench.py > gpurun_out/${TAG}_bench.log 2>&1
   step nccl1 env RLMD_BENCH_FORCE_DIST=1 timeout -k 10 240 python -u -m torch.distributed.run --nnodes=1 \
     --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 20 --warmup 5 \
-    --no-cpu-baseline --no-companion --k-sweep 8 --seeds-per-gpu "" > gpurun_out/${TAG}_bench_nccl1.log 2>&1
+    --no-cpu-baseline --no-companion --k-sweep 8 --seeds-per-gpu "" --seed-procs "" > gpurun_out/${TAG}_bench_nccl1.log 2>&1
   for C in c3 c4 c5; do
     step bench_$C timeout -k 10 300 python -u bench.py --config $C > gpurun_out/${TAG}_bench_$C.log 2>&1
   done

@@ -7,7 +7,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for C in ${CONFIGS:-c3 c5 c4}; do
-  BENCH="bench.py --config $C --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --variants= --steps 25 --warmup 5"
+  BENCH="bench.py --config $C --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --seed-procs= --variants= --steps 25 --warmup 5"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace_$C -o trace -- python3 $BENCH > $OUT/trace_$C.log 2>&1
   tail -n 1 $OUT/trace_$C.log | cut -c1-300
   if [ -n "${MFMA:-}" ]; then  # one MFMA-busy pass over the acting / learn kernels (its own run)

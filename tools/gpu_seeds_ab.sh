@@ -13,7 +13,7 @@ for spec in "$@"; do
   [ "$envs" = "-" ] && envs=""
   echo "== $name ($envs)"
   env $envs timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-companion \
-      --k-sweep '' --seeds-per-gpu "${SEEDS:-2,3,4}" > "$out/$name.json" 2> "$out/$name.err" || { echo "FAIL $name"; exit 1; }
+      --k-sweep '' --seed-procs '' --seeds-per-gpu "${SEEDS:-2,3,4}" > "$out/$name.json" 2> "$out/$name.err" || { echo "FAIL $name"; exit 1; }
   python - "$out/$name.json" <<'EOF'
 import json, sys
 line = [l for l in open(sys.argv[1]) if l.startswith("{")][-1]

@@ -16,7 +16,7 @@ for spec in $2; do
   [ "$ev" = "-" ] && ev=""
   D=$OUT/${cfg}_$n
   env $ev timeout -k 10 240 rocprofv3 --kernel-trace --stats -f csv -d $D -o t -- python3 bench.py --config $cfg \
-    --steps 20 --warmup 5 --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --variants= > $D.log 2>&1 \
+    --steps 20 --warmup 5 --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --seed-procs= --variants= > $D.log 2>&1 \
     || { echo "run failed $spec"; tail -5 $D.log; exit 1; }
   python3 - "$D" "$spec" >> $OUT/summary.txt <<'PY'
 import csv, sys, glob

@@ -106,7 +106,7 @@ def main(tag, config="c2"):
     rows = list(csv.DictReader(open(stats)))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     lines = [f"rocprofv3 --kernel-trace --stats: python bench.py --no-cpu-baseline --no-companion --k-sweep= "
-             f"--seeds-per-gpu= --steps 25 --warmup 5 "
+             f"--seeds-per-gpu= --seed-procs= --steps 25 --warmup 5 "
              f"(C2, 65,536 GBM lanes, SAC 256/256 bf16, K=8)", "",
              f"{'calls':>6} {'avg_us':>9} {'total_ms':>9} {'pct':>6}  kernel"]
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):
@@ -172,7 +172,7 @@ def config_summaries(tag):
         rows = list(csv.DictReader(open(stats)))
         tot = sum(float(r["TotalDurationNs"]) for r in rows)
         lines = [f"rocprofv3 --kernel-trace --stats: python bench.py --config {cfg} --no-cpu-baseline --no-companion "
-                 f"--k-sweep= --seeds-per-gpu= --variants= --steps 25 --warmup 5 ({name})", "",
+                 f"--k-sweep= --seeds-per-gpu= --seed-procs= --variants= --steps 25 --warmup 5 ({name})", "",
                  f"{'calls':>6} {'avg_us':>9} {'total_ms':>9} {'pct':>6}  kernel"]
         per_kernel = {}
         for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"])):

@@ -7,7 +7,7 @@ TAG=${1:-ic}
 OUT=gpurun_out/pmc_ic_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-BENCH="bench.py --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --steps 10 --warmup 3"
+BENCH="bench.py --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --seed-procs= --steps 10 --warmup 3"
 K="fwd_rows|qeval_rows|critic_update_kernel|actor_update_kernel|act_env_kernel"
 timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_IFETCH SQ_WAVES \
   --kernel-include-regex "$K" -f csv -d $OUT/sq -o sq -- python3 $BENCH > $OUT/sq.log 2>&1

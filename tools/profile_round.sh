@@ -12,7 +12,7 @@ TAG=${1:-r01}
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-BENCH="bench.py --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --steps 25 --warmup 5"
+BENCH="bench.py --no-cpu-baseline --no-companion --k-sweep= --seeds-per-gpu= --seed-procs= --steps 25 --warmup 5"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d $OUT/trace -o trace -- python3 $BENCH > $OUT/trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "act_env_kernel|fused_act_kernel|env_train_kernel" -f csv -d $OUT/fetch -o fetch -- python3 $BENCH > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "act_env_kernel|fused_act_kernel|env_train_kernel" -f csv -d $OUT/write -o write -- python3 $BENCH > $OUT/write.log 2>&1
