@@ -7,7 +7,7 @@ reference's five seeds.  The control for the N = 1 / K = 1 vectorised result
 vectorised single lane does not, the difference is in the vectorised loop's
 glue, not in the learner.
 
-    RLMD_CONVERGE_LOG=gpurun_out/gbm_single.jsonl python tools/probe/gbm_single.py 0-4 [--steps=50000]
+    RLMD_CONVERGE_LOG=gpurun_out/gbm_single.jsonl python tools/probe/gbm_single.py 0-4 [--steps=50000] [--prestep]
 """
 import os
 import sys
@@ -66,24 +66,21 @@ def main():
     import test_converge_gpu as t
 
     args = sys.argv[1:]
-    if "--alias" in args:
-        # the reference envs return one next_state array, mutated in place by every
-        # step (e.g. gbm_envs.py:179-181, 212), and the loop keeps `state = next_state`
-        # (rl_multiplicative.py:218-245): from an episode's second step on, the
-        # stored state IS the stored next state.  Reproduce that in the driver's env.
+    if "--prestep" in args:
+        # the round-5 build's semantics: a fresh next_state array per step, so the
+        # driver stores the true pre-step state.  The facade's default since round 6
+        # is the reference's: one next_state array mutated in place by every step
+        # (gbm_envs.py:125, 184-186, 212), which the loop stores after
+        # `state = next_state` (rl_multiplicative.py:213-245).
         from rlmd_amd import envs as envs_mod
 
         base_step = envs_mod._SingleEnv.step
 
-        def aliased_step(self, action):
+        def fresh_step(self, action):
             ns, r, d, risk = base_step(self, action)
-            buf = getattr(self, "_ns_buf", None)
-            if buf is None or buf.shape != ns.shape:
-                buf = self._ns_buf = np.empty_like(ns)
-            buf[...] = ns
-            return buf, r, d, risk
+            return np.array(ns, copy=True), r, d, risk
 
-        envs_mod._SingleEnv.step = aliased_step
+        envs_mod._SingleEnv.step = fresh_step
     steps = 50000
     for a in [a for a in args if a.startswith("--steps=")]:
         steps = int(a.split("=")[1])
