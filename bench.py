@@ -386,7 +386,7 @@ def dry_run(args):
             child += ["--lanes", str(args.lanes)]
         if args.replay:
             child += ["--replay", str(args.replay)]
-        seed_procs = SeedProcs(max(procs_T), child)
+        seed_procs = SeedProcs(max(procs_T), child, hw_queues=args.seed_proc_queues)
 
     import torch
     import torch.distributed as dist
@@ -435,7 +435,10 @@ class SeedProcs:
     wall-clock start and end); the group's rate is T x lanes x n_t over the span
     from the first start to the last end."""
 
-    def __init__(self, n, argv):
+    def __init__(self, n, argv, hw_queues=1):
+        """hw_queues: GPU_MAX_HW_QUEUES of each seed process (its trainer runs on one
+        stream; 1 keeps the processes' queues within what the hardware scheduler
+        maps at once)."""
         import subprocess
 
         self.procs = []
@@ -443,6 +446,8 @@ class SeedProcs:
             env = dict(os.environ)
             for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
                 env.pop(k, None)
+            if hw_queues:
+                env["GPU_MAX_HW_QUEUES"] = str(int(hw_queues))
             self.procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), "--seed-worker",
                                                 "--seed", str(420 + 1000 * (i + 1))] + argv, env=env,
                                                stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, bufsize=1))
@@ -461,7 +466,7 @@ class SeedProcs:
 
     def round(self, T, n_t, lanes):
         ps = self.procs[:T]
-        self._ask(ps, f"run {n_t}")
+        self._ask(ps, f"run {n_t} {T}")
         res = self._ask(ps, "go")
         span = max(r["t1"] for r in res) - min(r["t0"] for r in res)
         return {"env_steps_per_s": T * lanes * n_t / span, "span_s": span,
@@ -490,11 +495,19 @@ def seed_worker(args):
 
         sync = (lambda: None) if args.dry_run else torch.cuda.synchronize
         if cmd[0] == "run":
-            n_t = int(cmd[1])
+            n_t, T = int(cmd[1]), int(cmd[2]) if len(cmd) > 2 else 1
             if tr is None:
                 tr = DryTrainer(0) if args.dry_run else make_trainer(args, torch.device("cuda", 0), args.seed)
-                for _ in range(max(args.warmup, 3)):
-                    tr.step()
+            if not args.dry_run:
+                # the CU share of one of T seeds (rlmd_agent_set_cu_budget, as SeedGroup
+                # gives its seeds): the layer-2 column split stays off where T
+                # learners' grids would queue for the same CUs
+                from rlmd_amd import _abi
+
+                ncu = torch.cuda.get_device_properties(0).multi_processor_count
+                _abi.check(_abi.lib().rlmd_agent_set_cu_budget(tr.agent.h, max(ncu // max(T, 1), 1)))
+            for _ in range(max(args.warmup, 3)):
+                tr.step()
             sync()
             print(json.dumps({"ready": True}), flush=True)
         elif cmd[0] == "go":
@@ -558,6 +571,8 @@ def main():
                     help="independent seeds per GPU as one process each (own HIP queues), timed after the headline; "
                          "default '1,2,3,4' (C2, C4), '' otherwise; '' = off")
     ap.add_argument("--seed-worker", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--seed-proc-queues", type=int, default=1,
+                    help="GPU_MAX_HW_QUEUES of each --seed-procs process (0: inherit)")
     ap.add_argument("--slice-groups", type=int, default=1,
                     help="C4: lanes l, l' with l %% G == l' %% G trade the same shuffled slices; 1 (default) = one "
                          "shared stream, the reference's data regime; 0 = every lane its own")
@@ -616,7 +631,7 @@ def main():
             child += ["--lanes", str(args.lanes)]
         if args.replay:
             child += ["--replay", str(args.replay)]
-        seed_procs = SeedProcs(max(procs_T), child)
+        seed_procs = SeedProcs(max(procs_T), child, hw_queues=args.seed_proc_queues)
 
     import torch
     import torch.distributed as dist

@@ -21,8 +21,6 @@
 #include <math.h>
 #include <hip/hip_ext.h>
 
-#include <algorithm>
-
 #ifdef RLMD_TIMING
 namespace rlmd {
 namespace actrows {
@@ -44,25 +42,15 @@ namespace rlmd {
 namespace {
 using namespace actrows;
 
-#ifndef RLMD_ACT_PERSIST
-#define RLMD_ACT_PERSIST 0  // experiment builds: workgroups per CU of a persistent grid (0: one block per WG)
-#endif
 template <int H1P, int NB, int SP, int MA>
 __global__ void __launch_bounds__(256, H1P == 256 ? (MA == kMaxA ? 3 : 2) : 1) fused_act_kernel(FusedActArgs a) {
   RLMD_KERNARG_PREFETCH(a);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  auto epi = [&](int, int b, const float* acts, const float*) {
-    for (int j = 0; j < a.A; ++j) a.actions[(int64_t)b * a.A + j] = acts[j];
-  };
-  if constexpr (RLMD_ACT_PERSIST > 0) {
-    const int nblk = (a.n + kRows - 1) / kRows;
-    for (int blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-      act_rows<H1P, NB, SP, MA>(a, smem, [] {}, epi, blk, blk == (int)blockIdx.x);
-      __syncthreads();
-    }
-  } else {
-    act_rows<H1P, NB, SP, MA>(a, smem, [] {}, epi);
-  }
+  act_rows<H1P, NB, SP, MA>(
+      a, smem, [] {},
+      [&](int, int b, const float* acts, const float*) {
+        for (int j = 0; j < a.A; ++j) a.actions[(int64_t)b * a.A + j] = acts[j];
+      });
 }
 
 }  // namespace
@@ -108,14 +96,7 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
   int h1p, nb;
   RLMD_CHECK(fused_shape(c, h1p, nb), "fused acting: unsupported net shape");
   const FusedActArgs a = fused_act_args(c, obs, n, actions, actor_params, off, w2bf, mode, seed, ctr, eps);
-  unsigned nblk = (unsigned)((n + kRows - 1) / kRows);
-  if (RLMD_ACT_PERSIST > 0) {
-    int dev = 0, ncu = 256;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    nblk = std::min(nblk, (unsigned)(RLMD_ACT_PERSIST * ncu));
-  }
-  const dim3 grid(nblk);
+  const dim3 grid((unsigned)((n + kRows - 1) / kRows));
   const int sp = c.state_dim <= 8 ? 8 : 16;
   RLMD_CHECK(c.action_dim <= kMaxA4, "fused acting: at most 4 actions");
 #define ACT_LAUNCH1(H1P_, NB_, SP_, MA_)                                                                          \

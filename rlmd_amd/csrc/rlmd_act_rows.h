@@ -54,11 +54,8 @@ struct L1Tiles {
 // b, act, obs_row) runs on thread r < 64 of each valid row b with the row's
 // actions act[MA] (f32; MA = kMaxA, or kMaxA4 for 3-4 actions: twice the head
 // registers and partials) and its observation in LDS (obs_row[0 .. S)).
-// blk: the 64-row block (blockIdx.x unless a persistent caller loops over blocks);
-// stage_w1: stage W1 / b1 into LDS (a persistent caller's later blocks reuse them)
 template <int H1P, int NB, int SP, int MA, typename ProF, typename EpiF>
-__device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* smem, ProF pro, EpiF epi,
-                                         int blk = -1, bool stage_w1 = true) {
+__device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* smem, ProF pro, EpiF epi) {
   constexpr int kMaxA = MA;
   constexpr int HP = H1P + 8;  // bf16 row pitch: 16-B aligned fragment reads
   constexpr int NT = L1Tiles<H1P>::NT, NTP = L1Tiles<H1P>::NTP;
@@ -69,7 +66,7 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
   float* b1s = w1s + SP * 16 * NTP;                                               // [H1P]
   float* obs_s = b1s + H1P;                                                       // [64][SP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row0 = (blk < 0 ? (int)blockIdx.x : blk) * kRows;
+  const int row0 = blockIdx.x * kRows;
   const NetOff& o = a.off;
   const int S = a.S, A = a.A;
   RLMD_TSA(0, __builtin_amdgcn_s_memrealtime());
@@ -131,7 +128,7 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
       const int k = e / (16 * NTP), jt = e - k * (16 * NTP);
       const int jj = jt / NTP, t = jt - jj * NTP;
       const int c = isb ? e - SP * 16 * NTP : 16 * t + jj;
-      const bool wl = stage_w1 && e < nW && c < H1 && (isb || (t < NT && k < S));
+      const bool wl = e < nW && c < H1 && (isb || (t < NT && k < S));
       vw[j] = rlmd_ldf(rw, isb ? H1 * S + c : c * S + k, wl);
     }
 #pragma unroll
@@ -143,7 +140,7 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
       const int e = j * 256 + tid;
-      if (stage_w1 && e < nW) w1s[e] = vw[j];  // b1 follows w1g contiguously
+      if (e < nW) w1s[e] = vw[j];  // b1 follows w1g contiguously
     }
 #pragma unroll
     for (int j = 0; j < PO; ++j) {

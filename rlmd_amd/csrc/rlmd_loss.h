@@ -103,7 +103,15 @@ __device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
   return L;
 }
 
-__device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, CriticRow& o, const CriticLoads& L) {
+// block: form the block sums (o.s1, o.nan and the CIM kernel / TCAU truncation
+// that need them).  A caller that only needs the rows' losses and gradients
+// passes critic_loss_needs_block(a) (false for every loss but CIM and TCAU): the
+// two block reductions (six barriers) are skipped and o.s1 / o.nan / o.kern are 0.
+__device__ __forceinline__ bool critic_loss_needs_block(const LossArgs& a) {
+  return a.loss_type == RLMD_LOSS_CIM || a.loss_type == RLMD_LOSS_TCAU;
+}
+__device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, CriticRow& o, const CriticLoads& L,
+                                                bool block = true) {
   const int b = threadIdx.x, B = a.B;
   const bool in = b < B;
   const LearnState* st = a.st;
@@ -132,14 +140,27 @@ __device__ __forceinline__ void critic_row_loss(const LossArgs& a, float* red, C
   float s1[7] = {in ? e0 : 0.f, in ? e1 : 0.f, in ? y : 0.f, in ? q[0] : 0.f, in ? q[1] : 0.f,
                  in ? 1.f / (1.f + z0 * z0) : 0.f, in ? 1.f / (1.f + z1 * z1) : 0.f};
   float m1[1] = {(in && (isnan(q[0]) || isnan(q[1]) || isnan(y))) ? 1.f : 0.f};
-  block_allreduce<7, 1>(s1, m1, red);
-  const float me0 = s1[0] / B, me1 = s1[1] / B, my = s1[2] / B, mq0 = s1[3] / B, mq1 = s1[4] / B;
-  // R2: population variances (two-pass, like torch.std(unbiased=False))
-  float s2[5] = {in ? (e0 - me0) * (e0 - me0) : 0.f, in ? (e1 - me1) * (e1 - me1) : 0.f,
-                 in ? (y - my) * (y - my) : 0.f, in ? (q[0] - mq0) * (q[0] - mq0) : 0.f,
-                 in ? (q[1] - mq1) * (q[1] - mq1) : 0.f};
-  float m2[1] = {-INFINITY};
-  block_allreduce<5, 0>(s2, m2, red);
+  float s2[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+  float my = 0.f, mq0 = 0.f, mq1 = 0.f;
+  if (block) {  // workgroup-uniform
+    block_allreduce<7, 1>(s1, m1, red);
+    const float me0 = s1[0] / B, me1 = s1[1] / B;
+    my = s1[2] / B;
+    mq0 = s1[3] / B;
+    mq1 = s1[4] / B;
+    // R2: population variances (two-pass, like torch.std(unbiased=False))
+    s2[0] = in ? (e0 - me0) * (e0 - me0) : 0.f;
+    s2[1] = in ? (e1 - me1) * (e1 - me1) : 0.f;
+    s2[2] = in ? (y - my) * (y - my) : 0.f;
+    s2[3] = in ? (q[0] - mq0) * (q[0] - mq0) : 0.f;
+    s2[4] = in ? (q[1] - mq1) * (q[1] - mq1) : 0.f;
+    float m2[1] = {-INFINITY};
+    block_allreduce<5, 0>(s2, m2, red);
+  } else {
+#pragma unroll
+    for (int v = 0; v < 7; ++v) s1[v] = 0.f;
+    m1[0] = 0.f;
+  }
   const float kern[2] = {sqrtf(s2[0] / B), sqrtf(s2[1] / B)};
   // TCAU 3-sigma truncation (critic_loss.py:26-50)
   float yt[2] = {y, y}, qt_[2] = {q[0], q[1]};

@@ -43,6 +43,9 @@ constexpr int TW = 32;
 #ifndef RLMD_ABL
 #define RLMD_ABL 0
 #endif
+#ifndef RLMD_ROLE_SPLIT
+#define RLMD_ROLE_SPLIT 1  // role-specialised update bodies (0: one body, roles' loads predicated off)
+#endif
 template <int NW>
 __device__ __forceinline__ void upd_rank(uint64_t key, uint64_t* runs, int* out) {
   if constexpr ((RLMD_ABL & 1) != 0) {
@@ -220,15 +223,20 @@ struct ULds {
 // waves 4-7 for [j0 + 32, j0 + 64) — where the 32 x 32 form would leave waves
 // 4-7 on rows past B.  Half the tile workgroups: TD3 400/300's 2 x 153 of them
 // exceed the 256 CUs at one workgroup per CU (a second dispatch round); 2 x 88 do not.
+// Roles of the critic step's workgroups: an fc2.weight tile, an fc1 block, a head
+// workgroup (b2 / w3 of 32 fc2 rows, b3 on the first).  The role is a template
+// parameter of the body, so each workgroup issues exactly its own role's first
+// load round: issued predicated-off, the other roles' loads had cost a third of the
+// launch in texture-addresser issue (TA_TA_BUSY, profiles/r06_pmc_ta.json).
+enum { kRoleW2 = 0, kRoleW1 = 1, kRoleHead = 2 };
+
+template <int PREC, bool WIDE, int ROLE>
+__device__ __forceinline__ void critic_update_body(const CritUpdArgs& a, unsigned char* smem, int g, int t);
+
 template <int PREC, bool WIDE>
 __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   RLMD_KERNARG_PREFETCH(a);
-  using K = KT<PREC>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  float* dqs = reinterpret_cast<float*>(smem + ULds::dq);
-  float* part = reinterpret_cast<float*>(smem + ULds::part);
-  const RowDims& d = a.d;
-  const NetOff& co = a.co;
   // per critic: fc2.weight tiles, fc1 blocks, then head workgroups (b2 / w3 of 32
   // fc2 rows each, b3 on the first)
   const int per = a.n_w2 + a.n_w1 + a.ti;
@@ -241,15 +249,37 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     return;
   }
   const int g = blockIdx.x / per, t = blockIdx.x - g * per;
+#if RLMD_ROLE_SPLIT
+  if (t < a.n_w2) critic_update_body<PREC, WIDE, kRoleW2>(a, smem, g, t);
+  else if (t >= a.n_w2 + a.n_w1) critic_update_body<PREC, WIDE, kRoleHead>(a, smem, g, t);
+  else critic_update_body<PREC, WIDE, kRoleW1>(a, smem, g, t);
+#else
+  critic_update_body<PREC, WIDE, -1>(a, smem, g, t);
+#endif
+}
+
+// ROLE -1: one body for every role, the roles' loads issued predicated-off (the
+// round-5 form, RLMD_ROLE_SPLIT=0)
+template <int PREC, bool WIDE, int ROLE>
+__device__ __forceinline__ void critic_update_body(const CritUpdArgs& a, unsigned char* smem, int g, int t) {
+  using K = KT<PREC>;
+  float* dqs = reinterpret_cast<float*>(smem + ULds::dq);
+  float* part = reinterpret_cast<float*>(smem + ULds::part);
+  const RowDims& d = a.d;
+  const NetOff& co = a.co;
   const int B = d.B, H1 = d.H1, H2 = d.H2, H1p = d.H1p, H2p = d.H2p, X = d.X;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nrb = (B + 15) / 16;
-  const bool w2tile = t < a.n_w2, first_col = t >= a.n_w2 + a.n_w1;  // first_col: a head workgroup
+  // this workgroup's role; IS_* = the role's loads are compiled in
+  constexpr bool IS_W2 = ROLE < 0 || ROLE == kRoleW2, IS_W1 = ROLE < 0 || ROLE == kRoleW1,
+                 IS_HEAD = ROLE < 0 || ROLE == kRoleHead;
+  const bool w2tile = ROLE < 0 ? t < a.n_w2 : ROLE == kRoleW2;
+  const bool first_col = ROLE < 0 ? t >= a.n_w2 + a.n_w1 : ROLE == kRoleHead;  // first_col: a head workgroup
   constexpr int TJ = WIDE ? 2 * TW : TW;  // fc2.weight columns per tile
   constexpr int NH = WIDE ? 2 : 1;        // 32-column halves per tile
   const int i0 = w2tile ? (t / a.tj) * TW : first_col ? (t - a.n_w2 - a.n_w1) * TW : 0;
   const int j0 = w2tile ? (t % a.tj) * TJ : first_col ? 0 : (t - a.n_w2) * TW;
-  const bool w1blk = !w2tile && !first_col;
+  const bool w1blk = ROLE < 0 ? !w2tile && !first_col : ROLE == kRoleW1;
   const int wrow = WIDE ? (wave & 3) : wave;     // this wave's 64-row slice of the batch
   const int jw = j0 + (WIDE ? 32 * (wave >> 2) : 0);  // and its 32-column half
   const int64_t pbase = (int64_t)g * co.size;  // this critic's parameters in the Adam base
@@ -280,6 +310,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   const __amdgpu_buffer_rsrc_t rm2 = rlmd_rsrc(a.m2[g], (int64_t)nrb * H2p * 16),
                                rh1 = rlmd_rsrc(a.hp1[g], (int64_t)nrb * H1p * 16 * sizeof(typename K::T));
   float w3l[2];
+  if constexpr (IS_W2) {
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
     const int row = 64 * wrow + s * K::KS + K::RPL * (lane >> 4);
@@ -296,10 +327,12 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     const int i = i0 + 16 * h + (lane & 15);
     w3l[h] = rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), i, w2tile && i < H2);
   }
+  }
   // (b) Adam state of the owned parameters: 1024 elements per 32-column half, 2
   //     per thread and half
   int pidx[NH][2];
   AdamIn ain[NH][2];
+  if constexpr (IS_W2) {
 #pragma unroll
   for (int hf = 0; hf < NH; ++hf)
 #pragma unroll
@@ -309,12 +342,13 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       pidx[hf][e] = (w2tile && i < H2 && j < H1) ? (int)(pbase + co.w2 + (int64_t)i * H1 + j) : -1;
       ain[hf][e] = adam_load(a.adam, pidx[hf][e], polyak);
     }
+  }
   // (c) first-column tiles: this thread's column of h2 and [h2 > 0] over its 32 rows
   //     (thread: column i0 + tid % 32, rows [32 p, 32 p + 32) of part p = tid / 32)
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   constexpr int NV = 16 * sizeof(typename K::T) / 16;  // 16-byte loads per 16 rows of h2
   u32x4 fmb[2], fhv[2][NV];
-  {
+  if constexpr (IS_HEAD) {
     const int ci = tid & 31, p = tid >> 5, i = i0 + ci;
     const __amdgpu_buffer_rsrc_t rh2 = rlmd_rsrc(a.hp2[g], (int64_t)nrb * H2p * 16 * sizeof(typename K::T));
 #pragma unroll
@@ -342,14 +376,16 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
     if (w1blk && tid < 32 * 9 && (ci < X || ci == 8) && jr < H1)
       xpi = (int)(pbase + (ci == 8 ? co.b1 + jr : co.w1 + (int64_t)jr * X + ci));
   }
-  const AdamIn xin = adam_load(a.adam, xpi, polyak);
-  const float w3c = rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), i0 + (tid & 31), first_col && tid < 32);
+  AdamIn xin{};
+  if constexpr (IS_W1 || IS_HEAD) xin = adam_load(a.adam, xpi, polyak);
+  float w3c = 0.f;
+  if constexpr (IS_HEAD) w3c = rlmd_ldf(rlmd_rsrc(a.w3s[g], (int64_t)H2 * 4), i0 + (tid & 31), first_col && tid < 32);
   // (d) fc1 blocks: the critic inputs of this thread's 8 LDS slots and U1 of its
   //     column over its 32 rows
   float* xs = reinterpret_cast<float*>(smem + ULds::xs);
   float xv[8];
   f32x4 u1v[8], u1w[8];  // U1, and its second partial half (fwd_rows column split)
-  {
+  if constexpr (IS_W1) {
     const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.x, (int64_t)B * X * 4);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -377,7 +413,13 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   {
     float* red = reinterpret_cast<float*>(smem + ULds::red);
     CriticRow o;
+    // the block sums only where the loss itself needs them (CIM kernel, TCAU
+    // truncation): the statistics workgroups form the rest (rlmd_loss.h)
+#ifndef RLMD_LOSS_BLOCK_ALWAYS
+    critic_row_loss(a.loss, red, o, cl, critic_loss_needs_block(a.loss));
+#else
     critic_row_loss(a.loss, red, o, cl);
+#endif
     RLMD_TSU(2);
     const int kk = B > a.loss.k ? a.loss.k : B;
     bool sel = o.in;
@@ -394,7 +436,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   __syncthreads();
   RLMD_TSU(3);
 
-  if (w2tile) {
+  if (IS_W2 && w2tile) {
     // ---- dW2[i0.., j0..] = sum_b dh2[b, i] h1[b, j] over this wave's rows
     f32x4 acc[2][2];
 #pragma unroll
@@ -444,7 +486,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       if (j0 + 32 * hf < H1p)  // WIDE: the last tile's second half may lie past the padded width
         if (!(RLMD_ABL & 2)) tile_copies<PREC>(pcl + hf * 2 * 32 * 33, cd, polyak && cd.twc, i0, j0 + 32 * hf, H1p, H2p);
     RLMD_TSU(5);
-  } else if (first_col) {
+  } else if (IS_HEAD && first_col) {
     {
       // ---- db2[i] = w3[i] sum_b dq[b] [h2 > 0], dW3[i] = sum_b dq[b] h2[b, i]
       //      (thread: column i0 + tid % 32, rows [32 p, 32 p + 32) of part p = tid / 32)
@@ -484,7 +526,7 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
       }
       RLMD_TSU(6);
     }
-  } else {
+  } else if (IS_W1) {
     // ---- dW1[j, x] = sum_b dq[b] U1[b, j] x[b, x], db1[j] = sum_b dq[b] U1[b, j]
     //      (thread: fc1 row j0 + tid % 32, rows [32 p, 32 p + 32) of part p)
     const int cj = tid & 31, p = tid >> 5;
@@ -555,16 +597,38 @@ struct ALds {
   static constexpr int rank = runs + 512 * 8;       // int [3 * 512] (critic statistics: 3 ranks)
   static constexpr int red = rank + 3 * 512 * 4;    // 16 * 9 floats
   static constexpr int part = red + 16 * 9 * 4;     // f32 [8][4][256]
-  static constexpr int xs = part + 8 * 4 * 256 * 4; // f32 [512][8] states
-  static constexpr int pcl = xs + 512 * 8 * 4;      // f32 [2][32][33] stepped tile + targets (copies)
+  // f32 [512][8] states of an fc1 block: read before the barrier ahead of the
+  // block's partial sums, so they share part's bytes (68 KB in all: two actor
+  // steps of two seeds fit one CU)
+  static constexpr int xs = part;
+  static constexpr int pcl = part + 8 * 4 * 256 * 4;  // f32 [2][32][33] stepped tile + targets (copies)
   static constexpr int total = pcl + 2 * 32 * 33 * 4;
 };
+
+template <int PREC, int ROLE>
+__device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned char* smem);
 
 template <int PREC>
 __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   RLMD_KERNARG_PREFETCH(a);
-  using K = KT<PREC>;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  // roles as in critic_update_kernel: tiles, fc1 blocks, head workgroups, then the
+  // two critic-statistics workgroups (handled in the body's first branch)
+  const int t = blockIdx.x;
+#if RLMD_ROLE_SPLIT
+  if (t < a.n_w2) actor_update_body<PREC, kRoleW2>(a, smem);
+  else if (t < a.n_w2 + a.n_w1) actor_update_body<PREC, kRoleW1>(a, smem);
+  else actor_update_body<PREC, kRoleHead>(a, smem);  // heads and the statistics workgroups
+#else
+  actor_update_body<PREC, -1>(a, smem);
+#endif
+}
+
+template <int PREC, int ROLE>
+__device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned char* smem) {
+  using K = KT<PREC>;
+  constexpr bool IS_W2 = ROLE < 0 || ROLE == kRoleW2, IS_W1 = ROLE < 0 || ROLE == kRoleW1,
+                 IS_HEAD = ROLE < 0 || ROLE == kRoleHead;
   float* ghs = reinterpret_cast<float*>(smem + ALds::gh);
   float* ghp = reinterpret_cast<float*>(smem + ALds::ghp);
   float* part = reinterpret_cast<float*>(smem + ALds::part);
@@ -577,6 +641,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nrb = (B + 15) / 16;
   const int t = blockIdx.x;
+  (void)IS_W1;
   // workgroups: fc2.weight tiles, fc1 blocks, head workgroups (b2 and the heads
   // of 32 fc2 rows each), and two critic-statistics workgroups.  Every reader of
   // log alpha and the Cauchy scales takes the update's starting slot, the
@@ -591,9 +656,10 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   RLMD_TSA(14);
   RLMD_TSA(0);
   LearnState* st = a.st;
-  const bool stats_wg = sidx >= 0;
-  const bool w2tile = t < a.n_w2, first_col = !stats_wg && t >= a.n_w2 + a.n_w1;  // first_col: a head workgroup
-  const bool w1blk = !stats_wg && !w2tile && !first_col;
+  const bool stats_wg = IS_HEAD && sidx >= 0;
+  const bool w2tile = ROLE < 0 ? t < a.n_w2 : ROLE == kRoleW2;
+  const bool first_col = ROLE < 0 ? !stats_wg && t >= a.n_w2 + a.n_w1 : ROLE == kRoleHead && !stats_wg;  // a head workgroup
+  const bool w1blk = ROLE < 0 ? !stats_wg && !w2tile && !first_col : ROLE == kRoleW1;
   const int i0 = w2tile ? (t / a.tj) * TW : first_col ? (t - a.n_w2 - a.n_w1) * TW : 0;
   const int j0 = w2tile ? (t % a.tj) * TW : w1blk ? (t - a.n_w2) * TW : 0;
   const bool polyak = adam_polyak(a.adam);
@@ -666,6 +732,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   const __amdgpu_buffer_rsrc_t rm2 = rlmd_rsrc(a.am2, (int64_t)nrb * H2p * 16),
                                rh1 = rlmd_rsrc(a.hp1a, (int64_t)nrb * H1p * 16 * sizeof(typename K::T));
   const __amdgpu_buffer_rsrc_t rw = rlmd_rsrc(a.wheads, (int64_t)nh * H2 * 4);
+  if constexpr (IS_W2) {
 #pragma unroll
   for (int s = 0; s < NKS; ++s) {
     const int row = 64 * wave + s * K::KS + K::RPL * (lane >> 4);
@@ -692,6 +759,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     const int i = i0 + 16 * (blk >> 1) + 4 * (ln >> 4) + rg, j = j0 + 16 * (blk & 1) + (ln & 15);
     pidx[e] = (w2tile && i < H2 && j < H1) ? (int)(ao.w2 + (int64_t)i * H1 + j) : -1;
     ain[e] = adam_load(a.adam, pidx[e], polyak);
+  }
   }
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   constexpr int NV = 16 * sizeof(typename K::T) / 16;  // 16-byte loads per 16 rows of h2
@@ -722,7 +790,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     }
     RLMD_TSA(2);
     // the fc1 block operands: issued here, after the ranking, to bound register use
-    {
+    if constexpr (IS_W1) {
       const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.s, (int64_t)B * S * 4);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -745,7 +813,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     // thread's 32 rows, the heads' weights, and the Adam state of b2 / the heads'
     // rows (thread c * 32 + ci: c = 0 b2, 1..nh head c - 1) and biases (thread
     // 288 + h); on an fc1 block the Adam state of W1 / b1 (thread c * 32 + jj)
-    {
+    if constexpr (IS_HEAD) {
       const int ci = tid & 31, p = tid >> 5, i = i0 + ci;
       const __amdgpu_buffer_rsrc_t rh2 = rlmd_rsrc(a.hp2a, (int64_t)nrb * H2p * 16 * sizeof(typename K::T));
 #pragma unroll
@@ -765,6 +833,8 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         const int hq = head_at(q, A, sac);
         whc[q] = rlmd_ldf(rw, (int64_t)(hq < 0 ? 0 : hq) * H2 + i, first_col && hq >= 0 && i < H2);
       }
+    }
+    {
       const int c = tid >> 5, ii = i0 + (tid & 31), jr = j0 + (tid & 31);
       if (first_col && tid < 32 * 9 && c <= nh && ii < H2)
         xpi = (int)(c == 0 ? ao.b2 + ii : c - 1 < A ? ao.w3 + (int64_t)(c - 1) * H2 + ii
@@ -773,7 +843,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         xpi = (int)(tid - 288 < A ? ao.b3 + (tid - 288) : ao.b4 + (tid - 288 - A));
       if (w1blk && tid < 32 * 9 && (c < S || c == 8) && jr < H1)
         xpi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
-      xin = adam_load(a.adam, xpi, polyak);
+      if constexpr (IS_W1 || IS_HEAD) xin = adam_load(a.adam, xpi, polyak);
     }
     // ---- dL/da per row, then through the sampling and the heads (rlmd_policy.h)
     const float dv = sel ? -1.f / (float)kk : 0.f;
@@ -818,7 +888,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
   temperature_step();
   RLMD_TSA(4);
 
-  if (w2tile) {
+  if (IS_W2 && w2tile) {
     // ---- dW2 = sum_b dh2[b, i] h1[b, j], dh2 = [h2 > 0] (sum_h gh[b, h] W_head[h, i])
     f32x4 acc[2][2];
 #pragma unroll
@@ -867,7 +937,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
     __syncthreads();
     if (!(RLMD_ABL & 2)) tile_copies<PREC>(pcl, cd, polyak && cd.twc, i0, j0, H1p, H2p);
     RLMD_TSA(6);
-  } else if (first_col) {
+  } else if (IS_HEAD && first_col) {
     {
       // ---- db2[i] = sum_b dh2[b, i]; the heads dW_head[h, i] = sum_b gh[b, h] h2[b, i]
       const int ci = tid & 31, p = tid >> 5;
@@ -924,7 +994,7 @@ __global__ void __launch_bounds__(NT) actor_update_kernel(ActUpdArgs a) {
         }
       }
     }
-  } else {
+  } else if (IS_W1) {
     // ---- dW1[j, x] = sum_b dh1[b, j] s[b, x], db1[j]; dh1 = sum_h gh[b, h] U_h[b, j]
     const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
 #pragma unroll
