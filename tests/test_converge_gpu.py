@@ -177,15 +177,15 @@ P_MIN = 0.05
 
 
 # Dice_SH_InvA TD3 / MSE (C3's env and loss) at 65,536 lanes against the
-# reference's ten seeds: the build's growth is HIGHER and its leverage lower
-# (profiles/r06_converge_probe.jsonl: growth -0.31 .. 1.95 %/step, leverage 0.13 ..
-# 1.80, against the reference's -47.5 .. 1.9 %/step and -0.03 .. 1.98; Mann-Whitney
-# p = 0.035 / 0.075).  The round-5 N-sweep names the cause: many lanes in every
-# mini-batch (the vectorised data regime); at the reference's semantics (one lane,
+# reference's ten seeds: the build's growth is HIGHER (round 6 test run: growth 0.19
+# .. 2.45 %/step, leverage 0.19 .. 1.97, against the reference's -47.5 .. 1.9 %/step
+# and -0.03 .. 1.98; Mann-Whitney p = 0.011 / 0.218, profiles/r06_converge.jsonl).
+# The round-5 N-sweep names the cause: many lanes in every mini-batch (the
+# vectorised data regime); at the reference's semantics (one lane,
 # one update per step) the same vectorised path is consistent with it
 # (test_dice_sh_single_lane_consistent_with_reference).  Dice_SH's envs return a
 # new state array per step, so the stored-state aliasing does not apply here.
-C3_DEVIATION = pytest.mark.xfail(strict=False, reason="C3 at 65,536 lanes: growth above the reference's (p = 0.035 "
+C3_DEVIATION = pytest.mark.xfail(strict=False, reason="C3 at 65,536 lanes: growth above the reference's (p = 0.011 "
                                                       "at ten seeds a side), a vectorised-data-regime deviation "
                                                       "(DESIGN.md §5a)")
 
