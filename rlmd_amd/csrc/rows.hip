@@ -20,10 +20,6 @@
 #include <math.h>
 
 #include "learn_kernels.h"
-
-#ifndef RLMD_DEFER2
-#define RLMD_DEFER2 0  // experiment builds: a job's second fc2 stream issued after its first MLP
-#endif
 #include "rlmd_block.h"
 #include "rlmd_loss.h"
 #include "rlmd_policy.h"
@@ -784,10 +780,8 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     actor_const<NBW>(ka, an, a.ao, d);
     Pre<PREC, NBW, MULTI> pa, pc;
     pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
-#if !RLMD_DEFER2
     critic_const<NBW>(kc, cn, a.co, d, nb0);
     pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
-#endif
     const Noise2 nz = pre_nz ? noise_pre(smp, d, a.t_tag, row0) : Noise2{{0.f, 0.f}};
     RLMD_TSR(16 * job + 1);
     stage_commit(sr, s2, d.S, xs, L.ldx, row0, B);
@@ -795,12 +789,6 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     RLMD_TSR(16 * job + 2);
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
                                d.A, smem, L, nullptr, nullptr, row0, B);
-#if RLMD_DEFER2
-    // the target critic's operands after the policy's fc2 stream: issued at the
-    // start they queued beside the policy's own first load round
-    critic_const<NBW>(kc, cn, a.co, d, nb0);
-    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
-#endif
     RLMD_TSR(16 * job + 3);
     sample_rows(an.p, a.ao, d, smp, xs, L.ldx, hout, 0, a.t_tag, eps_next, a.t_noise_std, a.t_noise_clip,
                 a.t_clamp, job == 0 && !nxt && p == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz,
@@ -823,9 +811,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     critic_const<NBW>(kc, cn, a.co, d, nb0);
     Pre<PREC, NBW, MULTI> pc, pw;
     pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
-#if !RLMD_DEFER2
     if (upd) pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
-#endif
     stage_commit(sr, a.xsa, d.X, xs, L.ldx, row0, B);
     __syncthreads();
     if (job == 2) RLMD_TSR(61);
@@ -838,9 +824,6 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
       uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + L.m1s);
       // h1 is the same in both halves: half 0 writes it
       const FwdExtra<PREC> ex{p == 0 ? static_cast<T*>(a.hp1[g]) : nullptr, static_cast<T*>(a.hp2[g]), m1s, aU};
-#if RLMD_DEFER2
-      pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
-#endif
       mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
                                  nullptr, row0, B, nullptr, a.cm2[g], &ex, nb0, nbw);
       // the backward basis of these rows: U1 = [h1 > 0] * (([h2 > 0] w3) W2), so
@@ -1004,9 +987,7 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   critic_const<NBW>(kc, cn, a.co, d, nb0);
   float w1a[NBW][NHF];  // W1[c][S + j] of this lane's accumulator columns (fused actor update)
   if (upd) {
-#if !RLMD_DEFER2
     pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
-#endif
     const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(cn.p, a.co.size * 4);
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
@@ -1030,9 +1011,6 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     const uint8_t* m1s = reinterpret_cast<const uint8_t*>(smem + L.m1s);
     float* part = reinterpret_cast<float*>(smem + L.part);
     const FwdExtra<PREC> ex{nullptr, nullptr, reinterpret_cast<uint8_t*>(smem + L.m1s), aU};
-#if RLMD_DEFER2
-    pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
-#endif
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
                                nullptr, row0, B, nullptr, nullptr, &ex, nb0, nbw);
     f32x4 acc[NBW];
