@@ -567,6 +567,10 @@ def main():
     ap.add_argument("--seeds-per-gpu", default=None,
                     help="independent seeds per GPU timed after the headline (SeedGroup: one stream per seed); "
                          "default '2,3,4' (C2, C4), '2,4' otherwise; '' = off")
+    ap.add_argument("--seed-streams", default="cu,pool",
+                    help="SeedGroup stream kind(s) for --seeds-per-gpu, comma list: pool (torch's stream pool), "
+                         "hip (library streams), cu (CU-masked streams: a hardware queue each), cu_split "
+                         "(CU-masked, a 1/T interleaved CU share each); the first is the reported seeds_per_gpu")
     ap.add_argument("--seed-procs", default=None,
                     help="independent seeds per GPU as one process each (own HIP queues), timed after the headline; "
                          "default '1,2,3,4' (C2, C4), '' otherwise; '' = off")
@@ -729,15 +733,16 @@ def main():
     # several independent seeds per GPU (§8e "GPU g runs seeds {g, g+G, ...}"):
     # T whole trainers on T streams, the per-GPU throughput of a trial sweep
     seeds_spec = args.seeds_per_gpu if args.seeds_per_gpu is not None else ("2,3,4" if args.config in ("c2", "c4") else "2,4")
-    per_gpu = {}
+    per_mode = {}
+    stream_modes = [m.strip() for m in args.seed_streams.split(",") if m.strip()]
     if world == 1:
         from rlmd_amd.trainer import SeedGroup
 
-        for T in [int(v) for v in seeds_spec.split(",") if v.strip()]:
+        for mode, T in [(m, int(v)) for m in stream_modes for v in seeds_spec.split(",") if v.strip()]:
             grp = SeedGroup([420 + 1000 * i for i in range(T)], device=dev, env=cfg["env"], investor=cfg["investor"],
                             n_lanes=N, n_gambles=cfg["n"], algo=cfg["algo"], loss=args.loss, k_updates=K,
                             replay_capacity=replay, warmup_steps=0, smoothing_window=0, precision=args.precision,
-                            multi_steps=ms_n, dynamics="A", **kw)
+                            multi_steps=ms_n, dynamics="A", streams=mode, **kw)
             for _ in range(5):
                 grp.step()
             grp.synchronize()
@@ -747,9 +752,10 @@ def main():
                 grp.step()
             grp.synchronize()
             dt = time.perf_counter() - t0
-            per_gpu[str(T)] = {"env_steps_per_s": T * N * n_t / dt, "updates_per_s": T * K * n_t / dt,
-                               "ms_per_group_step": 1e3 * dt / n_t,
-                               "vs_one_seed": (T * N * n_t / dt) / (N * 1e3 / (1e3 * t_max / args.steps))}
+            per_mode.setdefault(mode, {})[str(T)] = {
+                "env_steps_per_s": T * N * n_t / dt, "updates_per_s": T * K * n_t / dt,
+                "ms_per_group_step": 1e3 * dt / n_t,
+                "vs_one_seed": (T * N * n_t / dt) / (N * 1e3 / (1e3 * t_max / args.steps))}
             del grp
     per_proc = {}
     if seed_procs is not None:
@@ -891,7 +897,9 @@ def main():
             "updates_per_s": K * args.steps * world / t_max,
             "seeds_per_gpu": {"note": "T independent seeds of this workload on one GPU (SeedGroup: own lanes, "
                                       "replay and learner per seed, one HIP stream each), per-GPU totals; eval not "
-                                      "amortised", **per_gpu} if per_gpu else None,
+                                      "amortised", "streams": stream_modes[0], **per_mode[stream_modes[0]],
+                              "other_streams": {m: per_mode[m] for m in stream_modes[1:]} or None}
+            if per_mode else None,
             "seeds_per_gpu_processes": {"note": "T independent seeds of this workload on one GPU, one process each "
                                                 "(own HIP hardware queues; the process-per-seed alternative to "
                                                 "SeedGroup's streams); per-GPU totals over the span from the first "

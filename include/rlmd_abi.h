@@ -32,6 +32,11 @@ int rlmd_device_sync(void);
  * release; *out receives the hipStream_t. */
 int rlmd_stream_create(void** out);
 int rlmd_stream_destroy(void* stream);
+/* A non-blocking stream restricted to the CUs whose bits are set in
+ * cu_mask[0 .. n_words) (bit i of word w: CU 32 w + i; hipExtStreamCreateWithCUMask).
+ * The HIP runtime gives each CU-masked stream a hardware queue of its own instead
+ * of a slot among the process's GPU_MAX_HW_QUEUES shared queues. */
+int rlmd_stream_create_cu(const uint32_t* cu_mask, int32_t n_words, void** out);
 
 /* --------------------------------------------------------------------- env */
 /* families (envs/<family>_envs.py) and investors */

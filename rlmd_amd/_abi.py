@@ -63,6 +63,7 @@ SIGNATURES = {
     "rlmd_last_error": (C.c_char_p, []),
     "rlmd_device_sync": (C.c_int, []),
     "rlmd_stream_create": (C.c_int, [P]),
+    "rlmd_stream_create_cu": (C.c_int, [P, I32, P]),
     "rlmd_stream_destroy": (C.c_int, [P]),
     "rlmd_env_create": (C.c_int, [C.POINTER(EnvCfg), P, I64, C.POINTER(P)]),
     "rlmd_env_destroy": (C.c_int, [P]),

@@ -32,6 +32,14 @@ int rlmd_stream_create(void** out) {
   return 0;
 }
 
+int rlmd_stream_create_cu(const uint32_t* cu_mask, int32_t n_words, void** out) {
+  RLMD_CHECK(out && cu_mask && n_words > 0, "null argument or empty CU mask");
+  hipStream_t s = nullptr;
+  RLMD_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)n_words, cu_mask));
+  *out = s;
+  return 0;
+}
+
 int rlmd_stream_destroy(void* stream) {
   RLMD_CHECK(stream, "null stream");
   RLMD_HIP(hipStreamDestroy((hipStream_t)stream));

@@ -46,6 +46,9 @@ constexpr int TW = 32;
 #ifndef RLMD_ROLE_SPLIT
 #define RLMD_ROLE_SPLIT 1  // role-specialised update bodies (0: one body, roles' loads predicated off)
 #endif
+#ifndef RLMD_W1_EARLY
+#define RLMD_W1_EARLY 1  // the actor step's fc1 block loads its operands before the ranking (0: after)
+#endif
 template <int NW>
 __device__ __forceinline__ void upd_rank(uint64_t key, uint64_t* runs, int* out) {
   if constexpr ((RLMD_ABL & 1) != 0) {
@@ -772,6 +775,40 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
   f32x4 uv[kUP][8];
   const int64_t ustride = (int64_t)nrb * H1p * 16;
   const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * 4);
+  // the fc1 block operands: the block's rows of s and its first kUP bases, and the
+  // Adam state of W1 / b1 (thread c * 32 + jj)
+  auto load_w1 = [&]() {
+    const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.s, (int64_t)B * S * 4);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int e = tid + q * NT, r = e >> 3, c = e & 7;
+      xv[q] = rlmd_ldf(rx, (int64_t)r * S + c, w1blk && r < B && c < S);
+    }
+    const int j = j0 + (tid & 31), p = tid >> 5;
+#pragma unroll
+    for (int h = 0; h < kUP; ++h)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int r = 32 * p + 4 * q;
+        const bool ok = w1blk && h < nh && r < nrb * 16 && j < H1p;
+        uv[h][q] = __builtin_bit_cast(
+            f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
+                                                         0, 0));
+      }
+  };
+  auto w1_adam = [&]() {
+    const int c = tid >> 5, jr = j0 + (tid & 31);
+    if (w1blk && tid < 32 * 9 && (c < S || c == 8) && jr < H1)
+      xpi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
+  };
+  // an fc1 block with its own body issues them with the first load round, under
+  // the loss and the ranking (the fc1 block is the actor step's last role to finish)
+  constexpr bool W1_EARLY = ROLE == kRoleW1 && RLMD_W1_EARLY;
+  if constexpr (W1_EARLY) {
+    load_w1();
+    w1_adam();
+    xin = adam_load(a.adam, xpi, polyak);
+  }
   {
     const float qb0 = a.qb[0][0], qb1 = a.nq > 1 ? a.qb[1][0] : 0.f;
     const float log_alpha = sac ? st->log_alpha[slot_rd(a.adam.cnt)] : 0.f;
@@ -789,26 +826,8 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
       sel = in && rank_of[tid] < kk;
     }
     RLMD_TSA(2);
-    // the fc1 block operands: issued here, after the ranking, to bound register use
-    if constexpr (IS_W1) {
-      const __amdgpu_buffer_rsrc_t rx = rlmd_rsrc(a.s, (int64_t)B * S * 4);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int e = tid + q * NT, r = e >> 3, c = e & 7;
-        xv[q] = rlmd_ldf(rx, (int64_t)r * S + c, w1blk && r < B && c < S);
-      }
-      const int j = j0 + (tid & 31), p = tid >> 5;
-#pragma unroll
-      for (int h = 0; h < kUP; ++h)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int r = 32 * p + 4 * q;
-          const bool ok = w1blk && h < nh && r < nrb * 16 && j < H1p;
-          uv[h][q] = __builtin_bit_cast(
-              f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
-                                                           0, 0));
-        }
-    }
+    // without role bodies, after the ranking, to bound register use
+    if constexpr (IS_W1 && !W1_EARLY) load_w1();
     // the first tile column's operands: h2 / [h2 > 0] of its column over the
     // thread's 32 rows, the heads' weights, and the Adam state of b2 / the heads'
     // rows (thread c * 32 + ci: c = 0 b2, 1..nh head c - 1) and biases (thread
@@ -835,15 +854,14 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
       }
     }
     {
-      const int c = tid >> 5, ii = i0 + (tid & 31), jr = j0 + (tid & 31);
+      const int c = tid >> 5, ii = i0 + (tid & 31);
       if (first_col && tid < 32 * 9 && c <= nh && ii < H2)
         xpi = (int)(c == 0 ? ao.b2 + ii : c - 1 < A ? ao.w3 + (int64_t)(c - 1) * H2 + ii
                                                    : ao.w4 + (int64_t)(c - 1 - A) * H2 + ii);
       if (first_col && i0 == 0 && tid >= 288 && tid < 288 + nh)
         xpi = (int)(tid - 288 < A ? ao.b3 + (tid - 288) : ao.b4 + (tid - 288 - A));
-      if (w1blk && tid < 32 * 9 && (c < S || c == 8) && jr < H1)
-        xpi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
-      if constexpr (IS_W1 || IS_HEAD) xin = adam_load(a.adam, xpi, polyak);
+      if constexpr (IS_W1 && !W1_EARLY) w1_adam();
+      if constexpr ((IS_W1 && !W1_EARLY) || IS_HEAD) xin = adam_load(a.adam, xpi, polyak);
     }
     // ---- dL/da per row, then through the sampling and the heads (rlmd_policy.h)
     const float dv = sel ? -1.f / (float)kk : 0.f;

@@ -322,6 +322,32 @@ def _hip_streams(device, n):
     return lst[:n]
 
 
+_CU_STREAMS = {}
+
+
+def _cu_streams(device, n, layout):
+    """n CU-masked streams (rlmd_stream_create_cu), kept for the process like
+    _hip_streams.  The HIP runtime gives a CU-masked stream a hardware queue of its
+    own, so no two seeds share a queue whatever the order of creation.  layout
+    "all": every stream may use every CU; "split": stream i gets the CUs c with
+    c % n == i (interleaved, so every XCD serves every seed)."""
+    ncu = torch.cuda.get_device_properties(device).multi_processor_count
+    words = (ncu + 31) // 32
+    out = []
+    with torch.cuda.device(device):
+        for i in range(n):
+            key = (str(device), layout, n if layout == "split" else 0, i)
+            if key not in _CU_STREAMS:
+                bits = np.zeros(words * 32, dtype=np.uint8)
+                bits[[c for c in range(ncu) if layout == "all" or c % n == i]] = 1
+                mask = np.packbits(bits.reshape(words, 32)[:, ::-1], axis=1).view(">u4").astype(np.uint32).ravel()
+                h = ctypes.c_void_p()
+                check(_abi.lib().rlmd_stream_create_cu(mask.ctypes.data_as(ctypes.c_void_p), words, ctypes.byref(h)))
+                _CU_STREAMS[key] = torch.cuda.ExternalStream(h.value, device=device)
+            out.append(_CU_STREAMS[key])
+    return out
+
+
 class SeedGroup:
     """Several independent seeds of one workload on one GPU (GPU g runs
     seeds {g, g + G, ...}; the reference's trial loop, rl_multiplicative.py:154-183,
@@ -339,12 +365,16 @@ class SeedGroup:
     where T learners' grids would queue for the same CUs (round-5 measurement at
     C2: T = 2 1.60 x one seed with the split, 1.71 x without)."""
 
-    def __init__(self, seeds, device="cuda:0", cu_budget="auto", streams="pool", **kw):
-        """streams: "pool" — torch's stream pool; a list — the caller's streams, one
+    def __init__(self, seeds, device="cuda:0", cu_budget="auto", streams="cu", **kw):
+        """streams: "cu" (default) — CU-masked streams over every CU, one hardware
+        queue each (round 6, C2: T = 2 / 3 / 4 at 1.64 / 2.04 / 2.17 x one seed,
+        against 1.67 / 1.37 / 2.16 x on torch's pool, whose T = 3 placement put two
+        seeds on one queue); "pool" — torch's stream pool; a list — the caller's streams, one
         per seed; "hip" — streams created for the
         group by the library's HIP runtime (rlmd_stream_create), wrapped as torch
         external streams: one process-wide list per device, seed i of every group
-        on its i-th stream (see _hip_streams)."""
+        on its i-th stream (see _hip_streams); "cu_split" — CU-masked streams
+        with a 1/T interleaved share of the CUs per seed (see _cu_streams)."""
         import torch
 
         self.device = torch.device(device)
@@ -357,6 +387,8 @@ class SeedGroup:
         self.cu_budget = cu_budget
         if streams == "hip":
             self.streams = _hip_streams(self.device, len(self.seeds))
+        elif streams in ("cu", "cu_split"):
+            self.streams = _cu_streams(self.device, len(self.seeds), "all" if streams == "cu" else "split")
         elif isinstance(streams, (list, tuple)):
             assert len(streams) == len(self.seeds), "one stream per seed"
             self.streams = list(streams)

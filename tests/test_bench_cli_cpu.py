@@ -66,5 +66,7 @@ def test_seed_processes_protocol():
     for T, r in sp.items():
         assert len(r["per_seed_ms_per_step"]) == int(T)
         assert r["env_steps_per_s"] == pytest.approx(int(T) * lanes * 5 / r["span_s"], rel=1e-12)
-        # the stand-in sleeps 2 ms per step in every process: the seeds overlap
-        assert r["span_s"] < int(T) * 5 * 0.002 * 0.9 or int(T) == 1
+        # the seeds overlap: the span is shorter than their own step times end to
+        # end (self-calibrated, so a loaded host that slows every step still passes)
+        serial = sum(ms * 5 / 1e3 for ms in r["per_seed_ms_per_step"])
+        assert r["span_s"] < 0.9 * serial or int(T) == 1

@@ -38,10 +38,13 @@ def _kw(golden, config):
 
 
 @pytest.mark.parametrize("config,T,streams", [("c2", 2, "pool"), ("c2", 4, "pool"), ("c4", 2, "pool"), ("c4", 4, "pool"),
-                                              ("c2", 3, "hip")])
+                                              ("c2", 3, "hip"), ("c2", 3, "cu"), ("c2", 3, "cu_split"),
+                                              ("c4", 4, "cu_split")])
 def test_seed_group_bit_equal_to_solo(golden, dev, config, T, streams):
     """streams="hip": the group's streams come from the library's runtime
-    (rlmd_stream_create) instead of torch's pool."""
+    (rlmd_stream_create) instead of torch's pool; "cu" / "cu_split": CU-masked
+    streams (rlmd_stream_create_cu, every CU / a 1/T interleaved share each).
+    A CU mask only restricts where workgroups run, so results stay bit-equal."""
     from rlmd_amd.trainer import SeedGroup, VecTrainer
 
     steps, K = 6, 4
