@@ -42,8 +42,8 @@ namespace rlmd {
 namespace {
 using namespace actrows;
 
-template <int H1P, int NB, int SP, int MA>
-__global__ void __launch_bounds__(256, H1P == 256 ? (MA == kMaxA ? 3 : 2) : 1) fused_act_kernel(FusedActArgs a) {
+template <int H1P, int NB, int SP, int MA, int WPC>
+__global__ void __launch_bounds__(256, H1P == 256 ? (MA == kMaxA ? WPC : 2) : 1) fused_act_kernel(FusedActArgs a) {
   RLMD_KERNARG_PREFETCH(a);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   act_rows<H1P, NB, SP, MA>(
@@ -99,9 +99,15 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
   const dim3 grid((unsigned)((n + kRows - 1) / kRows));
   const int sp = c.state_dim <= 8 ? 8 : 16;
   RLMD_CHECK(c.action_dim <= kMaxA4, "fused acting: at most 4 actions");
-#define ACT_LAUNCH1(H1P_, NB_, SP_, MA_)                                                                          \
-  hipExtLaunchKernelGGL((fused_act_kernel<H1P_, NB_, SP_, MA_>), grid, dim3(256), act_lds_bytes(H1P_, SP_, MA_), st, \
-                        ev_start, ev_stop, 0, a)
+  const bool wpc4 = act_wpc(h1p, c.action_dim <= kMaxA ? kMaxA : kMaxA4, grid.x) == 4;
+#define ACT_LAUNCH2(H1P_, NB_, SP_, MA_, W_)                                                                          \
+  hipExtLaunchKernelGGL((fused_act_kernel<H1P_, NB_, SP_, MA_, W_>), grid, dim3(256), act_lds_bytes(H1P_, SP_, MA_), \
+                        st, ev_start, ev_stop, 0, a)
+#define ACT_LAUNCH1(H1P_, NB_, SP_, MA_)                                                        \
+  do {                                                                                          \
+    if (wpc4) ACT_LAUNCH2(H1P_, NB_, SP_, MA_, ((H1P_) == 256 && (MA_) == kMaxA) ? 4 : 3);      \
+    else ACT_LAUNCH2(H1P_, NB_, SP_, MA_, 3);                                                   \
+  } while (0)
 #define ACT_LAUNCH(H1P_, NB_, SP_)                                            \
   {                                                                           \
     if (c.action_dim <= kMaxA) ACT_LAUNCH1(H1P_, NB_, SP_, kMaxA);            \
@@ -119,6 +125,7 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
   }
 #undef ACT_LAUNCH
 #undef ACT_LAUNCH1
+#undef ACT_LAUNCH2
   RLMD_LAUNCH_CHECK();
   return 0;
 }

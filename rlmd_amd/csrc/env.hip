@@ -778,8 +778,8 @@ struct ActEnvKargs {
   StatFold sf;
 };
 
-template <int FAM, int NG, int H1P, int NB, int SP, int MA>
-__global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA ? 3 : 2) : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
+template <int FAM, int NG, int H1P, int NB, int SP, int MA, int WPC>
+__global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA ? WPC : 2) : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
                                                       StatFold sf) {
   rlmd_kernarg_prefetch<(int)(offsetof(ActEnvKargs, sf) + sizeof(StatFold))>();
@@ -1482,9 +1482,15 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
   const bool ng1 = P.n == 1 && (P.fam != RLMD_MARKET || P.obs_days == 1);
   RLMD_CHECK(ng1 || P.fam != RLMD_DICE_SH, "fused acting + env step: dice_sh has one die");
   RLMD_CHECK(sp == 8 || P.fam == RLMD_MARKET, "fused acting + env step: state wider than 8 (market only)");
-#define FUSEDM(F, NG, H, B, SP, MA)                                                                                 \
-  hipExtLaunchKernelGGL((act_env_kernel<F, NG, H, B, SP, MA>), grid, block, actrows::act_lds_bytes(H, SP, MA), stream, \
+  const bool wpc4 = actrows::act_wpc(h1p, P.action_dim > actrows::kMaxA ? actrows::kMaxA4 : actrows::kMaxA, grid.x) == 4;
+#define FUSEDW(F, NG, H, B, SP, MA, W)                                                                                  \
+  hipExtLaunchKernelGGL((act_env_kernel<F, NG, H, B, SP, MA, W>), grid, block, actrows::act_lds_bytes(H, SP, MA), stream, \
                         ev_start, ev_stop, 0, a, env->P, step, obs, rb, ring_base, sf)
+#define FUSEDM(F, NG, H, B, SP, MA)                                                           \
+  do {                                                                                        \
+    if (wpc4) FUSEDW(F, NG, H, B, SP, MA, ((H) == 256 && (MA) == actrows::kMaxA) ? 4 : 3);    \
+    else FUSEDW(F, NG, H, B, SP, MA, 3);                                                      \
+  } while (0)
 #define FUSED(F, NG, H, B, SP) FUSEDM(F, NG, H, B, SP, actrows::kMaxA)
   // 3-4 actions: one gamble / asset and one observation day (env_act_fusable)
   const bool ma4 = P.action_dim > actrows::kMaxA;
@@ -1527,6 +1533,7 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
 #undef FUSED4
 #undef FUSED
 #undef FUSEDM
+#undef FUSEDW
   RLMD_LAUNCH_CHECK();
   env->pending_dst = ep_stats;
   if (ep_stats) {

@@ -24,8 +24,32 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kRows = 64;
+
 constexpr int kMaxA = 2;   // the headline shapes (one gamble / asset: investors A / B, Dice_SH A)
 constexpr int kMaxA4 = 4;  // the wide-action instantiation (investors C, Dice_SH B / C)
+
+// Workgroups per CU the 256-wide, two-action acting kernels are compiled for (the
+// WPC template argument: launch bounds).  At 3 they hold 140 VGPRs without
+// spills; at 4 (what their LDS allows, act_lds) they fit 128 VGPRs with 8-22
+// dwords spilled.  4 pays only when 3 per CU would leave a second dispatch round:
+// C2's 1,024 blocks (act_env 34.0 -> 32.4 us), not C4's 128 (19.6 -> 20.8 us).
+inline int act_wpc(int h1p, int ma, int64_t blocks) {
+  if (h1p != 256 || ma != kMaxA) return 3;
+  static int ncu[16] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return 3;
+  if (ncu[dev] == 0) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) return 3;
+    ncu[dev] = n;
+  }
+  static const int forced = [] {
+    const char* e = getenv("RLMD_ACT_WPC");  // 3 / 4: A/B runs
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 3 || forced == 4) return forced;
+  return blocks > 3LL * ncu[dev] ? 4 : 3;
+}
 
 
 // RNE f32 -> bf16, NaN kept quiet; branch-free (a select, not a divergent branch)
@@ -49,6 +73,31 @@ struct L1Tiles {
   static constexpr int NTP = (NT + 7) / 8 * 8 + 4;
 };
 
+// Dynamic LDS of the acting body (byte offsets).  h1 [64][HP] bf16 comes first.
+// Up to H1P = 256 the layer-1 tiles w1g and the head partials live inside h1's
+// bytes (alias): every wave takes its W1 operands into registers before any
+// wave writes h1, and a barrier after layer 2 precedes the partials.  That puts
+// a 256-wide block at 36 KB, four workgroups per CU (1,024 blocks of 65,536
+// lanes in one round instead of 768 + 256); wider nets keep separate regions.
+struct ActLds {
+  int h1, part, w1, b1, obs, total;
+  bool alias;
+};
+__host__ __device__ constexpr ActLds act_lds(int h1p, int sp, int ma) {
+  const int nt = h1p / 16, ntp = (nt + 7) / 8 * 8 + 4;
+  const int h1b = kRows * (h1p + 8) * 2, partb = 4 * kRows * 2 * ma * 4, w1b = sp * 16 * ntp * 4;
+  const bool al = h1p <= 256;
+  ActLds l{};
+  l.alias = al;
+  l.h1 = 0;
+  l.part = al ? 0 : h1b;
+  l.w1 = al ? 0 : h1b + partb;
+  l.b1 = al ? h1b : l.w1 + w1b;
+  l.obs = l.b1 + h1p * 4;
+  l.total = l.obs + kRows * sp * 4;
+  return l;
+}
+
 // The acting body for one 64-row block.  pro() runs once every thread has issued
 // its epilogue loads (a fused caller issues its own per-row loads there); epi(r,
 // b, act, obs_row) runs on thread r < 64 of each valid row b with the row's
@@ -59,12 +108,13 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
   constexpr int kMaxA = MA;
   constexpr int HP = H1P + 8;  // bf16 row pitch: 16-B aligned fragment reads
   constexpr int NT = L1Tiles<H1P>::NT, NTP = L1Tiles<H1P>::NTP;
-  unsigned short* h1s = reinterpret_cast<unsigned short*>(smem);                 // [64][HP]
-  float* part = reinterpret_cast<float*>(smem + kRows * HP * 2);                 // [4][64][2A]
+  constexpr ActLds LY = act_lds(H1P, SP, MA);
+  unsigned short* h1s = reinterpret_cast<unsigned short*>(smem + LY.h1);  // [64][HP]
+  float* part = reinterpret_cast<float*>(smem + LY.part);                 // [4][64][2A]
   const int H1 = a.H1, H2 = a.H2;
-  float* w1s = part + 4 * kRows * 2 * kMaxA;                                      // w1g [SP][16][NTP]
-  float* b1s = w1s + SP * 16 * NTP;                                               // [H1P]
-  float* obs_s = b1s + H1P;                                                       // [64][SP]
+  float* w1s = reinterpret_cast<float*>(smem + LY.w1);                    // w1g [SP][16][NTP]
+  float* b1s = reinterpret_cast<float*>(smem + LY.b1);                    // [H1P]
+  float* obs_s = reinterpret_cast<float*>(smem + LY.obs);                 // [64][SP]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * kRows;
   const NetOff& o = a.off;
@@ -140,7 +190,8 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
 #pragma unroll
     for (int j = 0; j < PW; ++j) {
       const int e = j * 256 + tid;
-      if (e < nW) w1s[e] = vw[j];  // b1 follows w1g contiguously
+      constexpr int nG = SP * 16 * NTP;
+      if (e < nW) (e < nG ? w1s[e] : b1s[e - nG]) = vw[j];
     }
 #pragma unroll
     for (int j = 0; j < PO; ++j) {
@@ -166,6 +217,18 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
     typedef float f32x8 __attribute__((ext_vector_type(8)));
     const int j = lane & 15, kl = lane >> 4;
     const int ra = 16 * wave + j;
+    // aliased layout: every group's W1 operands into registers, then a barrier,
+    // before this wave's first h1 store can overwrite w1g
+    constexpr int NG = LY.alias ? (NT + 7) / 8 : 1;
+    f32x8 bvg[NG][SP / 4];
+    if constexpr (LY.alias) {
+#pragma unroll
+      for (int g = 0; g < NG; ++g)
+#pragma unroll
+        for (int ks = 0; ks < SP / 4; ++ks)
+          bvg[g][ks] = *reinterpret_cast<const f32x8*>(&w1s[((4 * ks + kl) * 16 + j) * NTP + 8 * g]);
+      __syncthreads();
+    }
 #pragma unroll
     for (int t0 = 0; t0 < NT; t0 += 8) {
       f32x4 h[8];
@@ -176,7 +239,10 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
 #pragma unroll
       for (int ks = 0; ks < SP / 4; ++ks) {
         av[ks] = obs_s[ra * SP + 4 * ks + kl];
-        bv[ks] = *reinterpret_cast<const f32x8*>(&w1s[((4 * ks + kl) * 16 + j) * NTP + t0]);
+        if constexpr (LY.alias)
+          bv[ks] = bvg[t0 / 8][ks];
+        else
+          bv[ks] = *reinterpret_cast<const f32x8*>(&w1s[((4 * ks + kl) * 16 + j) * NTP + t0]);
       }
       f32x4 bias[8];
 #pragma unroll
@@ -229,6 +295,7 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
     }
   }
   RLMD_TSA(4, __builtin_amdgcn_s_memtime());
+  if constexpr (LY.alias) __syncthreads();  // the partials overwrite h1
   // -- epilogue: relu(h2 + b2) . heads, partial per row over this wave's columns
   //    (columns past H2 have zero weights and biases)
 #pragma unroll
@@ -297,10 +364,7 @@ inline bool fused_shape(const rlmd_agent_cfg& c, int& h1p, int& nb) {
 }
 
 // dynamic LDS of act_rows<h1p, *, sp, ma>
-inline size_t act_lds_bytes(int h1p, int sp, int ma = kMaxA) {
-  const int nt = h1p / 16, ntp = (nt + 7) / 8 * 8 + 4;
-  return (size_t)kRows * (h1p + 8) * 2 + 4 * kRows * 2 * ma * 4 + ((size_t)sp * 16 * ntp + h1p + kRows * sp) * 4;
-}
+inline size_t act_lds_bytes(int h1p, int sp, int ma = kMaxA) { return (size_t)act_lds(h1p, sp, ma).total; }
 
 // the acting body's action bound for an action count
 inline int act_ma(int action_dim) { return action_dim <= kMaxA ? kMaxA : kMaxA4; }
