@@ -86,7 +86,7 @@ def _random_batch(rng, B, S, A):
 
 @pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL)
 @pytest.mark.parametrize("loss", ["MSE", "HUB", "MAE", "HSC"])
-def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_lr_frac=0.1, s_dist="N"):
+def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_lr_frac=0.1, s_dist="N", dup=False):
     from rlmd_amd.agent import reference_init
 
     init = reference_init(algo, S, A, h1, h2, seed=11)
@@ -103,6 +103,9 @@ def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_
         s, a, r, s2, d = _random_batch(rng, B, S, A)
         ea = torch.from_numpy(draw().astype(np.float32))
         eb = torch.from_numpy(draw().astype(np.float32))
+        if dup:  # rows 2i + 1 repeat rows 2i: equal losses and actor objectives, ranked by row
+            for x in (s, a, r, s2, d, ea, eb):
+                x[1::2] = x[0::2]
         st = ag.learn_batch(s, a, r, s2, d, ea, eb if algo == "SAC" else None).double().cpu().numpy()
         loss_o, lt_o, lp_o = ora.learn(s.numpy(), a.numpy(), r.numpy(), s2.numpy(), d.numpy(), ea.numpy(),
                                        eb.numpy() if algo == "SAC" else None)
@@ -111,6 +114,14 @@ def test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, loss, max_
         lr = 3e-4 if algo == "SAC" else 1e-3
         assert_params_close(ag.params.cpu().numpy(), ora.P.numpy(), lr, f"step {step} params", max_lr_frac)
         assert_params_close(ag.target.cpu().numpy(), ora.T.numpy(), lr, f"step {step} targets", max_lr_frac)
+
+
+@pytest.mark.parametrize("algo,S,A,h1,h2,B,k", FULL[:2])
+def test_tied_rows_match_oracle(dev, algo, S, A, h1, h2, B, k):
+    """Mini-batches of repeated rows: every critic loss and actor objective value
+    occurs twice, so the top-k selections break ties by row (the oracle's stable
+    argsort, the kernels' (value, row) keys, rlmd_block.h block_rank)."""
+    test_full_size_fp32_matches_oracle(dev, algo, S, A, h1, h2, B, k, "MSE", dup=True)
 
 
 @pytest.mark.parametrize("loss", ["CAU", "TCAU", "CIM", "MSE2", "MSE4", "MSE6"])
