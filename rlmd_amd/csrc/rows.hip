@@ -36,6 +36,9 @@ constexpr int NW = NT / 64;   // waves
 constexpr int NHF = 4;        // heads reduced in the MFMA epilogue (more -> LDS dot products)
 constexpr int W1P = 8;        // fc1 inputs preloaded per thread (more -> read in the loop)
 constexpr int kHeadsMax = 2 * RLMD_MAX_ACTION;
+#ifndef RLMD_FWD_DEFER
+#define RLMD_FWD_DEFER 1  // fwd_rows: a job's second fragment stream issued after its first net's layer 2
+#endif
 
 #ifdef RLMD_TIMING
 // experiment builds only (tools/ts_probe.py): thread-0 s_memtime checkpoints of
@@ -520,14 +523,21 @@ __device__ void row_dots(const float* src, int lds, int ncols, int nh, const flo
   }
 }
 
+struct NoHook {
+  __device__ void operator()() const {}
+};
+
 // One 2-hidden-layer MLP forward over the block's rows (x in LDS), heads left in
 // hout[r][h] (no head bias).  pre: this net's fc2 fragments, already issued.
-template <int PREC, int NBW, bool MULTI>
+// after_l2 runs right after layer 2's MFMAs, once pre's registers are free: a
+// job issues its NEXT fragment stream there, under this net's epilogue, instead
+// of with the first load round, where it queued behind (and delayed) this one.
+template <int PREC, int NBW, bool MULTI, typename Hook = NoHook>
 __device__ __forceinline__ void mlp_rows(const RowNet& net, const NetOff& o, const FwdConst<NBW>& k, Pre<PREC, NBW, MULTI>& pre,
                          const float* xs, int ldx, int in, int nh, const float* wa, const float* wb, int na,
                          unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B,
                          uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr, const FwdExtra<PREC>* ex = nullptr,
-                         int nb0 = 0, int nbw = 0) {
+                         int nb0 = 0, int nbw = 0, Hook after_l2 = Hook()) {
   using T = typename CT<PREC>::T;
   T* a1 = reinterpret_cast<T*>(smem + L.a1);
   float* part = reinterpret_cast<float*>(smem + L.part);
@@ -542,6 +552,7 @@ __device__ __forceinline__ void mlp_rows(const RowNet& net, const NetOff& o, con
   f32x4 acc[NBW];
   const int H1p = pad32(o.h1);
   mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, nbw ? nbw : pad32(o.h2) / 16, acc, nb0);
+  after_l2();
   if (blockIdx.y == 2) RLMD_TSR(65);
   if (blockIdx.y == 4) RLMD_TSR(89);
   const bool fused = nh <= NHF;
@@ -780,15 +791,24 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     actor_const<NBW>(ka, an, a.ao, d);
     Pre<PREC, NBW, MULTI> pa, pc;
     pre_issue<PREC, NBW, MULTI>(pa, an.wc, H1p, H1p, H2p / 16);
-    critic_const<NBW>(kc, cn, a.co, d, nb0);
-    pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
+    // the target critic's constants and fc2 stream: issued after the policy's
+    // layer 2 (RLMD_FWD_DEFER; 0: with this first round)
+    auto issue_critic = [&] {
+      critic_const<NBW>(kc, cn, a.co, d, nb0);
+      pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
+    };
+    if constexpr (!RLMD_FWD_DEFER) issue_critic();
     const Noise2 nz = pre_nz ? noise_pre(smp, d, a.t_tag, row0) : Noise2{{0.f, 0.f}};
     RLMD_TSR(16 * job + 1);
     stage_commit(sr, s2, d.S, xs, L.ldx, row0, B);
     __syncthreads();
     RLMD_TSR(16 * job + 2);
-    mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
-                               d.A, smem, L, nullptr, nullptr, row0, B);
+    if constexpr (RLMD_FWD_DEFER)
+      mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
+                                 d.A, smem, L, nullptr, nullptr, row0, B, nullptr, nullptr, nullptr, 0, 0, issue_critic);
+    else
+      mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
+                                 d.A, smem, L, nullptr, nullptr, row0, B);
     RLMD_TSR(16 * job + 3);
     sample_rows(an.p, a.ao, d, smp, xs, L.ldx, hout, 0, a.t_tag, eps_next, a.t_noise_std, a.t_noise_clip,
                 a.t_clamp, job == 0 && !nxt && p == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz,
@@ -811,7 +831,11 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     critic_const<NBW>(kc, cn, a.co, d, nb0);
     Pre<PREC, NBW, MULTI> pc, pw;
     pre_issue<PREC, NBW, MULTI>(pc, cn.wc, H1p, H1p, nbw, nb0);
-    if (upd) pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
+    // the basis pass's stream (the transposed copy): after the forward's layer 2
+    auto issue_basis = [&] {
+      if (upd) pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
+    };
+    if constexpr (!RLMD_FWD_DEFER) issue_basis();
     stage_commit(sr, a.xsa, d.X, xs, L.ldx, row0, B);
     __syncthreads();
     if (job == 2) RLMD_TSR(61);
@@ -824,8 +848,12 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
       uint8_t* m1s = reinterpret_cast<uint8_t*>(smem + L.m1s);
       // h1 is the same in both halves: half 0 writes it
       const FwdExtra<PREC> ex{p == 0 ? static_cast<T*>(a.hp1[g]) : nullptr, static_cast<T*>(a.hp2[g]), m1s, aU};
-      mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
-                                 nullptr, row0, B, nullptr, a.cm2[g], &ex, nb0, nbw);
+      if constexpr (RLMD_FWD_DEFER)
+        mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
+                                   nullptr, row0, B, nullptr, a.cm2[g], &ex, nb0, nbw, issue_basis);
+      else
+        mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
+                                   nullptr, row0, B, nullptr, a.cm2[g], &ex, nb0, nbw);
       // the backward basis of these rows: U1 = [h1 > 0] * (([h2 > 0] w3) W2), so
       // that the critic update forms dh1 = dq * U1 once dq is known (update.hip);
       // a half's partial U1 over its fc2 columns
@@ -986,8 +1014,10 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
   FwdConst<NBW> kc;
   critic_const<NBW>(kc, cn, a.co, d, nb0);
   float w1a[NBW][NHF];  // W1[c][S + j] of this lane's accumulator columns (fused actor update)
+  // the basis pass's stream: after the forward's layer 2 (as fwd_rows' critic jobs)
+  auto issue_basis = [&] { pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0); };
   if (upd) {
-    pre_issue<PREC, NBW, MULTI>(pw, cn.wt, H2p, ke, H1p / 16, 0, ks0);
+    if constexpr (!RLMD_FWD_DEFER) issue_basis();
     const __amdgpu_buffer_rsrc_t rp = rlmd_rsrc(cn.p, a.co.size * 4);
 #pragma unroll
     for (int i = 0; i < NBW; ++i) {
@@ -1011,8 +1041,12 @@ __global__ void __launch_bounds__(NT) qeval_rows_kernel(QEvalArgs a) {
     const uint8_t* m1s = reinterpret_cast<const uint8_t*>(smem + L.m1s);
     float* part = reinterpret_cast<float*>(smem + L.part);
     const FwdExtra<PREC> ex{nullptr, nullptr, reinterpret_cast<uint8_t*>(smem + L.m1s), aU};
-    mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
-                               nullptr, row0, B, nullptr, nullptr, &ex, nb0, nbw);
+    if constexpr (RLMD_FWD_DEFER)
+      mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
+                                 nullptr, row0, B, nullptr, nullptr, &ex, nb0, nbw, issue_basis);
+    else
+      mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
+                                 nullptr, row0, B, nullptr, nullptr, &ex, nb0, nbw);
     f32x4 acc[NBW];
     mfma_rows<PREC, NBW, MULTI>(pw, aU, L.lda1, cn.wt, H2p, ke, H1p / 16, acc, 0, ks0);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
