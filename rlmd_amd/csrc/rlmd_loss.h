@@ -71,17 +71,20 @@ struct CriticLoads {
   // uniform scalars issued with the row loads: head biases, log alpha, Cauchy scales
   float tb[2], qb[2], log_alpha, cauchy[2];
 };
+// MAYSPLIT false: the caller knows a.qsplit == 1 and the second halves' loads are
+// not issued at all (predicated off they still cost an addresser wave-instruction).
+template <bool MAYSPLIT = true>
 __device__ __forceinline__ CriticLoads critic_row_load(const LossArgs& a) {
   const int b = threadIdx.x, B = a.B;
   const bool in = b < B;
   const int64_t nB = (int64_t)B * 4;
-  const bool h2 = a.qsplit > 1;  // second half of the partial sums (fwd_rows column split)
+  const bool h2 = MAYSPLIT && a.qsplit > 1;  // second half of the partial sums (fwd_rows column split)
   const int64_t nBq = h2 ? 2 * nB : nB;
   CriticLoads L;
   for (int g = 0; g < 2; ++g) {
     const __amdgpu_buffer_rsrc_t rt = rlmd_rsrc(a.tpart[g], nBq), rq = rlmd_rsrc(a.qpart[g], nBq);
-    L.qt[g] = rlmd_ldf(rt, b, in) + rlmd_ldf(rt, B + b, in && h2);
-    L.q[g] = rlmd_ldf(rq, b, in) + rlmd_ldf(rq, B + b, in && h2);
+    L.qt[g] = rlmd_ldf(rt, b, in) + (MAYSPLIT ? rlmd_ldf(rt, B + b, in && h2) : 0.f);
+    L.q[g] = rlmd_ldf(rq, b, in) + (MAYSPLIT ? rlmd_ldf(rq, B + b, in && h2) : 0.f);
   }
   L.rw = rlmd_ldf(rlmd_rsrc(a.r, nB), b, in);
   // optional operands through zero-sized resources when absent (the load then

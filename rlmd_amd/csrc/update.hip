@@ -46,6 +46,9 @@ constexpr int TW = 32;
 #ifndef RLMD_ROLE_SPLIT
 #define RLMD_ROLE_SPLIT 1  // role-specialised update bodies (0: one body, roles' loads predicated off)
 #endif
+#ifndef RLMD_SPLIT_SPEC
+#define RLMD_SPLIT_SPEC 1  // critic step bodies specialised on fwd_rows' column split (0: one body, halves predicated)
+#endif
 #ifndef RLMD_W1_EARLY
 #define RLMD_W1_EARLY 1  // the actor step's fc1 block loads its operands before the ranking (0: after)
 #endif
@@ -233,10 +236,13 @@ struct ULds {
 // launch in texture-addresser issue (TA_TA_BUSY, profiles/r06_pmc_ta.json).
 enum { kRoleW2 = 0, kRoleW1 = 1, kRoleHead = 2 };
 
-template <int PREC, bool WIDE, int ROLE>
+template <int PREC, bool WIDE, int ROLE, bool SPLIT>
 __device__ __forceinline__ void critic_update_body(const CritUpdArgs& a, unsigned char* smem, int g, int t);
 
-template <int PREC, bool WIDE>
+// SPLIT false (fwd_rows unsplit, a.loss.qsplit == 1): the bodies without the
+// second halves' loads of q / target q / U1 — predicated off, each still cost the
+// texture addresser a wave-instruction
+template <int PREC, bool WIDE, bool SPLIT>
 __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   RLMD_KERNARG_PREFETCH(a);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -253,17 +259,17 @@ __global__ void __launch_bounds__(NT) critic_update_kernel(CritUpdArgs a) {
   }
   const int g = blockIdx.x / per, t = blockIdx.x - g * per;
 #if RLMD_ROLE_SPLIT
-  if (t < a.n_w2) critic_update_body<PREC, WIDE, kRoleW2>(a, smem, g, t);
-  else if (t >= a.n_w2 + a.n_w1) critic_update_body<PREC, WIDE, kRoleHead>(a, smem, g, t);
-  else critic_update_body<PREC, WIDE, kRoleW1>(a, smem, g, t);
+  if (t < a.n_w2) critic_update_body<PREC, WIDE, kRoleW2, SPLIT>(a, smem, g, t);
+  else if (t >= a.n_w2 + a.n_w1) critic_update_body<PREC, WIDE, kRoleHead, SPLIT>(a, smem, g, t);
+  else critic_update_body<PREC, WIDE, kRoleW1, SPLIT>(a, smem, g, t);
 #else
-  critic_update_body<PREC, WIDE, -1>(a, smem, g, t);
+  critic_update_body<PREC, WIDE, -1, SPLIT>(a, smem, g, t);
 #endif
 }
 
 // ROLE -1: one body for every role, the roles' loads issued predicated-off (the
 // round-5 form, RLMD_ROLE_SPLIT=0)
-template <int PREC, bool WIDE, int ROLE>
+template <int PREC, bool WIDE, int ROLE, bool SPLIT>
 __device__ __forceinline__ void critic_update_body(const CritUpdArgs& a, unsigned char* smem, int g, int t) {
   using K = KT<PREC>;
   float* dqs = reinterpret_cast<float*>(smem + ULds::dq);
@@ -304,7 +310,7 @@ __device__ __forceinline__ void critic_update_body(const CritUpdArgs& a, unsigne
   //      Branch-free: every load is issued by every workgroup, predicated through
   //      the range check on its role (a load inside `if (role)` is copied out of
   //      its registers at the merge, which waits for it on the spot)
-  const CriticLoads cl = critic_row_load(a.loss);
+  const CriticLoads cl = critic_row_load<SPLIT>(a.loss);
   // (a) dW2 tile: per wave rows [64 w, 64 w + 64), per K-step the A masks (two i
   //     sub-blocks) and B fragments (two j sub-blocks)
   constexpr int NKS = 64 / K::KS;
@@ -396,7 +402,7 @@ __device__ __forceinline__ void critic_update_body(const CritUpdArgs& a, unsigne
       xv[q] = rlmd_ldf(rx, (int64_t)r * X + c, w1blk && r < B && c < X);
     }
     const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
-    const bool us = a.loss.qsplit > 1;
+    const bool us = SPLIT && a.loss.qsplit > 1;
     const int64_t ustr = (int64_t)nrb * H1p * 16;
     const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.u1[g], ustr * (us ? 2 : 1) * 4);
 #pragma unroll
@@ -405,8 +411,11 @@ __device__ __forceinline__ void critic_update_body(const CritUpdArgs& a, unsigne
       const bool ok = w1blk && r < nrb * 16 && j < H1p;
       u1v[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
                                              ru, ok ? (int)(rp_idx(r, H1p, j) * 4) : 0x7fffffff, 0, 0));
-      u1w[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             ru, (ok && us) ? (int)((ustr + rp_idx(r, H1p, j)) * 4) : 0x7fffffff, 0, 0));
+      if constexpr (SPLIT)
+        u1w[q] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                                               ru, (ok && us) ? (int)((ustr + rp_idx(r, H1p, j)) * 4) : 0x7fffffff, 0, 0));
+      else
+        u1w[q] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
 
@@ -1113,17 +1122,20 @@ int critic_update_launch(const CritUpdArgs& a, hipStream_t st) {
              "critic update: tile grid inconsistent with the widths");
   RLMD_CHECK(a.cstats.B <= NT, "critic statistics workgroups: mini-batch up to 512 rows");
   const dim3 grid(2 * (a.n_w2 + a.n_w1 + a.ti) + (a.cstats.B > 0 ? 2 : 0));
+  const bool split = !RLMD_SPLIT_SPEC || a.loss.qsplit > 1;
+#define CRIT_LAUNCH(P_, W_)                                                                                  \
+  do {                                                                                                       \
+    if (split) hipLaunchKernelGGL((critic_update_kernel<P_, W_, true>), grid, dim3(NT), ULds::total, st, a);  \
+    else hipLaunchKernelGGL((critic_update_kernel<P_, W_, false>), grid, dim3(NT), ULds::total, st, a);      \
+  } while (0)
   if (d.prec == RLMD_BF16) {
-    if (wide)
-      hipLaunchKernelGGL((critic_update_kernel<RLMD_BF16, true>), grid, dim3(NT), ULds::total, st, a);
-    else
-      hipLaunchKernelGGL((critic_update_kernel<RLMD_BF16, false>), grid, dim3(NT), ULds::total, st, a);
+    if (wide) CRIT_LAUNCH(RLMD_BF16, true);
+    else CRIT_LAUNCH(RLMD_BF16, false);
   } else {
-    if (wide)
-      hipLaunchKernelGGL((critic_update_kernel<RLMD_FP32, true>), grid, dim3(NT), ULds::total, st, a);
-    else
-      hipLaunchKernelGGL((critic_update_kernel<RLMD_FP32, false>), grid, dim3(NT), ULds::total, st, a);
+    if (wide) CRIT_LAUNCH(RLMD_FP32, true);
+    else CRIT_LAUNCH(RLMD_FP32, false);
   }
+#undef CRIT_LAUNCH
   RLMD_LAUNCH_CHECK();
   return 0;
 }
