@@ -39,6 +39,9 @@ constexpr int kHeadsMax = 2 * RLMD_MAX_ACTION;
 #ifndef RLMD_FWD_DEFER
 #define RLMD_FWD_DEFER 1  // fwd_rows: a job's second fragment stream issued after its first net's layer 2
 #endif
+#ifndef RLMD_SAMPLE_NL
+#define RLMD_SAMPLE_NL 1  // fwd_rows: load-free policy sampling on the production path (sample_rows<true>)
+#endif
 
 #ifdef RLMD_TIMING
 // experiment builds only (tools/ts_probe.py): thread-0 s_memtime checkpoints of
@@ -616,6 +619,13 @@ __device__ __forceinline__ Noise2 noise_pre(const SampleCfg& smp, const RowDims&
 // action into xs[:, S:S+A] and xa_out (nullable).  Same arithmetic as
 // learn.hip's actor_head_kernel.  mode 0 stochastic, 1 deterministic.  hb: the
 // head biases preloaded (A <= 2) when has_hb, else read here.
+// NL (no loads): the caller guarantees has_hb, A <= 2, eps_in == nullptr and has_nz
+// (or mode 1): the body then issues no global load.  A load here is waited on
+// with vmcnt(0) at its branch's merge, and vmcnt also counts every load and
+// store issued before it — a deferred fragment stream (fwd_rows' target critic,
+// issued under the policy's epilogue) or the write-through row-packed stores of
+// the policy's h1 / h2 — so the sampling waited for all of them.
+template <bool NL = false>
 __device__ __forceinline__ void sample_rows(const float* p, const NetOff& ao, const RowDims& d, const SampleCfg& smp, float* xs,
                             int ldx, const float* hout, int mode, int tag, const float* eps_in, float noise_std,
                             float noise_clip, int clamp_noise, float* logp_out, float* save, float* xa_out, int row0,
@@ -627,17 +637,23 @@ __device__ __forceinline__ void sample_rows(const float* p, const NetOff& ao, co
   const bool valid = b < B, sac = d.algo == RLMD_SAC;
   const uint32_t c1 = smp.ctr;
   float lp_sum = 0.f, m2_sum = 0.f, hld_sum = 0.f, jac_sum = 0.f;
-  const bool pre = has_hb && A <= 2;
-  for (int j = 0; j < A; ++j) {
-    const float mu = hout[r * kHeadsMax + j] + (pre ? (j == 0 ? hbv.mu[0] : hbv.mu[1]) : p[ao.b3 + j]);
+  const bool pre = NL || (has_hb && A <= 2);
+  for (int j = 0; j < (NL ? 2 : A); ++j) {
+    if (NL && j >= A) break;
+    const float mu = hout[r * kHeadsMax + j] + (pre ? (j == 0 ? hbv.mu[0] : hbv.mu[1]) : (NL ? 0.f : p[ao.b3 + j]));
     float noise = 0.f;
-    if (mode == 0 && valid)
-      noise = eps_in ? eps_in[(int64_t)b * A + j]
-                     : (has_nz && A <= 2 ? (j == 0 ? nz2.v[0] : nz2.v[1])
-                                         : policy_draw(smp.dist, smp.seed, (uint32_t)b, c1, (uint32_t)tag, j));
+    if (mode == 0 && valid) {
+      if constexpr (NL)
+        noise = j == 0 ? nz2.v[0] : nz2.v[1];
+      else
+        noise = eps_in ? eps_in[(int64_t)b * A + j]
+                       : (has_nz && A <= 2 ? (j == 0 ? nz2.v[0] : nz2.v[1])
+                                           : policy_draw(smp.dist, smp.seed, (uint32_t)b, c1, (uint32_t)tag, j));
+    }
     float act;
     if (sac) {
-      const float ls_raw = hout[r * kHeadsMax + A + j] + (pre ? (j == 0 ? hbv.ls[0] : hbv.ls[1]) : p[ao.b4 + j]);
+      const float ls_raw =
+          hout[r * kHeadsMax + A + j] + (pre ? (j == 0 ? hbv.ls[0] : hbv.ls[1]) : (NL ? 0.f : p[ao.b4 + j]));
       const PolicyComp pc = policy_comp(smp.dist, mu, ls_raw, noise, smp.ls_min, smp.ls_max);
       if (mode == 1) {
         act = tanhf(pc.mu) * smp.max_action;
@@ -810,9 +826,15 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
       mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
                                  d.A, smem, L, nullptr, nullptr, row0, B);
     RLMD_TSR(16 * job + 3);
-    sample_rows(an.p, a.ao, d, smp, xs, L.ldx, hout, 0, a.t_tag, eps_next, a.t_noise_std, a.t_noise_clip,
-                a.t_clamp, job == 0 && !nxt && p == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz,
-                pre_nz);
+    // load-free sampling on the production path (no injected noise): see sample_rows
+    if (RLMD_SAMPLE_NL && pre_nz && d.A <= 2)
+      sample_rows<true>(an.p, a.ao, d, smp, xs, L.ldx, hout, 0, a.t_tag, nullptr, a.t_noise_std, a.t_noise_clip,
+                        a.t_clamp, job == 0 && !nxt && p == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb,
+                        true, nz, true);
+    else
+      sample_rows(an.p, a.ao, d, smp, xs, L.ldx, hout, 0, a.t_tag, eps_next, a.t_noise_std, a.t_noise_clip,
+                  a.t_clamp, job == 0 && !nxt && p == 0 ? a.logp_next : nullptr, nullptr, nullptr, row0, B, hb, true, nz,
+                  pre_nz);
     __syncthreads();
     RLMD_TSR(16 * job + 4);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
@@ -891,8 +913,12 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
                                d.A, smem, L, fa ? nullptr : a.h1a, fa ? nullptr : a.h2a, row0, B, a.am1, a.am2, &ex);
     RLMD_TSR(82);
-    sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, a.a_mode, a.a_tag, a.eps_cur, 0.f, 0.f, 0, a.logp, a.save,
-                a.xsan, row0, B, hb, true, nz, pre_nz);
+    if (RLMD_SAMPLE_NL && (pre_nz || a.a_mode == 1) && a.eps_cur == nullptr && d.A <= 2)
+      sample_rows<true>(an.p, a.ao, d, a.smp, xs, L.ldx, hout, a.a_mode, a.a_tag, nullptr, 0.f, 0.f, 0, a.logp, a.save,
+                        a.xsan, row0, B, hb, true, nz, true);
+    else
+      sample_rows(an.p, a.ao, d, a.smp, xs, L.ldx, hout, a.a_mode, a.a_tag, a.eps_cur, 0.f, 0.f, 0, a.logp, a.save,
+                  a.xsan, row0, B, hb, true, nz, pre_nz);
     RLMD_TSR(83);
   }
   RLMD_TSJ(45 + job);
