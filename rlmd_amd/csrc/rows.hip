@@ -39,6 +39,9 @@ constexpr int kHeadsMax = 2 * RLMD_MAX_ACTION;
 #ifndef RLMD_FWD_DEFER
 #define RLMD_FWD_DEFER 1  // fwd_rows: a job's second fragment stream issued after its first net's layer 2
 #endif
+#ifndef RLMD_L1_BATCH
+#define RLMD_L1_BATCH 1  // row kernels' layer 1: a batch of rows' inputs read from LDS together
+#endif
 #ifndef RLMD_SAMPLE_NL
 #define RLMD_SAMPLE_NL 1  // fwd_rows: load-free policy sampling on the production path (sample_rows<true>)
 #endif
@@ -397,27 +400,66 @@ __device__ __forceinline__ void layer1(const FwdConst<NBW>& k, const float* p, c
   const int nr = m.r1 - m.r0;
   const float* w = p + o.w1 + (int64_t)m.c * in;
   uint64_t mk[(MR + 7) / 8] = {};  // the thread's mask bytes, row r0 + rr at byte rr
-  for (int r = m.r0; r < m.r1; ++r) {
+  // row r0 + rr's unit: relu(acc + b1) into the A operand, h1_out, the mask bytes
+  auto emit = [&](int rr, float acc) {
+    const int r = m.r0 + rr;
     float v = 0.f;
     if (m.c < H1) {
-      float acc = 0.f;
-      // xs rows are zero padded to ldx >= W1P and k.w1[j] = 0 for j >= in: no branch
-      // between the LDS reads, so a row's W1P reads issue together
-#pragma unroll
-      for (int j = 0; j < W1P; ++j) acc = fmaf(xs[r * ldx + j], k.w1[j], acc);
-      for (int j = W1P; j < in; ++j) acc = fmaf(xs[r * ldx + j], w[j], acc);
       v = fmaxf(acc + k.b1, 0.f);
       if (h1_out && row0 + r < B) h1_out[(int64_t)(row0 + r) * H1 + m.c] = v;
     }
     a1[r * lda1 + m.c] = CT<PREC>::cvt(v);
     if (ex && ex->m1s) ex->m1s[r * H1p + m.c] = v > 0.f ? 1 : 0;
-    const int rr = r - m.r0;
     const uint64_t bit = (uint64_t)(v > 0.f ? 1u : 0u) << (8 * (rr & 7));
     if constexpr (MR > 8) {
       if (rr < 8) mk[0] |= bit;
       else mk[1] |= bit;
     } else {
       mk[0] |= bit;
+    }
+  };
+  if (RLMD_L1_BATCH && in <= W1P && (ldx & 3) == 0) {
+    // every input in registers (k.w1, zero past in): a batch of rows' xs as 16-byte
+    // LDS reads issued together, then their dots (j ascending, as below).  The
+    // per-row loop waited one LDS round trip per row, its bounds being run-time.
+    constexpr int LB = MR < 8 ? MR : 8;
+    static_assert(W1P == 8, "the batched dots below read 8 inputs per row");
+#pragma unroll
+    for (int b0 = 0; b0 < MR; b0 += LB) {
+      float4 xv[LB][2];
+#pragma unroll
+      for (int i = 0; i < LB; ++i) {
+        const int r = m.r0 + b0 + i < R ? m.r0 + b0 + i : R - 1;  // rows past this thread's: read, unused
+        xv[i][0] = *reinterpret_cast<const float4*>(xs + r * ldx);
+        xv[i][1] = *reinterpret_cast<const float4*>(xs + r * ldx + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < LB; ++i) {
+        if (b0 + i < nr) {
+          float acc = 0.f;
+          acc = fmaf(xv[i][0].x, k.w1[0], acc);
+          acc = fmaf(xv[i][0].y, k.w1[1], acc);
+          acc = fmaf(xv[i][0].z, k.w1[2], acc);
+          acc = fmaf(xv[i][0].w, k.w1[3], acc);
+          acc = fmaf(xv[i][1].x, k.w1[4], acc);
+          acc = fmaf(xv[i][1].y, k.w1[5], acc);
+          acc = fmaf(xv[i][1].z, k.w1[6], acc);
+          acc = fmaf(xv[i][1].w, k.w1[7], acc);
+          emit(b0 + i, acc);
+        }
+      }
+    }
+  } else {
+    for (int r = m.r0; r < m.r1; ++r) {
+      float acc = 0.f;
+      if (m.c < H1) {
+        // xs rows are zero padded to ldx >= W1P and k.w1[j] = 0 for j >= in: no branch
+        // between the LDS reads, so a row's W1P reads issue together
+#pragma unroll
+        for (int j = 0; j < W1P; ++j) acc = fmaf(xs[r * ldx + j], k.w1[j], acc);
+        for (int j = W1P; j < in; ++j) acc = fmaf(xs[r * ldx + j], w[j], acc);
+      }
+      emit(r - m.r0, acc);
     }
   }
   if (m.r0 < R) {
@@ -540,32 +582,38 @@ __device__ __forceinline__ void mlp_rows(const RowNet& net, const NetOff& o, con
                          const float* xs, int ldx, int in, int nh, const float* wa, const float* wb, int na,
                          unsigned char* smem, const Lds& L, float* h1_out, float* h2_out, int row0, int B,
                          uint8_t* m1_out = nullptr, uint8_t* m2_out = nullptr, const FwdExtra<PREC>* ex = nullptr,
-                         int nb0 = 0, int nbw = 0, Hook after_l2 = Hook()) {
+                         int nb0 = 0, int nbw = 0, Hook after_l2 = Hook(), int ts = -1) {
   using T = typename CT<PREC>::T;
   T* a1 = reinterpret_cast<T*>(smem + L.a1);
   float* part = reinterpret_cast<float*>(smem + L.part);
   float* hout = reinterpret_cast<float*>(smem + L.hout);
   float* h2s = reinterpret_cast<float*>(smem + L.h2s);
+  (void)ts;  // job 0's stamps (RLMD_TIMING builds): slots ts .. ts + 4
   layer1<PREC, NBW>(k, net.p, o, xs, ldx, in, a1, L.lda1, h1_out, m1_out, row0, B, ex);
   if (blockIdx.y == 2) RLMD_TSR(63);
   if (blockIdx.y == 4) RLMD_TSR(87);
+  if (blockIdx.y == 0 && ts >= 0) RLMD_TSR(ts);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(64);
   if (blockIdx.y == 4) RLMD_TSR(88);
+  if (blockIdx.y == 0 && ts >= 0) RLMD_TSR(ts + 1);
   f32x4 acc[NBW];
   const int H1p = pad32(o.h1);
   mfma_rows<PREC, NBW, MULTI>(pre, a1, L.lda1, net.wc, H1p, H1p, nbw ? nbw : pad32(o.h2) / 16, acc, nb0);
   after_l2();
   if (blockIdx.y == 2) RLMD_TSR(65);
   if (blockIdx.y == 4) RLMD_TSR(89);
+  if (blockIdx.y == 0 && ts >= 0) RLMD_TSR(ts + 2);
   const bool fused = nh <= NHF;
   fwd_epilogue<NBW, PREC>(acc, k, o, nh, h2_out, m2_out, fused ? nullptr : h2s, L.ldh2, part, row0, B, ex, L.lda1,
                           nb0, nbw);
   if (blockIdx.y == 2) RLMD_TSR(66);
   if (blockIdx.y == 4) RLMD_TSR(90);
+  if (blockIdx.y == 0 && ts >= 0) RLMD_TSR(ts + 3);
   __syncthreads();
   if (blockIdx.y == 2) RLMD_TSR(67);
   if (blockIdx.y == 4) RLMD_TSR(91);
+  if (blockIdx.y == 0 && ts >= 0) RLMD_TSR(ts + 4);
   if (fused) {
     if ((int)threadIdx.x < R * nh) {
       const int r = threadIdx.x % R, h = threadIdx.x / R;
@@ -821,7 +869,8 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     RLMD_TSR(16 * job + 2);
     if constexpr (RLMD_FWD_DEFER)
       mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
-                                 d.A, smem, L, nullptr, nullptr, row0, B, nullptr, nullptr, nullptr, 0, 0, issue_critic);
+                                 d.A, smem, L, nullptr, nullptr, row0, B, nullptr, nullptr, nullptr, 0, 0, issue_critic,
+                                 6);
     else
       mlp_rows<PREC, NBW, MULTI>(an, a.ao, ka, pa, xs, L.ldx, d.S, na, an.p + a.ao.w3, sac ? an.p + a.ao.w4 : nullptr,
                                  d.A, smem, L, nullptr, nullptr, row0, B);
@@ -838,7 +887,7 @@ __global__ void __launch_bounds__(NT) fwd_rows_kernel(FwdRowsArgs a) {
     __syncthreads();
     RLMD_TSR(16 * job + 4);
     mlp_rows<PREC, NBW, MULTI>(cn, a.co, kc, pc, xs, L.ldx, d.X, 1, cn.p + a.co.w3, nullptr, 1, smem, L, nullptr,
-                               nullptr, row0, B, nullptr, nullptr, nullptr, nb0, nbw);
+                               nullptr, row0, B, nullptr, nullptr, nullptr, nb0, nbw, NoHook(), 22);
     RLMD_TSR(16 * job + 5);
     float* qt = (nxt ? a.qtn[job] : a.qt[job]) + p * B;
     if ((int)threadIdx.x < R && row0 + (int)threadIdx.x < B) qt[row0 + threadIdx.x] = hout[threadIdx.x * kHeadsMax];

@@ -78,6 +78,9 @@ def run():
             print(f"  {i}->{j}: {np.median(r[:, j] - r[:, i]):10.0f} cycles")
         print("  total", np.median(r[:, idx[-1]] - r[:, idx[0]]))
     seq("fwd_rows target job 0", [0, 1, 2, 3, 4, 5])
+    seq("fwd_rows job 0 policy MLP (staged -> layer 1 -> barrier -> layer 2 -> epilogue -> barrier -> heads)",
+        [2, 6, 7, 8, 9, 10, 3])
+    seq("fwd_rows job 0 target critic MLP (sampled -> same phases)", [4, 22, 23, 24, 25, 26, 5])
     seq("fwd_rows critic job 2", [60, 61, 63, 64, 65, 66, 67, 62])
     seq("abwd_rows", [96, 95, 97, 98, 99, 100, 101, 103, 104, 105, 108, 109, 106, 107, 110, 111])
     seq("cbwd_rows (0, 0, 0)", [112, 113, 114, 115, 116, 117, 118])
