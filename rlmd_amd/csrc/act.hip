@@ -46,7 +46,7 @@ template <int H1P, int NB, int SP, int MA, int WPC>
 __global__ void __launch_bounds__(256, H1P == 256 ? (MA == kMaxA ? WPC : 2) : 1) fused_act_kernel(FusedActArgs a) {
   RLMD_KERNARG_PREFETCH(a);
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  act_rows<H1P, NB, SP, MA>(
+  act_rows<H1P, NB, SP, MA, act_park(H1P, SP, MA, WPC)>(
       a, smem, [] {},
       [&](int, int b, const float* acts, const float*) {
         for (int j = 0; j < a.A; ++j) a.actions[(int64_t)b * a.A + j] = acts[j];
@@ -101,8 +101,8 @@ int fused_act_launch(const rlmd_agent_cfg& c, const float* obs, int64_t n, float
   RLMD_CHECK(c.action_dim <= kMaxA4, "fused acting: at most 4 actions");
   const bool wpc4 = act_wpc(h1p, c.action_dim <= kMaxA ? kMaxA : kMaxA4, grid.x) == 4;
 #define ACT_LAUNCH2(H1P_, NB_, SP_, MA_, W_)                                                                          \
-  hipExtLaunchKernelGGL((fused_act_kernel<H1P_, NB_, SP_, MA_, W_>), grid, dim3(256), act_lds_bytes(H1P_, SP_, MA_), \
-                        st, ev_start, ev_stop, 0, a)
+  hipExtLaunchKernelGGL((fused_act_kernel<H1P_, NB_, SP_, MA_, W_>), grid, dim3(256),                           \
+                        act_lds_bytes(H1P_, SP_, MA_, act_park(H1P_, SP_, MA_, W_)), st, ev_start, ev_stop, 0, a)
 #define ACT_LAUNCH1(H1P_, NB_, SP_, MA_)                                                        \
   do {                                                                                          \
     if (wpc4) ACT_LAUNCH2(H1P_, NB_, SP_, MA_, ((H1P_) == 256 && (MA_) == kMaxA) ? 4 : 3);      \

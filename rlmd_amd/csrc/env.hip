@@ -778,6 +778,9 @@ struct ActEnvKargs {
   StatFold sf;
 };
 
+#ifndef RLMD_ACT_PARK
+#define RLMD_ACT_PARK 1  // act_env_kernel: the lane state and draw parked in LDS across the acting body
+#endif
 template <int FAM, int NG, int H1P, int NB, int SP, int MA, int WPC>
 __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA ? WPC : 2) : 1) act_env_kernel(rlmd::FusedActArgs a, EnvParams P, uint32_t step,
                                                       float* obs, rlmd::ReplayView rb, int64_t ring_base,
@@ -807,7 +810,33 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
       ep_base = P.ep_rows ? P.ep_cnt[lane >> 6] : 0u;
     }
   };
+  // the lane state and draw through LDS (rlmd_act_rows.h park()): [word][64 rows]
+  constexpr bool PARK = RLMD_ACT_PARK && rlmd::actrows::act_park(H1P, SP, MA, WPC);
+  constexpr rlmd::actrows::ActLds LYP = rlmd::actrows::act_lds(H1P, SP, MA, PARK);
+  uint32_t* pk = reinterpret_cast<uint32_t*>(smem + LYP.total);
+  constexpr int kR = rlmd::actrows::kRows;
+  auto park = [&] {
+    if (PARK && tid < kR) {
+      const uint64_t wb = __builtin_bit_cast(uint64_t, w0), db = __builtin_bit_cast(uint64_t, dr0);
+      pk[0 * kR + tid] = (uint32_t)wb;
+      pk[1 * kR + tid] = (uint32_t)(wb >> 32);
+      pk[2 * kR + tid] = (uint32_t)db;
+      pk[3 * kR + tid] = (uint32_t)(db >> 32);
+      pk[4 * kR + tid] = (uint32_t)t;
+      pk[5 * kR + tid] = ep;
+      pk[6 * kR + tid] = ep_base;
+      pk[7 * kR + tid] = (uint32_t)start;
+    }
+  };
   auto epi = [&](int, int b, const float* acts, const float* obs_row) {
+    if constexpr (PARK) {
+      w0 = __builtin_bit_cast(double, (uint64_t)pk[0 * kR + tid] | ((uint64_t)pk[1 * kR + tid] << 32));
+      dr0 = __builtin_bit_cast(double, (uint64_t)pk[2 * kR + tid] | ((uint64_t)pk[3 * kR + tid] << 32));
+      t = (int)pk[4 * kR + tid];
+      ep = pk[5 * kR + tid];
+      ep_base = pk[6 * kR + tid];
+      start = (int)pk[7 * kR + tid];
+    }
     const int S = P.state_dim, A = P.action_dim;
     // the action by a fixed selection chain (no runtime-indexed register array)
     auto act = [&](int i) -> float {
@@ -883,7 +912,7 @@ __global__ void __launch_bounds__(256, H1P == 256 ? (MA == rlmd::actrows::kMaxA 
       P.time[b] = t + 1;
     }
   };
-  rlmd::actrows::act_rows<H1P, NB, SP, MA>(a, smem, pro, epi);
+  rlmd::actrows::act_rows<H1P, NB, SP, MA, PARK>(a, smem, pro, epi, park);
   if (sf.part_out) {  // the block's finished-episode statistics, as env_train_kernel
     __shared__ double red[3][256 / 64];
 #pragma unroll
@@ -1484,7 +1513,9 @@ int env_act_train(rlmd_env_t env, const ReplayView& rb, int64_t ring_base, uint3
   RLMD_CHECK(sp == 8 || P.fam == RLMD_MARKET, "fused acting + env step: state wider than 8 (market only)");
   const bool wpc4 = actrows::act_wpc(h1p, P.action_dim > actrows::kMaxA ? actrows::kMaxA4 : actrows::kMaxA, grid.x) == 4;
 #define FUSEDW(F, NG, H, B, SP, MA, W)                                                                                  \
-  hipExtLaunchKernelGGL((act_env_kernel<F, NG, H, B, SP, MA, W>), grid, block, actrows::act_lds_bytes(H, SP, MA), stream, \
+  hipExtLaunchKernelGGL((act_env_kernel<F, NG, H, B, SP, MA, W>), grid, block,                                        \
+                        actrows::act_lds_bytes(H, SP, MA, RLMD_ACT_PARK && actrows::act_park(H, SP, MA, W)) +               \
+                            (RLMD_ACT_PARK && actrows::act_park(H, SP, MA, W) ? actrows::kParkBytes : 0), stream,            \
                         ev_start, ev_stop, 0, a, env->P, step, obs, rb, ring_base, sf)
 #define FUSEDM(F, NG, H, B, SP, MA)                                                           \
   do {                                                                                        \

@@ -80,10 +80,12 @@ struct L1Tiles {
 // a 256-wide block at 36 KB, four workgroups per CU (1,024 blocks of 65,536
 // lanes in one round instead of 768 + 256); wider nets keep separate regions.
 struct ActLds {
-  int h1, part, w1, b1, obs, total;
+  int h1, part, w1, b1, obs, samp, total;
   bool alias;
 };
-__host__ __device__ constexpr ActLds act_lds(int h1p, int sp, int ma) {
+// park: the parked instantiations (4 workgroups per CU, act_park) also hold the
+// sampling rows' head biases and noise in LDS
+__host__ __device__ constexpr ActLds act_lds(int h1p, int sp, int ma, bool park = false) {
   const int nt = h1p / 16, ntp = (nt + 7) / 8 * 8 + 4;
   const int h1b = kRows * (h1p + 8) * 2, partb = 4 * kRows * 2 * ma * 4, w1b = sp * 16 * ntp * 4;
   const bool al = h1p <= 256;
@@ -94,7 +96,8 @@ __host__ __device__ constexpr ActLds act_lds(int h1p, int sp, int ma) {
   l.w1 = al ? 0 : h1b + partb;
   l.b1 = al ? h1b : l.w1 + w1b;
   l.obs = l.b1 + h1p * 4;
-  l.total = l.obs + kRows * sp * 4;
+  l.samp = l.obs + kRows * sp * 4;  // the sampling rows' head biases and noise [3][ma][64] (parked)
+  l.total = l.samp + (park ? 3 * ma * kRows * 4 : 0);
   return l;
 }
 
@@ -103,18 +106,35 @@ __host__ __device__ constexpr ActLds act_lds(int h1p, int sp, int ma) {
 // b, act, obs_row) runs on thread r < 64 of each valid row b with the row's
 // actions act[MA] (f32; MA = kMaxA, or kMaxA4 for 3-4 actions: twice the head
 // registers and partials) and its observation in LDS (obs_row[0 .. S)).
-template <int H1P, int NB, int SP, int MA, typename ProF, typename EpiF>
-__device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* smem, ProF pro, EpiF epi) {
+struct NoPark {
+  __device__ void operator()() const {}
+};
+// park() runs once this thread's staging loads have landed (after their LDS
+// stores, before the barrier): a fused caller moves the per-row values its pro()
+// loaded into LDS there (kParkBytes past act_lds().total), so that they are not
+// held in registers across the body — at 4 workgroups per CU (128 VGPRs) they
+// were spilled to scratch, each spill store waiting for its load on the spot
+constexpr int kParkWords = 8;
+constexpr int kParkBytes = kRows * kParkWords * 4;
+// PARK: the 4-workgroups-per-CU instantiations (128 VGPRs), whose values held
+// across the body were spilled; act_park(H1P, SP, MA, WPC)
+__host__ __device__ constexpr bool act_park(int h1p, int sp, int ma, int wpc) {
+  return h1p == 256 && sp == 8 && ma == kMaxA && wpc == 4;  // act_lds + kParkBytes fit 40 KB
+}
+template <int H1P, int NB, int SP, int MA, bool PARK, typename ProF, typename EpiF, typename ParkF = NoPark>
+__device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* smem, ProF pro, EpiF epi,
+                                         ParkF park = ParkF()) {
   constexpr int kMaxA = MA;
   constexpr int HP = H1P + 8;  // bf16 row pitch: 16-B aligned fragment reads
   constexpr int NT = L1Tiles<H1P>::NT, NTP = L1Tiles<H1P>::NTP;
-  constexpr ActLds LY = act_lds(H1P, SP, MA);
+  constexpr ActLds LY = act_lds(H1P, SP, MA, PARK);
   unsigned short* h1s = reinterpret_cast<unsigned short*>(smem + LY.h1);  // [64][HP]
   float* part = reinterpret_cast<float*>(smem + LY.part);                 // [4][64][2A]
   const int H1 = a.H1, H2 = a.H2;
   float* w1s = reinterpret_cast<float*>(smem + LY.w1);                    // w1g [SP][16][NTP]
   float* b1s = reinterpret_cast<float*>(smem + LY.b1);                    // [H1P]
   float* obs_s = reinterpret_cast<float*>(smem + LY.obs);                 // [64][SP]
+  float* samp_s = reinterpret_cast<float*>(smem + LY.samp);               // [3][MA][64]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row0 = blockIdx.x * kRows;
   const NetOff& o = a.off;
@@ -198,6 +218,17 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
       const int e = j * 256 + tid;
       if (e < nO) obs_s[e] = vo[j];
     }
+    // the sampling threads' head biases and noise to LDS, read back at sampling
+    // time: held in registers across the body they were spilled (see park())
+    if (PARK && tid < kRows) {
+#pragma unroll
+      for (int j = 0; j < kMaxA; ++j) {
+        samp_s[(0 * kMaxA + j) * kRows + tid] = mu_b[j];
+        samp_s[(1 * kMaxA + j) * kRows + tid] = ls_b[j];
+        samp_s[(2 * kMaxA + j) * kRows + tid] = nz[j];
+      }
+    }
+    park();
   }
   // layer-2 B fragments of the first K step: issued now, consumed after layer 1
   // fragment (band NB wave + nb, K-step s): 64 lanes x 16 B at ((band * H1P/32 + s) * 64 + lane) * 8
@@ -324,24 +355,32 @@ __device__ __forceinline__ void act_rows(const FusedActArgs& a, unsigned char* s
   }
   __syncthreads();
   RLMD_TSA(5, __builtin_amdgcn_s_memtime());
-  // -- per row: sum the 4 wave partials, sample, write the action
-  if (tid < kRows && row0 + tid < a.n) {
-    const int r = tid, b = row0 + tid;
+  // -- per row: sum the 4 wave partials, sample, write the action.  The row
+  //    index and the algorithm flag are formed here from opaque scalar copies:
+  //    at 128 VGPRs the compiler had kept them in VGPRs from the prologue and
+  //    spilled them (a scratch reload and its wait at sampling time)
+  int row0_l = row0, algo_l = a.algo;
+  if constexpr (PARK) {
+    asm volatile("s_mov_b32 %0, %1" : "=s"(row0_l) : "s"(row0));
+    asm volatile("s_mov_b32 %0, %1" : "=s"(algo_l) : "s"(a.algo));
+  }
+  if (tid < kRows && row0_l + tid < a.n) {
+    const int r = tid, b = row0_l + tid;
     float acts[kMaxA];
 #pragma unroll
     for (int j = 0; j < kMaxA; ++j) acts[j] = 0.f;
 #pragma unroll
     for (int j = 0; j < kMaxA; ++j) {
       if (j >= A) break;
-      float mu = mu_b[j], ls_raw = 0.f;
+      float mu = PARK ? samp_s[(0 * kMaxA + j) * kRows + r] : mu_b[j], ls_raw = 0.f;
       for (int w = 0; w < 4; ++w) mu += part[(w * kRows + r) * 2 * kMaxA + j];
-      if (a.algo == RLMD_SAC) {
-        ls_raw = ls_b[j];
+      if (algo_l == RLMD_SAC) {
+        ls_raw = PARK ? samp_s[(1 * kMaxA + j) * kRows + r] : ls_b[j];
         for (int w = 0; w < 4; ++w) ls_raw += part[(w * kRows + r) * 2 * kMaxA + A + j];
       }
-      const float noise = nz[j];
+      const float noise = PARK ? samp_s[(2 * kMaxA + j) * kRows + r] : nz[j];
       float act;
-      if (a.algo == RLMD_SAC) {
+      if (algo_l == RLMD_SAC) {
         const PolicyComp pc = policy_comp(a.dist, mu, ls_raw, noise, a.ls_min, a.ls_max);
         act = tanhf(a.mode == 1 ? pc.mu : pc.u) * a.max_action;
       } else {
@@ -364,7 +403,9 @@ inline bool fused_shape(const rlmd_agent_cfg& c, int& h1p, int& nb) {
 }
 
 // dynamic LDS of act_rows<h1p, *, sp, ma>
-inline size_t act_lds_bytes(int h1p, int sp, int ma = kMaxA) { return (size_t)act_lds(h1p, sp, ma).total; }
+inline size_t act_lds_bytes(int h1p, int sp, int ma = kMaxA, bool park = false) {
+  return (size_t)act_lds(h1p, sp, ma, park).total;
+}
 
 // the acting body's action bound for an action count
 inline int act_ma(int action_dim) { return action_dim <= kMaxA ? kMaxA : kMaxA4; }
