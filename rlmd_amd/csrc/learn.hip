@@ -901,7 +901,7 @@ int learn_body(rlmd_agent_s* ag, const Batch& mb, const float* eps_a, const floa
       au.tj = d.H1p / 32;
       au.ti = d.H2p / 32;
       au.n_w2 = au.ti * au.tj;
-      au.n_w1 = d.H1p / 32;
+      au.n_w1 = actor_update_n_w1(d);
       au.qsplit = qsplit;
       RLMD_TRY(actor_update_launch(au, st));
       return 0;

@@ -59,6 +59,7 @@ struct ActUpdArgs {
 };
 
 size_t critic_update_lds();
+int actor_update_n_w1(const RowDims& d);  // fc1 blocks of the actor step (TW1 units each)
 int critic_update_tj(const RowDims& d);  // fc2.weight tile columns of the critic step (32 x 64 tiles at B <= 256)
 int actor_update_launch(const ActUpdArgs& a, hipStream_t st);
 int critic_update_launch(const CritUpdArgs& a, hipStream_t st);

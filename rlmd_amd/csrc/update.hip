@@ -37,7 +37,16 @@ namespace {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int NT = 512;
+#ifndef RLMD_W1_HALF
+#define RLMD_W1_HALF 1  // the actor step's fc1 blocks 16 units wide (0: 32): twice the blocks, half the bases each
+#endif
 constexpr int TW = 32;
+// the actor step's fc1 block width: its bases (nh x B x TW1 f32) made it the
+// launch's last workgroup to finish at 32 (128 KB of loads at C2)
+constexpr int TW1 = RLMD_W1_HALF ? 16 : 32;
+constexpr int kW1G = NT / TW1;      // row groups of an fc1 block (a thread per unit and group)
+constexpr int kW1R = 512 / kW1G;    // rows per group (B <= 512)
+constexpr int kW1Q = kW1R / 4;      // f32x4 base loads per thread and head
 // timing ablations (experiment builds only, RLMD_EXTRA_FLAGS=-DRLMD_ABL=<bits>; the
 // results are wrong): 1 no ranking (rank = row), 2 no optimiser step / copies
 #ifndef RLMD_ABL
@@ -673,7 +682,7 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
   const bool first_col = ROLE < 0 ? !stats_wg && t >= a.n_w2 + a.n_w1 : ROLE == kRoleHead && !stats_wg;  // a head workgroup
   const bool w1blk = ROLE < 0 ? !stats_wg && !w2tile && !first_col : ROLE == kRoleW1;
   const int i0 = w2tile ? (t / a.tj) * TW : first_col ? (t - a.n_w2 - a.n_w1) * TW : 0;
-  const int j0 = w2tile ? (t % a.tj) * TW : w1blk ? (t - a.n_w2) * TW : 0;
+  const int j0 = w2tile ? (t % a.tj) * TW : w1blk ? (t - a.n_w2) * TW1 : 0;
   const bool polyak = adam_polyak(a.adam);
   const CopyDst cd = copy_dst(a.adam, 0);
   auto step = [&](int pi, float gv, const AdamIn& in) {
@@ -781,7 +790,7 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
   AdamIn xin;
   float xv[8];
   constexpr int kUP = 2;  // bases prefetched per fc1-block thread (the rest load in the loop)
-  f32x4 uv[kUP][8];
+  f32x4 uv[kUP][kW1Q];
   const int64_t ustride = (int64_t)nrb * H1p * 16;
   const __amdgpu_buffer_rsrc_t ru = rlmd_rsrc(a.ua, ustride * nh * 4);
   // the fc1 block operands: the block's rows of s and its first kUP bases, and the
@@ -793,12 +802,12 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
       const int e = tid + q * NT, r = e >> 3, c = e & 7;
       xv[q] = rlmd_ldf(rx, (int64_t)r * S + c, w1blk && r < B && c < S);
     }
-    const int j = j0 + (tid & 31), p = tid >> 5;
+    const int j = j0 + tid % TW1, p = tid / TW1;
 #pragma unroll
     for (int h = 0; h < kUP; ++h)
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int r = 32 * p + 4 * q;
+      for (int q = 0; q < kW1Q; ++q) {
+        const int r = kW1R * p + 4 * q;
         const bool ok = w1blk && h < nh && r < nrb * 16 && j < H1p;
         uv[h][q] = __builtin_bit_cast(
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
@@ -806,8 +815,8 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
       }
   };
   auto w1_adam = [&]() {
-    const int c = tid >> 5, jr = j0 + (tid & 31);
-    if (w1blk && tid < 32 * 9 && (c < S || c == 8) && jr < H1)
+    const int c = tid / TW1, jr = j0 + tid % TW1;
+    if (w1blk && tid < TW1 * 9 && (c < S || c == 8) && jr < H1)
       xpi = (int)(c == 8 ? ao.b1 + jr : ao.w1 + (int64_t)jr * S + c);
   };
   // an fc1 block with its own body issues them with the first load round, under
@@ -1023,15 +1032,15 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
     }
   } else if (IS_W1) {
     // ---- dW1[j, x] = sum_b dh1[b, j] s[b, x], db1[j]; dh1 = sum_h gh[b, h] U_h[b, j]
-    const int cj = tid & 31, p = tid >> 5, j = j0 + cj;
+    const int cj = tid % TW1, p = tid / TW1, j = j0 + cj;
 #pragma unroll
     for (int q = 0; q < 8; ++q) xs[tid + q * NT] = xv[q];
     __syncthreads();
-    // dh1 of the thread's 32 rows: heads in order, the first from registers
-    f32x4 du[8];
+    // dh1 of the thread's kW1R rows: heads in order, the first from registers
+    f32x4 du[kW1Q];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const int r = 32 * p + 4 * q;
+    for (int q = 0; q < kW1Q; ++q) {
+      const int r = kW1R * p + 4 * q;
       du[q] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int h = 0; h < kUP; ++h)
@@ -1039,26 +1048,26 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
         for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(r + e) * kHM + h], uv[h][q][e], du[q][e]);
     }
     for (int h = kUP; h < nh; ++h) {
-      f32x4 u[8];
+      f32x4 u[kW1Q];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int r = 32 * p + 4 * q;
+      for (int q = 0; q < kW1Q; ++q) {
+        const int r = kW1R * p + 4 * q;
         const bool ok = r < nrb * 16 && j < H1p;
         u[q] = __builtin_bit_cast(
             f32x4, __builtin_amdgcn_raw_buffer_load_b128(ru, ok ? (int)((h * ustride + rp_idx(r, H1p, j)) * 4) : 0x7fffffff,
                                                          0, 0));
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
+      for (int q = 0; q < kW1Q; ++q)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(32 * p + 4 * q + e) * kHM + h], u[q][e], du[q][e]);
+        for (int e = 0; e < 4; ++e) du[q][e] = fmaf(ghs[(kW1R * p + 4 * q + e) * kHM + h], u[q][e], du[q][e]);
     }
     float acc[9];
 #pragma unroll
     for (int c = 0; c < 9; ++c) acc[c] = 0.f;
 #pragma unroll 2
-    for (int q = 0; q < 8; ++q) {
-      const int r = 32 * p + 4 * q;
+    for (int q = 0; q < kW1Q; ++q) {
+      const int r = kW1R * p + 4 * q;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         acc[8] += du[q][e];
@@ -1069,12 +1078,12 @@ __device__ __forceinline__ void actor_update_body(const ActUpdArgs& a, unsigned 
     RLMD_TSA(5);
     __syncthreads();
 #pragma unroll
-    for (int c = 0; c < 9; ++c) part[(p * 9 + c) * 32 + cj] = acc[c];
+    for (int c = 0; c < 9; ++c) part[(p * 9 + c) * TW1 + cj] = acc[c];
     __syncthreads();
-    if (xpi >= 0) {  // 32 rows x (S + 1) outputs, thread c * 32 + jj (Adam state prefetched)
-      const int jj = tid & 31, c = tid >> 5;
+    if (xpi >= 0) {  // TW1 rows x (S + 1) outputs, thread c * TW1 + jj (Adam state prefetched)
+      const int jj = tid % TW1, c = tid / TW1;
       float vsum = 0.f;
-      for (int q = 0; q < 16; ++q) vsum += part[(q * 9 + c) * 32 + jj];
+      for (int q = 0; q < kW1G; ++q) vsum += part[(q * 9 + c) * TW1 + jj];
       step(xpi, vsum, xin);
     }
   }
@@ -1096,12 +1105,14 @@ extern "C" int rlmd_debug_ts_aupd(unsigned long long* out) {
 #endif
 
 size_t critic_update_lds() { return (size_t)ULds::total; }
+int actor_update_n_w1(const RowDims& d) { return d.H1p / TW1; }
 int critic_update_tj(const RowDims& d) { return d.B <= 256 ? (d.H1p / TW + 1) / 2 : d.H1p / TW; }
 
 int actor_update_launch(const ActUpdArgs& a, hipStream_t st) {
   const RowDims& d = a.d;
   RLMD_CHECK(d.B <= NT && d.S <= 8 && d.A <= kAM, "actor update: B <= 512, state width <= 8, actions <= 2");
-  RLMD_CHECK(a.tj == d.H1p / TW && a.ti * TW >= d.H2p && a.n_w2 == a.ti * a.tj && a.n_w1 == d.H1p / TW,
+  RLMD_CHECK(a.tj == d.H1p / TW && a.ti * TW >= d.H2p && a.n_w2 == a.ti * a.tj && a.n_w1 == d.H1p / TW1 &&
+                 d.H1p % TW1 == 0,
              "actor update: tile grid inconsistent with the widths");
   RLMD_CHECK(a.cstats.B <= NT, "critic statistics workgroup: mini-batch up to 512 rows");
   const dim3 grid(a.n_w2 + a.n_w1 + a.ti + (a.cstats.B > 0 ? 2 : 0));
