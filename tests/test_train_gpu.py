@@ -223,6 +223,41 @@ def test_fused_bf16_act_matches_emulated_reference(dev, algo, S, A, h1, h2):
     assert not torch.equal(sto_philox, det)
 
 
+@pytest.mark.parametrize("algo,S,A", [("SAC", 5, 1), ("SAC", 6, 2), ("TD3", 5, 1)])
+def test_fused_act_four_per_cu_bit_equal(dev, algo, S, A):
+    """At 65,539 rows (1,025 blocks, more than 3 per CU fit in one dispatch round) the
+    256-wide acting kernel runs 4 workgroups per CU with its sampling rows' head
+    biases and noise parked in LDS (rlmd_act_rows.h act_park); at 4,099 rows the same
+    body runs 3 per CU with them in registers.  Actions of the shared rows are
+    bit-equal — deterministic, injected noise and Philox noise (keyed by row and
+    counter) — and the large launch matches the torch restatement like the small one."""
+    from rlmd_amd.agent import DeviceAgent, reference_init
+
+    h1 = h2 = 256
+    init = reference_init(algo, S, A, h1, h2, seed=5)
+    ag = DeviceAgent(algo, S, A, h1, h2, 512, 256, init=init, precision="bf16", device=dev)
+    p, t = _flat_init(algo, S, A, h1, h2, init)
+    ora = ol.OracleLearner(algo, S, A, h1, h2, 512, 256, "MSE", p, t)
+    rng = np.random.default_rng(2)
+    big, small = 65539, 4099
+    obs = torch.from_numpy(rng.standard_normal((big, S)).astype(np.float32))
+    eps = torch.from_numpy(rng.standard_normal((big, A)).astype(np.float32))
+    with torch.no_grad():
+        got = {n: (ag.act(obs[:n], mode=1).cpu(), ag.act(obs[:n], mode=0, eps=eps[:n]).cpu(),
+                   ag.act(obs[:n], mode=0, noise_ctr=7).cpu()) for n in (big, small)}
+    for i, name in enumerate(("deterministic", "injected noise", "Philox noise")):
+        assert torch.equal(got[big][i][:small], got[small][i]), name
+    ref_det, ref_sto = _bf16_act_reference(ora.nets(ora.P)["actor"], obs, eps, algo, ora.max_action, ora.ls_min,
+                                           ora.ls_max, ora.policy_noise)
+    for g, ref in ((got[big][0], ref_det), (got[big][1], ref_sto)):
+        err = (g - ref).abs()
+        assert (err <= 1e-4).float().mean().item() >= 0.999, err.max().item()
+        assert err.max().item() <= 1e-3
+    phil = got[big][2]
+    assert torch.isfinite(phil).all() and (phil.abs() <= ora.max_action).all()
+    assert np.unique(phil.numpy()).size > big // 2
+
+
 def test_policy_steps_apply_action_window_and_learn(dev):
     from rlmd_amd.trainer import VecTrainer
 
