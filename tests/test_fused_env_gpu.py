@@ -152,6 +152,33 @@ def test_fused_equals_unfused(golden, dev, env, inv, n, obs_days, algo):
     np.testing.assert_array_equal(pa, pb)  # the K = 1 updates learned from identical rings
 
 
+@pytest.mark.parametrize("algo", ["SAC", "TD3"])
+def test_fused_equals_unfused_four_per_cu(golden, dev, algo):
+    """As above at 65,600 lanes (1,025 acting blocks): both the fused act_env_kernel and
+    the two-launch path's acting kernel run 4 workgroups per CU with their per-row
+    values parked in LDS (act_env: the lane state and draw too)."""
+    N, T = 65600, 4
+    out = []
+    for fused in (1, 0):
+        tr, _ = _trainer(dev, golden, "gbm", "A", algo, N, T, k=1, seed=9, n=1, obs_days=1)
+        tr.set_fused(fused)
+        for t in range(T):
+            tr.step()
+            assert tr.last_fused() == bool(fused)
+        ring = read_ring(tr, 0, N * T)
+        w, tt = tr.env.lane_state()
+        out.append((ring, w, tt, tr.obs.cpu().numpy(), tr.agent.params.cpu().numpy().copy()))
+        del tr
+    (ra, wa, ta, oa, pa), (rb, wb, tb, ob, pb) = out
+    for name, x, y in zip(("s", "a", "r", "s2", "d"), ra, rb):
+        np.testing.assert_array_equal(x, y, err_msg=f"ring {name}")
+    np.testing.assert_array_equal(wa, wb)
+    np.testing.assert_array_equal(ta, tb)
+    np.testing.assert_array_equal(oa, ob)
+    np.testing.assert_array_equal(pa, pb)
+    assert np.unique(ra[1][:, 0]).size > N  # stochastic policy actions over the T steps
+
+
 @pytest.mark.parametrize("fused", [1, 0])
 @pytest.mark.parametrize("env,inv,n,obs_days", [("gbm", "A", 1, 1), ("coin", "B", 1, 1), ("dice", "C", 1, 1),
                                                 ("market", "A", 1, 1), ("market", "B", 1, 5),
